@@ -1,0 +1,316 @@
+// BatchNorm2d (training + eval) for NHWC bf16 activations with fp32 statistics (SURVEY.md §2.8 K-05,
+// K-06, K-07; reference modules: pytorch_code/model_ops/resnet.py:20-35, 45-63).
+//
+// The statistics pass is normally FUSED into the producing convolution's epilogue
+// (gemm_mfma.hip writes per-64-row partial (sum, sumsq) slabs); `pdnn_bn_stats` is the standalone
+// version for inputs that were not produced by our conv.  The normalisation itself is usually fused
+// into the CONSUMING convolution's operand loader (affine + ReLU prologue), so the only materialising
+// kernel in a ResNet block is `pdnn_bn_apply` at the block output, which also fuses the residual
+// branch (identity, or the downsample conv's own BN) and the final ReLU.
+//
+// Slab layout shared by every partial-statistics producer: [rows][2][C] fp32 — for partial row i,
+// slab[(2i)*C + c] = sum, slab[(2i+1)*C + c] = sum of squares (or, in backward, sum(g) / sum(g*xhat)).
+//
+// Memory layout: x is [L][C] with L = N*H*W, channel fastest.  Each thread owns 8 consecutive channels
+// (16-byte loads, Guideline 13); C must be a multiple of 8 and C/8 <= 256.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+// finalize partial sums -> mean, invstd, scale/shift (+ running-stat update).  One thread/channel,
+// fp64 accumulation across partial rows.
+__global__ void bn_finalize_kernel(const float* __restrict__ slab, int rows, int C, double L, float eps,
+                                   float momentum, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* run_mean, float* run_var,
+                                   float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < rows; ++r) {
+        s += slab[(long)(2 * r) * C + c];
+        q += slab[(long)(2 * r + 1) * C + c];
+    }
+    const double mean = s / L;
+    double var = q / L - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+        const double unb = L > 1 ? var * L / (L - 1) : var;
+        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
+        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+    }
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    if (mean_out) mean_out[c] = (float)mean;
+    if (invstd_out) invstd_out[c] = inv;
+    scale_out[c] = g * inv;
+    shift_out[c] = b - (float)mean * g * inv;
+}
+
+// eval-mode scale/shift from running statistics
+__global__ void bn_eval_coeff_kernel(int C, float eps, const float* gamma, const float* beta,
+                                     const float* rm, const float* rv, float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float inv = rsqrtf(rv[c] + eps);
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    scale[c] = g * inv;
+    shift[c] = b - rm[c] * g * inv;
+}
+
+// Per-channel partial sum / sumsq over a grid-strided row range.
+__global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__ x, long L, int C,
+                                                      float* __restrict__ slab) {
+    __shared__ float red[2][NT * 8];
+    const int CG = C >> 3;                 // channel groups of 8
+    const int RPI = NT / CG;               // rows per iteration
+    const int t = threadIdx.x, cg = t % CG, rr = t / CG;
+    float s[8] = {0}, q[8] = {0};
+    if (rr < RPI) {
+        for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
+            float v[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(x + r * C + cg * 8), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s[j] += v[j]; q[j] += v[j] * v[j]; }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][t * 8 + j] = s[j]; red[1][t * 8 + j] = q[j]; }
+    __syncthreads();
+    for (int c = t; c < C; c += NT) {
+        const int g = c >> 3, j = c & 7;
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + g) * 8 + j]; b += red[1][(k * CG + g) * 8 + j]; }
+        slab[(long)(2 * blockIdx.x) * C + c] = a;
+        slab[(long)(2 * blockIdx.x + 1) * C + c] = b;
+    }
+}
+
+// y = act(x*scale + shift + residual'), residual' = res (identity) or res*rscale + rshift
+__global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ x, long L, int C,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const bf16_t* __restrict__ res,
+                                                      const float* __restrict__ rscale,
+                                                      const float* __restrict__ rshift, int relu,
+                                                      bf16_t* __restrict__ y) {
+    const int CG = C >> 3;
+    const long total = L * CG;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+        const long r = i / CG;
+        const int c = (int)(i - r * CG) * 8;
+        float v[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(x + r * C + c), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], scale[c + j], shift[c + j]);
+        if (res) {
+            float rv[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(res + r * C + c), rv);
+            if (rscale) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += fmaf(rv[j], rscale[c + j], rshift[c + j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+        }
+        if (relu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        *reinterpret_cast<u16x8_t*>(y + r * C + c) = pack8(v);
+    }
+}
+
+// mask modes for the backward: 0 none, 1 mask = (msrc > 0), 2 mask = (x*mscale + mshift > 0)
+__device__ __forceinline__ void masked_grad(const bf16_t* g, const bf16_t* x, const bf16_t* msrc,
+                                            const float* mscale, const float* mshift, int mode, long off,
+                                            int c, float* gm, float* xv) {
+    unpack8(*reinterpret_cast<const u16x8_t*>(g + off), gm);
+    unpack8(*reinterpret_cast<const u16x8_t*>(x + off), xv);
+    if (mode == 1) {
+        float m[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(msrc + off), m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
+    } else if (mode == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], mscale[c + j], mshift[c + j]) > 0.f ? gm[j] : 0.f;
+    }
+}
+
+// partial sums of gm and gm*xhat (xhat = (x-mean)*invstd) for one or two BNs sharing gm.
+__global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int mode,
+    const bf16_t* __restrict__ msrc, const float* __restrict__ mscale, const float* __restrict__ mshift,
+    float* __restrict__ slab, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
+    const float* __restrict__ invstd2, float* __restrict__ slab2) {
+    __shared__ float red[2][NT * 8];
+    const int CG = C >> 3, RPI = NT / CG;
+    const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
+    float s[8] = {0}, q[8] = {0}, s2[8] = {0}, q2[8] = {0};
+    float mu[8], is[8], mu2[8], is2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        mu[j] = mean[c + j]; is[j] = invstd[c + j];
+        mu2[j] = x2 ? mean2[c + j] : 0.f; is2[j] = x2 ? invstd2[c + j] : 0.f;
+    }
+    if (rr < RPI) {
+        for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
+            float gm[8], xv[8];
+            masked_grad(g, x, msrc, mscale, mshift, mode, r * C + c, c, gm, xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s[j] += gm[j]; q[j] += gm[j] * (xv[j] - mu[j]) * is[j]; }
+            if (x2) {
+                float x2v[8];
+                unpack8(*reinterpret_cast<const u16x8_t*>(x2 + r * C + c), x2v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) q2[j] += gm[j] * (x2v[j] - mu2[j]) * is2[j];
+            }
+        }
+    }
+    for (int pass = 0; pass < (x2 ? 2 : 1); ++pass) {
+        float* out = pass ? slab2 : slab;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[0][t * 8 + j] = s[j];
+            red[1][t * 8 + j] = pass ? q2[j] : q[j];
+        }
+        __syncthreads();
+        for (int cc = t; cc < C; cc += NT) {
+            const int gg = cc >> 3, j = cc & 7;
+            float a = 0.f, b = 0.f;
+            for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + gg) * 8 + j]; b += red[1][(k * CG + gg) * 8 + j]; }
+            out[(long)(2 * blockIdx.x) * C + cc] = a;
+            out[(long)(2 * blockIdx.x + 1) * C + cc] = b;
+        }
+        __syncthreads();
+    }
+}
+
+// sum partial rows -> dbeta (= sum gm), dgamma (= sum gm*xhat).  Optionally accumulate (+=).
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows, int C, float* dgamma,
+                                       float* dbeta, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < rows; ++r) {
+        s += slab[(long)(2 * r) * C + c];
+        q += slab[(long)(2 * r + 1) * C + c];
+    }
+    if (accumulate) { dbeta[c] += (float)s; dgamma[c] += (float)q; }
+    else { dbeta[c] = (float)s; dgamma[c] = (float)q; }
+}
+
+// dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L); optionally also a second BN's dx2 and/or gm.
+__global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ dgamma, const float* __restrict__ dbeta, int mode,
+    const bf16_t* __restrict__ msrc, const float* __restrict__ mscale, const float* __restrict__ mshift,
+    bf16_t* __restrict__ dx, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
+    const float* __restrict__ invstd2, const float* __restrict__ gamma2, const float* __restrict__ dgamma2,
+    const float* __restrict__ dbeta2, bf16_t* __restrict__ dx2, bf16_t* __restrict__ gm_out) {
+    const int CG = C >> 3;
+    const long total = L * CG;
+    const float invL = (float)(1.0 / (double)L);
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+        const long r = i / CG;
+        const int c = (int)(i - r * CG) * 8;
+        const long off = r * C + c;
+        float gm[8], xv[8], o[8];
+        masked_grad(g, x, msrc, mscale, mshift, mode, off, c, gm, xv);
+        if (dx) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float is = invstd[c + j];
+                const float xh = (xv[j] - mean[c + j]) * is;
+                const float k = (gamma ? gamma[c + j] : 1.f) * is;
+                o[j] = k * (gm[j] - dbeta[c + j] * invL - xh * dgamma[c + j] * invL);
+            }
+            *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
+        }
+        if (x2) {
+            float x2v[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(x2 + off), x2v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float is = invstd2[c + j];
+                const float xh = (x2v[j] - mean2[c + j]) * is;
+                const float k = (gamma2 ? gamma2[c + j] : 1.f) * is;
+                o[j] = k * (gm[j] - dbeta2[c + j] * invL - xh * dgamma2[c + j] * invL);
+            }
+            *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
+        }
+        if (gm_out) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
+    }
+}
+
+inline unsigned reduce_grid(long L, int C) {
+    const int rpi = NT / (C / 8);
+    long g = (L + rpi * 64 - 1) / (rpi * 64);   // >= 64 rows per thread-row
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+}  // namespace
+
+PDNN_API int pdnn_bn_reduce_rows(long L, int C) { return (int)reduce_grid(L, C); }
+
+PDNN_API int pdnn_bn_finalize(const float* slab, int rows, int C, double L, float eps, float momentum,
+                              const float* gamma, const float* beta, float* run_mean, float* run_var,
+                              float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slab, rows, C, L, eps,
+                       momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm,
+                                const float* rv, float* scale, float* shift, hipStream_t st) {
+    hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, eps, gamma, beta,
+                       rm, rv, scale, shift);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_stats(const bf16_t* x, long L, int C, float* slab, hipStream_t st) {
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(reduce_grid(L, C)), dim3(NT), 0, st, x, L, C, slab);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_apply(const bf16_t* x, long L, int C, const float* scale, const float* shift,
+                           const bf16_t* res, const float* rscale, const float* rshift, int relu, bf16_t* y,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(L * (C / 8), NT)), dim3(NT), 0, st, x, L, C, scale,
+                       shift, res, rscale, rshift, relu, y);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
+                                const float* invstd, int mode, const bf16_t* msrc, const float* mscale,
+                                const float* mshift, float* slab, const bf16_t* x2, const float* mean2,
+                                const float* invstd2, float* slab2, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(reduce_grid(L, C)), dim3(NT), 0, st, g, x, L, C, mean,
+                       invstd, mode, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dgamma, float* dbeta,
+                                  int accumulate, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slab, rows, C, dgamma,
+                       dbeta, accumulate);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_bn_bwd_apply(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* dgamma,
+                               const float* dbeta, int mode, const bf16_t* msrc, const float* mscale,
+                               const float* mshift, bf16_t* dx, const bf16_t* x2, const float* mean2,
+                               const float* invstd2, const float* gamma2, const float* dgamma2,
+                               const float* dbeta2, bf16_t* dx2, bf16_t* gm_out, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(L * (C / 8), NT)), dim3(NT), 0, st, g, x, L, C,
+                       mean, invstd, gamma, dgamma, dbeta, mode, msrc, mscale, mshift, dx, x2, mean2, invstd2,
+                       gamma2, dgamma2, dbeta2, dx2, gm_out);
+    PDNN_LAUNCH_RET;
+}

@@ -1,0 +1,91 @@
+// Shared device helpers for the CDNA4 (gfx950) kernel library.
+//
+// Conventions used by every kernel in this directory:
+//  * bf16 tensors are passed as raw `uint16_t*` (bit pattern), converted with the helpers below;
+//    the float->bf16 conversion is a plain `__bf16` cast, which hipcc lowers to
+//    `v_cvt_pk_bf16_f32` (round-to-nearest-even, NaN preserving).
+//  * Every launcher is `extern "C" int pdnn_<name>(..., hipStream_t)` returning the hipError_t of the
+//    launch, so the Python side can raise loudly.  No launcher allocates or synchronises: they are
+//    safe inside hipGraph capture (cdna_hip_programming.md Guideline 9).
+//  * Wavefront = 64 lanes.  Block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PDNN_API extern "C" __attribute__((visibility("default")))
+#define PDNN_LAUNCH_RET return (int)hipGetLastError()
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA A/B operand (16x16x32 / 32x32x16)
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 accumulator fragment
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 accumulator fragment
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+    return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(bf16_t, b);
+}
+
+template <typename T> struct Ld;
+template <> struct Ld<float> {
+    static __device__ __forceinline__ float get(const float* p, long i) { return p[i]; }
+    static __device__ __forceinline__ void put(float* p, long i, float v) { p[i] = v; }
+};
+template <> struct Ld<bf16_t> {
+    static __device__ __forceinline__ float get(const bf16_t* p, long i) { return bf2f(p[i]); }
+    static __device__ __forceinline__ void put(bf16_t* p, long i, float v) { p[i] = f2bf(v); }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64).  `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+}
+
+// Unpack 8 bf16 (16 bytes) to floats and back.
+__device__ __forceinline__ void unpack8(const u16x8_t& v, float* f) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = bf2f(v[i]);
+}
+__device__ __forceinline__ u16x8_t pack8(const float* f) {
+    u16x8_t v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = f2bf(f[i]);
+    return v;
+}
+
+__host__ __device__ constexpr inline long cdiv(long a, long b) { return (a + b - 1) / b; }
+
+// Grid size for grid-stride memory-bound kernels: <= 8 blocks/CU * 256 CUs (Guideline 11).
+inline unsigned stream_grid(long work_items, int per_block) {
+    long g = (work_items + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    return (unsigned)g;
+}

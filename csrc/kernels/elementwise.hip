@@ -1,0 +1,133 @@
+// Elementwise kernels (SURVEY.md §2.8 K-06 ReLU, K-07 residual add, K-10 sigmoid + derivative,
+// K-17 input preprocessing, K-18 GELU).  All vectorised 16 bytes per lane (Guideline 13).
+// Reference call sites: MPI_code/src/util/util.h:84-123 (Relu/Sigmoid and their gradients),
+// pytorch_code/model_ops/resnet.py:32-35 (relu, residual add), pure_py_code/nn/nn_utils.py:4-8.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+// op: 0 relu, 1 sigmoid, 2 gelu(tanh), 3 identity
+__device__ __forceinline__ float act_f(float x, int op) {
+    if (op == 0) return fmaxf(x, 0.f);
+    if (op == 1) return 1.f / (1.f + __expf(-x));
+    if (op == 2) {
+        const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+        return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+    }
+    return x;
+}
+// derivative given the INPUT x (relu/gelu) or the OUTPUT y (sigmoid, y(1-y) as in util.h:115-123)
+__device__ __forceinline__ float act_d(float x, int op) {
+    if (op == 0) return x > 0.f ? 1.f : 0.f;
+    if (op == 1) { const float y = 1.f / (1.f + __expf(-x)); return y * (1.f - y); }
+    if (op == 2) {
+        const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+        const float u = k0 * (x + k1 * x * x * x);
+        const float t = tanhf(u);
+        return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+    }
+    return 1.f;
+}
+
+__global__ void __launch_bounds__(NT) act_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long n8,
+                                                     int op) {
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+        float v[8];
+        unpack8(reinterpret_cast<const u16x8_t*>(x)[i], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_f(v[j], op);
+        reinterpret_cast<u16x8_t*>(y)[i] = pack8(v);
+    }
+}
+__global__ void __launch_bounds__(NT) act_bwd_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ x,
+                                                     bf16_t* __restrict__ dx, long n8, int op) {
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+        float gv[8], xv[8];
+        unpack8(reinterpret_cast<const u16x8_t*>(g)[i], gv);
+        unpack8(reinterpret_cast<const u16x8_t*>(x)[i], xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] *= act_d(xv[j], op);
+        reinterpret_cast<u16x8_t*>(dx)[i] = pack8(gv);
+    }
+}
+// y = a*alpha + b*beta (bf16)
+__global__ void __launch_bounds__(NT) add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                 bf16_t* __restrict__ y, long n8, float alpha, float beta) {
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+        float av[8], bv[8];
+        unpack8(reinterpret_cast<const u16x8_t*>(a)[i], av);
+        unpack8(reinterpret_cast<const u16x8_t*>(b)[i], bv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) av[j] = av[j] * alpha + bv[j] * beta;
+        reinterpret_cast<u16x8_t*>(y)[i] = pack8(av);
+    }
+}
+// NCHW (fp32 or bf16) -> NHWC bf16 with the channel dim zero-padded to Cp (stem input, K-17)
+template <typename T>
+__global__ void __launch_bounds__(NT) nchw_to_nhwc_kernel(const T* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                                          int C, int HW, int Cp) {
+    const long total = (long)N * HW;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+        const long n = i / HW, p = i - n * HW;
+        for (int c = 0; c < Cp; ++c)
+            y[i * Cp + c] = c < C ? f2bf(Ld<T>::get(x, (n * C + c) * HW + p)) : (bf16_t)0;
+    }
+}
+// NHWC bf16 (channels Cp) -> NCHW fp32 gradient of the first C channels
+__global__ void __launch_bounds__(NT) nhwc_to_nchw_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                              int N, int C, int HW, int Cp) {
+    const long total = (long)N * C * HW;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+        const long p = i % HW, nc = i / HW, c = nc % C, n = nc / C;
+        y[i] = bf2f(x[(n * HW + p) * Cp + c]);
+    }
+}
+// column sums of a [rows][cols] bf16 matrix into fp32 (bias gradient of a Linear, K-03 fused column sum)
+__global__ void __launch_bounds__(NT) colsum_kernel(const bf16_t* __restrict__ x, long rows, int cols,
+                                                    float* __restrict__ out, int accumulate) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int rq = threadIdx.x >> 6;
+    __shared__ float red[4][64];
+    float s = 0.f;
+    if (c < cols)
+        for (long r = rq; r < rows; r += 4) s += bf2f(x[r * cols + c]);
+    red[rq][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (rq == 0 && c < cols) {
+        const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        out[c] = accumulate ? out[c] + t : t;
+    }
+}
+}  // namespace
+
+PDNN_API int pdnn_act_fwd(const bf16_t* x, bf16_t* y, long n, int op, hipStream_t st) {
+    hipLaunchKernelGGL(act_fwd_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, x, y, n / 8, op);
+    PDNN_LAUNCH_RET;
+}
+PDNN_API int pdnn_act_bwd(const bf16_t* g, const bf16_t* x, bf16_t* dx, long n, int op, hipStream_t st) {
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, g, x, dx, n / 8, op);
+    PDNN_LAUNCH_RET;
+}
+PDNN_API int pdnn_add(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, float alpha, float beta, hipStream_t st) {
+    hipLaunchKernelGGL(add_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, a, b, y, n / 8, alpha, beta);
+    PDNN_LAUNCH_RET;
+}
+PDNN_API int pdnn_nchw_to_nhwc(const void* x, int x_bf16, bf16_t* y, int N, int C, int HW, int Cp, hipStream_t st) {
+    if (x_bf16)
+        hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(stream_grid((long)N * HW, NT)), dim3(NT), 0, st,
+                           (const bf16_t*)x, y, N, C, HW, Cp);
+    else
+        hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(stream_grid((long)N * HW, NT)), dim3(NT), 0, st,
+                           (const float*)x, y, N, C, HW, Cp);
+    PDNN_LAUNCH_RET;
+}
+PDNN_API int pdnn_nhwc_to_nchw_f32(const bf16_t* x, float* y, int N, int C, int HW, int Cp, hipStream_t st) {
+    hipLaunchKernelGGL(nhwc_to_nchw_f32_kernel, dim3(stream_grid((long)N * C * HW, NT)), dim3(NT), 0, st, x, y, N, C,
+                       HW, Cp);
+    PDNN_LAUNCH_RET;
+}
+PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int accumulate, hipStream_t st) {
+    hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, x, rows, cols, out, accumulate);
+    PDNN_LAUNCH_RET;
+}

@@ -1,0 +1,700 @@
+// MFMA implicit-GEMM engine for gfx950 (CDNA4): bf16 operands, fp32 accumulation.
+//
+// One templated kernel computes  C[m][n] = sum_k A(m,k) * B(n,k)  for every GEMM-shaped op of the
+// framework:
+//
+//   op                      A operand (M x K)                    B operand (N x K)
+//   linear fwd   Y=XW^T     X [M][K]            (A_KMAJOR)       W [N][K]           (B_KMAJOR)
+//   linear dgrad dX=dY W    dY [M][N]           (A_KMAJOR)       W [N][K] as [k][n] (B_MNMAJOR)
+//   linear wgrad dW=dY^T X  dY as [k=m][n]      (A_MNMAJOR)      X as [k=m][n]      (B_MNMAJOR)
+//   conv fwd                im2col(In)          (A_CONV)         W [Ko][R][S][C]    (B_KMAJOR)
+//   conv dgrad              col2im-gather(dOut) (A_CONVT)        W as [(r,s,ko)][c] (B_WT)
+//   conv wgrad              dOut as [k=pix][ko] (A_MNMAJOR)      im2col(In) [pix][(r,s,c)] (B_IM2COL)
+//
+// (The reference computes these with cblas_dgemm / torch CPU ops: MPI_code/src/util/util.h:35-81,
+//  MPI_code/src/nn/nn_layer.h:97-178, pytorch_code/model_ops/resnet.py:19-28.)
+//
+// Design (cdna_hip_programming.md §5):
+//  * 256 threads = 4 waves in a 2x2 arrangement, block tile 128x128, K-step 64, every wave owns a
+//    64x64 sub-tile = 4x4 `v_mfma_f32_16x16x32_bf16` fragments (16x16x32 holds a higher clock than
+//    32x32x16 on random data: MI355X_MICROARCH.md DVFS item 7).
+//  * Operands are staged global -> registers -> LDS (double buffered, one barrier per K-step, the
+//    next tile's global loads issued before the MFMAs and written to LDS after them: T14).  Register
+//    staging (not glds) because the conv loaders gather with zero-fill predicates and the optional
+//    BN-affine+ReLU prologue transforms the data on its way to LDS.
+//  * K-major LDS images (rows of 64 bf16 = 128 B) are read with ds_read_b128 through the XOR swizzle
+//    chunk ^ ((row>>1)&7), which is conflict-free for the 16x16x32 fragment read pattern.
+//    MN-major images ([k][mn] rows of 128 or 64 bf16) are read with the CDNA4 transpose read
+//    `ds_read_b64_tr_b16` (T10) through a row-dependent even-chunk XOR that makes every 32-lane half
+//    conflict-free.  That is how the reduction-major operands of the weight gradients reach MFMA
+//    without any transpose pass over HBM.
+//  * MFMA is issued with swapped operands (B fragment as src A) so each lane holds 4 consecutive
+//    output columns; the epilogue stages the fp32 tile through LDS and writes 16-byte bf16 rows or
+//    256-byte contiguous fp32 atomic rows (MI355X_MICROARCH.md "Global float atomics", access shape).
+//  * Epilogue fusions: alpha, bias, ReLU, per-column BatchNorm partial statistics (sum, sum of
+//    squares of the bf16-rounded outputs, one slab row per 64-row wave tile), or fp32 atomic
+//    accumulation for split-K weight gradients.
+//  * XCD-aware bijective block remap (T1) so neighbouring tiles share an XCD's L2.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+enum AMode { A_KMAJOR = 0, A_MNMAJOR = 1, A_CONV = 2, A_CONVT = 3 };
+enum BMode { B_KMAJOR = 0, B_MNMAJOR = 1, B_WT = 2, B_IM2COL = 3 };
+enum EMode { E_BF16 = 0, E_F32 = 1, E_ATOMIC = 2 };
+
+// Granlund-Montgomery unsigned division by a runtime-invariant divisor (valid for n < 2^31).
+struct FastDiv {
+    uint32_t d, m, s;
+};
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+struct ConvGeom {
+    int Nimg, H, W, C;      // activation tensor of the gather (NHWC)
+    int Ho, Wo, R, S;       // the "other" spatial extent and filter size
+    int st, pad;
+    int Ko;                 // output channels (for A_CONVT / B_WT reduction index)
+    FastDiv dHW, dW, dC, dS, dKo;  // divisors used by the gathers
+};
+
+struct GemmArgs {
+    int M, N, K;
+    const bf16_t* A; long lda;
+    const bf16_t* B; long ldb;
+    ConvGeom g;
+    const float* pro_scale;   // optional fused prologue  x -> relu(x*scale[c] + shift[c])
+    const float* pro_shift;
+    void* C; long ldc;
+    float alpha;
+    const float* bias;        // per-column bias (E_BF16 / E_F32)
+    int relu;
+    float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
+    int ktiles_per_split;     // split-K (grid.z)
+};
+
+// ---------------------------------------------------------------------------------------------
+// LDS image helpers
+// ---------------------------------------------------------------------------------------------
+// K-major image: [rows][64] bf16, 128-byte rows, 16-byte chunk c of row r stored at chunk c^((r>>1)&7).
+__device__ __forceinline__ int kimg_off(int row, int chunk) {   // in bf16 elements
+    return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
+}
+// MN-major image: [64 k-rows][W] bf16, W in {64,128}; chunk XOR with an even, row-dependent value.
+template <int W>
+__device__ __forceinline__ int mimg_off(int krow, int chunk) {
+    int sw;
+    if constexpr (W == 128) sw = ((krow & 3) | ((krow >> 1) & 4)) << 1;     // 16 chunks / row
+    else sw = (((krow >> 1) & 1) | ((krow >> 2) & 2)) << 1;                 // 8 chunks / row
+    return krow * W + ((chunk ^ sw) << 3);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8_t frag_kmajor(const bf16_t* img, int row, int ks, int lane) {
+    const int chunk = ks * 4 + (lane >> 4);
+    u16x8_t v = *reinterpret_cast<const u16x8_t*>(img + kimg_off(row, chunk));
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// Fragment of 16 columns [col0, col0+16) x 32 k (k0 = 32*ks) from an MN-major image via two
+// transpose reads: lane 4q+p of each 16-lane group addresses row (k0 + 8g + q [+4]), columns
+// col0 + 4p .. +3; lane i receives column col0+i of the four rows.
+template <int W>
+__device__ __forceinline__ bf16x8_t frag_mnmajor(const bf16_t* img, int col0, int ks, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = col0 + 4 * p;
+    const int chunk = col >> 3, within = col & 7;
+    const int r0 = ks * 32 + 8 * g + q;
+    const bf16_t* p0 = img + mimg_off<W>(r0, chunk) + within;
+    const bf16_t* p1 = img + mimg_off<W>(r0 + 4, chunk) + within;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__device__ __forceinline__ u16x8_t zero8() {
+    u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    return z;
+}
+__device__ __forceinline__ u16x8_t ldg16(const bf16_t* p) {
+    return *reinterpret_cast<const u16x8_t*>(p);
+}
+
+__device__ __forceinline__ u16x8_t affine_relu8(u16x8_t v, const float* sc, const float* sh) {
+    const float4 s0 = *reinterpret_cast<const float4*>(sc);
+    const float4 s1 = *reinterpret_cast<const float4*>(sc + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sh);
+    const float4 h1 = *reinterpret_cast<const float4*>(sh + 4);
+    const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    u16x8_t o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(fmaxf(fmaf(bf2f(v[j]), s[j], h[j]), 0.f));
+    return o;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Operand loaders.  ROWS = the operand's tile extent along M (or N).  Every thread moves
+// ROWS/32 16-byte chunks per K-step for both image kinds.
+// ---------------------------------------------------------------------------------------------
+// ---- K-major operands: row = tile row (m or n), 8 chunks of 8 k per row ----------------------
+template <int ROWS, int KIND, bool PRO>   // KIND: 0 plain, 1 conv gather, 2 conv-transposed gather
+struct KLoader {
+    static constexpr int NCH = ROWS / 32;
+    const bf16_t* base[NCH];   // plain: row pointer; conv: image base pointer of the row's pixel
+    int hb[NCH], wb[NCH];      // conv: top-left input coordinate of the row's window
+    bool vrow[NCH];
+    int ch;                    // chunk column (fixed per thread)
+    int r, s, c;               // conv: current (r, s, c) of this thread's chunk column
+    int kcur;                  // current k of this thread's chunk
+
+    __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int rows_total,
+                                         int row0, int tid) {
+        ch = tid & 7;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int row = row0 + (tid >> 3) + 32 * i;
+            vrow[i] = row < rows_total;
+            const int rr = vrow[i] ? row : 0;
+            if constexpr (KIND == 0) {
+                base[i] = ptr + (long)rr * ld;
+            } else {
+                const ConvGeom& g = a.g;
+                // row -> (n, y, x) of the output grid (fwd: Ho x Wo; transposed: H x W of dIn)
+                const uint32_t n = fdiv((uint32_t)rr, g.dHW);
+                const uint32_t rem = (uint32_t)rr - n * g.dHW.d;
+                const uint32_t y = fdiv(rem, g.dW);
+                const uint32_t x = rem - y * g.dW.d;
+                if constexpr (KIND == 1) {
+                    hb[i] = (int)y * g.st - g.pad;
+                    wb[i] = (int)x * g.st - g.pad;
+                    base[i] = ptr + (long)n * g.H * g.W * g.C;
+                } else {
+                    hb[i] = (int)y + g.pad;
+                    wb[i] = (int)x + g.pad;
+                    base[i] = ptr + (long)n * g.Ho * g.Wo * g.Ko;
+                }
+            }
+        }
+        kcur = ch * 8;
+        if constexpr (KIND == 1) {
+            const ConvGeom& g = a.g;
+            const uint32_t rs = fdiv((uint32_t)kcur, g.dC);
+            c = kcur - rs * g.C;
+            r = fdiv(rs, g.dS);
+            s = rs - r * g.S;
+        } else if constexpr (KIND == 2) {
+            const ConvGeom& g = a.g;
+            const uint32_t rs = fdiv((uint32_t)kcur, g.dKo);
+            c = kcur - rs * g.Ko;
+            r = fdiv(rs, g.dS);
+            s = rs - r * g.S;
+        }
+    }
+    __device__ __forceinline__ void seek(const GemmArgs& a, int k) {   // jump to K offset k (split-K)
+        kcur = k + ch * 8;
+        if constexpr (KIND == 1) {
+            const uint32_t rs = fdiv((uint32_t)kcur, a.g.dC);
+            c = kcur - rs * a.g.C;
+            r = fdiv(rs, a.g.dS);
+            s = rs - r * a.g.S;
+        } else if constexpr (KIND == 2) {
+            const uint32_t rs = fdiv((uint32_t)kcur, a.g.dKo);
+            c = kcur - rs * a.g.Ko;
+            r = fdiv(rs, a.g.dS);
+            s = rs - r * a.g.S;
+        }
+    }
+    __device__ __forceinline__ void load(const GemmArgs& a, int Ktot, u16x8_t* reg) {
+        const bool kv = kcur < Ktot;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            if constexpr (KIND == 0) {
+                reg[i] = (vrow[i] && kv) ? ldg16(base[i] + kcur) : zero8();
+            } else if constexpr (KIND == 1) {
+                const ConvGeom& g = a.g;
+                const int hi = hb[i] + r, wi = wb[i] + s;
+                const bool v = vrow[i] && kv && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                u16x8_t x = v ? ldg16(base[i] + ((long)hi * g.W + wi) * g.C + c) : zero8();
+                if constexpr (PRO) {
+                    if (v) x = affine_relu8(x, a.pro_scale + c, a.pro_shift + c);
+                }
+                reg[i] = x;
+            } else {
+                const ConvGeom& g = a.g;
+                int th = hb[i] - r, tw = wb[i] - s;
+                bool v = vrow[i] && kv && th >= 0 && tw >= 0;
+                if (g.st != 1) {
+                    v = v && (th % g.st == 0) && (tw % g.st == 0);
+                    th /= g.st;
+                    tw /= g.st;
+                }
+                v = v && th < g.Ho && tw < g.Wo;
+                reg[i] = v ? ldg16(base[i] + ((long)th * g.Wo + tw) * g.Ko + c) : zero8();
+            }
+        }
+    }
+    __device__ __forceinline__ void advance(const GemmArgs& a) {
+        kcur += BK;
+        if constexpr (KIND == 1) {
+            c += BK;
+            while (c >= a.g.C) { c -= a.g.C; if (++s == a.g.S) { s = 0; ++r; } }
+        } else if constexpr (KIND == 2) {
+            c += BK;
+            while (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.S) { s = 0; ++r; } }
+        }
+    }
+    __device__ __forceinline__ void store(bf16_t* img, const u16x8_t* reg, int tid) const {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int row = (tid >> 3) + 32 * i;
+            *reinterpret_cast<u16x8_t*>(img + kimg_off(row, ch)) = reg[i];
+        }
+    }
+};
+
+// ---- MN-major operands: rows of the image are k, columns are m (or n) -------------------------
+// KIND: 0 plain [k][ld] matrix, 1 weight-transposed gather (B_WT), 2 im2col of an NHWC tensor
+template <int W, int KIND, bool PRO>
+struct MLoader {
+    static constexpr int CPR = W / 8;           // chunks per image row
+    static constexpr int RPP = NT / CPR;        // image rows covered per pass
+    static constexpr int NCH = 64 / RPP;        // = W / 32
+    int ch, col;           // chunk column, global column index of this thread's chunk
+    bool vcol;
+    int krow0;             // first image row of this thread
+    const bf16_t* ptr;
+    long ld;
+    // im2col: the column's (r, s, c) is fixed per block
+    int cr, cs, cc;
+    int kbase;
+
+    __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld_, int cols_total,
+                                         int col0, int tid) {
+        ch = tid % CPR;
+        krow0 = tid / CPR;
+        col = col0 + ch * 8;
+        vcol = col < cols_total;
+        ptr = p;
+        ld = ld_;
+        kbase = 0;
+        if constexpr (KIND == 2) {
+            const ConvGeom& g = a.g;
+            const int cl = vcol ? col : 0;
+            const uint32_t rs = fdiv((uint32_t)cl, g.dC);
+            cc = cl - rs * g.C;
+            cr = fdiv(rs, g.dS);
+            cs = rs - cr * g.S;
+        }
+    }
+    __device__ __forceinline__ void seek(const GemmArgs&, int k) { kbase = k; }
+    __device__ __forceinline__ void load(const GemmArgs& a, int Ktot, u16x8_t* reg) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int k = kbase + krow0 + RPP * i;
+            const bool v = vcol && k < Ktot;
+            if constexpr (KIND == 0) {
+                reg[i] = v ? ldg16(ptr + (long)k * ld + col) : zero8();
+            } else if constexpr (KIND == 1) {
+                // reduction index k = (r*S + s)*Ko + ko ; weight W[ko][r][s][c], column = c
+                const ConvGeom& g = a.g;
+                const int kk = v ? k : 0;
+                const uint32_t rs = fdiv((uint32_t)kk, g.dKo);
+                const int ko = kk - rs * g.Ko;
+                reg[i] = v ? ldg16(ptr + ((long)ko * g.R * g.S + rs) * g.C + col) : zero8();
+            } else {
+                // reduction index k = output pixel (n, yo, xo); column = (r, s, c) of the input window
+                const ConvGeom& g = a.g;
+                const int kk = v ? k : 0;
+                const uint32_t n = fdiv((uint32_t)kk, g.dHW);
+                const uint32_t rem = (uint32_t)kk - n * g.dHW.d;
+                const uint32_t yo = fdiv(rem, g.dW);
+                const uint32_t xo = rem - yo * g.dW.d;
+                const int hi = (int)yo * g.st - g.pad + cr, wi = (int)xo * g.st - g.pad + cs;
+                const bool vv = v && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                u16x8_t x = vv ? ldg16(ptr + (((long)n * g.H + hi) * g.W + wi) * g.C + cc) : zero8();
+                if constexpr (PRO) {
+                    if (vv) x = affine_relu8(x, a.pro_scale + cc, a.pro_shift + cc);
+                }
+                reg[i] = x;
+            }
+        }
+    }
+    __device__ __forceinline__ void advance(const GemmArgs&) { kbase += BK; }
+    __device__ __forceinline__ void store(bf16_t* img, const u16x8_t* reg, int) const {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i)
+            *reinterpret_cast<u16x8_t*>(img + mimg_off<W>(krow0 + RPP * i, ch)) = reg[i];
+    }
+};
+
+template <int AM, bool PRO> struct ASel;
+template <bool PRO> struct ASel<A_KMAJOR, PRO> { using T = KLoader<128, 0, false>; static constexpr bool K = true; };
+template <bool PRO> struct ASel<A_CONV, PRO> { using T = KLoader<128, 1, PRO>; static constexpr bool K = true; };
+template <bool PRO> struct ASel<A_CONVT, PRO> { using T = KLoader<128, 2, false>; static constexpr bool K = true; };
+template <bool PRO> struct ASel<A_MNMAJOR, PRO> { using T = MLoader<128, 0, false>; static constexpr bool K = false; };
+template <int BM_, bool PRO> struct BSel;
+template <bool PRO> struct BSel<B_KMAJOR, PRO> { using T = KLoader<128, 0, false>; static constexpr bool K = true; };
+template <bool PRO> struct BSel<B_MNMAJOR, PRO> { using T = MLoader<128, 0, false>; static constexpr bool K = false; };
+template <bool PRO> struct BSel<B_WT, PRO> { using T = MLoader<128, 1, false>; static constexpr bool K = false; };
+template <bool PRO> struct BSel<B_IM2COL, PRO> { using T = MLoader<128, 2, PRO>; static constexpr bool K = false; };
+
+constexpr int BMt = 128, BNt = 128;
+constexpr int TILE_ELEMS = 128 * BK;                 // bf16 elements per operand image
+constexpr int CPAD = 4;                              // fp32 C-stage row padding
+constexpr int SMEM_BYTES = (BMt * (BNt + CPAD) * 4) > (4 * TILE_ELEMS * 2) ? (BMt * (BNt + CPAD) * 4)
+                                                                           : (4 * TILE_ELEMS * 2);
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    // Bijective: blocks b, b+8, b+16... (same XCD under round-robin dispatch) get consecutive tiles.
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <int AM, int BMODE, int EM, bool PRO_A, bool PRO_B>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const sbase = reinterpret_cast<bf16_t*>(smem);   // [buf][A|B][128*64]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (a.M + BMt - 1) / BMt, tiles_n = (a.N + BNt - 1) / BNt;
+    const int nwg = tiles_m * tiles_n;
+    const int t = xcd_remap(blockIdx.x, nwg);
+    // N fastest: consecutive tiles of one XCD share the same A rows (activations, the big operand).
+    const int tm = t / tiles_n, tn = t % tiles_n;
+    const int m0 = tm * BMt, n0 = tn * BNt;
+
+    const int ktiles = (a.K + BK - 1) / BK;
+    const int kt0 = blockIdx.z * a.ktiles_per_split;
+    const int kt1 = min(ktiles, kt0 + a.ktiles_per_split);
+    if (kt0 >= kt1) return;
+
+    using LA = typename ASel<AM, PRO_A>::T;
+    using LB = typename BSel<BMODE, PRO_B>::T;
+    constexpr bool AK = ASel<AM, PRO_A>::K;
+    constexpr bool BKm = BSel<BMODE, PRO_B>::K;
+    LA la;
+    LB lb;
+    la.init(a, a.A, a.lda, a.M, m0, tid);
+    lb.init(a, a.B, a.ldb, a.N, n0, tid);
+    if (kt0) { la.seek(a, kt0 * BK); lb.seek(a, kt0 * BK); }
+
+    u16x8_t ra[LA::NCH], rb[LB::NCH];
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    la.load(a, a.K, ra);
+    lb.load(a, a.K, rb);
+    la.store(sbase, ra, tid);
+    lb.store(sbase + TILE_ELEMS, rb, tid);
+    __syncthreads();
+
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) {
+            la.advance(a);
+            lb.advance(a);
+            la.load(a, a.K, ra);
+            lb.load(a, a.K, rb);
+        }
+        const bf16_t* A_ = sbase + cur * 2 * TILE_ELEMS;
+        const bf16_t* B_ = A_ + TILE_ELEMS;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8_t af[4], bfr[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                if constexpr (AK) af[f] = frag_kmajor(A_, wm * 64 + f * 16 + (lane & 15), ks, lane);
+                else af[f] = frag_mnmajor<128>(A_, wm * 64 + f * 16, ks, lane);
+                if constexpr (BKm) bfr[f] = frag_kmajor(B_, wn * 64 + f * 16 + (lane & 15), ks, lane);
+                else bfr[f] = frag_mnmajor<128>(B_, wn * 64 + f * 16, ks, lane);
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+        }
+        if (more) {
+            bf16_t* nA = sbase + (cur ^ 1) * 2 * TILE_ELEMS;
+            la.store(nA, ra, tid);
+            lb.store(nA + TILE_ELEMS, rb, tid);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+
+    // ---------------- epilogue ----------------
+    // lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + j] in acc[fm][fn][j]
+    float* cs = reinterpret_cast<float*>(smem);
+    constexpr int LDC_S = BNt + CPAD;
+    const int lm = lane & 15, lg = lane >> 4;
+
+    if constexpr (EM == E_BF16) {
+        if (a.stats) {
+            // per-column partial sums over this wave's 64 rows (masked rows excluded)
+#pragma unroll
+            for (int fn = 0; fn < 4; ++fn) {
+                float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) {
+                    const int m = m0 + wm * 64 + fm * 16 + lm;
+                    if (m < a.M) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            float v = acc[fm][fn][j] * a.alpha;
+                            v = bf2f(f2bf(v));
+                            s[j] += v;
+                            q[j] += v * v;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        s[j] += __shfl_xor(s[j], o, 64);
+                        q[j] += __shfl_xor(q[j], o, 64);
+                    }
+                }
+                const int n = n0 + wn * 64 + fn * 16 + 4 * lg;
+                if (lm == 0 && n < a.N) {
+                    const long row = (long)(tm * 2 + wm) * 2;
+                    float* ps = a.stats + row * a.N + n;
+                    float* pq = a.stats + (row + 1) * a.N + n;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (n + j < a.N) { ps[j] = s[j]; pq[j] = q[j]; }
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();   // done with the operand images; reuse LDS as the fp32 C stage
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) {
+            const int r = wm * 64 + fm * 16 + lm;
+            const int c = wn * 64 + fn * 16 + 4 * lg;
+            *reinterpret_cast<f32x4_t*>(cs + r * LDC_S + c) = acc[fm][fn];
+        }
+    __syncthreads();
+
+    if constexpr (EM == E_ATOMIC) {
+        // 256 threads: each wave sweeps rows; 64 lanes x 2 columns -> 128 contiguous fp32 per row
+        float* C = reinterpret_cast<float*>(a.C);
+        for (int r = wave; r < BMt; r += 4) {
+            const int m = m0 + r;
+            if (m >= a.M) break;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = lane + 64 * h;
+                const int n = n0 + c;
+                if (n < a.N) atomicAdd(C + (long)m * a.ldc + n, a.alpha * cs[r * LDC_S + c]);
+            }
+        }
+    } else {
+        // each thread writes 8 consecutive columns of a row: 16 threads per 128-column row
+        const int cgrp = tid & 15;
+        for (int r = tid >> 4; r < BMt; r += NT / 16) {
+            const int m = m0 + r;
+            if (m >= a.M) break;
+            const int n = n0 + cgrp * 8;
+            if (n >= a.N) continue;
+            float v[8];
+            const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(cs + r * LDC_S + cgrp * 8);
+            const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(cs + r * LDC_S + cgrp * 8 + 4);
+            v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
+            v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[j] *= a.alpha;
+                if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
+                if (a.relu) v[j] = fmaxf(v[j], 0.f);
+            }
+            if constexpr (EM == E_BF16) {
+                bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc + n;
+                if (n + 8 <= a.N) {
+                    *reinterpret_cast<u16x8_t*>(C) = pack8(v);
+                } else {
+                    for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = f2bf(v[j]);
+                }
+            } else {
+                float* C = reinterpret_cast<float*>(a.C) + (long)m * a.ldc + n;
+                if (n + 8 <= a.N) {
+                    *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4*>(C + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                } else {
+                    for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = v[j];
+                }
+            }
+        }
+    }
+}
+
+FastDiv make_fdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d ? d : 1;
+    uint32_t l = 0;
+    while ((1ull << l) < f.d) ++l;
+    f.s = l;
+    f.m = (uint32_t)((((1ull << l) - f.d) << 32) / f.d + 1);
+    return f;
+}
+
+template <int AM, int BMODE, int EM, bool PA, bool PB>
+int launch(const GemmArgs& a, int splits, hipStream_t st) {
+    const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNt));
+    dim3 grid(tiles, 1, splits);
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB>), grid, dim3(NT), SMEM_BYTES, st, a);
+    PDNN_LAUNCH_RET;
+}
+
+int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
+    // enough workgroups to cover 256 CUs twice, but keep >= 4 K-steps per split
+    int want = (512 + tiles - 1) / tiles;
+    int s = want < max_splits ? want : max_splits;
+    int cap = ktiles / 4;
+    if (s > cap) s = cap;
+    return s < 1 ? 1 : s;
+}
+
+void fill_geom(ConvGeom& g, int Nimg, int H, int W, int C, int Ho, int Wo, int R, int S, int st, int pad,
+               int Ko) {
+    g.Nimg = Nimg; g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo; g.R = R; g.S = S;
+    g.st = st; g.pad = pad; g.Ko = Ko;
+    g.dC = make_fdiv(C); g.dS = make_fdiv(S); g.dKo = make_fdiv(Ko);
+}
+
+}  // namespace
+
+static bool g_attr_done = false;
+template <int AM, int BMODE, int EM, bool PA, bool PB>
+static void set_attr() {
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<AM, BMODE, EM, PA, PB>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+}
+static void ensure_attrs() {
+    if (g_attr_done) return;
+    g_attr_done = true;
+    set_attr<A_KMAJOR, B_KMAJOR, E_BF16, false, false>();
+    set_attr<A_KMAJOR, B_KMAJOR, E_F32, false, false>();
+    set_attr<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>();
+    set_attr<A_KMAJOR, B_MNMAJOR, E_F32, false, false>();
+    set_attr<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false>();
+    set_attr<A_CONV, B_KMAJOR, E_BF16, false, false>();
+    set_attr<A_CONV, B_KMAJOR, E_BF16, true, false>();
+    set_attr<A_CONVT, B_WT, E_BF16, false, false>();
+    set_attr<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>();
+    set_attr<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>();
+}
+
+// ------------------------------------------------------------------------------------------------
+// C API
+// ------------------------------------------------------------------------------------------------
+
+// Y[M][N] (bf16 or fp32) = alpha * X[M][K] . W[N][K]^T (+ bias) (relu)
+PDNN_API int pdnn_gemm_nt(const bf16_t* X, long ldx, const bf16_t* W, long ldw, void* Y, long ldy,
+                          int M, int N, int K, float alpha, const float* bias, int relu, int out_f32,
+                          hipStream_t st) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = W; a.ldb = ldw; a.C = Y; a.ldc = ldy;
+    a.alpha = alpha; a.bias = bias; a.relu = relu; a.ktiles_per_split = (int)cdiv(K, BK);
+    return out_f32 ? launch<A_KMAJOR, B_KMAJOR, E_F32, false, false>(a, 1, st)
+                   : launch<A_KMAJOR, B_KMAJOR, E_BF16, false, false>(a, 1, st);
+}
+
+// Y[M][N] = alpha * X[M][K] . W[K][N]     (W row-major [K][N]: reduction-major B)
+PDNN_API int pdnn_gemm_nn(const bf16_t* X, long ldx, const bf16_t* W, long ldw, void* Y, long ldy,
+                          int M, int N, int K, float alpha, int out_f32, hipStream_t st) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = W; a.ldb = ldw; a.C = Y; a.ldc = ldy;
+    a.alpha = alpha; a.ktiles_per_split = (int)cdiv(K, BK);
+    return out_f32 ? launch<A_KMAJOR, B_MNMAJOR, E_F32, false, false>(a, 1, st)
+                   : launch<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>(a, 1, st);
+}
+
+// Cf32[M][N] += alpha * X[K][M]^T . Y[K][N]   (both reduction-major; split-K fp32 atomics).
+// Cf32 must be initialised by the caller (zero for a fresh gradient).
+PDNN_API int pdnn_gemm_tn_acc(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* C, long ldc,
+                              int M, int N, int K, float alpha, hipStream_t st) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = Y; a.ldb = ldy; a.C = C; a.ldc = ldc;
+    a.alpha = alpha;
+    const int ktiles = (int)cdiv(K, BK), tiles = (int)(cdiv(M, BMt) * cdiv(N, BNt));
+    const int splits = pick_splits(a, ktiles, tiles, 256);
+    a.ktiles_per_split = (int)cdiv(ktiles, splits);
+    return launch<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false>(a, (int)cdiv(ktiles, a.ktiles_per_split), st);
+}
+
+// Convolution forward, NHWC bf16 activations, weight [Ko][R][S][C] bf16 (== torch channels_last).
+// Optional fused prologue relu(x*scale[c]+shift[c]) on the input, optional BN partial statistics
+// of the output (stats: [2*ceil(M/128)*2][N] floats, see pdnn_bn_stats_finalize).
+PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int C,
+                           int Ko, int R, int S, int st, int pad, int Ho, int Wo,
+                           const float* pro_scale, const float* pro_shift, float* stats,
+                           hipStream_t stream) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = Nimg * Ho * Wo; a.N = Ko; a.K = R * S * C;
+    a.A = x; a.B = w; a.ldb = (long)R * S * C; a.C = y; a.ldc = Ko; a.alpha = 1.f;
+    fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+    a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
+    a.pro_scale = pro_scale; a.pro_shift = pro_shift; a.stats = stats;
+    a.ktiles_per_split = (int)cdiv(a.K, BK);
+    if (pro_scale) return launch<A_CONV, B_KMAJOR, E_BF16, true, false>(a, 1, stream);
+    return launch<A_CONV, B_KMAJOR, E_BF16, false, false>(a, 1, stream);
+}
+
+// Convolution data gradient: dx[N][H][W][C] = sum over (r, s, ko) dy[...] * w[ko][r][s][c].
+PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nimg, int H, int W, int C,
+                             int Ko, int R, int S, int st, int pad, int Ho, int Wo, float* stats,
+                             hipStream_t stream) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = Nimg * H * W; a.N = C; a.K = R * S * Ko;
+    a.A = dy; a.B = w; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
+    fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+    a.g.dHW = make_fdiv(H * W); a.g.dW = make_fdiv(W);
+    a.ktiles_per_split = (int)cdiv(a.K, BK);
+    return launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);
+}
+
+// Convolution weight gradient (accumulating into fp32 dw[Ko][R][S][C]): split-K over output pixels.
+PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C,
+                             int Ko, int R, int S, int st, int pad, int Ho, int Wo,
+                             const float* pro_scale, const float* pro_shift, hipStream_t stream) {
+    ensure_attrs();
+    GemmArgs a{};
+    a.M = Ko; a.N = R * S * C; a.K = Nimg * Ho * Wo;
+    a.A = dy; a.lda = Ko; a.B = x; a.C = dw; a.ldc = (long)R * S * C; a.alpha = 1.f;
+    fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+    a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
+    a.pro_scale = pro_scale; a.pro_shift = pro_shift;
+    const int ktiles = (int)cdiv(a.K, BK), tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNt));
+    const int splits = pick_splits(a, ktiles, tiles, 1024);
+    a.ktiles_per_split = (int)cdiv(ktiles, splits);
+    const int nz = (int)cdiv(ktiles, a.ktiles_per_split);
+    if (pro_scale) return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
+    return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
+}
+
+// Number of stats rows the fused epilogue writes for M output rows (2 wave-rows per 128-row tile).
+PDNN_API int pdnn_gemm_stats_rows(int M) { return (int)cdiv(M, BMt) * 2; }

@@ -1,0 +1,138 @@
+"""ctypes binding of the in-tree HIP kernel library ``_lib/libpdnn_kernels.so``.
+
+The launchers are plain ``extern "C"`` functions taking raw device pointers and a ``hipStream_t``; we
+pass ``torch.cuda.current_stream().cuda_stream`` so every kernel is ordered on torch's stream (and is
+captured by ``torch.cuda.CUDAGraph`` when a graph capture is active).  The library is loaded after
+``import torch`` so it binds to the HIP runtime torch already loaded (same SONAME
+``libamdhip64.so.7``) — one runtime, shared streams.
+
+There is deliberately no silent fallback: if a CUDA tensor reaches an op and the library cannot be
+loaded, :func:`lib` raises.  CPU tensors never touch this module (the ops use the PyTorch reference
+implementation on CPU so the test-suite runs on the GPU-less dev box).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIBDIR = Path(__file__).resolve().parent.parent / "_lib"
+_LIB = None
+_ERR = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+D = ctypes.c_double
+
+# name -> argtypes (every launcher returns int = hipError_t)
+_SIGS = {
+    "pdnn_gemm_nt": [P, L, P, L, P, L, I, I, I, F, P, I, I, P],
+    "pdnn_gemm_nn": [P, L, P, L, P, L, I, I, I, F, I, P],
+    "pdnn_gemm_tn_acc": [P, L, P, L, P, L, I, I, I, F, P],
+    "pdnn_conv_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "pdnn_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "pdnn_gemm_stats_rows": [I],
+    "pdnn_bn_reduce_rows": [L, I],
+    "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P],
+    "pdnn_bn_eval_coeff": [I, F, P, P, P, P, P, P, P],
+    "pdnn_bn_stats": [P, L, I, P, P],
+    "pdnn_bn_apply": [P, L, I, P, P, P, P, P, I, P, P],
+    "pdnn_bn_bwd_reduce": [P, P, L, I, P, P, I, P, P, P, P, P, P, P, P, P],
+    "pdnn_bn_bwd_finalize": [P, I, I, P, P, I, P],
+    "pdnn_bn_bwd_apply": [P, P, L, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_maxpool_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "pdnn_maxpool_bwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "pdnn_avgpool_fwd": [P, P, I, I, I, P],
+    "pdnn_avgpool_bwd": [P, P, I, I, I, P],
+    "pdnn_xent_fwd": [P, L, I, I, P, I, P, P, P, P, I, P],
+    "pdnn_xent_bwd": [P, L, I, I, P, I, P, P, F, P, L, I, P],
+    "pdnn_sgd_step": [P, P, P, P, L, F, F, F, F, I, P, F, I, P],
+    "pdnn_adam_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, F, P, F, P],
+    "pdnn_cast_f32_bf16": [P, P, L, F, P],
+    "pdnn_cast_bf16_f32": [P, P, L, F, I, P],
+    "pdnn_scale_f32": [P, L, F, P, I, P],
+    "pdnn_axpy_f32": [P, P, L, F, P],
+    "pdnn_sumsq_f32": [P, L, P, P],
+    "pdnn_act_fwd": [P, P, L, I, P],
+    "pdnn_act_bwd": [P, P, P, L, I, P],
+    "pdnn_add": [P, P, P, L, F, F, P],
+    "pdnn_nchw_to_nhwc": [P, I, P, I, I, I, I, P],
+    "pdnn_nhwc_to_nchw_f32": [P, P, I, I, I, I, P],
+    "pdnn_colsum": [P, L, I, P, I, P],
+    "pdnn_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
+    "pdnn_layernorm_bwd": [P, P, P, P, P, P, P, P, I, I, P, P],
+    "pdnn_attn_fwd": [P, P, P, P, P, I, I, I, I, L, L, F, I, P],
+    "pdnn_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, L, L, F, I, P],
+    "pdnn_gemm_fp8_nt": [P, L, P, L, P, L, I, I, I, F, P, I, P],
+    "pdnn_quant_fp8": [P, P, L, P, P, P],
+    "pdnn_amax_f32": [P, L, P, I, P],
+}
+
+
+def lib_path() -> Path:
+    return _LIBDIR / "libpdnn_kernels.so"
+
+
+def _load():
+    global _LIB, _ERR
+    if _LIB is not None or _ERR is not None:
+        return _LIB
+    p = lib_path()
+    if not p.exists() and os.environ.get("PDNN_AUTOBUILD", "1") == "1":
+        try:
+            from .. import _build
+            _build.build_kernels()
+        except Exception as e:  # pragma: no cover - reported via _ERR
+            _ERR = f"could not build {p}: {e}"
+            return None
+    try:
+        lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:
+        _ERR = f"could not load {p}: {e}"
+        return None
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    _LIB = lib
+    return _LIB
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def lib():
+    """The loaded kernel library; raises (never falls back) if it is unavailable."""
+    l = _load()
+    if l is None:
+        raise RuntimeError(f"pytorch_distributed_nn_amd: HIP kernel library unavailable ({_ERR}). "
+                           "Run `python -m pytorch_distributed_nn_amd._build` (hipcc, gfx950).")
+    return l
+
+
+def stream(dev=None) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise HipError(f"{name} failed with hipError {rc}")
+    return rc

@@ -1,0 +1,247 @@
+"""Block-level fused ResNet ops for the GPU path (NHWC bf16 activations, fp32 BN statistics).
+
+A whole Bottleneck / BasicBlock / stem is ONE autograd Function whose forward and backward are
+hand-scheduled sequences of HIP kernels (reference modules: pytorch_code/model_ops/resnet.py:14-64;
+the reference's layer-wise "Split" backward that streams gradients out early, resnet_split.py:235-326,
+is replaced by DDP bucket hooks firing as each block's backward completes).
+
+Fusion plan of a Bottleneck (x -> out):
+
+  forward                                          what is written to HBM
+  t1 = conv1x1(x)          + BN1 partial stats      t1
+  t2 = conv3x3(relu(bn1(t1)))  (BN1+ReLU applied     t2       (a1 never materialised)
+       in conv2's operand loader) + BN2 stats
+  t3 = conv1x1(relu(bn2(t2)))  + BN3 stats           t3       (a2 never materialised)
+  td = conv1x1/s(x)        + BNd stats  (if downsample)
+  out = relu(bn3(t3) + bnd(td) | x)   one kernel    out
+
+  backward mirrors it: one reduce + one apply kernel per BN (ReLU masks recomputed from t and the BN
+  affine, or read from `out`), conv wgrads read the virtual activations relu(bn(t)) through the same
+  fused prologue, dgrads are implicit GEMMs on the weight without any transposed copy.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .functional import weight_bf16
+
+F32 = torch.float32
+
+
+def _bn_train(slab, M, bn_params, bufs, mom, eps):
+    gamma, beta = bn_params
+    rm, rv = bufs
+    rows = slab.shape[0] // 2
+    return K.bn_finalize(slab, rows, M, eps, mom, gamma, beta, rm, rv)
+
+
+def _bn_eval(bn_params, bufs, eps):
+    gamma, beta = bn_params
+    rm, rv = bufs
+    sc, sh = K.bn_eval_coeff(eps, gamma, beta, rm, rv)
+    return rm, torch.rsqrt(rv + eps), sc, sh
+
+
+def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
+    t, slab = K.conv_fwd(x, wk, st, pad, pro=pro, want_stats=training)
+    M = t.numel() // t.shape[-1]
+    if training:
+        mean, inv, sc, sh = _bn_train(slab, M, bn_params, bufs, mom, eps)
+    else:
+        mean, inv, sc, sh = _bn_eval(bn_params, bufs, eps)
+    return t, mean, inv, sc, sh
+
+
+def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None):
+    slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
+    dgamma, dbeta = K.bn_bwd_finalize(slab, rows)
+    dt, _, _ = K.bn_bwd_apply(g2d, t2d, mean, inv, gamma, dgamma, dbeta, mode=mode, msrc=msrc, mscale=msc,
+                              mshift=msh)
+    return dt, dgamma, dbeta
+
+
+def _krsc_grad(dw):
+    """fp32 [K][R][S][C] -> [K][C][R][S] view with channels_last strides (the parameter's layout)."""
+    return dw.permute(0, 3, 1, 2)
+
+
+class BottleneckFn(torch.autograd.Function):
+    """Bottleneck (expansion 4): params = (w1,g1,b1, w2,g2,b2, w3,g3,b3[, wd,gd,bd])."""
+
+    @staticmethod
+    def forward(ctx, x, conf, bufs, shadows, *params):
+        stride, training, mom, eps = conf
+        down = len(params) == 12
+        w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
+        k1, k2, k3 = shadows[:3]
+        t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
+        t2, m2, i2, s2, h2 = _conv_bn(t1, k2, stride, 1, (s1, h1), training, (g2, b2), bufs[2:4], mom, eps)
+        t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
+        C3 = t3.shape[-1]
+        if down:
+            wd, gd, bd = params[9:]
+            td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (gd, bd), bufs[6:8], mom, eps)
+            out = K.bn_apply(t3.view(-1, C3), s3, h3, res=td.view(-1, C3), rscale=sd, rshift=hd, relu=True)
+        else:
+            td = md = idd = None
+            out = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True)
+        out = out.view(t3.shape)
+        ctx.save_for_backward(x, t1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+                              g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None)
+        ctx.conf = (stride, training, down)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x, t1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+         g1, g2, g3, gd, k1, k2, k3, kd) = ctx.saved_tensors
+        stride, training, down = ctx.conf
+        if not training:
+            raise RuntimeError("fused Bottleneck backward requires training-mode BatchNorm")
+        gout = gout.contiguous()
+        C3 = t3.shape[-1]
+        g2d, t3_2d, out2d = gout.view(-1, C3), t3.view(-1, C3), out.view(-1, C3)
+        # block output BN3 (+BNd) with the ReLU mask of `out`
+        slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=1, msrc=out2d,
+                                             x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
+        dg3, db3 = K.bn_bwd_finalize(slab3, rows)
+        if down:
+            dgd, dbd = K.bn_bwd_finalize(slabd, rows)
+            dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d,
+                                         x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
+                                         dbeta2=dbd)
+            gres = None
+        else:
+            dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d, want_gm=True)
+        dt3 = dt3.view(t3.shape)
+        # conv3 (input = relu(bn2(t2)), virtual)
+        dw3 = K.conv_wgrad(t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        da2 = K.conv_dgrad(dt3, k3, t2.shape, 1, 0)
+        C2 = t2.shape[-1]
+        dt2, dg2, db2 = _bn_back(da2.view(-1, C2), t2.view(-1, C2), m2, i2, g2, 2, msc=s2, msh=h2)
+        dt2 = dt2.view(t2.shape)
+        dw2 = K.conv_wgrad(t1, dt2, 3, 3, stride, 1, pro=(s1, h1))
+        da1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1)
+        C1 = t1.shape[-1]
+        dt1, dg1, db1 = _bn_back(da1.view(-1, C1), t1.view(-1, C1), m1, i1, g1, 2, msc=s1, msh=h1)
+        dt1 = dt1.view(t1.shape)
+        dw1 = K.conv_wgrad(x, dt1, 1, 1, 1, 0)
+        dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0)
+        if down:
+            dtd = dtd.view(td.shape)
+            dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
+            dx2 = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
+            dx = K.add(dx, dx2)
+            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3,
+                     _krsc_grad(dwd), dgd, dbd)
+        else:
+            dx = K.add(dx, gres.view(x.shape))
+            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3)
+        return (dx, None, None, None) + grads
+
+
+class BasicBlockFn(torch.autograd.Function):
+    """BasicBlock (expansion 1): params = (w1,g1,b1, w2,g2,b2[, wd,gd,bd])."""
+
+    @staticmethod
+    def forward(ctx, x, conf, bufs, shadows, *params):
+        stride, training, mom, eps = conf
+        down = len(params) == 9
+        w1, g1, b1, w2, g2, b2 = params[:6]
+        k1, k2 = shadows[:2]
+        t1, m1, i1, s1, h1 = _conv_bn(x, k1, stride, 1, None, training, (g1, b1), bufs[0:2], mom, eps)
+        t2, m2, i2, s2, h2 = _conv_bn(t1, k2, 1, 1, (s1, h1), training, (g2, b2), bufs[2:4], mom, eps)
+        C2 = t2.shape[-1]
+        if down:
+            wd, gd, bd = params[6:]
+            td, md, idd, sd, hd = _conv_bn(x, shadows[2], stride, 0, None, training, (gd, bd), bufs[4:6], mom, eps)
+            out = K.bn_apply(t2.view(-1, C2), s2, h2, res=td.view(-1, C2), rscale=sd, rshift=hd, relu=True)
+        else:
+            td = md = idd = None
+            out = K.bn_apply(t2.view(-1, C2), s2, h2, res=x.view(-1, C2), relu=True)
+        out = out.view(t2.shape)
+        ctx.save_for_backward(x, t1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
+                              params[7] if down else None, k1, k2, shadows[2] if down else None)
+        ctx.conf = (stride, training, down)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x, t1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
+        stride, training, down = ctx.conf
+        if not training:
+            raise RuntimeError("fused BasicBlock backward requires training-mode BatchNorm")
+        gout = gout.contiguous()
+        C2 = t2.shape[-1]
+        g2d, t2_2d, out2d = gout.view(-1, C2), t2.view(-1, C2), out.view(-1, C2)
+        slab2, slabd, rows = K.bn_bwd_reduce(g2d, t2_2d, m2, i2, mode=1, msrc=out2d,
+                                             x2=td.view(-1, C2) if down else None, mean2=md, invstd2=idd)
+        dg2, db2 = K.bn_bwd_finalize(slab2, rows)
+        if down:
+            dgd, dbd = K.bn_bwd_finalize(slabd, rows)
+            dt2, dtd, _ = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, x2=td.view(-1, C2),
+                                         mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd, dbeta2=dbd)
+            gres = None
+        else:
+            dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, want_gm=True)
+        dt2 = dt2.view(t2.shape)
+        dw2 = K.conv_wgrad(t1, dt2, 3, 3, 1, 1, pro=(s1, h1))
+        da1 = K.conv_dgrad(dt2, k2, t1.shape, 1, 1)
+        C1 = t1.shape[-1]
+        dt1, dg1, db1 = _bn_back(da1.view(-1, C1), t1.view(-1, C1), m1, i1, g1, 2, msc=s1, msh=h1)
+        dt1 = dt1.view(t1.shape)
+        dw1 = K.conv_wgrad(x, dt1, 3, 3, stride, 1)
+        dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1)
+        if down:
+            dtd = dtd.view(td.shape)
+            dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
+            dx = K.add(dx, K.conv_dgrad(dtd, kd, x.shape, stride, 0))
+            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dwd), dgd, dbd)
+        else:
+            dx = K.add(dx, gres.view(x.shape))
+            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2)
+        return (dx, None, None, None) + grads
+
+
+class StemFn(torch.autograd.Function):
+    """conv(k, stride, pad) -> BN -> ReLU [-> maxpool(3, 2, 1)] on a channel-padded NHWC input.
+
+    params = (w, gamma, beta); the weight shadow is zero-padded to the input's channel count."""
+
+    @staticmethod
+    def forward(ctx, x, conf, bufs, shadows, w, gamma, beta):
+        stride, pad, pool, training, mom, eps = conf
+        kpad = shadows[0]
+        t, m, i, s, h = _conv_bn(x, kpad, stride, pad, None, training, (gamma, beta), bufs, mom, eps)
+        C = t.shape[-1]
+        a = K.bn_apply(t.view(-1, C), s, h, relu=True).view(t.shape)
+        if pool:
+            y, idx = K.maxpool_fwd(a, 3, 2, 1)
+        else:
+            y, idx = a, None
+        ctx.save_for_backward(x, t, a, idx, m, i, gamma)
+        ctx.conf = (stride, pad, pool, w.shape, kpad.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, t, a, idx, m, i, gamma = ctx.saved_tensors
+        stride, pad, pool, wshape, kshape = ctx.conf
+        gy = gy.contiguous()
+        ga = K.maxpool_bwd(gy, idx, a.shape, 3, 2, 1) if pool else gy
+        C = t.shape[-1]
+        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 1, msrc=a.view(-1, C))
+        dt = dt.view(t.shape)
+        dwk = K.conv_wgrad(x, dt, kshape[1], kshape[2], stride, pad)     # [K][R][S][Cpad]
+        dw = dwk[:, :, :, : wshape[1]].permute(0, 3, 1, 2)
+        # the stem input is the data batch: no input gradient is produced
+        return None, None, None, None, dw, dg, db
+
+
+def stem_shadow(w, cpad):
+    """bf16 [K][R][S][Cpad] weight for a channel-padded stem input."""
+    k = weight_bf16(w, krsc=True)
+    if k.shape[-1] != cpad:
+        k = torch.nn.functional.pad(k, (0, cpad - k.shape[-1])).contiguous()
+    return k

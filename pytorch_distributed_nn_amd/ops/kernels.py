@@ -1,0 +1,338 @@
+"""Typed Python wrappers around the HIP launchers (one function per kernel entry point).
+
+Every wrapper checks the shape / dtype / layout contract the kernel assumes *on the host* before
+launching (a bad launch can take down the whole GPU box), allocates outputs with torch's caching
+allocator, and launches on torch's current stream.  Activations are NHWC bf16 tensors of shape
+(N, H, W, C); conv weights are bf16 tensors whose memory is [K][R][S][C] (torch ``channels_last``).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._backend import call, lib, ptr, stream
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _chk(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _is_krsc(w):
+    K, C, R, S = w.shape
+    return w.stride() == (R * S * C, 1, S * C, C)
+
+
+def _bf16_c(t, name):
+    _chk(t.dtype == BF16 and t.is_cuda, f"{name}: expected CUDA bf16, got {t.dtype} {t.device}")
+    _chk(t.is_contiguous(), f"{name}: expected contiguous tensor")
+    _chk(t.data_ptr() % 16 == 0, f"{name}: 16-byte alignment required")
+
+
+# ----------------------------------------------------------------------------------- GEMM / conv
+def gemm_nt(x, w, bias=None, relu=False, out_f32=False, alpha=1.0, out=None):
+    """y[M][N] = alpha * x[M][K] @ w[N][K]^T (+bias)(relu).  x, w bf16 row-major."""
+    M, K = x.shape
+    N, K2 = w.shape
+    _chk(K == K2 and K % 8 == 0, f"gemm_nt: K mismatch/alignment {x.shape} {w.shape}")
+    _chk(x.stride(1) == 1 and w.stride(1) == 1 and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0,
+         "gemm_nt: rows must be K-contiguous, 16B aligned")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=F32 if out_f32 else BF16)
+    _chk(N % 8 == 0 or out_f32, "gemm_nt: N % 8 for bf16 output")
+    call("pdnn_gemm_nt", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), M, N, K,
+         float(alpha), ptr(bias), int(relu), int(out_f32), stream())
+    return out
+
+
+def gemm_nn(x, w, out_f32=False, alpha=1.0, out=None):
+    """y[M][N] = alpha * x[M][K] @ w[K][N]."""
+    M, K = x.shape
+    K2, N = w.shape
+    _chk(K == K2 and N % 8 == 0 and K % 8 == 0, f"gemm_nn: bad shapes {x.shape} {w.shape}")
+    _chk(x.stride(1) == 1 and w.stride(1) == 1, "gemm_nn: row-major operands")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=F32 if out_f32 else BF16)
+    call("pdnn_gemm_nn", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), M, N, K,
+         float(alpha), int(out_f32), stream())
+    return out
+
+
+def gemm_tn_acc(x, y, out, alpha=1.0):
+    """out[M][N] (fp32) += alpha * x[K][M]^T @ y[K][N]."""
+    K, M = x.shape
+    K2, N = y.shape
+    _chk(K == K2 and M % 8 == 0 and N % 8 == 0, f"gemm_tn: bad shapes {x.shape} {y.shape}")
+    _chk(out.dtype == F32 and out.shape == (M, N) and out.stride(1) == 1, "gemm_tn: fp32 [M][N] output")
+    call("pdnn_gemm_tn_acc", ptr(x), x.stride(0), ptr(y), y.stride(0), ptr(out), out.stride(0), M, N, K,
+         float(alpha), stream())
+    return out
+
+
+def conv_out_hw(H, W, R, S, st, pad):
+    return (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+
+
+def stats_rows(M: int) -> int:
+    return lib().pdnn_gemm_stats_rows(M)
+
+
+def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
+    """x: NHWC bf16 (N,H,W,C); w: bf16 [K][R][S][C] memory (shape K,C,R,S channels_last or K,R,S,C).
+    pro: optional (scale, shift) fp32 [C] -> input transformed relu(x*scale+shift) on load.
+    Returns (y NHWC bf16, stats slab or None)."""
+    _bf16_c(x, "conv_fwd.x")
+    N, H, W, C = x.shape
+    _bf16_c(w, "conv_fwd.w")
+    K, R, S, C2 = w.shape
+    _chk(C2 == C, f"conv_fwd: weight {tuple(w.shape)} must be [K][R][S][C] with C={C}")
+    _chk(C % 8 == 0 and K % 8 == 0, f"conv_fwd: channels must be multiples of 8 (C={C}, K={K})")
+    Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
+    y = torch.empty(N, Ho, Wo, K, device=x.device, dtype=BF16)
+    stats = None
+    if want_stats:
+        stats = torch.empty(2 * stats_rows(N * Ho * Wo), K, device=x.device, dtype=F32)
+    sc, sh = pro if pro is not None else (None, None)
+    call("pdnn_conv_fwd", ptr(x), ptr(w), ptr(y), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
+         ptr(stats), stream())
+    return y, stats
+
+
+def conv_dgrad(dy, w, x_shape, st, pad):
+    _bf16_c(dy, "conv_dgrad.dy")
+    N, H, W, C = x_shape
+    _bf16_c(w, "conv_dgrad.w")
+    K, R, S, C2 = w.shape
+    _chk(C2 == C, "conv_dgrad: weight [K][R][S][C]")
+    _, Ho, Wo, K2 = dy.shape
+    _chk(K2 == K and C % 8 == 0 and K % 8 == 0, "conv_dgrad: channel mismatch")
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    call("pdnn_conv_dgrad", ptr(dy), ptr(w), ptr(dx), N, H, W, C, K, R, S, st, pad, Ho, Wo, None, stream())
+    return dx
+
+
+def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
+    """fp32 dW [K][R][S][C] (accumulated into `out` if given, else fresh zeros)."""
+    _bf16_c(x, "conv_wgrad.x")
+    _bf16_c(dy, "conv_wgrad.dy")
+    N, H, W, C = x.shape
+    _, Ho, Wo, K = dy.shape
+    if out is None:
+        out = torch.zeros(K, R, S, C, device=x.device, dtype=F32)
+    sc, sh = pro if pro is not None else (None, None)
+    call("pdnn_conv_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
+         stream())
+    return out
+
+
+# ----------------------------------------------------------------------------------- BatchNorm
+def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
+    C = slab.shape[1]
+    mean = torch.empty(C, device=slab.device, dtype=F32)
+    invstd = torch.empty_like(mean)
+    scale = torch.empty_like(mean)
+    shift = torch.empty_like(mean)
+    call("pdnn_bn_finalize", ptr(slab), rows, C, float(L), float(eps), float(momentum), ptr(gamma), ptr(beta),
+         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
+    return mean, invstd, scale, shift
+
+
+def bn_eval_coeff(eps, gamma, beta, rm, rv):
+    C = rm.numel()
+    scale = torch.empty(C, device=rm.device, dtype=F32)
+    shift = torch.empty_like(scale)
+    call("pdnn_bn_eval_coeff", C, float(eps), ptr(gamma), ptr(beta), ptr(rm), ptr(rv), ptr(scale), ptr(shift),
+         stream())
+    return scale, shift
+
+
+def bn_stats(x2d):
+    L, C = x2d.shape
+    _chk(C % 8 == 0 and C <= 2048, f"bn_stats: C={C}")
+    rows = lib().pdnn_bn_reduce_rows(L, C)
+    slab = torch.empty(2 * rows, C, device=x2d.device, dtype=F32)
+    call("pdnn_bn_stats", ptr(x2d), L, C, ptr(slab), stream())
+    return slab, rows
+
+
+def bn_apply(x2d, scale, shift, res=None, rscale=None, rshift=None, relu=True, out=None):
+    L, C = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    call("pdnn_bn_apply", ptr(x2d), L, C, ptr(scale), ptr(shift), ptr(res), ptr(rscale), ptr(rshift), int(relu),
+         ptr(out), stream())
+    return out
+
+
+def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=None, x2=None, mean2=None,
+                  invstd2=None):
+    L, C = x.shape
+    rows = lib().pdnn_bn_reduce_rows(L, C)
+    slab = torch.empty(2 * rows, C, device=x.device, dtype=F32)
+    slab2 = torch.empty_like(slab) if x2 is not None else None
+    call("pdnn_bn_bwd_reduce", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
+         ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), stream())
+    return slab, slab2, rows
+
+
+def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False):
+    C = slab.shape[1]
+    if dgamma is None:
+        dgamma = torch.empty(C, device=slab.device, dtype=F32)
+        dbeta = torch.empty_like(dgamma)
+    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), stream())
+    return dgamma, dbeta
+
+
+def bn_bwd_apply(g, x, mean, invstd, gamma, dgamma, dbeta, mode=0, msrc=None, mscale=None, mshift=None,
+                 want_dx=True, x2=None, mean2=None, invstd2=None, gamma2=None, dgamma2=None, dbeta2=None,
+                 want_gm=False):
+    dx = torch.empty_like(x) if want_dx else None
+    dx2 = torch.empty_like(x) if x2 is not None else None
+    gm = torch.empty_like(x) if want_gm else None
+    L, C = x.shape
+    call("pdnn_bn_bwd_apply", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(dgamma), ptr(dbeta),
+         int(mode), ptr(msrc), ptr(mscale), ptr(mshift), ptr(dx), ptr(x2), ptr(mean2), ptr(invstd2), ptr(gamma2),
+         ptr(dgamma2), ptr(dbeta2), ptr(dx2), ptr(gm), stream())
+    return dx, dx2, gm
+
+
+# ----------------------------------------------------------------------------------- pooling
+def maxpool_fwd(x, k, st, pad):
+    _bf16_c(x, "maxpool.x")
+    N, H, W, C = x.shape
+    _chk(C % 8 == 0, "maxpool: C % 8")
+    Ho, Wo = conv_out_hw(H, W, k, k, st, pad)
+    y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=BF16)
+    idx = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.uint8)
+    call("pdnn_maxpool_fwd", ptr(x), ptr(y), ptr(idx), N, H, W, C, Ho, Wo, k, st, pad, stream())
+    return y, idx
+
+
+def maxpool_bwd(dy, idx, x_shape, k, st, pad):
+    N, H, W, C = x_shape
+    _, Ho, Wo, _ = dy.shape
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    call("pdnn_maxpool_bwd", ptr(dy.contiguous()), ptr(idx), ptr(dx), N, H, W, C, Ho, Wo, k, st, pad, stream())
+    return dx
+
+
+def avgpool_fwd(x):
+    _bf16_c(x, "avgpool.x")
+    N, H, W, C = x.shape
+    _chk(C % 8 == 0 and C <= 2048, "avgpool: C")
+    y = torch.empty(N, C, device=x.device, dtype=BF16)
+    call("pdnn_avgpool_fwd", ptr(x), ptr(y), N, H * W, C, stream())
+    return y
+
+
+def avgpool_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    call("pdnn_avgpool_bwd", ptr(dy.contiguous()), ptr(dx), N, H * W, C, stream())
+    return dx
+
+
+# ----------------------------------------------------------------------------------- loss
+def xent_fwd(logits, labels, ignore_index=-100):
+    R, V = logits.shape
+    _chk(logits.stride(1) == 1, "xent: row-major logits")
+    dt = 1 if logits.dtype == BF16 else 0
+    _chk(logits.dtype in (BF16, F32), "xent: bf16/fp32 logits")
+    loss = torch.empty(R, device=logits.device, dtype=F32)
+    lse = torch.empty(R, device=logits.device, dtype=F32)
+    acc = torch.zeros(2, device=logits.device, dtype=F32)
+    call("pdnn_xent_fwd", ptr(logits), logits.stride(0), R, V, ptr(labels), int(ignore_index), ptr(loss), ptr(lse),
+         ptr(acc), ptr(acc[1:]), dt, stream())
+    return loss, lse, acc
+
+
+def xent_bwd(logits, labels, lse, gscale_dev, denom, ignore_index=-100):
+    R, V = logits.shape
+    d = torch.empty_like(logits)
+    dt = 1 if logits.dtype == BF16 else 0
+    call("pdnn_xent_bwd", ptr(logits), logits.stride(0), R, V, ptr(labels), int(ignore_index), ptr(lse),
+         ptr(gscale_dev), float(denom), ptr(d), d.stride(0), dt, stream())
+    return d
+
+
+# ----------------------------------------------------------------------------------- elementwise
+ACT = {"relu": 0, "sigmoid": 1, "gelu": 2, "identity": 3}
+
+
+def act_fwd(x, op):
+    _bf16_c(x, "act.x")
+    _chk(x.numel() % 8 == 0, "act: numel % 8")
+    y = torch.empty_like(x)
+    call("pdnn_act_fwd", ptr(x), ptr(y), x.numel(), ACT[op], stream())
+    return y
+
+
+def act_bwd(g, x, op):
+    g = g.contiguous()
+    dx = torch.empty_like(x)
+    call("pdnn_act_bwd", ptr(g), ptr(x), ptr(dx), x.numel(), ACT[op], stream())
+    return dx
+
+
+def add(a, b, alpha=1.0, beta=1.0, out=None):
+    out = torch.empty_like(a) if out is None else out
+    call("pdnn_add", ptr(a), ptr(b.contiguous()), ptr(out), a.numel(), float(alpha), float(beta), stream())
+    return out
+
+
+def nchw_to_nhwc(x, cpad):
+    N, C, H, W = x.shape
+    x = x.contiguous()
+    y = torch.empty(N, H, W, cpad, device=x.device, dtype=BF16)
+    call("pdnn_nchw_to_nhwc", ptr(x), int(x.dtype == BF16), ptr(y), N, C, H * W, cpad, stream())
+    return y
+
+
+def nhwc_to_nchw_f32(x, C):
+    N, H, W, Cp = x.shape
+    y = torch.empty(N, C, H, W, device=x.device, dtype=F32)
+    call("pdnn_nhwc_to_nchw_f32", ptr(x), ptr(y), N, C, H * W, Cp, stream())
+    return y
+
+
+def colsum(x2d, out=None, accumulate=False):
+    R, C = x2d.shape
+    if out is None:
+        out = torch.empty(C, device=x2d.device, dtype=F32)
+    call("pdnn_colsum", ptr(x2d), R, C, ptr(out), int(accumulate), stream())
+    return out
+
+
+# ----------------------------------------------------------------------------------- optim / buckets
+def sgd_step(p, g, buf, shadow, lr, momentum, dampening, wd, nesterov, gscale_dev=None, gscale=1.0, first=False):
+    call("pdnn_sgd_step", ptr(p), ptr(g), ptr(buf), ptr(shadow), p.numel(), float(lr), float(momentum),
+         float(dampening), float(wd), int(nesterov), ptr(gscale_dev), float(gscale), int(first), stream())
+
+
+def adam_step(p, g, m, v, shadow, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale_dev=None, gscale=1.0):
+    call("pdnn_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(b1), float(b2),
+         float(eps), float(wd), int(decoupled), float(bc1), float(bc2), ptr(gscale_dev), float(gscale), stream())
+
+
+def cast_f32_bf16(x, y, scale=1.0):
+    call("pdnn_cast_f32_bf16", ptr(x), ptr(y), x.numel(), float(scale), stream())
+
+
+def cast_bf16_f32(x, y, scale=1.0, accumulate=False):
+    call("pdnn_cast_bf16_f32", ptr(x), ptr(y), x.numel(), float(scale), int(accumulate), stream())
+
+
+def scale_(x, scale=1.0, dev_scale=None, invert=False):
+    call("pdnn_scale_f32", ptr(x), x.numel(), float(scale), ptr(dev_scale), int(invert), stream())
+
+
+def axpy_(y, x, a):
+    call("pdnn_axpy_f32", ptr(y), ptr(x), y.numel(), float(a), stream())
+
+
+def sumsq(x, out):
+    call("pdnn_sumsq_f32", ptr(x), x.numel(), ptr(out), stream())
+    return out

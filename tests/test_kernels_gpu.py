@@ -1,0 +1,221 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (SURVEY.md §7.4
+``tests/kernels``).  Inputs are rounded to bf16 first so the reference sees exactly what the kernel sees;
+tolerances are relative to the reference's max magnitude (bf16 output rounding is ~4e-3)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.fixture(scope="module")
+def K():
+    from pytorch_distributed_nn_amd.ops import kernels, _backend
+    assert _backend.available(), "HIP kernel library must load on a GPU box"
+    return kernels
+
+
+def rnd(*s, scale=1.0):
+    return (torch.randn(*s, device="cuda") * scale).to(BF)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 256), (200, 136, 72), (1000, 1000, 2048), (64, 8, 8), (4096, 768, 3072)])
+def test_gemm_nt(K, M, N, Kd):
+    x, w = rnd(M, Kd), rnd(N, Kd)
+    b = torch.randn(N, device="cuda")
+    y = K.gemm_nt(x, w, bias=b)
+    ref = x.float() @ w.float().t() + b
+    assert rel(y, ref) < 1e-2
+    y32 = K.gemm_nt(x, w, out_f32=True, relu=True)
+    assert rel(y32, F.relu(x.float() @ w.float().t())) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 256), (200, 136, 72), (512, 2048, 1000)])
+def test_gemm_nn(K, M, N, Kd):
+    x, w = rnd(M, Kd), rnd(Kd, N)
+    y = K.gemm_nn(x, w)
+    assert rel(y, x.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 256), (136, 200, 72), (1000, 2048, 256), (768, 3072, 8192)])
+def test_gemm_tn_acc(K, M, N, Kd):
+    x, y = rnd(Kd, M), rnd(Kd, N)
+    out = torch.zeros(M, N, device="cuda")
+    K.gemm_tn_acc(x, y, out)
+    assert rel(out, x.float().t() @ y.float()) < 2e-3
+
+
+CONV_SHAPES = [
+    # N, H, W, C, Ko, R, stride, pad
+    (2, 8, 8, 64, 64, 1, 1, 0),
+    (2, 9, 9, 64, 128, 3, 1, 1),
+    (2, 14, 14, 128, 128, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+    (3, 7, 7, 512, 2048, 1, 1, 0),
+    (2, 56, 56, 64, 256, 1, 1, 0),
+]
+
+
+def conv_ref(x, w, st, pad):
+    # x NHWC, w [K][R][S][C]
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, st, pad).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv_fwd(K, shape, pro):
+    N, H, W, C, Ko, R, st, pad = shape
+    x, w = rnd(N, H, W, C), rnd(Ko, R, R, C, scale=0.1)
+    prolog = None
+    xin = x
+    if pro:
+        sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
+        prolog = (sc, sh)
+        xin = F.relu(x.float() * sc + sh).to(BF)
+    y, stats = K.conv_fwd(x, w, st, pad, pro=prolog, want_stats=True)
+    ref = conv_ref(xin, w, st, pad)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1.5e-2
+    # fused BN partial statistics of the bf16 output
+    yf = y.float().reshape(-1, Ko)
+    s = stats.view(-1, 2, Ko).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_dgrad(K, shape):
+    N, H, W, C, Ko, R, st, pad = shape
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = rnd(Ko, R, R, C, scale=0.1)
+    y = F.conv2d(x, w.float().permute(0, 3, 1, 2), None, st, pad)
+    dy = rnd(*y.permute(0, 2, 3, 1).shape)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dx = K.conv_dgrad(dy, w, (N, H, W, C), st, pad)
+    assert rel(dx, x.grad.permute(0, 2, 3, 1)) < 1.5e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv_wgrad(K, shape, pro):
+    N, H, W, C, Ko, R, st, pad = shape
+    x = rnd(N, H, W, C)
+    xin = x
+    prolog = None
+    if pro:
+        sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
+        prolog = (sc, sh)
+        xin = F.relu(x.float() * sc + sh).to(BF)
+    w = torch.zeros(Ko, C, R, R, device="cuda", requires_grad=True)
+    y = F.conv2d(xin.float().permute(0, 3, 1, 2), w, None, st, pad)
+    dy = rnd(*y.permute(0, 2, 3, 1).shape)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dw = K.conv_wgrad(x, dy, R, R, st, pad, pro=prolog)
+    assert rel(dw, w.grad.permute(0, 2, 3, 1)) < 5e-3
+
+
+def test_bn_train_fwd_bwd(K):
+    L, C = 4096, 256
+    x = rnd(L, C, scale=2.0) + 0.5
+    gamma, beta = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    slab, rows = K.bn_stats(x)
+    mean, inv, sc, sh = K.bn_finalize(slab, rows, L, 1e-5, 0.1, gamma, beta, rm, rv)
+    xf = x.float()
+    assert torch.allclose(mean, xf.mean(0), atol=1e-3)
+    assert torch.allclose(inv, torch.rsqrt(xf.var(0, unbiased=False) + 1e-5), rtol=1e-3)
+    assert torch.allclose(rv, 0.9 + 0.1 * xf.var(0, unbiased=True), rtol=1e-3)
+    y = K.bn_apply(x, sc, sh, relu=True)
+    xr = xf.clone().requires_grad_(True)
+    g_, b_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    ref = F.relu(F.batch_norm(xr, None, None, g_, b_, True, 0.1, 1e-5))
+    assert rel(y, ref) < 1e-2
+    gy = rnd(L, C)
+    ref.backward(gy.float())
+    slab, _, rows = K.bn_bwd_reduce(gy, x, mean, inv, mode=1, msrc=y)
+    dg, db = K.bn_bwd_finalize(slab, rows)
+    dx, _, _ = K.bn_bwd_apply(gy, x, mean, inv, gamma, dg, db, mode=1, msrc=y)
+    assert rel(dg, g_.grad) < 2e-2 and rel(db, b_.grad) < 2e-2
+    assert rel(dx, xr.grad) < 3e-2
+
+
+def test_maxpool(K):
+    x = torch.randn(2, 17, 17, 64, device="cuda").to(BF).requires_grad_(False)
+    y, idx = K.maxpool_fwd(x, 3, 2, 1)
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 1e-6
+    g = rnd(*y.shape)
+    ref.backward(g.float().permute(0, 3, 1, 2))
+    dx = K.maxpool_bwd(g, idx, x.shape, 3, 2, 1)
+    assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_avgpool(K):
+    x = rnd(4, 7, 7, 2048)
+    y = K.avgpool_fwd(x)
+    assert rel(y, x.float().mean((1, 2))) < 1e-2
+    g = rnd(4, 2048)
+    dx = K.avgpool_bwd(g, x.shape)
+    assert rel(dx, (g.float() / 49)[:, None, None, :].expand(4, 7, 7, 2048)) < 1e-2
+
+
+@pytest.mark.parametrize("V", [10, 1000, 50257])
+def test_xent(K, V):
+    R = 64
+    lg = rnd(R, V, scale=3.0)
+    y = torch.randint(0, V, (R,), device="cuda")
+    y[3] = -100
+    loss, lse, acc = K.xent_fwd(lg, y)
+    lr = lg.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, y, reduction="sum")
+    assert abs(acc[0].item() - ref.item()) / abs(ref.item()) < 1e-4
+    ref.backward()
+    gs = torch.ones(1, device="cuda")
+    d = K.xent_bwd(lg, y, lse, gs, 1.0)
+    assert rel(d, lr.grad) < 1e-2
+
+
+def test_sgd_adam(K):
+    n = 10007
+    p, g = torch.randn(n, device="cuda"), torch.randn(n, device="cuda")
+    buf = torch.zeros(n, device="cuda")
+    sh = torch.empty(n, device="cuda", dtype=BF)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.SGD([pr], lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for first in (True, False):
+        pr.grad = g.clone()
+        opt.step()
+        K.sgd_step(p, g, buf, sh, 0.1, 0.9, 0.0, 1e-4, True, first=first)
+    assert torch.allclose(p, pr.detach(), atol=1e-6)
+    assert rel(sh, p) < 5e-3
+    p2 = torch.randn(n, device="cuda")
+    m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    pr2 = p2.clone().requires_grad_(True)
+    opt2 = torch.optim.AdamW([pr2], lr=1e-3, weight_decay=0.01)
+    for t in (1, 2, 3):
+        pr2.grad = g.clone()
+        opt2.step()
+        K.adam_step(p2, g, m, v, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, True, 1 - 0.9 ** t, 1 - 0.999 ** t)
+    assert torch.allclose(p2, pr2.detach(), atol=1e-6)
+
+
+@pytest.mark.parametrize("op", ["relu", "sigmoid", "gelu"])
+def test_act(K, op):
+    x = rnd(4096)
+    y = K.act_fwd(x, op)
+    xr = x.float().clone().requires_grad_(True)
+    f = {"relu": F.relu, "sigmoid": torch.sigmoid, "gelu": lambda t: F.gelu(t, approximate="tanh")}[op]
+    r = f(xr)
+    assert rel(y, r) < 1e-2
+    g = rnd(4096)
+    r.backward(g.float())
+    assert rel(K.act_bwd(g, x, op), xr.grad) < 2e-2
