@@ -1,0 +1,113 @@
+"""Headline benchmark (BASELINE.json): samples/sec of ResNet-50 DDP training on 1..8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model resnet50]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One process per GPU (RCCL over xGMI for N > 1).  Model: ResNet-50, ImageNet layout (224x224x3 input,
+1000 classes), random init; data: synthetic device-resident tensors of that shape.  Compute dtype bf16
+(NHWC activations, fp32 accumulation, fp32 master weights / BN statistics / gradients), optimizer:
+fused SGD with momentum 0.9 + weight decay, full step timed (forward, backward, bucketed all-reduce,
+optimizer).  Per-GPU batch is fixed as N grows (weak scaling).  Rank 0 prints one JSON line with the
+WHOLE-JOB samples/sec (max step time over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+STOCK_PYTORCH_1GPU = 6629.4   # profiles/stock_pytorch_resnet50.jsonl: torch autocast-bf16 channels_last, bs256
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    a = ap.parse_args()
+
+    from pytorch_distributed_nn_amd.parallel import runtime
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.optim import SGD, flatten_module
+    from pytorch_distributed_nn_amd.ops import functional as OF
+
+    env = runtime.init_process_group()
+    world = runtime.world_size()
+    dev = runtime.device()
+    torch.manual_seed(1234 + env.rank)
+
+    model = build_model(a.model, num_classes=1000).to(dev)
+    if world > 1:
+        net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
+    else:
+        flatten_module(model)
+        net = model
+    opt = SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5)
+
+    B, S = a.batch, a.image_size
+    xs = [torch.randn(B, 3, S, S, device=dev).to(torch.bfloat16) for _ in range(2)]
+    ys = [torch.randint(0, 1000, (B,), device=dev) for _ in range(2)]
+
+    def step(i):
+        opt.zero_grad()
+        out = net(xs[i % 2])
+        loss = OF.cross_entropy(out, ys[i % 2])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        loss = step(i)
+    runtime.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i)
+    runtime.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    ms = 1e3 * dt / a.steps
+    value = B * world * a.steps / dt
+    if env.rank == 0:
+        print(json.dumps({
+            "metric": "samples/sec (whole node) ResNet-50 DDP",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "vs_stock_pytorch_rocm": round(value / (STOCK_PYTORCH_1GPU * world), 4),
+            "dtype": "bf16",
+            "data": "synthetic (device-resident random 224x224x3 images, random labels), random-init weights",
+            "final_loss": round(float(loss), 4),
+            "config": {"model": f"{a.model} (ImageNet layout, 224x224, 1000 classes)", "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
+                       "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb},
+        }), flush=True)
+    runtime.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,8 +18,31 @@
 namespace {
 constexpr int NT = 256;
 
-// finalize partial sums -> mean, invstd, scale/shift (+ running-stat update).  One thread/channel,
-// fp64 accumulation across partial rows.
+// Level-1 reduction of a partial-statistics slab [rows][2][C] -> [RB][2][C]: block (cx, ry) sums the
+// rows ry, ry+RB, ... for 64 channels with 4 row lanes (coalesced 256-byte row segments).
+__global__ void __launch_bounds__(NT) slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                          float* __restrict__ out) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
+    const int RB = gridDim.y;
+    __shared__ float red[2][4][64];
+    float s = 0.f, q = 0.f;
+    if (c < C) {
+        for (int r = blockIdx.y + RB * lr; r < rows; r += RB * 4) {
+            s += slab[(long)(2 * r) * C + c];
+            q += slab[(long)(2 * r + 1) * C + c];
+        }
+    }
+    red[0][lr][threadIdx.x & 63] = s;
+    red[1][lr][threadIdx.x & 63] = q;
+    __syncthreads();
+    if (lr == 0 && c < C) {
+        const int l = threadIdx.x;
+        out[(long)(2 * blockIdx.y) * C + c] = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+        out[(long)(2 * blockIdx.y + 1) * C + c] = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
+    }
+}
+
+// finalize (few) partial rows -> mean, invstd, scale/shift (+ running-stat update), fp64 accumulation.
 __global__ void bn_finalize_kernel(const float* __restrict__ slab, int rows, int C, double L, float eps,
                                    float momentum, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* run_mean, float* run_var,
@@ -86,7 +109,8 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
     }
 }
 
-// y = act(x*scale + shift + residual'), residual' = res (identity) or res*rscale + rshift
+// y = act(x*scale + shift + residual'), residual' = res (identity) or res*rscale + rshift.
+// Each thread owns one fixed group of 8 channels (coefficients in registers) and strides over rows.
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ x, long L, int C,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
@@ -94,31 +118,33 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
                                                       const float* __restrict__ rscale,
                                                       const float* __restrict__ rshift, int relu,
                                                       bf16_t* __restrict__ y) {
-    const int CG = C >> 3;
-    const long total = L * CG;
-    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-        const long r = i / CG;
-        const int c = (int)(i - r * CG) * 8;
-        float v[8];
-        unpack8(*reinterpret_cast<const u16x8_t*>(x + r * C + c), v);
+    const int CG = C >> 3, RPI = NT / CG;
+    const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
+    if (rr >= RPI) return;
+    float sc[8], sh[8], rs[8], rh[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], scale[c + j], shift[c + j]);
+    for (int j = 0; j < 8; ++j) {
+        sc[j] = scale[c + j]; sh[j] = shift[c + j];
+        rs[j] = rscale ? rscale[c + j] : 1.f; rh[j] = rscale ? rshift[c + j] : 0.f;
+    }
+    for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
+        const long off = r * C + c;
+        float v[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(x + off), v);
         if (res) {
             float rv[8];
-            unpack8(*reinterpret_cast<const u16x8_t*>(res + r * C + c), rv);
-            if (rscale) {
+            unpack8(*reinterpret_cast<const u16x8_t*>(res + off), rv);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] += fmaf(rv[j], rscale[c + j], rshift[c + j]);
-            } else {
+            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], fmaf(rv[j], rs[j], sh[j] + rh[j]));
+        } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] += rv[j];
-            }
+            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
         }
         if (relu) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
         }
-        *reinterpret_cast<u16x8_t*>(y + r * C + c) = pack8(v);
+        *reinterpret_cast<u16x8_t*>(y + off) = pack8(v);
     }
 }
 
@@ -203,7 +229,8 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows,
     else { dbeta[c] = (float)s; dgamma[c] = (float)q; }
 }
 
-// dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L); optionally also a second BN's dx2 and/or gm.
+// dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
+// registers; optionally also a second BN's dx2 (shared gm) and/or gm itself.
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
@@ -212,35 +239,50 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     bf16_t* __restrict__ dx, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
     const float* __restrict__ invstd2, const float* __restrict__ gamma2, const float* __restrict__ dgamma2,
     const float* __restrict__ dbeta2, bf16_t* __restrict__ dx2, bf16_t* __restrict__ gm_out) {
-    const int CG = C >> 3;
-    const long total = L * CG;
+    const int CG = C >> 3, RPI = NT / CG;
+    const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
+    if (rr >= RPI) return;
     const float invL = (float)(1.0 / (double)L);
-    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-        const long r = i / CG;
-        const int c = (int)(i - r * CG) * 8;
+    float k1[8], A1[8], B1[8], k2[8], A2[8], B2[8], ms[8], mh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float is = invstd[c + j], k = (gamma ? gamma[c + j] : 1.f) * is;
+        const float dg = dgamma[c + j] * invL, db = dbeta[c + j] * invL;
+        k1[j] = k; A1[j] = -k * is * dg; B1[j] = k * (mean[c + j] * is * dg - db);
+        if (x2) {
+            const float is2 = invstd2[c + j], kk = (gamma2 ? gamma2[c + j] : 1.f) * is2;
+            const float dg2 = dgamma2[c + j] * invL, db2 = dbeta2[c + j] * invL;
+            k2[j] = kk; A2[j] = -kk * is2 * dg2; B2[j] = kk * (mean2[c + j] * is2 * dg2 - db2);
+        } else {
+            k2[j] = A2[j] = B2[j] = 0.f;
+        }
+        ms[j] = mode == 2 ? mscale[c + j] : 0.f;
+        mh[j] = mode == 2 ? mshift[c + j] : 0.f;
+    }
+    for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
         const long off = r * C + c;
         float gm[8], xv[8], o[8];
-        masked_grad(g, x, msrc, mscale, mshift, mode, off, c, gm, xv);
+        unpack8(*reinterpret_cast<const u16x8_t*>(g + off), gm);
+        unpack8(*reinterpret_cast<const u16x8_t*>(x + off), xv);
+        if (mode == 1) {
+            float m[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(msrc + off), m);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
+        } else if (mode == 2) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+        }
         if (dx) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float is = invstd[c + j];
-                const float xh = (xv[j] - mean[c + j]) * is;
-                const float k = (gamma ? gamma[c + j] : 1.f) * is;
-                o[j] = k * (gm[j] - dbeta[c + j] * invL - xh * dgamma[c + j] * invL);
-            }
+            for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gm[j], fmaf(xv[j], A1[j], B1[j]));
             *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
         }
         if (x2) {
             float x2v[8];
             unpack8(*reinterpret_cast<const u16x8_t*>(x2 + off), x2v);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float is = invstd2[c + j];
-                const float xh = (x2v[j] - mean2[c + j]) * is;
-                const float k = (gamma2 ? gamma2[c + j] : 1.f) * is;
-                o[j] = k * (gm[j] - dbeta2[c + j] * invL - xh * dgamma2[c + j] * invL);
-            }
+            for (int j = 0; j < 8; ++j) o[j] = fmaf(k2[j], gm[j], fmaf(x2v[j], A2[j], B2[j]));
             *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
         }
         if (gm_out) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
@@ -258,11 +300,19 @@ inline unsigned reduce_grid(long L, int C) {
 
 PDNN_API int pdnn_bn_reduce_rows(long L, int C) { return (int)reduce_grid(L, C); }
 
+// work: >= 2 * 64 * C floats of scratch for the level-1 reduction
 PDNN_API int pdnn_bn_finalize(const float* slab, int rows, int C, double L, float eps, float momentum,
                               const float* gamma, const float* beta, float* run_mean, float* run_var,
                               float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
-                              hipStream_t st) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slab, rows, C, L, eps,
+                              float* work, hipStream_t st) {
+    const float* src = slab;
+    int r = rows;
+    if (rows > 64) {
+        hipLaunchKernelGGL(slab_reduce_kernel, dim3((C + 63) / 64, 64), dim3(NT), 0, st, slab, rows, C, work);
+        src = work;
+        r = 64;
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, r, C, L, eps,
                        momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out);
     PDNN_LAUNCH_RET;
 }
@@ -297,8 +347,15 @@ PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C,
 }
 
 PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dgamma, float* dbeta,
-                                  int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slab, rows, C, dgamma,
+                                  int accumulate, float* work, hipStream_t st) {
+    const float* src = slab;
+    int r = rows;
+    if (rows > 64) {
+        hipLaunchKernelGGL(slab_reduce_kernel, dim3((C + 63) / 64, 64), dim3(NT), 0, st, slab, rows, C, work);
+        src = work;
+        r = 64;
+    }
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, r, C, dgamma,
                        dbeta, accumulate);
     PDNN_LAUNCH_RET;
 }

@@ -59,7 +59,10 @@ struct ConvGeom {
     int Ho, Wo, R, S;       // the "other" spatial extent and filter size
     int st, pad;
     int Ko;                 // output channels (for A_CONVT / B_WT reduction index)
-    FastDiv dHW, dW, dC, dS, dKo;  // divisors used by the gathers
+    // transposed-conv parity class (dgrad with stride > 1 is split into st*st dense sub-problems):
+    // output pixels h = hc*st + ph, taps r = r0 + st*ir (ir < Rc); identical to a plain conv when st == 1
+    int ph, pw, r0, s0, Sc;
+    FastDiv dHW, dW, dC, dS, dKo, dSc;  // divisors used by the gathers
 };
 
 struct GemmArgs {
@@ -75,6 +78,7 @@ struct GemmArgs {
     int relu;
     float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
     int ktiles_per_split;     // split-K (grid.z)
+    int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -178,8 +182,8 @@ struct KLoader {
                     wb[i] = (int)x * g.st - g.pad;
                     base[i] = ptr + (long)n * g.H * g.W * g.C;
                 } else {
-                    hb[i] = (int)y + g.pad;
-                    wb[i] = (int)x + g.pad;
+                    hb[i] = (int)y * g.st + g.ph + g.pad;
+                    wb[i] = (int)x * g.st + g.pw + g.pad;
                     base[i] = ptr + (long)n * g.Ho * g.Wo * g.Ko;
                 }
             }
@@ -191,12 +195,12 @@ struct KLoader {
             c = kcur - rs * g.C;
             r = fdiv(rs, g.dS);
             s = rs - r * g.S;
-        } else if constexpr (KIND == 2) {
+        } else if constexpr (KIND == 2) {     // r, s = tap indices within the parity class
             const ConvGeom& g = a.g;
             const uint32_t rs = fdiv((uint32_t)kcur, g.dKo);
             c = kcur - rs * g.Ko;
-            r = fdiv(rs, g.dS);
-            s = rs - r * g.S;
+            r = fdiv(rs, g.dSc);
+            s = rs - r * g.Sc;
         }
     }
     __device__ __forceinline__ void seek(const GemmArgs& a, int k) {   // jump to K offset k (split-K)
@@ -209,8 +213,8 @@ struct KLoader {
         } else if constexpr (KIND == 2) {
             const uint32_t rs = fdiv((uint32_t)kcur, a.g.dKo);
             c = kcur - rs * a.g.Ko;
-            r = fdiv(rs, a.g.dS);
-            s = rs - r * a.g.S;
+            r = fdiv(rs, a.g.dSc);
+            s = rs - r * a.g.Sc;
         }
     }
     __device__ __forceinline__ void load(const GemmArgs& a, int Ktot, u16x8_t* reg) {
@@ -230,10 +234,9 @@ struct KLoader {
                 reg[i] = x;
             } else {
                 const ConvGeom& g = a.g;
-                int th = hb[i] - r, tw = wb[i] - s;
+                int th = hb[i] - (g.r0 + g.st * r), tw = wb[i] - (g.s0 + g.st * s);
                 bool v = vrow[i] && kv && th >= 0 && tw >= 0;
-                if (g.st != 1) {
-                    v = v && (th % g.st == 0) && (tw % g.st == 0);
+                if (g.st != 1) {     // exact by construction of the parity class
                     th /= g.st;
                     tw /= g.st;
                 }
@@ -249,7 +252,7 @@ struct KLoader {
             while (c >= a.g.C) { c -= a.g.C; if (++s == a.g.S) { s = 0; ++r; } }
         } else if constexpr (KIND == 2) {
             c += BK;
-            while (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.S) { s = 0; ++r; } }
+            while (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.Sc) { s = 0; ++r; } }
         }
     }
     __device__ __forceinline__ void store(bf16_t* img, const u16x8_t* reg, int tid) const {
@@ -309,7 +312,9 @@ struct MLoader {
                 const int kk = v ? k : 0;
                 const uint32_t rs = fdiv((uint32_t)kk, g.dKo);
                 const int ko = kk - rs * g.Ko;
-                reg[i] = v ? ldg16(ptr + ((long)ko * g.R * g.S + rs) * g.C + col) : zero8();
+                const uint32_t ir = fdiv(rs, g.dSc);
+                const int rr = g.r0 + g.st * (int)ir, ss = g.s0 + g.st * (int)(rs - ir * g.Sc);
+                reg[i] = v ? ldg16(ptr + ((long)ko * g.R * g.S + rr * g.S + ss) * g.C + col) : zero8();
             } else {
                 // reduction index k = output pixel (n, yo, xo); column = (r, s, c) of the input window
                 const ConvGeom& g = a.g;
@@ -526,15 +531,23 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
                 if (a.relu) v[j] = fmaxf(v[j], 0.f);
             }
+            long orow = m;
+            if (a.scatter) {
+                const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
+                const uint32_t rem = (uint32_t)m - nn * a.g.dHW.d;
+                const uint32_t hc = fdiv(rem, a.g.dW);
+                const uint32_t wc = rem - hc * a.g.dW.d;
+                orow = ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
+            }
             if constexpr (EM == E_BF16) {
-                bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc + n;
+                bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc + n;
                 if (n + 8 <= a.N) {
                     *reinterpret_cast<u16x8_t*>(C) = pack8(v);
                 } else {
                     for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = f2bf(v[j]);
                 }
             } else {
-                float* C = reinterpret_cast<float*>(a.C) + (long)m * a.ldc + n;
+                float* C = reinterpret_cast<float*>(a.C) + orow * a.ldc + n;
                 if (n + 8 <= a.N) {
                     *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
                     *reinterpret_cast<float4*>(C + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -578,6 +591,7 @@ void fill_geom(ConvGeom& g, int Nimg, int H, int W, int C, int Ho, int Wo, int R
     g.Nimg = Nimg; g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo; g.R = R; g.S = S;
     g.st = st; g.pad = pad; g.Ko = Ko;
     g.dC = make_fdiv(C); g.dS = make_fdiv(S); g.dKo = make_fdiv(Ko);
+    g.ph = g.pw = g.r0 = g.s0 = 0; g.Sc = S; g.dSc = make_fdiv(S);
 }
 
 }  // namespace
@@ -664,17 +678,42 @@ PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg
 }
 
 // Convolution data gradient: dx[N][H][W][C] = sum over (r, s, ko) dy[...] * w[ko][r][s][c].
+// stride > 1 is decomposed into st*st parity classes of dx pixels; each class is a dense implicit GEMM
+// over only the taps that reach it (no MFMA work on the zero-stuffed positions of the transposed conv).
 PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nimg, int H, int W, int C,
                              int Ko, int R, int S, int st, int pad, int Ho, int Wo, float* stats,
                              hipStream_t stream) {
     ensure_attrs();
-    GemmArgs a{};
-    a.M = Nimg * H * W; a.N = C; a.K = R * S * Ko;
-    a.A = dy; a.B = w; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
-    fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
-    a.g.dHW = make_fdiv(H * W); a.g.dW = make_fdiv(W);
-    a.ktiles_per_split = (int)cdiv(a.K, BK);
-    return launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);
+    bool any_empty = false;
+    for (int ph = 0; ph < st; ++ph)
+        for (int pw = 0; pw < st; ++pw) {
+            const int r0 = (ph + pad) % st, s0 = (pw + pad) % st;
+            const int Rc = r0 < R ? (R - r0 + st - 1) / st : 0, Sc = s0 < S ? (S - s0 + st - 1) / st : 0;
+            const int Hc = ph < H ? (H - ph + st - 1) / st : 0, Wc = pw < W ? (W - pw + st - 1) / st : 0;
+            if (Hc * Wc > 0 && Rc * Sc == 0) any_empty = true;
+        }
+    if (any_empty) {
+        hipError_t e = hipMemsetAsync(dx, 0, (size_t)Nimg * H * W * C * sizeof(bf16_t), stream);
+        if (e != hipSuccess) return (int)e;
+    }
+    for (int ph = 0; ph < st; ++ph)
+        for (int pw = 0; pw < st; ++pw) {
+            const int r0 = (ph + pad) % st, s0 = (pw + pad) % st;
+            const int Rc = r0 < R ? (R - r0 + st - 1) / st : 0, Sc = s0 < S ? (S - s0 + st - 1) / st : 0;
+            const int Hc = ph < H ? (H - ph + st - 1) / st : 0, Wc = pw < W ? (W - pw + st - 1) / st : 0;
+            if (Rc * Sc == 0 || Hc * Wc == 0) continue;
+            GemmArgs a{};
+            a.M = Nimg * Hc * Wc; a.N = C; a.K = Rc * Sc * Ko;
+            a.A = dy; a.B = w; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
+            fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+            a.g.ph = ph; a.g.pw = pw; a.g.r0 = r0; a.g.s0 = s0; a.g.Sc = Sc; a.g.dSc = make_fdiv(Sc);
+            a.g.dHW = make_fdiv(Hc * Wc); a.g.dW = make_fdiv(Wc);
+            a.scatter = st > 1;
+            a.ktiles_per_split = (int)cdiv(a.K, BK);
+            const int rc = launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);
+            if (rc) return rc;
+        }
+    return 0;
 }
 
 // Convolution weight gradient (accumulating into fp32 dw[Ko][R][S][C]): split-K over output pixels.

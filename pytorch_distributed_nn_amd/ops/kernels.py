@@ -134,8 +134,9 @@ def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
     invstd = torch.empty_like(mean)
     scale = torch.empty_like(mean)
     shift = torch.empty_like(mean)
+    work = torch.empty(2 * 64 * C, device=slab.device, dtype=F32) if rows > 64 else None
     call("pdnn_bn_finalize", ptr(slab), rows, C, float(L), float(eps), float(momentum), ptr(gamma), ptr(beta),
-         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
+         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(work), stream())
     return mean, invstd, scale, shift
 
 
@@ -182,7 +183,8 @@ def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False):
     if dgamma is None:
         dgamma = torch.empty(C, device=slab.device, dtype=F32)
         dbeta = torch.empty_like(dgamma)
-    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), stream())
+    work = torch.empty(2 * 64 * C, device=slab.device, dtype=F32) if rows > 64 else None
+    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), stream())
     return dgamma, dbeta
 
 

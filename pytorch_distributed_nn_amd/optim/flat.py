@@ -1,0 +1,116 @@
+"""Flat parameter arena: every trainable parameter of a model lives in ONE contiguous fp32 buffer.
+
+Why (MI355X-first): with 288 GB of HBM per GPU memory is not the constraint, launch count and
+passes over memory are.  A single flat buffer lets
+
+* the optimizer update all parameters in one kernel launch (instead of a per-tensor loop — the
+  reference applies updates tensor by tensor: pytorch_code/sync_replicas_master_nn.py:22-28,216-219),
+* DDP buckets be zero-copy *views* of the flat gradient buffer (the reference flattens/copies every
+  bucket: data_parallel_dist.py:247,262-263),
+* the init broadcast be one collective (reference: one broadcast per tensor, data_parallel_dist.py:45-46),
+* the bf16 compute shadow of all weights be refreshed in the optimizer pass itself.
+
+Layout: parameters are placed in registration (forward) order, each start aligned to 64 elements
+(256 B), 4-D conv weights in channels_last order ([K][R][S][C]) so the shadow slice is exactly what
+the implicit-GEMM kernels read.  ``p.data`` / ``p.grad`` become views into ``data`` / ``grad``.
+"""
+from __future__ import annotations
+
+import torch
+
+ALIGN = 64
+
+
+def _cl_strides(shape):
+    K, C, R, S = shape
+    return (R * S * C, 1, S * C, C)
+
+
+class FlatParams:
+    def __init__(self, params, device=None, shadow: bool | None = None, align: int = ALIGN):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("FlatParams: no trainable parameters")
+        device = torch.device(device) if device is not None else self.params[0].device
+        self.device = device
+        self.offsets, off = [], 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + align - 1) // align * align
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        use_shadow = (device.type == "cuda") if shadow is None else shadow
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device) if use_shadow else None
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            if p.dim() == 4:
+                dv = torch.as_strided(self.data, p.shape, _cl_strides(p.shape), o)
+                gv = torch.as_strided(self.grad, p.shape, _cl_strides(p.shape), o)
+            else:
+                dv = self.data[o:o + n].view(p.shape)
+                gv = self.grad[o:o + n].view(p.shape)
+            dv.copy_(p.detach().to(device=device, dtype=torch.float32))
+            p.data = dv
+            p.grad = gv
+            p._pdnn_flat = self
+            if self.shadow is not None:
+                if p.dim() == 4:
+                    K, C, R, S = p.shape
+                    p._pdnn_shadow = self.shadow[o:o + n].view(K, R, S, C)
+                else:
+                    p._pdnn_shadow = self.shadow[o:o + n].view(p.shape)
+        self.refresh_shadow()
+
+    # ------------------------------------------------------------------
+    def refresh_shadow(self):
+        """Re-cast the fp32 master weights into the bf16 shadow (after load_state_dict / broadcast)."""
+        if self.shadow is None:
+            return
+        if self.data.is_cuda:
+            from ..ops import kernels as K
+            K.cast_f32_bf16(self.data, self.shadow)
+        else:
+            self.shadow.copy_(self.data)
+        self.mark_shadow_fresh()
+
+    def mark_shadow_fresh(self):
+        for p in self.params:
+            p._pdnn_shadow_ver = p._version
+
+    def zero_grad(self):
+        self.grad.zero_()
+        # a torch optimizer/zero_grad(set_to_none=True) may have detached the views: re-attach
+        for p, o in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * o:
+                n = p.numel()
+                p.grad = (torch.as_strided(self.grad, p.shape, _cl_strides(p.shape), o) if p.dim() == 4
+                          else self.grad[o:o + n].view(p.shape))
+
+    def param_range(self, params):
+        """(start, end) of the flat range covering exactly `params` (in arena order), else None."""
+        idx = {id(p): i for i, p in enumerate(self.params)}
+        ids = [idx.get(id(p)) for p in params]
+        if any(i is None for i in ids) or not ids:
+            return None
+        ids_sorted = sorted(ids)
+        if ids_sorted != list(range(ids_sorted[0], ids_sorted[-1] + 1)):
+            return None
+        start = self.offsets[ids_sorted[0]]
+        last = ids_sorted[-1]
+        end = self.offsets[last + 1] if last + 1 < len(self.params) else self.numel
+        return start, end
+
+
+def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatParams:
+    """Move ``module``'s trainable parameters into a :class:`FlatParams` arena (idempotent)."""
+    fp = getattr(module, "_pdnn_flat", None)
+    if fp is not None:
+        return fp
+    fp = FlatParams(module.parameters(), device=device, shadow=shadow)
+    module._pdnn_flat = fp
+
+    def _post_load(mod, incompatible):
+        fp.refresh_shadow()
+    module.register_load_state_dict_post_hook(_post_load)
+    return fp

@@ -1,0 +1,176 @@
+"""Fused flat-buffer optimizers: SGD (momentum / dampening / weight decay / Nesterov) and Adam / AdamW.
+
+torch.optim-compatible API (``param_groups``, ``zero_grad``, ``state_dict``/``load_state_dict``,
+``step(closure)``), semantics identical to ``torch.optim.SGD`` / ``Adam`` / ``AdamW``.
+
+When a param group covers a contiguous range of a :class:`~.flat.FlatParams` arena (the normal case:
+``SGD(model.parameters())`` after ``flatten_module``/DDP) the whole group is ONE kernel launch
+(``optim.hip``) that also refreshes the bf16 weight shadow and applies the gradient averaging factor
+(``grad_scale``, or a device-side scale such as 1/alive-count for the straggler-tolerant modes).  Groups
+that are not flat fall back to one launch per tensor (GPU) or the torch reference update (CPU).
+
+Reference parity: the PS master applies ``param -= lr * avg_grad`` (sync_replicas_master_nn.py:22-28,
+216-219) and ignores --momentum (defect D9); the C++ master fuses the average into the update as
+``ApplyGrad(lr / count)`` (sync_replicas_master_nn.h:124-128); the TF stack uses Adam
+(distributed_train.py:160).  Here momentum IS honoured and the average is fused the C++ way.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .flat import FlatParams
+
+
+def _flat_of(params):
+    fps = {id(getattr(p, "_pdnn_flat", None)) for p in params}
+    if len(fps) != 1:
+        return None, None
+    fp = getattr(params[0], "_pdnn_flat", None)
+    if fp is None:
+        return None, None
+    rng = fp.param_range(params)
+    return (fp, rng) if rng is not None else (None, None)
+
+
+class _FusedBase(torch.optim.Optimizer):
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self.grad_scale = 1.0          # host-side factor (e.g. 1/world_size when grads are summed)
+        self.grad_scale_dev = None     # optional device scalar (e.g. 1/alive for k-of-n)
+        self._flat_cache = {}
+
+    def _group_flat(self, gi, group):
+        if gi not in self._flat_cache:
+            self._flat_cache[gi] = _flat_of(group["params"])
+        return self._flat_cache[gi]
+
+    def zero_grad(self, set_to_none: bool = False):
+        done = set()
+        for group in self.param_groups:
+            for p in group["params"]:
+                fp = getattr(p, "_pdnn_flat", None)
+                if fp is not None:
+                    if id(fp) not in done:
+                        fp.zero_grad()
+                        done.add(id(fp))
+                elif p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.detach_()
+                        p.grad.zero_()
+
+
+class SGD(_FusedBase):
+    def __init__(self, params, lr=0.01, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            lr, mom, damp, wd, nest = (group["lr"], group["momentum"], group["dampening"], group["weight_decay"],
+                                       group["nesterov"])
+            fp, rng = self._group_flat(gi, group)
+            if fp is not None and fp.data.is_cuda:
+                from ..ops import kernels as K
+                s, e = rng
+                st = self.state.setdefault(f"flat{gi}", {})
+                first = "momentum_buffer" not in st
+                if mom != 0 and first:
+                    st["momentum_buffer"] = torch.zeros(e - s, device=fp.data.device)
+                buf = st.get("momentum_buffer")
+                K.sgd_step(fp.data[s:e], fp.grad[s:e], buf, fp.shadow[s:e] if fp.shadow is not None else None,
+                           lr, mom, damp, wd, nest, self.grad_scale_dev, self.grad_scale, first)
+                continue
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad
+                if self.grad_scale != 1.0:
+                    g = g * self.grad_scale
+                if self.grad_scale_dev is not None:
+                    g = g * self.grad_scale_dev
+                if wd != 0:
+                    g = g.add(p, alpha=wd)
+                if mom != 0:
+                    st = self.state[p]
+                    if "momentum_buffer" not in st:
+                        st["momentum_buffer"] = g.clone().detach()
+                    else:
+                        st["momentum_buffer"].mul_(mom).add_(g, alpha=1 - damp)
+                    b = st["momentum_buffer"]
+                    g = g.add(b, alpha=mom) if nest else b
+                p.add_(g, alpha=-lr)
+        return loss
+
+
+class Adam(_FusedBase):
+    decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            fp, rng = self._group_flat(gi, group)
+            if fp is not None and fp.data.is_cuda:
+                from ..ops import kernels as K
+                s, e = rng
+                st = self.state.setdefault(f"flat{gi}", {})
+                if "step" not in st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros(e - s, device=fp.data.device)
+                    st["exp_avg_sq"] = torch.zeros(e - s, device=fp.data.device)
+                st["step"] += 1
+                t = st["step"]
+                K.adam_step(fp.data[s:e], fp.grad[s:e], st["exp_avg"], st["exp_avg_sq"],
+                            fp.shadow[s:e] if fp.shadow is not None else None, lr, b1, b2, eps, wd,
+                            self.decoupled, 1 - b1 ** t, 1 - b2 ** t, self.grad_scale_dev, self.grad_scale)
+                continue
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad * self.grad_scale
+                if self.grad_scale_dev is not None:
+                    g = g * self.grad_scale_dev
+                st = self.state[p]
+                if "step" not in st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                t = st["step"]
+                if self.decoupled:
+                    p.mul_(1 - lr * wd)
+                elif wd:
+                    g = g.add(p, alpha=wd)
+                st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+                st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+                denom = (st["exp_avg_sq"] / (1 - b2 ** t)).sqrt_().add_(eps)
+                p.addcdiv_(st["exp_avg"], denom, value=-lr / (1 - b1 ** t))
+        return loss
+
+
+class AdamW(Adam):
+    decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+
+__all__ = ["SGD", "Adam", "AdamW", "FlatParams"]

@@ -1,0 +1,233 @@
+"""DistributedDataParallel over RCCL (xGMI) — the north-star primitive (SURVEY.md §2.6 PAR-DP-ALLREDUCE,
+§3.3; reference fork: pytorch_code/data_parallel_dist/data_parallel_dist.py:29-267).
+
+What it does, and how it differs from the reference's design:
+
+* **Init broadcast** of all parameters and buffers from rank 0 as ONE collective over the flat parameter
+  arena (+ one coalesced broadcast of buffers) — the reference issues one broadcast per tensor
+  (data_parallel_dist.py:45-46).
+* **Buckets are zero-copy views** of the flat fp32 gradient buffer (``optim.FlatParams``), assigned in
+  **reverse** parameter order (the order gradients are produced in backward), with a small first bucket
+  so communication starts as early as possible.  The reference fills ~1 MB buckets in *forward* order
+  and flattens/copies each one (defect D11; data_parallel_dist.py:70-83, 247, 262-263).
+* **Overlap without Python threads**: a post-accumulate-grad hook counts ready parameters; when a
+  bucket is complete its ``all_reduce`` is issued immediately (asynchronously, RCCL runs it on its own
+  HIP stream ordered after the compute stream), strictly in bucket order so every rank issues the same
+  collective sequence.  An autograd end-of-backward callback launches any remaining buckets (unused
+  parameters) and waits.  The reference spawns one reduction thread + one process group per bucket
+  (data_parallel_dist.py:211-267).
+* **Averaging** uses RCCL's native AVG reduction (one pass, no extra scale kernel); on gloo (CPU) it is
+  SUM followed by a scale.
+* **Bucket sizing for xGMI**: each MI355X has 7 point-to-point xGMI links; a large bucket lets RCCL
+  spread one collective across many channels/links, small buckets are latency bound (~10-30 us per
+  collective).  Defaults: 1 MiB first bucket, 32 MiB afterwards (ResNet-50's 102 MB of fp32 gradients =
+  4-5 collectives) — sweep with ``tools/bench_allreduce.py``.
+* **Straggler tolerance** (PAR-DP-KILL / PAR-DP-BACKUP in all-reduce form): a rank
+  marked not-alive contributes zeros; the alive count is all-reduced alongside the buckets and the
+  optimizer divides by it (device scalar, no host sync) — the count-correct average of the C++ master
+  (sync_replicas_master_nn.h:125), fixing the reference's divide-by-(N-1) defect D3.
+* Optional **bf16 gradient compression** on the wire (``comm_dtype=torch.bfloat16``).
+"""
+from __future__ import annotations
+
+import contextlib
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..optim.flat import flatten_module
+
+
+def _is_nccl(pg):
+    try:
+        return dist.get_backend(pg) == "nccl"
+    except Exception:
+        return False
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
+                 first_bucket_cap_mb: float = 1.0, broadcast_buffers: bool = False, comm_dtype=None,
+                 average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.flat = flatten_module(module)
+        self.broadcast_buffers = broadcast_buffers
+        self.comm_dtype = comm_dtype
+        self.average = average
+        self.straggler_mode = straggler_mode
+        self.tracer = tracer
+        self.nccl = _is_nccl(process_group)
+        self._sync = True
+        self.alive = True
+        self.grad_scale_dev = None
+        self._buffers_list = [b for b in module.buffers() if b is not None and b.numel() > 0]
+        self._broadcast_init()
+        self._build_buckets(bucket_cap_mb, first_bucket_cap_mb)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.flat.params]
+        self._reset()
+        self.step_comm_log = []
+
+    # ------------------------------------------------------------------ init broadcast (C-13)
+    @torch.no_grad()
+    def _broadcast_init(self):
+        if self.world == 1:
+            return
+        dist.broadcast(self.flat.data, 0, group=self.pg)
+        self._broadcast_buffers()
+        self.flat.refresh_shadow()
+
+    @torch.no_grad()
+    def _broadcast_buffers(self):
+        if self.world == 1 or not self._buffers_list:
+            return
+        by_dtype = {}
+        for b in self._buffers_list:
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for dt, bufs in by_dtype.items():
+            flat = torch.cat([b.reshape(-1) for b in bufs])
+            dist.broadcast(flat, 0, group=self.pg)
+            o = 0
+            for b in bufs:
+                n = b.numel()
+                b.copy_(flat[o:o + n].view_as(b))
+                o += n
+
+    # ------------------------------------------------------------------ buckets
+    def _build_buckets(self, cap_mb, first_mb):
+        fp = self.flat
+        n = len(fp.params)
+        ends = fp.offsets[1:] + [fp.numel]
+        buckets, cur, cur_bytes = [], [], 0
+        cap = first_mb * 2 ** 20
+        for i in reversed(range(n)):
+            nb = (ends[i] - fp.offsets[i]) * 4
+            if cur and cur_bytes + nb > cap:          # close the bucket before it would overflow
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+                cap = cap_mb * 2 ** 20
+            cur.append(i)
+            cur_bytes += nb
+        if cur:
+            buckets.append(cur)
+        self.buckets = []
+        self._pbucket = {}
+        for bi, idxs in enumerate(buckets):
+            lo, hi = min(idxs), max(idxs)
+            self.buckets.append((fp.offsets[lo], ends[hi], len(idxs)))
+            for i in idxs:
+                self._pbucket[id(fp.params[i])] = bi
+        if self.comm_dtype is not None:
+            self._wire = [torch.empty(e - s, dtype=self.comm_dtype, device=fp.grad.device) for s, e, _ in self.buckets]
+
+    def bucket_sizes_mb(self):
+        return [(e - s) * 4 / 2 ** 20 for s, e, _ in self.buckets]
+
+    # ------------------------------------------------------------------ per-backward state
+    def _reset(self):
+        self._ready = [0] * len(self.buckets)
+        self._next = 0
+        self._works = []
+        self._armed = False
+
+    def _on_grad(self, p):
+        if not self._sync or self.world == 1:
+            return
+        if not self._armed:
+            self._armed = True
+            self._t0 = time.perf_counter()
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+            if self.straggler_mode:
+                self._launch_alive()
+        b = self._pbucket[id(p)]
+        self._ready[b] += 1
+        while self._next < len(self.buckets) and self._ready[self._next] == self.buckets[self._next][2]:
+            self._launch(self._next)
+            self._next += 1
+
+    def _op(self):
+        if self.straggler_mode or not self.average:
+            return dist.ReduceOp.SUM
+        return dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
+
+    def _launch_alive(self):
+        dev = self.flat.grad.device
+        self._alive_t = torch.full((1,), 1.0 if self.alive else 0.0, device=dev)
+        self._works.append((-1, dist.all_reduce(self._alive_t, op=dist.ReduceOp.SUM, group=self.pg,
+                                                async_op=True)))
+
+    def _launch(self, b):
+        s, e, _ = self.buckets[b]
+        view = self.flat.grad[s:e]
+        if self.straggler_mode and not self.alive:
+            view.zero_()                       # zero contribution: collective stays matched
+        t = view
+        if self.comm_dtype is not None:
+            t = self._wire[b]
+            scale = 1.0 / self.world if (self.average and not self.straggler_mode) else 1.0
+            if view.is_cuda:
+                from ..ops import kernels as K
+                K.cast_f32_bf16(view, t, scale) if t.dtype == torch.bfloat16 else t.copy_(view * scale)
+            else:
+                t.copy_(view * scale)
+            op = dist.ReduceOp.SUM
+        else:
+            op = self._op()
+        if self.tracer is not None:
+            self.tracer.instant(f"allreduce_bucket{b}", args={"mb": (e - s) * 4 / 2 ** 20})
+        self._works.append((b, dist.all_reduce(t, op=op, group=self.pg, async_op=True)))
+
+    def _finish(self):
+        while self._next < len(self.buckets):      # buckets holding unused parameters
+            self._launch(self._next)
+            self._next += 1
+        for b, w in self._works:
+            w.wait()
+        fp = self.flat
+        if self.comm_dtype is not None:
+            for b, (s, e, _) in enumerate(self.buckets):
+                fp.grad[s:e].copy_(self._wire[b])
+        elif self.average and not self.straggler_mode and not self.nccl:
+            fp.grad.mul_(1.0 / self.world)
+        if self.straggler_mode:
+            # 1 / max(alive, 1) as a device scalar, consumed by the fused optimizer without a host sync
+            self.grad_scale_dev = torch.reciprocal(self._alive_t.clamp_min(1.0))
+            for opt in getattr(self, "_optimizers", []):
+                opt.grad_scale_dev = self.grad_scale_dev
+        self.step_comm_log.append(time.perf_counter() - self._t0)
+        self._reset()
+
+    # ------------------------------------------------------------------ public API
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.world > 1 and self.module.training:
+            self._broadcast_buffers()
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = old
+
+    def set_alive(self, alive: bool):
+        """Straggler mode: this rank's gradient contributes (True) or is dropped this step (False)."""
+        self.alive = bool(alive)
+
+    def attach_optimizer(self, opt):
+        """Let the fused optimizer consume the device-side 1/alive scale in straggler mode."""
+        self._optimizers = getattr(self, "_optimizers", []) + [opt]
+        return opt
+
+    def zero_grad(self):
+        self.flat.zero_grad()
+
+    def state_dict(self, *a, **kw):   # "module."-prefixed keys like torch DDP (data_parallel_dist.py:38)
+        return super().state_dict(*a, **kw)

@@ -1,0 +1,79 @@
+"""Helpers to run a function in `world` CPU processes over gloo (the modern "mpirun -n N on one host",
+SURVEY.md §4)."""
+import os
+import socket
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _to_np(obj):
+    import torch
+    if isinstance(obj, torch.Tensor):
+        return ("__tensor__", obj.detach().cpu().numpy().copy())
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_np(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _to_np(v) for k, v in obj.items()}
+    return obj
+
+
+def _from_np(obj):
+    import torch
+    if isinstance(obj, tuple) and len(obj) == 2 and obj[0] == "__tensor__":
+        return torch.from_numpy(obj[1])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_from_np(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _from_np(v) for k, v in obj.items()}
+    return obj
+
+
+def _entry(rank, world, port, fn, args, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import torch
+        torch.set_num_threads(1)
+        from pytorch_distributed_nn_amd.parallel import runtime
+        runtime.init_process_group(backend="gloo", device="cpu")
+        res = fn(rank, world, *args)
+        q.put((rank, "ok", _to_np(res)))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        try:
+            from pytorch_distributed_nn_amd.parallel import runtime
+            runtime.destroy()
+        except Exception:
+            pass
+
+
+def run_world(fn, world=2, args=(), timeout=180):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, status, res = q.get(timeout=timeout)
+            if status != "ok":
+                raise AssertionError(f"rank {rank} failed:\n{res}")
+            out[rank] = _from_np(res)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return [out[r] for r in range(world)]

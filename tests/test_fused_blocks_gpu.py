@@ -1,0 +1,82 @@
+"""Each fused ResNet block (one autograd node = a hand-scheduled HIP kernel sequence) against the CPU
+fp32 reference forward/backward of the same nn.Module: output, input gradient, every parameter gradient
+and the BN running statistics.  Shapes keep >= 256 elements per BN channel so batch statistics are
+well conditioned and the comparison measures kernel numerics, not bf16 noise amplified by tiny batches."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _check_block(block, x_nchw, tol_out=3e-2, tol_grad=6e-2):
+    ref = block
+    gpu = copy.deepcopy(block).cuda()
+    xr = x_nchw.clone().requires_grad_(True)
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xg = x_nchw.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16).requires_grad_(True)
+    yg = gpu.forward_nhwc(xg)
+    yg.backward(g.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16))
+    assert rel(yg, yr.permute(0, 2, 3, 1)) < tol_out
+    assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < tol_grad
+    for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
+        assert rel(pg.grad, pr.grad) < tol_grad, (n, rel(pg.grad, pr.grad))
+    for (n, br), (_, bg) in zip(ref.named_buffers(), gpu.named_buffers()):
+        if br.dtype.is_floating_point:
+            assert rel(bg, br) < 2e-2, n
+
+
+@pytest.mark.parametrize("inp,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2), (128, 64, 2)])
+def test_bottleneck(inp, planes, stride):
+    from pytorch_distributed_nn_amd.models.resnet import Bottleneck
+    torch.manual_seed(0)
+    blk = Bottleneck(inp, planes, stride, "downsample")
+    _check_block(blk, torch.randn(4, inp, 16, 16))
+
+
+@pytest.mark.parametrize("inp,planes,stride", [(64, 64, 1), (64, 128, 2)])
+def test_basic_block(inp, planes, stride):
+    from pytorch_distributed_nn_amd.models.resnet import BasicBlock
+    torch.manual_seed(0)
+    blk = BasicBlock(inp, planes, stride, "shortcut")
+    _check_block(blk, torch.randn(4, inp, 16, 16))
+
+
+@pytest.mark.parametrize("imagenet", [True, False])
+def test_stem(imagenet):
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.ops.fused_resnet import StemFn, stem_shadow
+    torch.manual_seed(0)
+    k, st, pad = (7, 2, 3) if imagenet else (3, 1, 1)
+    conv = nn.Conv2d(3, 64, k, st, pad, bias=False)
+    bn = nn.BatchNorm2d(64)
+    x = torch.randn(4, 3, 32, 32)
+    y = F.relu(bn(conv(x)))
+    if imagenet:
+        y = F.max_pool2d(y, 3, 2, 1)
+    g = torch.randn_like(y)
+    y.backward(g)
+    conv_g, bn_g = copy.deepcopy(conv).cuda(), copy.deepcopy(bn).cuda()
+    conv_g.weight.grad = None
+    bn_g.weight.grad = bn_g.bias.grad = None
+    xin = OF.nchw_to_nhwc_input(x.cuda())
+    assert xin.shape == (4, 32, 32, 8)
+    assert rel(xin[..., :3], x.permute(0, 2, 3, 1)) < 1e-2 and xin[..., 3:].abs().max() == 0
+    yg = StemFn.apply(xin, (st, pad, imagenet, True, 0.1, 1e-5), [bn_g.running_mean, bn_g.running_var],
+                      [stem_shadow(conv_g.weight, 8)], conv_g.weight, bn_g.weight, bn_g.bias)
+    yg.backward(g.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16))
+    assert rel(yg, y.permute(0, 2, 3, 1)) < 3e-2
+    assert rel(conv_g.weight.grad, conv.weight.grad) < 6e-2
+    assert rel(bn_g.weight.grad, bn.weight.grad) < 6e-2
+    assert rel(bn_g.bias.grad, bn.bias.grad) < 6e-2
+    assert rel(bn_g.running_var, bn.running_var) < 2e-2

@@ -61,6 +61,8 @@ CONV_SHAPES = [
     (2, 32, 32, 8, 64, 7, 2, 3),
     (3, 7, 7, 512, 2048, 1, 1, 0),
     (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 15, 15, 64, 64, 3, 2, 1),
+    (2, 15, 15, 64, 128, 1, 2, 0),
 ]
 
 

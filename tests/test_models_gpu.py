@@ -1,0 +1,74 @@
+"""End-to-end numerics of the fused GPU model paths against the CPU fp32 reference forward/backward of
+the SAME module (identical weights): logits, loss, every parameter gradient, BN running statistics."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _run(model, x, y):
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    model.zero_grad(set_to_none=True)
+    out = model(x)
+    loss = OF.cross_entropy(out, y)
+    loss.backward()
+    return out, loss
+
+
+@pytest.mark.parametrize("name,shape,nc", [
+    ("resnet50", (8, 3, 128, 128), 1000),
+    ("ResNet18", (8, 3, 32, 32), 10),
+    ("ResNet50", (8, 3, 32, 32), 10),
+    ("LeNet", (8, 1, 28, 28), 10),
+    ("mlp_cpp", (16, 784), 10),
+])
+def test_model_matches_cpu_reference(name, shape, nc):
+    from pytorch_distributed_nn_amd.models import build_model
+    torch.manual_seed(0)
+    ref = build_model(name, nc)
+    gpu = copy.deepcopy(ref).cuda()
+    x = torch.randn(*shape)
+    y = torch.randint(0, nc, (shape[0],))
+    out_r, loss_r = _run(ref, x, y)
+    out_g, loss_g = _run(gpu, x.cuda(), y.cuda())
+    # deep bf16 networks: compare with a magnitude-relative bound and direction (cosine) of every grad
+    assert rel(out_g, out_r) < 1e-1, (name, rel(out_g, out_r))
+    assert abs(loss_g.item() - loss_r.item()) < 3e-2 * max(1.0, abs(loss_r.item()))
+    for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
+        assert pg.grad is not None, n
+        cos = torch.nn.functional.cosine_similarity(pg.grad.float().cpu().flatten(), pr.grad.flatten(), dim=0)
+        assert cos > 0.97, (name, n, float(cos), rel(pg.grad, pr.grad))
+    for (n, br), (_, bg) in zip(ref.named_buffers(), gpu.named_buffers()):
+        if br.dtype.is_floating_point:
+            assert rel(bg, br) < 3e-2, (name, n)
+        else:
+            assert torch.equal(bg.cpu(), br), (name, n)
+
+
+def test_resnet50_train_step_flat_sgd():
+    """A few fused-SGD steps on the flat arena reduce the loss on a fixed batch (memorisation)."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.optim import SGD, flatten_module
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    torch.manual_seed(0)
+    m = build_model("resnet50").cuda()
+    flatten_module(m)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9)
+    x = torch.randn(16, 3, 64, 64, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 1000, (16,), device="cuda")
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        loss = OF.cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(l == l for l in losses)
+    assert losses[-1] < losses[0], losses
