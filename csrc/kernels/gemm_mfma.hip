@@ -279,6 +279,7 @@ struct MLoader {
     // im2col: the column's (r, s, c) is fixed per block
     int cr, cs, cc;
     int kbase;
+    float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];   // fused-prologue coefficients of this thread's 8 channels
 
     __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld_, int cols_total,
                                          int col0, int tid) {
@@ -296,6 +297,10 @@ struct MLoader {
             cc = cl - rs * g.C;
             cr = fdiv(rs, g.dS);
             cs = rs - cr * g.S;
+            if constexpr (PRO) {   // the column (hence the channel) is fixed for the whole K loop
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { psc[j] = a.pro_scale[cc + j]; psh[j] = a.pro_shift[cc + j]; }
+            }
         }
     }
     __device__ __forceinline__ void seek(const GemmArgs&, int k) { kbase = k; }
@@ -327,7 +332,10 @@ struct MLoader {
                 const bool vv = v && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
                 u16x8_t x = vv ? ldg16(ptr + (((long)n * g.H + hi) * g.W + wi) * g.C + cc) : zero8();
                 if constexpr (PRO) {
-                    if (vv) x = affine_relu8(x, a.pro_scale + cc, a.pro_shift + cc);
+                    if (vv) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) x[j] = f2bf(fmaxf(fmaf(bf2f(x[j]), psc[j], psh[j]), 0.f));
+                    }
                 }
                 reg[i] = x;
             }
@@ -346,17 +354,20 @@ template <bool PRO> struct ASel<A_KMAJOR, PRO> { using T = KLoader<128, 0, false
 template <bool PRO> struct ASel<A_CONV, PRO> { using T = KLoader<128, 1, PRO>; static constexpr bool K = true; };
 template <bool PRO> struct ASel<A_CONVT, PRO> { using T = KLoader<128, 2, false>; static constexpr bool K = true; };
 template <bool PRO> struct ASel<A_MNMAJOR, PRO> { using T = MLoader<128, 0, false>; static constexpr bool K = false; };
-template <int BM_, bool PRO> struct BSel;
-template <bool PRO> struct BSel<B_KMAJOR, PRO> { using T = KLoader<128, 0, false>; static constexpr bool K = true; };
-template <bool PRO> struct BSel<B_MNMAJOR, PRO> { using T = MLoader<128, 0, false>; static constexpr bool K = false; };
-template <bool PRO> struct BSel<B_WT, PRO> { using T = MLoader<128, 1, false>; static constexpr bool K = false; };
-template <bool PRO> struct BSel<B_IM2COL, PRO> { using T = MLoader<128, 2, PRO>; static constexpr bool K = false; };
+template <int BMODE, bool PRO, int W> struct BSel;
+template <bool PRO, int W> struct BSel<B_KMAJOR, PRO, W> { using T = KLoader<W, 0, false>; static constexpr bool K = true; };
+template <bool PRO, int W> struct BSel<B_MNMAJOR, PRO, W> { using T = MLoader<W, 0, false>; static constexpr bool K = false; };
+template <bool PRO, int W> struct BSel<B_WT, PRO, W> { using T = MLoader<W, 1, false>; static constexpr bool K = false; };
+template <bool PRO, int W> struct BSel<B_IM2COL, PRO, W> { using T = MLoader<W, 2, PRO>; static constexpr bool K = false; };
 
-constexpr int BMt = 128, BNt = 128;
-constexpr int TILE_ELEMS = 128 * BK;                 // bf16 elements per operand image
-constexpr int CPAD = 4;                              // fp32 C-stage row padding
-constexpr int SMEM_BYTES = (BMt * (BNt + CPAD) * 4) > (4 * TILE_ELEMS * 2) ? (BMt * (BNt + CPAD) * 4)
-                                                                           : (4 * TILE_ELEMS * 2);
+constexpr int BMt = 128;
+constexpr int CPAD = 4;                              // fp32 C-stage row padding (atomic epilogue only)
+template <int BNW, int EM>
+constexpr int smem_bytes() {
+    const int ops = 2 * (BMt + BNW) * BK * 2;        // double-buffered A and B images
+    const int cst = EM == E_ATOMIC ? BMt * (BNW + CPAD) * 4 : 0;
+    return ops > cst ? ops : cst;
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     // Bijective: blocks b, b+8, b+16... (same XCD under round-robin dispatch) get consecutive tiles.
@@ -364,19 +375,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-template <int AM, int BMODE, int EM, bool PRO_A, bool PRO_B>
+// BNW = block tile width (128, or 64 for the N <= 64 layers so no half-empty tiles are computed).
+template <int AM, int BMODE, int EM, bool PRO_A, bool PRO_B, int BNW>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
+    constexpr int WTN = BNW / 2, FN = WTN / 16;      // wave tile 64 x WTN, FN column fragments
+    constexpr int BUF = (BMt + BNW) * BK;            // bf16 elements per (A|B) buffer
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* const sbase = reinterpret_cast<bf16_t*>(smem);   // [buf][A|B][128*64]
+    bf16_t* const sbase = reinterpret_cast<bf16_t*>(smem);   // [buf][A 128x64 | B BNWx64]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int tiles_m = (a.M + BMt - 1) / BMt, tiles_n = (a.N + BNt - 1) / BNt;
+    const int tiles_m = (a.M + BMt - 1) / BMt, tiles_n = (a.N + BNW - 1) / BNW;
     const int nwg = tiles_m * tiles_n;
     const int t = xcd_remap(blockIdx.x, nwg);
     // N fastest: consecutive tiles of one XCD share the same A rows (activations, the big operand).
     const int tm = t / tiles_n, tn = t % tiles_n;
-    const int m0 = tm * BMt, n0 = tn * BNt;
+    const int m0 = tm * BMt, n0 = tn * BNW;
 
     const int ktiles = (a.K + BK - 1) / BK;
     const int kt0 = blockIdx.z * a.ktiles_per_split;
@@ -384,9 +398,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     if (kt0 >= kt1) return;
 
     using LA = typename ASel<AM, PRO_A>::T;
-    using LB = typename BSel<BMODE, PRO_B>::T;
+    using LB = typename BSel<BMODE, PRO_B, BNW>::T;
     constexpr bool AK = ASel<AM, PRO_A>::K;
-    constexpr bool BKm = BSel<BMODE, PRO_B>::K;
+    constexpr bool BKm = BSel<BMODE, PRO_B, BNW>::K;
     LA la;
     LB lb;
     la.init(a, a.A, a.lda, a.M, m0, tid);
@@ -394,49 +408,52 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     if (kt0) { la.seek(a, kt0 * BK); lb.seek(a, kt0 * BK); }
 
     u16x8_t ra[LA::NCH], rb[LB::NCH];
-    f32x4_t acc[4][4];
+    f32x4_t acc[4][FN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     la.load(a, a.K, ra);
     lb.load(a, a.K, rb);
     la.store(sbase, ra, tid);
-    lb.store(sbase + TILE_ELEMS, rb, tid);
+    lb.store(sbase + BMt * BK, rb, tid);
     __syncthreads();
 
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (more) {
+        if (more) {   // issue the next tile's global loads before this tile's MFMAs (T14)
             la.advance(a);
             lb.advance(a);
             la.load(a, a.K, ra);
             lb.load(a, a.K, rb);
         }
-        const bf16_t* A_ = sbase + cur * 2 * TILE_ELEMS;
-        const bf16_t* B_ = A_ + TILE_ELEMS;
+        const bf16_t* A_ = sbase + cur * BUF;
+        const bf16_t* B_ = A_ + BMt * BK;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            bf16x8_t af[4], bfr[4];
+            bf16x8_t af[4], bfr[FN];
 #pragma unroll
             for (int f = 0; f < 4; ++f) {
                 if constexpr (AK) af[f] = frag_kmajor(A_, wm * 64 + f * 16 + (lane & 15), ks, lane);
                 else af[f] = frag_mnmajor<128>(A_, wm * 64 + f * 16, ks, lane);
-                if constexpr (BKm) bfr[f] = frag_kmajor(B_, wn * 64 + f * 16 + (lane & 15), ks, lane);
-                else bfr[f] = frag_mnmajor<128>(B_, wn * 64 + f * 16, ks, lane);
+            }
+#pragma unroll
+            for (int f = 0; f < FN; ++f) {
+                if constexpr (BKm) bfr[f] = frag_kmajor(B_, wn * WTN + f * 16 + (lane & 15), ks, lane);
+                else bfr[f] = frag_mnmajor<BNW>(B_, wn * WTN + f * 16, ks, lane);
             }
 #pragma unroll
             for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < 4; ++fn)
+                for (int fn = 0; fn < FN; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
         }
-        if (more) {
-            bf16_t* nA = sbase + (cur ^ 1) * 2 * TILE_ELEMS;
+        if (more) {   // write the next tile after the MFMAs, then one barrier
+            bf16_t* nA = sbase + (cur ^ 1) * BUF;
             la.store(nA, ra, tid);
-            lb.store(nA + TILE_ELEMS, rb, tid);
+            lb.store(nA + BMt * BK, rb, tid);
         }
         __syncthreads();
         cur ^= 1;
@@ -444,15 +461,36 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
     // ---------------- epilogue ----------------
     // lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + j] in acc[fm][fn][j]
-    float* cs = reinterpret_cast<float*>(smem);
-    constexpr int LDC_S = BNt + CPAD;
     const int lm = lane & 15, lg = lane >> 4;
 
-    if constexpr (EM == E_BF16) {
-        if (a.stats) {
+    if constexpr (EM == E_ATOMIC) {
+        // stage the fp32 tile through LDS so every atomic wave-instruction covers 256 contiguous bytes
+        float* cs = reinterpret_cast<float*>(smem);
+        constexpr int LDC_S = BNW + CPAD;
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+                *reinterpret_cast<f32x4_t*>(cs + (wm * 64 + fm * 16 + lm) * LDC_S + wn * WTN + fn * 16 + 4 * lg) =
+                    acc[fm][fn];
+        __syncthreads();
+        float* C = reinterpret_cast<float*>(a.C);
+        for (int r = wave; r < BMt; r += 4) {
+            const int m = m0 + r;
+            if (m >= a.M) break;
+#pragma unroll
+            for (int h = 0; h < BNW / 64; ++h) {
+                const int c = lane + 64 * h;
+                const int n = n0 + c;
+                if (n < a.N) atomicAdd(C + (long)m * a.ldc + n, a.alpha * cs[r * LDC_S + c]);
+            }
+        }
+        return;
+    } else {
+        if (EM == E_BF16 && a.stats) {
             // per-column partial sums over this wave's 64 rows (masked rows excluded)
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn) {
+            for (int fn = 0; fn < FN; ++fn) {
                 float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm) {
@@ -475,7 +513,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                         q[j] += __shfl_xor(q[j], o, 64);
                     }
                 }
-                const int n = n0 + wn * 64 + fn * 16 + 4 * lg;
+                const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
                 if (lm == 0 && n < a.N) {
                     const long row = (long)(tm * 2 + wm) * 2;
                     float* ps = a.stats + row * a.N + n;
@@ -487,50 +525,12 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 }
             }
         }
-    }
-    __syncthreads();   // done with the operand images; reuse LDS as the fp32 C stage
+        // direct register -> global stores: each lane writes 4 consecutive columns of one row; a wave's
+        // fragment covers 16 rows x 16 columns and the fn loop completes 2*WTN-byte row segments in L2.
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-            const int r = wm * 64 + fm * 16 + lm;
-            const int c = wn * 64 + fn * 16 + 4 * lg;
-            *reinterpret_cast<f32x4_t*>(cs + r * LDC_S + c) = acc[fm][fn];
-        }
-    __syncthreads();
-
-    if constexpr (EM == E_ATOMIC) {
-        // 256 threads: each wave sweeps rows; 64 lanes x 2 columns -> 128 contiguous fp32 per row
-        float* C = reinterpret_cast<float*>(a.C);
-        for (int r = wave; r < BMt; r += 4) {
-            const int m = m0 + r;
-            if (m >= a.M) break;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = lane + 64 * h;
-                const int n = n0 + c;
-                if (n < a.N) atomicAdd(C + (long)m * a.ldc + n, a.alpha * cs[r * LDC_S + c]);
-            }
-        }
-    } else {
-        // each thread writes 8 consecutive columns of a row: 16 threads per 128-column row
-        const int cgrp = tid & 15;
-        for (int r = tid >> 4; r < BMt; r += NT / 16) {
-            const int m = m0 + r;
-            if (m >= a.M) break;
-            const int n = n0 + cgrp * 8;
-            if (n >= a.N) continue;
-            float v[8];
-            const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(cs + r * LDC_S + cgrp * 8);
-            const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(cs + r * LDC_S + cgrp * 8 + 4);
-            v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
-            v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                v[j] *= a.alpha;
-                if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
-                if (a.relu) v[j] = fmaxf(v[j], 0.f);
-            }
+        for (int fm = 0; fm < 4; ++fm) {
+            const int m = m0 + wm * 64 + fm * 16 + lm;
+            if (m >= a.M) continue;
             long orow = m;
             if (a.scatter) {
                 const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
@@ -539,20 +539,32 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 const uint32_t wc = rem - hc * a.g.dW.d;
                 orow = ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
             }
-            if constexpr (EM == E_BF16) {
-                bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc + n;
-                if (n + 8 <= a.N) {
-                    *reinterpret_cast<u16x8_t*>(C) = pack8(v);
-                } else {
-                    for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = f2bf(v[j]);
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
+                if (n >= a.N) continue;
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[j] = acc[fm][fn][j] * a.alpha;
+                    if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
+                    if (a.relu) v[j] = fmaxf(v[j], 0.f);
                 }
-            } else {
-                float* C = reinterpret_cast<float*>(a.C) + orow * a.ldc + n;
-                if (n + 8 <= a.N) {
-                    *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
-                    *reinterpret_cast<float4*>(C + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                if constexpr (EM == E_BF16) {
+                    bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc + n;
+                    if (n + 4 <= a.N) {
+                        u16x4_t o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                        *reinterpret_cast<u16x4_t*>(C) = o;
+                    } else {
+                        for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = f2bf(v[j]);
+                    }
                 } else {
-                    for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = v[j];
+                    float* C = reinterpret_cast<float*>(a.C) + orow * a.ldc + n;
+                    if (n + 4 <= a.N && (a.ldc & 3) == 0) {
+                        *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = v[j];
+                    }
                 }
             }
         }
@@ -569,13 +581,30 @@ FastDiv make_fdiv(uint32_t d) {
     return f;
 }
 
-template <int AM, int BMODE, int EM, bool PA, bool PB>
-int launch(const GemmArgs& a, int splits, hipStream_t st) {
-    const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNt));
+template <int AM, int BMODE, int EM, bool PA, bool PB, int BNW>
+int launch_w(const GemmArgs& a, int splits, hipStream_t st) {
+    static bool attr = false;
+    constexpr int SM = smem_bytes<BNW, EM>();
+    if (!attr) {
+        attr = true;
+        (void)hipFuncSetAttribute((const void*)gemm_kernel<AM, BMODE, EM, PA, PB, BNW>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, SM);
+    }
+    const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW));
     dim3 grid(tiles, 1, splits);
-    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB>), grid, dim3(NT), SMEM_BYTES, st, a);
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), SM, st, a);
     PDNN_LAUNCH_RET;
 }
+
+// N <= 64: a 128x64 block tile; otherwise 128x128.
+template <int AM, int BMODE, int EM, bool PA, bool PB>
+int launch(const GemmArgs& a, int splits, hipStream_t st) {
+    if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st);
+    return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st);
+}
+
+template <int BNW>
+int tiles_of(const GemmArgs& a) { return (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW)); }
 
 int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
     // enough workgroups to cover 256 CUs twice, but keep >= 4 K-steps per split
@@ -596,26 +625,7 @@ void fill_geom(ConvGeom& g, int Nimg, int H, int W, int C, int Ho, int Wo, int R
 
 }  // namespace
 
-static bool g_attr_done = false;
-template <int AM, int BMODE, int EM, bool PA, bool PB>
-static void set_attr() {
-    (void)hipFuncSetAttribute((const void*)gemm_kernel<AM, BMODE, EM, PA, PB>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
-}
-static void ensure_attrs() {
-    if (g_attr_done) return;
-    g_attr_done = true;
-    set_attr<A_KMAJOR, B_KMAJOR, E_BF16, false, false>();
-    set_attr<A_KMAJOR, B_KMAJOR, E_F32, false, false>();
-    set_attr<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>();
-    set_attr<A_KMAJOR, B_MNMAJOR, E_F32, false, false>();
-    set_attr<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false>();
-    set_attr<A_CONV, B_KMAJOR, E_BF16, false, false>();
-    set_attr<A_CONV, B_KMAJOR, E_BF16, true, false>();
-    set_attr<A_CONVT, B_WT, E_BF16, false, false>();
-    set_attr<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>();
-    set_attr<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>();
-}
+static void ensure_attrs() {}
 
 // ------------------------------------------------------------------------------------------------
 // C API
@@ -652,7 +662,7 @@ PDNN_API int pdnn_gemm_tn_acc(const bf16_t* X, long ldx, const bf16_t* Y, long l
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = Y; a.ldb = ldy; a.C = C; a.ldc = ldc;
     a.alpha = alpha;
-    const int ktiles = (int)cdiv(K, BK), tiles = (int)(cdiv(M, BMt) * cdiv(N, BNt));
+    const int ktiles = (int)cdiv(K, BK), tiles = N <= 64 ? tiles_of<64>(a) : tiles_of<128>(a);
     const int splits = pick_splits(a, ktiles, tiles, 256);
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
     return launch<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false>(a, (int)cdiv(ktiles, a.ktiles_per_split), st);
@@ -727,7 +737,7 @@ PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int N
     fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift;
-    const int ktiles = (int)cdiv(a.K, BK), tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNt));
+    const int ktiles = (int)cdiv(a.K, BK), tiles = a.N <= 64 ? tiles_of<64>(a) : tiles_of<128>(a);
     const int splits = pick_splits(a, ktiles, tiles, 1024);
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
     const int nz = (int)cdiv(ktiles, a.ktiles_per_split);

@@ -180,7 +180,7 @@ class _Linear(torch.autograd.Function):
             K.gemm_tn_acc(gy, x2, dw)
             dw = dw[: wshape[0], : wshape[1]]
         if has_bias and ctx.needs_input_grad[2]:
-            db = K.colsum(gy)[: wshape[0]]
+            db = K.colsum(gy)              # shape of the (possibly padded) bias input
         return dx, dw, db, None, None
 
 

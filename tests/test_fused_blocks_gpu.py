@@ -11,11 +11,17 @@ pytestmark = pytest.mark.gpu
 
 
 def rel(a, b):
-    a, b = a.float().cpu(), b.float().cpu()
-    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+    """relative L2 error.  Max-abs is the wrong metric through ReLU masks / max-pool argmax: a bf16 value
+    rounding across 0 (or a tie) legitimately reroutes an O(1) gradient element."""
+    a, b = a.float().cpu().flatten(), b.float().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-def _check_block(block, x_nchw, tol_out=3e-2, tol_grad=6e-2):
+def cos(a, b):
+    return torch.nn.functional.cosine_similarity(a.float().cpu().flatten(), b.float().cpu().flatten(), dim=0).item()
+
+
+def _check_block(block, x_nchw, tol_out=2e-2, tol_grad=6e-2):
     ref = block
     gpu = copy.deepcopy(block).cuda()
     xr = x_nchw.clone().requires_grad_(True)
@@ -27,8 +33,10 @@ def _check_block(block, x_nchw, tol_out=3e-2, tol_grad=6e-2):
     yg.backward(g.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16))
     assert rel(yg, yr.permute(0, 2, 3, 1)) < tol_out
     assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < tol_grad
+    assert cos(xg.grad, xr.grad.permute(0, 2, 3, 1)) > 0.995
     for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
         assert rel(pg.grad, pr.grad) < tol_grad, (n, rel(pg.grad, pr.grad))
+        assert cos(pg.grad, pr.grad) > 0.995, (n, cos(pg.grad, pr.grad))
     for (n, br), (_, bg) in zip(ref.named_buffers(), gpu.named_buffers()):
         if br.dtype.is_floating_point:
             assert rel(bg, br) < 2e-2, n

@@ -9,8 +9,9 @@ pytestmark = pytest.mark.gpu
 
 
 def rel(a, b):
-    a, b = a.float().cpu(), b.float().cpu()
-    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+    """relative L2 error (see test_fused_blocks_gpu.rel for why not max-abs)."""
+    a, b = a.float().cpu().flatten(), b.float().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
 def _run(model, x, y):
@@ -39,12 +40,12 @@ def test_model_matches_cpu_reference(name, shape, nc):
     out_r, loss_r = _run(ref, x, y)
     out_g, loss_g = _run(gpu, x.cuda(), y.cuda())
     # deep bf16 networks: compare with a magnitude-relative bound and direction (cosine) of every grad
-    assert rel(out_g, out_r) < 1e-1, (name, rel(out_g, out_r))
+    assert rel(out_g, out_r) < 5e-2, (name, rel(out_g, out_r))
     assert abs(loss_g.item() - loss_r.item()) < 3e-2 * max(1.0, abs(loss_r.item()))
     for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
         assert pg.grad is not None, n
         cos = torch.nn.functional.cosine_similarity(pg.grad.float().cpu().flatten(), pr.grad.flatten(), dim=0)
-        assert cos > 0.97, (name, n, float(cos), rel(pg.grad, pr.grad))
+        assert cos > 0.98, (name, n, float(cos), rel(pg.grad, pr.grad))
     for (n, br), (_, bg) in zip(ref.named_buffers(), gpu.named_buffers()):
         if br.dtype.is_floating_point:
             assert rel(bg, br) < 3e-2, (name, n)

@@ -1,0 +1,69 @@
+"""Parameter-server mode on CPU/gloo (PAR-DP-PS / PAR-DP-KILL / PAR-DP-BACKUP; SURVEY.md §5.3 fault
+injection: sleep-based stragglers as in pure_py_code/distributed_worker.py:131-132)."""
+import os
+import tempfile
+
+import pytest
+import torch
+
+from dist_utils import run_world
+
+
+def _data(seed=0, n=512):
+    g = torch.Generator().manual_seed(seed)
+    centers = torch.randn(10, 784, generator=g) * 2
+    y = torch.randint(0, 10, (n,), generator=g)
+    x = centers[y] + 0.5 * torch.randn(n, 784, generator=g)
+    return x, y
+
+
+def _ps_job(rank, world, comm_type, k, straggler, out_dir, steps):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    model = build_model("mlp2", 10)
+    x, y = _data()
+    cfg = PSConfig(comm_type=comm_type, num_aggregate=k, evaluator=True, eval_interval=5, lr=0.05, momentum=0.5,
+                   max_steps=steps, out_dir=out_dir, inject_straggler=straggler)
+
+    def batches():
+        i = 0
+        while True:
+            sl = slice((i * 32) % 512, (i * 32) % 512 + 32)
+            yield x[sl], y[sl]
+            i += 1
+
+    def evaluate(m):
+        with torch.no_grad():
+            out = m(x)
+            return float(OF.cross_entropy(out, y)), float((out.argmax(1) != y).float().mean())
+
+    res = run_ps(model, cfg, torch.device("cpu"), loss_fn=OF.cross_entropy, batches=batches(), eval_fn=evaluate)
+    # every rank ends with identical weights (final push)
+    w = torch.cat([p.detach().flatten() for p in model.parameters()])
+    return res, w
+
+
+@pytest.mark.parametrize("comm_type", ["Bcast", "Async"])
+def test_ps_full_sync_learns(comm_type):
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_job, 4, (comm_type, 0, {}, out, 20))
+    master_log, evaluator_rows = res[0][0], res[1][0]
+    assert all(r["count"] == 2 for r in master_log)                 # both workers every step
+    assert evaluator_rows[-1][2] < evaluator_rows[0][2]             # loss decreased
+    for r in res[1:]:
+        assert torch.equal(r[1], res[0][1])
+    assert any(f.startswith("time_loss_out_") for f in os.listdir(out))
+
+
+def test_ps_k_of_n_kill_with_straggler():
+    """k=1 of 2 workers, rank 3 sleeps 30 ms per layer: it is killed (aborts its backward) and the
+    master averages over the real count (1)."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_job, 4, ("Bcast", 1, {3: 30}, out, 8))
+    master_log = res[0][0]
+    aborted_rank3 = res[3][0]
+    assert all(r["count"] == 1 for r in master_log)
+    assert sum(2 in r["arrived"] for r in master_log) >= 6          # the fast worker wins most steps
+    assert aborted_rank3 >= 4                                       # straggler was short-circuited
