@@ -79,6 +79,11 @@ struct GemmArgs {
     float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
     int ktiles_per_split;     // split-K (grid.z)
     int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
+    int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
+    // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
+    const bf16_t* ep_res;
+    const bf16_t* ep_x;
+    const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -248,11 +253,25 @@ struct KLoader {
     __device__ __forceinline__ void advance(const GemmArgs& a) {
         kcur += BK;
         if constexpr (KIND == 1) {
-            c += BK;
-            while (c >= a.g.C) { c -= a.g.C; if (++s == a.g.S) { s = 0; ++r; } }
+            if (a.g.C >= BK) {          // C % 64 == 0: at most one wrap per K-step
+                c += BK;
+                if (c >= a.g.C) { c -= a.g.C; if (++s == a.g.S) { s = 0; ++r; } }
+            } else {                    // few channels (the 7x7 stem, C = 8): re-derive (r, s, c)
+                const uint32_t rs = fdiv((uint32_t)kcur, a.g.dC);
+                c = kcur - rs * a.g.C;
+                r = fdiv(rs, a.g.dS);
+                s = rs - r * a.g.S;
+            }
         } else if constexpr (KIND == 2) {
-            c += BK;
-            while (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.Sc) { s = 0; ++r; } }
+            if (a.g.Ko >= BK) {
+                c += BK;
+                if (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.Sc) { s = 0; ++r; } }
+            } else {
+                const uint32_t rs = fdiv((uint32_t)kcur, a.g.dKo);
+                c = kcur - rs * a.g.Ko;
+                r = fdiv(rs, a.g.dSc);
+                s = rs - r * a.g.Sc;
+            }
         }
     }
     __device__ __forceinline__ void store(bf16_t* img, const u16x8_t* reg, int tid) const {
@@ -487,24 +506,103 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         }
         return;
     } else {
-        if (EM == E_BF16 && a.stats) {
-            // per-column partial sums over this wave's 64 rows (masked rows excluded)
+        // One pass over the accumulators: alpha / bias / ReLU, optional residual add, then either
+        //  (fwd)  per-column BN partial statistics of the bf16-rounded output, or
+        //  (bwd)  BN-backward fusion: g -> gm = g * [t*mscale + mshift > 0] (the ReLU mask of the BN's
+        //         output, recomputed from the BN input t), store gm, and per-column partials of
+        //         sum(gm) and sum(gm * xhat), xhat = (t - mean) * invstd,
+        // and direct register -> global stores (each lane writes 4 consecutive columns of one row).
+        const bool bnb = a.ep_x != nullptr;
+        const bool want_stats = EM == E_BF16 && (a.stats != nullptr);
+        long orow[4];
+        bool mv[4];
 #pragma unroll
-            for (int fn = 0; fn < FN; ++fn) {
-                float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+        for (int fm = 0; fm < 4; ++fm) {
+            const int m = m0 + wm * 64 + fm * 16 + lm;
+            mv[fm] = m < a.M;
+            orow[fm] = m;
+            if (a.scatter && mv[fm]) {
+                const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
+                const uint32_t rem = (uint32_t)m - nn * a.g.dHW.d;
+                const uint32_t hc = fdiv(rem, a.g.dW);
+                const uint32_t wc = rem - hc * a.g.dW.d;
+                orow[fm] = ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
+            }
+        }
+        // issue every epilogue load first so they are all in flight together (the kernel runs at low
+        // occupancy; loads issued one fragment at a time would expose their full latency serially)
+        u16x4_t rv[4][FN], tv[4][FN];
+        if constexpr (EM == E_BF16) {
 #pragma unroll
-                for (int fm = 0; fm < 4; ++fm) {
-                    const int m = m0 + wm * 64 + fm * 16 + lm;
-                    if (m < a.M) {
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) {
+                    const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
+                    const bool ok = mv[fm] && n + 4 <= a.N;
+                    const long off = orow[fm] * a.ldc + n;
+                    rv[fm][fn] = (a.ep_res && ok) ? *reinterpret_cast<const u16x4_t*>(a.ep_res + off) : u16x4_t{0, 0, 0, 0};
+                    tv[fm][fn] = (bnb && ok) ? *reinterpret_cast<const u16x4_t*>(a.ep_x + off) : u16x4_t{0, 0, 0, 0};
+                }
+        }
+        uint32_t pk[4][FN][2];     // packed bf16 results (2 dwords = 4 columns per lane and fragment)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
+            const bool nv = n < a.N, n4 = n + 4 <= a.N;
+            float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+            float bmu[4], bis[4], bms[4], bmh[4];
+            if (bnb && n4) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bmu[j] = a.ep_mean[n + j]; bis[j] = a.ep_invstd[n + j];
+                    bms[j] = a.ep_mscale[n + j]; bmh[j] = a.ep_mshift[n + j];
+                }
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) {
+                const bool ok = mv[fm] && nv;
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[j] = acc[fm][fn][j] * a.alpha;
+                    if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
+                    if (a.relu) v[j] = fmaxf(v[j], 0.f);
+                }
+                if constexpr (EM == E_BF16) {
+                    if (a.ep_res) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] += bf2f(rv[fm][fn][j]);
+                    }
+                    if (bnb) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            float v = acc[fm][fn][j] * a.alpha;
-                            v = bf2f(f2bf(v));
-                            s[j] += v;
-                            q[j] += v * v;
+                            const float t = bf2f(tv[fm][fn][j]);
+                            const float gm = (ok && n4 && fmaf(t, bms[j], bmh[j]) > 0.f) ? bf2f(f2bf(v[j])) : 0.f;
+                            v[j] = gm;
+                            s[j] += gm;
+                            q[j] += ok && n4 ? gm * (t - bmu[j]) * bis[j] : 0.f;
+                        }
+                    } else if (want_stats && ok) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float r = bf2f(f2bf(v[j]));
+                            s[j] += r;
+                            q[j] += r * r;
                         }
                     }
+                    pk[fm][fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                    pk[fm][fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                } else {
+                    if (!ok) continue;
+                    float* C = reinterpret_cast<float*>(a.C) + orow[fm] * a.ldc + n;
+                    if (n4 && (a.ldc & 3) == 0) {
+                        *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = v[j];
+                    }
                 }
+            }
+            if (want_stats) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -513,9 +611,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                         q[j] += __shfl_xor(q[j], o, 64);
                     }
                 }
-                const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
-                if (lm == 0 && n < a.N) {
-                    const long row = (long)(tm * 2 + wm) * 2;
+                if (lm == 0 && nv) {
+                    const long row = (long)(a.stats_row0 + tm * 2 + wm) * 2;
                     float* ps = a.stats + row * a.N + n;
                     float* pq = a.stats + (row + 1) * a.N + n;
 #pragma unroll
@@ -525,45 +622,25 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 }
             }
         }
-        // direct register -> global stores: each lane writes 4 consecutive columns of one row; a wave's
-        // fragment covers 16 rows x 16 columns and the fn loop completes 2*WTN-byte row segments in L2.
+        if constexpr (EM == E_BF16) {
+            // Lanes l, l+16, l+32, l+48 hold columns 0-3 / 4-7 / 8-11 / 12-15 of the same row.  One
+            // permlane16_swap per dword between fragments (fn, fn+1) gives every lane 16 contiguous bytes:
+            // 16-lane row g of the wave then holds fragment fn + (g & 1), columns 8*(g >> 1) .. +7.
+            // Half the store instructions, 64-byte row segments (cdna_hip_programming.md T21, 16x16 form).
 #pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            const int m = m0 + wm * 64 + fm * 16 + lm;
-            if (m >= a.M) continue;
-            long orow = m;
-            if (a.scatter) {
-                const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
-                const uint32_t rem = (uint32_t)m - nn * a.g.dHW.d;
-                const uint32_t hc = fdiv(rem, a.g.dW);
-                const uint32_t wc = rem - hc * a.g.dW.d;
-                orow = ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
-            }
+            for (int fm = 0; fm < 4; ++fm) {
 #pragma unroll
-            for (int fn = 0; fn < FN; ++fn) {
-                const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
-                if (n >= a.N) continue;
-                float v[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    v[j] = acc[fm][fn][j] * a.alpha;
-                    if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
-                    if (a.relu) v[j] = fmaxf(v[j], 0.f);
-                }
-                if constexpr (EM == E_BF16) {
-                    bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc + n;
-                    if (n + 4 <= a.N) {
-                        u16x4_t o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-                        *reinterpret_cast<u16x4_t*>(C) = o;
-                    } else {
-                        for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = f2bf(v[j]);
-                    }
-                } else {
-                    float* C = reinterpret_cast<float*>(a.C) + orow * a.ldc + n;
-                    if (n + 4 <= a.N && (a.ldc & 3) == 0) {
-                        *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-                        for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = v[j];
+                for (int fp = 0; fp < FN / 2; ++fp) {
+                    const auto s0 = __builtin_amdgcn_permlane16_swap(pk[fm][2 * fp][0], pk[fm][2 * fp + 1][0], false, false);
+                    const auto s1 = __builtin_amdgcn_permlane16_swap(pk[fm][2 * fp][1], pk[fm][2 * fp + 1][1], false, false);
+                    const int n = n0 + wn * WTN + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
+                    if (mv[fm] && n + 8 <= a.N) {
+                        uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + orow[fm] * a.ldc + n) = o;
+                    } else if (mv[fm] && n < a.N) {
+                        const uint32_t w4[4] = {s0[0], s1[0], s0[1], s1[1]};
+                        bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + orow[fm] * a.ldc + n;
+                        for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = (bf16_t)(w4[j >> 1] >> (16 * (j & 1)));
                     }
                 }
             }
@@ -590,9 +667,13 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)gemm_kernel<AM, BMODE, EM, PA, PB, BNW>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, SM);
     }
+    // a single K-step per block (K <= 64: the 1x1 "expand" convs) never touches the second operand
+    // buffer: launch with half the LDS so twice as many blocks are resident per CU
+    int sm = SM;
+    if (a.ktiles_per_split <= 1 && EM != E_ATOMIC) sm = (BMt + BNW) * BK * 2;
     const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW));
     dim3 grid(tiles, 1, splits);
-    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), SM, st, a);
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), sm, st, a);
     PDNN_LAUNCH_RET;
 }
 
@@ -690,39 +771,74 @@ PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg
 // Convolution data gradient: dx[N][H][W][C] = sum over (r, s, ko) dy[...] * w[ko][r][s][c].
 // stride > 1 is decomposed into st*st parity classes of dx pixels; each class is a dense implicit GEMM
 // over only the taps that reach it (no MFMA work on the zero-stuffed positions of the transposed conv).
+struct DgradClass { int ph, pw, r0, s0, Rc, Sc, Hc, Wc; };
+static int dgrad_classes(int H, int W, int R, int S, int st, int pad, DgradClass* out, bool* any_empty) {
+    int n = 0;
+    *any_empty = false;
+    for (int ph = 0; ph < st; ++ph)
+        for (int pw = 0; pw < st; ++pw) {
+            DgradClass c;
+            c.ph = ph; c.pw = pw;
+            c.r0 = (ph + pad) % st; c.s0 = (pw + pad) % st;
+            c.Rc = c.r0 < R ? (R - c.r0 + st - 1) / st : 0;
+            c.Sc = c.s0 < S ? (S - c.s0 + st - 1) / st : 0;
+            c.Hc = ph < H ? (H - ph + st - 1) / st : 0;
+            c.Wc = pw < W ? (W - pw + st - 1) / st : 0;
+            if (c.Hc * c.Wc == 0) continue;
+            if (c.Rc * c.Sc == 0) { *any_empty = true; continue; }
+            out[n++] = c;
+        }
+    return n;
+}
+
+// Number of stats wave-rows (slab rows / 2) the fused dgrad epilogue writes.
+PDNN_API int pdnn_conv_dgrad_stats_rows(int Nimg, int H, int W, int R, int S, int st, int pad) {
+    DgradClass cl[16];
+    bool e;
+    const int n = dgrad_classes(H, W, R, S, st, pad, cl, &e);
+    int rows = 0;
+    for (int i = 0; i < n; ++i) rows += (int)cdiv((long)Nimg * cl[i].Hc * cl[i].Wc, BMt) * 2;
+    return rows;
+}
+
+// Convolution data gradient: dx[N][H][W][C] = sum over (r, s, ko) dy[...] * w[ko][r][s][c] (+ res).
+// stride > 1 is decomposed into st*st parity classes of dx pixels; each class is a dense implicit GEMM
+// over only the taps that reach it (no MFMA work on the zero-stuffed positions of the transposed conv).
+// Optional epilogue fusions: `res` is added to dx; with `bn_x` the output is the BN-backward masked
+// gradient gm = dx * [bn_x*mscale + mshift > 0] and `stats` receives the partial sums of gm and
+// gm * (bn_x - mean) * invstd (the BatchNorm backward reduction, see batchnorm.hip).
 PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nimg, int H, int W, int C,
                              int Ko, int R, int S, int st, int pad, int Ho, int Wo, float* stats,
-                             hipStream_t stream) {
+                             const bf16_t* res, const bf16_t* bn_x, const float* bn_mean, const float* bn_invstd,
+                             const float* bn_mscale, const float* bn_mshift, hipStream_t stream) {
     ensure_attrs();
-    bool any_empty = false;
-    for (int ph = 0; ph < st; ++ph)
-        for (int pw = 0; pw < st; ++pw) {
-            const int r0 = (ph + pad) % st, s0 = (pw + pad) % st;
-            const int Rc = r0 < R ? (R - r0 + st - 1) / st : 0, Sc = s0 < S ? (S - s0 + st - 1) / st : 0;
-            const int Hc = ph < H ? (H - ph + st - 1) / st : 0, Wc = pw < W ? (W - pw + st - 1) / st : 0;
-            if (Hc * Wc > 0 && Rc * Sc == 0) any_empty = true;
-        }
-    if (any_empty) {
-        hipError_t e = hipMemsetAsync(dx, 0, (size_t)Nimg * H * W * C * sizeof(bf16_t), stream);
+    DgradClass cl[16];
+    bool any_empty;
+    const int ncl = dgrad_classes(H, W, R, S, st, pad, cl, &any_empty);
+    if (any_empty) {   // pixels no tap reaches: zero (or the residual)
+        const size_t bytes = (size_t)Nimg * H * W * C * sizeof(bf16_t);
+        hipError_t e = (res && !bn_x) ? hipMemcpyAsync(dx, res, bytes, hipMemcpyDeviceToDevice, stream)
+                                      : hipMemsetAsync(dx, 0, bytes, stream);
         if (e != hipSuccess) return (int)e;
     }
-    for (int ph = 0; ph < st; ++ph)
-        for (int pw = 0; pw < st; ++pw) {
-            const int r0 = (ph + pad) % st, s0 = (pw + pad) % st;
-            const int Rc = r0 < R ? (R - r0 + st - 1) / st : 0, Sc = s0 < S ? (S - s0 + st - 1) / st : 0;
-            const int Hc = ph < H ? (H - ph + st - 1) / st : 0, Wc = pw < W ? (W - pw + st - 1) / st : 0;
-            if (Rc * Sc == 0 || Hc * Wc == 0) continue;
-            GemmArgs a{};
-            a.M = Nimg * Hc * Wc; a.N = C; a.K = Rc * Sc * Ko;
-            a.A = dy; a.B = w; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
-            fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
-            a.g.ph = ph; a.g.pw = pw; a.g.r0 = r0; a.g.s0 = s0; a.g.Sc = Sc; a.g.dSc = make_fdiv(Sc);
-            a.g.dHW = make_fdiv(Hc * Wc); a.g.dW = make_fdiv(Wc);
-            a.scatter = st > 1;
-            a.ktiles_per_split = (int)cdiv(a.K, BK);
-            const int rc = launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);
-            if (rc) return rc;
-        }
+    int row0 = 0;
+    for (int i = 0; i < ncl; ++i) {
+        const DgradClass& c = cl[i];
+        GemmArgs a{};
+        a.M = Nimg * c.Hc * c.Wc; a.N = C; a.K = c.Rc * c.Sc * Ko;
+        a.A = dy; a.B = w; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
+        fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+        a.g.ph = c.ph; a.g.pw = c.pw; a.g.r0 = c.r0; a.g.s0 = c.s0; a.g.Sc = c.Sc; a.g.dSc = make_fdiv(c.Sc);
+        a.g.dHW = make_fdiv(c.Hc * c.Wc); a.g.dW = make_fdiv(c.Wc);
+        a.scatter = st > 1;
+        a.stats_row0 = row0;
+        a.ep_res = res;
+        a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+        a.ktiles_per_split = (int)cdiv(a.K, BK);
+        const int rc = launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);
+        if (rc) return rc;
+        row0 += (int)cdiv(a.M, BMt) * 2;
+    }
     return 0;
 }
 

@@ -1,0 +1,269 @@
+"""Datasets, readers and the prefetching loader (see package docstring)."""
+from __future__ import annotations
+
+import os
+import queue
+import threading
+from pathlib import Path
+
+import numpy as np
+import torch
+
+MNIST_SEED = 66478      # pytorch_code/mnist/mnist.py:35
+
+
+class DataSet:
+    """Arrays + epoch-wrapping ``next_batch`` with a reshuffle at every epoch boundary."""
+
+    def __init__(self, images: np.ndarray, labels: np.ndarray, seed: int = MNIST_SEED, shuffle: bool = True):
+        assert len(images) == len(labels)
+        self.images, self.labels = images, labels
+        self.num_examples = len(images)
+        self.epochs_completed = 0
+        self._index = 0
+        self._rng = np.random.RandomState(seed)
+        self._shuffle = shuffle
+        if shuffle:
+            self._perm()
+
+    def _perm(self):
+        p = self._rng.permutation(self.num_examples)
+        self.images, self.labels = self.images[p], self.labels[p]
+
+    def next_batch(self, batch_size: int):
+        start = self._index
+        if start + batch_size > self.num_examples:
+            # finish the epoch with the remaining rows, reshuffle, continue (mnist.py:102-131)
+            rest = self.num_examples - start
+            xi, yi = self.images[start:], self.labels[start:]
+            self.epochs_completed += 1
+            if self._shuffle:
+                self._perm()
+            self._index = batch_size - rest
+            return (np.concatenate([xi, self.images[: self._index]]),
+                    np.concatenate([yi, self.labels[: self._index]]))
+        self._index += batch_size
+        return self.images[start:self._index], self.labels[start:self._index]
+
+    def __len__(self):
+        return self.num_examples
+
+
+# ------------------------------------------------------------------------------------------------ MNIST
+def write_mnist_like(dir_, n_train=256, n_test=64, seed=0):
+    """Write synthetic MNIST-format IDX files (same magic numbers/shapes) — used by tests and offline runs."""
+    from ..utils.native import idx_write
+    d = Path(dir_)
+    d.mkdir(parents=True, exist_ok=True)
+    rng = np.random.RandomState(seed)
+    for split, n in (("train", n_train), ("t10k", n_test)):
+        labels = rng.randint(0, 10, n).astype(np.uint8)
+        imgs = (rng.rand(n, 28, 28) * 64).astype(np.uint8)
+        for i, l in enumerate(labels):     # a learnable pattern: a bright column per class
+            imgs[i, 4:24, 2 + 2 * l] = 255
+        idx_write(d / f"{split}-images-idx3-ubyte", imgs)
+        idx_write(d / f"{split}-labels-idx1-ubyte", labels)
+    return d
+
+
+def read_mnist(dir_, reshape: bool = True, flat: bool = False, one_hot: bool = False, seed: int = MNIST_SEED):
+    """-> (train DataSet, test DataSet).  Files: {train,t10k}-{images-idx3,labels-idx1}-ubyte."""
+    from ..utils.native import idx_read
+    d = Path(dir_)
+    out = []
+    for split in ("train", "t10k"):
+        imgs = idx_read(d / f"{split}-images-idx3-ubyte").astype(np.float32) / 255.0 - 0.5
+        labels = idx_read(d / f"{split}-labels-idx1-ubyte").astype(np.int64)
+        if flat:
+            imgs = imgs.reshape(len(imgs), -1)
+        elif reshape:
+            imgs = imgs.reshape(len(imgs), 1, 28, 28)
+        if one_hot:
+            labels = np.eye(10, dtype=np.float32)[labels]
+        out.append(DataSet(imgs, labels, seed=seed, shuffle=split == "train"))
+    return out[0], out[1]
+
+
+# ------------------------------------------------------------------------------------------------ CIFAR-10
+def read_cifar10(dir_, normalize: bool = True, seed: int = 0):
+    """CIFAR-10 binary version: each record = 1 label byte + 3072 pixel bytes (R plane, G plane, B plane).
+    Returns (train DataSet, test DataSet) with NCHW float32 images."""
+    d = Path(dir_)
+
+    def load(files):
+        raw = np.concatenate([np.fromfile(d / f, dtype=np.uint8) for f in files])
+        raw = raw.reshape(-1, 3073)
+        labels = raw[:, 0].astype(np.int64)
+        imgs = raw[:, 1:].reshape(-1, 3, 32, 32).astype(np.float32) / 255.0   # planes are already CHW
+        if normalize:
+            mean = np.array([0.4914, 0.4822, 0.4465], np.float32)[:, None, None]
+            std = np.array([0.2470, 0.2435, 0.2616], np.float32)[:, None, None]
+            imgs = (imgs - mean) / std
+        return imgs, labels
+
+    tr = load([f"data_batch_{i}.bin" for i in range(1, 6) if (d / f"data_batch_{i}.bin").exists()])
+    te = load(["test_batch.bin"]) if (d / "test_batch.bin").exists() else tr
+    return DataSet(*tr, seed=seed), DataSet(*te, seed=seed, shuffle=False)
+
+
+def augment_crop_flip(x: np.ndarray, pad: int = 4, rng=None) -> np.ndarray:
+    """Random crop with zero padding + horizontal flip (reference cifar10.py:458-494), NCHW batch."""
+    rng = rng or np.random
+    n, c, h, w = x.shape
+    xp = np.pad(x, ((0, 0), (0, 0), (pad, pad), (pad, pad)))
+    out = np.empty_like(x)
+    for i in range(n):
+        dy, dx = rng.randint(0, 2 * pad + 1, 2)
+        img = xp[i, :, dy:dy + h, dx:dx + w]
+        out[i] = img[:, :, ::-1] if rng.rand() < 0.5 else img
+    return out
+
+
+# ------------------------------------------------------------------------------------------------ synthetic
+class SyntheticDataset:
+    """Random inputs/labels of a given shape, generated once on the target device (benchmarks)."""
+
+    def __init__(self, shape, num_classes=1000, n_batches=2, batch_size=256, device="cpu", dtype=torch.float32,
+                 seed=0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.batches = []
+        for _ in range(n_batches):
+            x = torch.randn(batch_size, *shape, generator=g).to(device=device, dtype=dtype)
+            y = torch.randint(0, num_classes, (batch_size,), generator=g).to(device)
+            self.batches.append((x, y))
+        self._i = 0
+
+    def next_batch(self, batch_size=None):
+        b = self.batches[self._i % len(self.batches)]
+        self._i += 1
+        return b
+
+    def __iter__(self):
+        while True:
+            yield self.next_batch()
+
+
+class SyntheticTokens:
+    """Random token sequences for language models: (input ids, next-token targets)."""
+
+    def __init__(self, vocab, seq_len, batch_size, device="cpu", n_batches=2, seed=0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.batches = []
+        for _ in range(n_batches):
+            t = torch.randint(0, vocab, (batch_size, seq_len + 1), generator=g).to(device)
+            self.batches.append((t[:, :-1].contiguous(), t[:, 1:].contiguous()))
+        self._i = 0
+
+    def next_batch(self, batch_size=None):
+        b = self.batches[self._i % len(self.batches)]
+        self._i += 1
+        return b
+
+    def __iter__(self):
+        while True:
+            yield self.next_batch()
+
+
+# ------------------------------------------------------------------------------------------------ loader
+class DataLoader:
+    """Batches from a :class:`DataSet`, sharded by rank, prefetched by a background thread into pinned
+    memory and copied to the device asynchronously on a side stream.
+
+    ``rank``/``world`` shard the sample stream (each rank draws every world-th batch), so DDP ranks see
+    disjoint data like torch's DistributedSampler."""
+
+    def __init__(self, dataset: DataSet, batch_size: int, device="cpu", prefetch: int = 4, rank: int = 0,
+                 world: int = 1, transform=None, drop_last: bool = True):
+        self.ds, self.bs = dataset, batch_size
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world
+        self.transform = transform
+        self.q: queue.Queue = queue.Queue(maxsize=prefetch)
+        self._stop = False
+        self._pin = self.device.type == "cuda"
+        self._thread = threading.Thread(target=self._worker, daemon=True)
+        self._thread.start()
+        self._stream = torch.cuda.Stream(self.device) if self._pin else None
+
+    def _worker(self):
+        while not self._stop:
+            for _ in range(self.rank):
+                self.ds.next_batch(self.bs)
+            x, y = self.ds.next_batch(self.bs)
+            for _ in range(self.world - 1 - self.rank):
+                self.ds.next_batch(self.bs)
+            if self.transform is not None:
+                x = self.transform(x)
+            xt, yt = torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(np.ascontiguousarray(y))
+            if self._pin:
+                xt, yt = xt.pin_memory(), yt.pin_memory()
+            self.q.put((xt, yt))
+
+    def next_batch(self, batch_size=None):
+        x, y = self.q.get()
+        if self._pin:
+            with torch.cuda.stream(self._stream):
+                x = x.to(self.device, non_blocking=True)
+                y = y.to(self.device, non_blocking=True)
+            torch.cuda.current_stream(self.device).wait_stream(self._stream)
+            x.record_stream(torch.cuda.current_stream(self.device))
+            y.record_stream(torch.cuda.current_stream(self.device))
+        return x, y
+
+    def __iter__(self):
+        while True:
+            yield self.next_batch()
+
+    def __len__(self):
+        return len(self.ds) // (self.bs * self.world)
+
+    def close(self):
+        self._stop = True
+
+
+class MNISTDataset(torch.utils.data.Dataset):
+    """torch Dataset over a MNIST :class:`DataSet` (PT-12 datasets/__init__.py:5-27)."""
+
+    def __init__(self, dataset: DataSet, transform=None, target_transform=None):
+        self.ds, self.transform, self.target_transform = dataset, transform, target_transform
+
+    def __getitem__(self, i):
+        x, y = torch.from_numpy(np.asarray(self.ds.images[i])), int(self.ds.labels[i])
+        if self.transform:
+            x = self.transform(x)
+        if self.target_transform:
+            y = self.target_transform(y)
+        return x, y
+
+    def __len__(self):
+        return len(self.ds)
+
+    def next_batch(self, batch_size):
+        x, y = self.ds.next_batch(batch_size)
+        return torch.from_numpy(x), torch.from_numpy(np.asarray(y))
+
+
+class Cifar10Dataset(MNISTDataset):
+    """torch Dataset over a CIFAR-10 :class:`DataSet` (PT-12 datasets/__init__.py:29-51)."""
+
+
+def dataset_from_args(name: str, data_dir: str | None, synthetic: bool, device, batch_size: int, model_name: str):
+    """(train, test) sources for the CLI: real files when present, otherwise synthetic of the right shape."""
+    name = name.upper()
+    if not synthetic and data_dir and os.path.isdir(data_dir):
+        if name == "MNIST":
+            flat = model_name.lower().startswith("mlp")
+            return read_mnist(data_dir, flat=flat)
+        if name == "CIFAR10":
+            return read_cifar10(data_dir)
+    shape = {"MNIST": (1, 28, 28), "CIFAR10": (3, 32, 32), "IMAGENET": (3, 224, 224)}[name]
+    if model_name.lower().startswith("mlp"):
+        shape = (int(np.prod(shape)),)
+    nc = 1000 if name == "IMAGENET" else 10
+    n = 4 * batch_size
+    rng = np.random.RandomState(0)
+    centers = rng.randn(nc, *shape).astype(np.float32)
+    y = rng.randint(0, nc, n)
+    x = (centers[y] + 0.5 * rng.randn(n, *shape)).astype(np.float32)
+    return DataSet(x, y.astype(np.int64)), DataSet(x[: 2 * batch_size], y[: 2 * batch_size].astype(np.int64),
+                                                   shuffle=False)

@@ -34,7 +34,8 @@ _SIGS = {
     "pdnn_gemm_nn": [P, L, P, L, P, L, I, I, I, F, I, P],
     "pdnn_gemm_tn_acc": [P, L, P, L, P, L, I, I, I, F, P],
     "pdnn_conv_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
-    "pdnn_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "pdnn_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P],
+    "pdnn_conv_dgrad_stats_rows": [I, I, I, I, I, I, I],
     "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "pdnn_gemm_stats_rows": [I],
     "pdnn_bn_reduce_rows": [L, I],

@@ -61,6 +61,16 @@ def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None):
     return dt, dgamma, dbeta
 
 
+def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma):
+    """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
+    one apply pass produces dt (the gradient w.r.t. the BN input t)."""
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh))
+    dgamma, dbeta = K.bn_bwd_finalize(slab, slab.shape[0] // 2)
+    C = t.shape[-1]
+    dt, _, _ = K.bn_bwd_apply(gm.view(-1, C), t.view(-1, C), mean, inv, gamma, dgamma, dbeta, mode=0)
+    return dt.view(t.shape), dgamma, dbeta
+
+
 def _krsc_grad(dw):
     """fp32 [K][R][S][C] -> [K][C][R][S] view with channels_last strides (the parameter's layout)."""
     return dw.permute(0, 3, 1, 2)
@@ -117,26 +127,19 @@ class BottleneckFn(torch.autograd.Function):
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
         dw3 = K.conv_wgrad(t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
-        da2 = K.conv_dgrad(dt3, k3, t2.shape, 1, 0)
-        C2 = t2.shape[-1]
-        dt2, dg2, db2 = _bn_back(da2.view(-1, C2), t2.view(-1, C2), m2, i2, g2, 2, msc=s2, msh=h2)
-        dt2 = dt2.view(t2.shape)
+        dt2, dg2, db2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2)
         dw2 = K.conv_wgrad(t1, dt2, 3, 3, stride, 1, pro=(s1, h1))
-        da1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1)
-        C1 = t1.shape[-1]
-        dt1, dg1, db1 = _bn_back(da1.view(-1, C1), t1.view(-1, C1), m1, i1, g1, 2, msc=s1, msh=h1)
-        dt1 = dt1.view(t1.shape)
+        dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1)
         dw1 = K.conv_wgrad(x, dt1, 1, 1, 1, 0)
-        dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0)
         if down:
             dtd = dtd.view(td.shape)
             dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
-            dx2 = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
-            dx = K.add(dx, dx2)
+            dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
+            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=dxd)          # residual add fused
             grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3,
                      _krsc_grad(dwd), dgd, dbd)
         else:
-            dx = K.add(dx, gres.view(x.shape))
+            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape))
             grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3)
         return (dx, None, None, None) + grads
 
@@ -187,19 +190,16 @@ class BasicBlockFn(torch.autograd.Function):
             dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, want_gm=True)
         dt2 = dt2.view(t2.shape)
         dw2 = K.conv_wgrad(t1, dt2, 3, 3, 1, 1, pro=(s1, h1))
-        da1 = K.conv_dgrad(dt2, k2, t1.shape, 1, 1)
-        C1 = t1.shape[-1]
-        dt1, dg1, db1 = _bn_back(da1.view(-1, C1), t1.view(-1, C1), m1, i1, g1, 2, msc=s1, msh=h1)
-        dt1 = dt1.view(t1.shape)
+        dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1)
         dw1 = K.conv_wgrad(x, dt1, 3, 3, stride, 1)
-        dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1)
         if down:
             dtd = dtd.view(td.shape)
             dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
-            dx = K.add(dx, K.conv_dgrad(dtd, kd, x.shape, stride, 0))
+            dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
+            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=dxd)
             grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dwd), dgd, dbd)
         else:
-            dx = K.add(dx, gres.view(x.shape))
+            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape))
             grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2)
         return (dx, None, None, None) + grads
 

@@ -100,7 +100,12 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     return y, stats
 
 
-def conv_dgrad(dy, w, x_shape, st, pad):
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None):
+    """dx = conv_transpose(dy, w) (+ res).
+
+    bn = (t, mean, invstd, mscale, mshift): fuse the BatchNorm backward of the layer that produced t:
+    returns (gm, slab) where gm = dx * [t*mscale + mshift > 0] and slab holds the partial sums of gm and
+    gm*(t-mean)*invstd (finalize with bn_bwd_finalize)."""
     _bf16_c(dy, "conv_dgrad.dy")
     N, H, W, C = x_shape
     _bf16_c(w, "conv_dgrad.w")
@@ -109,8 +114,20 @@ def conv_dgrad(dy, w, x_shape, st, pad):
     _, Ho, Wo, K2 = dy.shape
     _chk(K2 == K and C % 8 == 0 and K % 8 == 0, "conv_dgrad: channel mismatch")
     dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
-    call("pdnn_conv_dgrad", ptr(dy), ptr(w), ptr(dx), N, H, W, C, K, R, S, st, pad, Ho, Wo, None, stream())
-    return dx
+    slab = None
+    t = mean = inv = msc = msh = None
+    if bn is not None:
+        t, mean, inv, msc, msh = bn
+        _bf16_c(t, "conv_dgrad.bn_x")
+        _chk(tuple(t.shape) == (N, H, W, C), "conv_dgrad: bn_x shape")
+        rows = lib().pdnn_conv_dgrad_stats_rows(N, H, W, R, S, st, pad)
+        slab = torch.empty(2 * rows, C, device=dy.device, dtype=F32)
+    if res is not None:
+        _bf16_c(res, "conv_dgrad.res")
+        _chk(tuple(res.shape) == (N, H, W, C), "conv_dgrad: res shape")
+    call("pdnn_conv_dgrad", ptr(dy), ptr(w), ptr(dx), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(slab), ptr(res),
+         ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), stream())
+    return (dx, slab) if bn is not None else dx
 
 
 def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):

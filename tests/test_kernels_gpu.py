@@ -221,3 +221,30 @@ def test_act(K, op):
     g = rnd(4096)
     r.backward(g.float())
     assert rel(K.act_bwd(g, x, op), xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 128, 128, 3, 2, 1), (2, 9, 9, 64, 128, 3, 1, 1), (2, 8, 8, 256, 64, 1, 1, 0)])
+def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
+    """dgrad epilogue fusions: residual add, and BN-backward ReLU masking + reduction (sum gm, sum gm*xhat)."""
+    N, H, W, C, Ko, R, st, pad = shape
+    w = rnd(Ko, R, R, C, scale=0.1)
+    Ho, Wo = K.conv_out_hw(H, W, R, R, st, pad)
+    dy = rnd(N, Ho, Wo, Ko)
+    x = torch.zeros(N, C, H, W, device="cuda", requires_grad=True)
+    y = F.conv2d(x, w.float().permute(0, 3, 1, 2), None, st, pad)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dx_ref = x.grad.permute(0, 2, 3, 1)
+    res = rnd(N, H, W, C)
+    dx = K.conv_dgrad(dy, w, (N, H, W, C), st, pad, res=res)
+    assert rel(dx, dx_ref + res.float()) < 1.5e-2
+    t = rnd(N, H, W, C) + 0.3
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), st, pad, bn=(t, mean, inv, sc, sh))
+    mask = (t.float() * sc + sh) > 0
+    gm_ref = dx_ref.to(BF).float() * mask
+    assert rel(gm, gm_ref) < 1.5e-2
+    sums = slab.view(-1, 2, C).sum(0)
+    xh = (t.float() - mean) * inv
+    assert torch.allclose(sums[0], gm_ref.reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
+    assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
