@@ -43,17 +43,27 @@ __global__ void __launch_bounds__(NT) slab_reduce_kernel(const float* __restrict
 }
 
 // finalize (few) partial rows -> mean, invstd, scale/shift (+ running-stat update), fp64 accumulation.
-__global__ void bn_finalize_kernel(const float* __restrict__ slab, int rows, int C, double L, float eps,
-                                   float momentum, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* run_mean, float* run_var,
-                                   float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// Block = 64 channels x 4 row-lanes (rows strided by 4, combined through LDS).
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ slab, int rows, int C, double L,
+                                                         float eps, float momentum, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* run_mean,
+                                                         float* run_var, float* mean_out, float* invstd_out,
+                                                         float* scale_out, float* shift_out) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
+    __shared__ double red[2][4][64];
     double s = 0.0, q = 0.0;
-    for (int r = 0; r < rows; ++r) {
-        s += slab[(long)(2 * r) * C + c];
-        q += slab[(long)(2 * r + 1) * C + c];
-    }
+    if (c < C)
+        for (int r = lr; r < rows; r += 4) {
+            s += slab[(long)(2 * r) * C + c];
+            q += slab[(long)(2 * r + 1) * C + c];
+        }
+    red[0][lr][threadIdx.x & 63] = s;
+    red[1][lr][threadIdx.x & 63] = q;
+    __syncthreads();
+    if (lr != 0 || c >= C) return;
+    const int l = threadIdx.x;
+    s = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+    q = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
     const double mean = s / L;
     double var = q / L - mean * mean;
     if (var < 0) var = 0;
@@ -216,15 +226,23 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
 }
 
 // sum partial rows -> dbeta (= sum gm), dgamma (= sum gm*xhat).  Optionally accumulate (+=).
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows, int C, float* dgamma,
-                                       float* dbeta, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+__global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows, int C,
+                                                             float* dgamma, float* dbeta, int accumulate) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
+    __shared__ double red[2][4][64];
     double s = 0.0, q = 0.0;
-    for (int r = 0; r < rows; ++r) {
-        s += slab[(long)(2 * r) * C + c];
-        q += slab[(long)(2 * r + 1) * C + c];
-    }
+    if (c < C)
+        for (int r = lr; r < rows; r += 4) {
+            s += slab[(long)(2 * r) * C + c];
+            q += slab[(long)(2 * r + 1) * C + c];
+        }
+    red[0][lr][threadIdx.x & 63] = s;
+    red[1][lr][threadIdx.x & 63] = q;
+    __syncthreads();
+    if (lr != 0 || c >= C) return;
+    const int l = threadIdx.x;
+    s = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+    q = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
     if (accumulate) { dbeta[c] += (float)s; dgamma[c] += (float)q; }
     else { dbeta[c] = (float)s; dgamma[c] = (float)q; }
 }
@@ -312,7 +330,7 @@ PDNN_API int pdnn_bn_finalize(const float* slab, int rows, int C, double L, floa
         src = work;
         r = 64;
     }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, r, C, L, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, st, src, r, C, L, eps,
                        momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out);
     PDNN_LAUNCH_RET;
 }
@@ -355,7 +373,7 @@ PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dga
         src = work;
         r = 64;
     }
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, src, r, C, dgamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, st, src, r, C, dgamma,
                        dbeta, accumulate);
     PDNN_LAUNCH_RET;
 }

@@ -42,7 +42,7 @@ namespace {
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-enum AMode { A_KMAJOR = 0, A_MNMAJOR = 1, A_CONV = 2, A_CONVT = 3 };
+enum AMode { A_KMAJOR = 0, A_MNMAJOR = 1, A_CONV = 2, A_CONVT = 3, A_IM2COL = 4 };
 enum BMode { B_KMAJOR = 0, B_MNMAJOR = 1, B_WT = 2, B_IM2COL = 3 };
 enum EMode { E_BF16 = 0, E_F32 = 1, E_ATOMIC = 2 };
 
@@ -80,6 +80,7 @@ struct GemmArgs {
     int ktiles_per_split;     // split-K (grid.z)
     int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
     int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
+    int transC;               // E_ATOMIC: accumulate C^T (C[n * ldc + m])
     // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
     const bf16_t* ep_res;
     const bf16_t* ep_x;
@@ -373,6 +374,7 @@ template <bool PRO> struct ASel<A_KMAJOR, PRO> { using T = KLoader<128, 0, false
 template <bool PRO> struct ASel<A_CONV, PRO> { using T = KLoader<128, 1, PRO>; static constexpr bool K = true; };
 template <bool PRO> struct ASel<A_CONVT, PRO> { using T = KLoader<128, 2, false>; static constexpr bool K = true; };
 template <bool PRO> struct ASel<A_MNMAJOR, PRO> { using T = MLoader<128, 0, false>; static constexpr bool K = false; };
+template <bool PRO> struct ASel<A_IM2COL, PRO> { using T = MLoader<128, 2, PRO>; static constexpr bool K = false; };
 template <int BMODE, bool PRO, int W> struct BSel;
 template <bool PRO, int W> struct BSel<B_KMAJOR, PRO, W> { using T = KLoader<W, 0, false>; static constexpr bool K = true; };
 template <bool PRO, int W> struct BSel<B_MNMAJOR, PRO, W> { using T = MLoader<W, 0, false>; static constexpr bool K = false; };
@@ -494,6 +496,21 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                     acc[fm][fn];
         __syncthreads();
         float* C = reinterpret_cast<float*>(a.C);
+        if (a.transC) {
+            // C is stored transposed (C^T[n][m], row stride ldc): each wave sweeps columns n, its lanes the
+            // tile's 128 rows m -> 2 x 256 contiguous bytes per atomic wave-instruction
+            for (int c = wave; c < BNW; c += 4) {
+                const int n = n0 + c;
+                if (n >= a.N) break;
+#pragma unroll
+                for (int h = 0; h < BMt / 64; ++h) {
+                    const int r = lane + 64 * h;
+                    const int m = m0 + r;
+                    if (m < a.M) atomicAdd(C + (long)n * a.ldc + m, a.alpha * cs[r * LDC_S + c]);
+                }
+            }
+            return;
+        }
         for (int r = wave; r < BMt; r += 4) {
             const int m = m0 + r;
             if (m >= a.M) break;
@@ -848,8 +865,16 @@ PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int N
                              const float* pro_scale, const float* pro_shift, hipStream_t stream) {
     ensure_attrs();
     GemmArgs a{};
-    a.M = Ko; a.N = R * S * C; a.K = Nimg * Ho * Wo;
-    a.A = dy; a.lda = Ko; a.B = x; a.C = dw; a.ldc = (long)R * S * C; a.alpha = 1.f;
+    const bool swap = Ko <= 64 && R * S * C >= 128;   // put the small Ko dimension on the 64-wide N tile
+    a.K = Nimg * Ho * Wo;
+    if (swap) {   // dW^T[(r,s,c)][ko] = im2col(x)^T . dy  -> stored transposed into dw[ko][(r,s,c)]
+        a.M = R * S * C; a.N = Ko;
+        a.A = x; a.B = dy; a.ldb = Ko; a.transC = 1;
+    } else {      // dW[ko][(r,s,c)] = dy^T . im2col(x)
+        a.M = Ko; a.N = R * S * C;
+        a.A = dy; a.lda = Ko; a.B = x;
+    }
+    a.C = dw; a.ldc = (long)R * S * C; a.alpha = 1.f;
     fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift;
@@ -857,6 +882,10 @@ PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int N
     const int splits = pick_splits(a, ktiles, tiles, 1024);
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
     const int nz = (int)cdiv(ktiles, a.ktiles_per_split);
+    if (swap) {
+        if (pro_scale) return launch<A_IM2COL, B_MNMAJOR, E_ATOMIC, true, false>(a, nz, stream);
+        return launch<A_IM2COL, B_MNMAJOR, E_ATOMIC, false, false>(a, nz, stream);
+    }
     if (pro_scale) return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
     return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
 }

@@ -1,0 +1,174 @@
+"""``distnn-train`` command line (PT-01 pytorch_code/distributed_nn.py:36-102, PT-07 single_machine.py:28-55,
+S4 tf flags).  All reference flag names and defaults are accepted verbatim:
+
+  --batch-size 128  --test-batch-size 1000  --epochs 100  --lr 0.01  --momentum 0.5  --no-cuda  --seed 1
+  --log-interval 10  --network LeNet  --dataset MNIST  --comm-type Bcast|Async  --num-aggregate 5
+
+New:  --mode ddp|ps|single (default: ps when --comm-type is Bcast/Async and world > 1, i.e. the
+reference's behaviour; ddp when --comm-type AllReduce), --comm-type AllReduce, --bucket-cap-mb,
+--dtype bf16|fp32, --synthetic, --data-dir, --max-steps, --optimizer sgd|adam|adamw, --weight-decay,
+--n-to-collect (backup workers), --interval-ms, --no-shortcircuit, --evaluator,
+--inject-straggler RANK:MS[,RANK:MS], --straggler-mode (k-of-n inside DDP), --checkpoint-dir, --resume,
+--trace FILE, --metrics FILE.
+
+Launch:  torchrun --nproc-per-node N -m pytorch_distributed_nn_amd.cli ...   or   mpirun -n N python -m ...
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import torch
+
+
+def add_fit_args(p: argparse.ArgumentParser):
+    p.add_argument("--batch-size", type=int, default=128, metavar="N")
+    p.add_argument("--test-batch-size", type=int, default=1000, metavar="N")
+    p.add_argument("--epochs", type=int, default=100, metavar="N")
+    p.add_argument("--lr", type=float, default=0.01, metavar="LR")
+    p.add_argument("--momentum", type=float, default=0.5, metavar="M")
+    p.add_argument("--no-cuda", action="store_true", default=False)
+    p.add_argument("--seed", type=int, default=1, metavar="S")
+    p.add_argument("--log-interval", type=int, default=10, metavar="N")
+    p.add_argument("--network", type=str, default="LeNet", metavar="N")
+    p.add_argument("--dataset", type=str, default="MNIST", metavar="N")
+    p.add_argument("--comm-type", type=str, default="Bcast", choices=["Bcast", "Async", "AllReduce"])
+    p.add_argument("--num-aggregate", type=int, default=5, metavar="N")
+    # --- new
+    p.add_argument("--mode", type=str, default=None, choices=["ddp", "ps", "single"])
+    p.add_argument("--bucket-cap-mb", type=float, default=32.0)
+    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--data-dir", type=str, default=None)
+    p.add_argument("--max-steps", type=int, default=None)
+    p.add_argument("--optimizer", type=str, default="sgd", choices=["sgd", "adam", "adamw"])
+    p.add_argument("--weight-decay", type=float, default=0.0)
+    p.add_argument("--n-to-collect", type=int, default=0)
+    p.add_argument("--interval-ms", type=float, default=0.0)
+    p.add_argument("--no-shortcircuit", action="store_true")
+    p.add_argument("--evaluator", action="store_true")
+    p.add_argument("--eval-interval", type=int, default=10)
+    p.add_argument("--inject-straggler", type=str, default="")
+    p.add_argument("--straggler-mode", action="store_true")
+    p.add_argument("--checkpoint-dir", type=str, default=None)
+    p.add_argument("--resume", type=str, default=None)
+    p.add_argument("--trace", type=str, default=None)
+    p.add_argument("--metrics", type=str, default=None)
+    p.add_argument("--out-dir", type=str, default="outfiles")
+    return p
+
+
+def parse_stragglers(s: str) -> dict:
+    out = {}
+    for part in filter(None, s.split(",")):
+        r, ms = part.split(":")
+        out[int(r)] = float(ms)
+    return out
+
+
+def main(argv=None):
+    args = add_fit_args(argparse.ArgumentParser(description="pytorch_distributed_nn_amd trainer")).parse_args(argv)
+    from .data.datasets import DataLoader, dataset_from_args
+    from .models import build_model
+    from .ops import functional as OF
+    from .optim import SGD, Adam, AdamW, flatten_module
+    from .parallel import runtime
+    from .parallel.ddp import DistributedDataParallel
+    from .trainer import Trainer
+
+    torch.manual_seed(args.seed)
+    env = runtime.init_process_group(device="cpu" if args.no_cuda else None)
+    world, rank = runtime.world_size(), runtime.rank()
+    dev = torch.device("cpu") if args.no_cuda or not torch.cuda.is_available() else runtime.device()
+    mode = args.mode or ("single" if world == 1 else ("ddp" if args.comm_type == "AllReduce" else "ps"))
+
+    train_ds, test_ds = dataset_from_args(args.dataset, args.data_dir, args.synthetic, dev, args.batch_size,
+                                          args.network)
+    nc = 1000 if args.dataset.upper() == "IMAGENET" else 10
+    model = build_model(args.network, nc).to(dev)
+    xdt = torch.bfloat16 if (dev.type == "cuda" and args.dtype == "bf16") else torch.float32
+
+    def to_dev(batch):
+        x, y = batch
+        return x.to(dev, dtype=xdt, non_blocking=True), y.to(dev, non_blocking=True)
+
+    if mode == "ps":
+        from .parallel.ps import PSConfig, run_ps
+        cfg = PSConfig(comm_type=args.comm_type if args.comm_type != "AllReduce" else "Bcast",
+                       num_aggregate=args.num_aggregate if args.n_to_collect == 0 else 0,
+                       n_to_collect=args.n_to_collect, shortcircuit=not args.no_shortcircuit,
+                       interval_ms=args.interval_ms, evaluator=args.evaluator, eval_interval=args.eval_interval,
+                       inject_straggler=parse_stragglers(args.inject_straggler), lr=args.lr, momentum=args.momentum,
+                       weight_decay=args.weight_decay, max_steps=args.max_steps or 1000, out_dir=args.out_dir)
+        n_workers = world - (2 if args.evaluator else 1)
+        wrank = max(0, rank - (2 if args.evaluator else 1))
+        loader = DataLoader(train_ds, args.batch_size, "cpu", rank=wrank, world=max(1, n_workers))
+
+        def batches():
+            while True:
+                yield to_dev(loader.next_batch())
+
+        def evaluate(m):
+            with torch.no_grad():
+                x, y = test_ds.next_batch(min(args.test_batch_size, len(test_ds)))
+                out = m(torch.as_tensor(x).to(dev, dtype=xdt))
+                yt = torch.as_tensor(y).to(dev)
+                return float(OF.cross_entropy(out, yt)), float((out.argmax(1) != yt).float().mean())
+
+        out = run_ps(model, cfg, dev, loss_fn=OF.cross_entropy, batches=batches(), eval_fn=evaluate)
+        if rank == 0:
+            print(f"Master: finished {len(out)} steps; gradients used per step: {[r['count'] for r in out][-10:]}")
+        runtime.destroy()
+        return out
+
+    net = model
+    if mode == "ddp" and world > 1:
+        net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, straggler_mode=args.straggler_mode)
+    else:
+        flatten_module(model)
+    params = model.parameters()
+    if args.optimizer == "sgd":
+        opt = SGD(params, lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    elif args.optimizer == "adam":
+        opt = Adam(params, lr=args.lr, weight_decay=args.weight_decay)
+    else:
+        opt = AdamW(params, lr=args.lr, weight_decay=args.weight_decay)
+    if isinstance(net, DistributedDataParallel):
+        net.attach_optimizer(opt)
+    strag = parse_stragglers(args.inject_straggler)
+    if rank in strag:
+        import time as _t
+        for p in model.parameters():
+            p.register_post_accumulate_grad_hook(lambda _p, d=strag[rank] / 1e3: _t.sleep(d))
+
+    loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world)
+
+    class _DevLoader:
+        def __iter__(self):
+            while True:
+                yield to_dev(loader.next_batch())
+
+        def __len__(self):
+            return len(loader)
+
+    tr = Trainer(net, opt, OF.cross_entropy, dev, rank, world, args.log_interval, args.metrics,
+                 args.trace, args.checkpoint_dir, arch=args.network, printer=print if rank == 0 else (lambda *a: None))
+    if args.resume:
+        tr.resume(args.resume)
+    hist = tr.train(_DevLoader(), epochs=args.epochs, max_steps=args.max_steps, batch_size=args.batch_size,
+                    dataset_size=len(train_ds))
+    test_loader = DataLoader(test_ds, min(args.test_batch_size, len(test_ds)), "cpu")
+
+    class _TestLoader:
+        def __iter__(self):
+            while True:
+                yield to_dev(test_loader.next_batch())
+
+    if rank == 0:
+        tr.evaluate(_TestLoader(), 1)
+    runtime.destroy()
+    return hist
+
+
+if __name__ == "__main__":
+    main()

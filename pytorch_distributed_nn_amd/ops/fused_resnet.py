@@ -9,8 +9,8 @@ Fusion plan of a Bottleneck (x -> out):
 
   forward                                          what is written to HBM
   t1 = conv1x1(x)          + BN1 partial stats      t1
-  t2 = conv3x3(relu(bn1(t1)))  (BN1+ReLU applied     t2       (a1 never materialised)
-       in conv2's operand loader) + BN2 stats
+  a1 = relu(bn1(t1))       (one streaming pass)     a1       (the 3x3 conv gathers each element 9x)
+  t2 = conv3x3(a1)         + BN2 stats              t2
   t3 = conv1x1(relu(bn2(t2)))  + BN3 stats           t3       (a2 never materialised)
   td = conv1x1/s(x)        + BNd stats  (if downsample)
   out = relu(bn3(t3) + bnd(td) | x)   one kernel    out
@@ -86,7 +86,11 @@ class BottleneckFn(torch.autograd.Function):
         w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
         k1, k2, k3 = shadows[:3]
         t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
-        t2, m2, i2, s2, h2 = _conv_bn(t1, k2, stride, 1, (s1, h1), training, (g2, b2), bufs[2:4], mom, eps)
+        # a1 = relu(bn1(t1)) is materialised once: the 3x3 conv gathers every element 9 times, so applying
+        # the BN affine in its operand loader would cost 9x the VALU work (fwd and wgrad)
+        C1 = t1.shape[-1]
+        a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)
+        t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
         t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
         C3 = t3.shape[-1]
         if down:
@@ -97,14 +101,14 @@ class BottleneckFn(torch.autograd.Function):
             td = md = idd = None
             out = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True)
         out = out.view(t3.shape)
-        ctx.save_for_backward(x, t1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+        ctx.save_for_backward(x, t1, a1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None)
         ctx.conf = (stride, training, down)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        (x, t1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+        (x, t1, a1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
          g1, g2, g3, gd, k1, k2, k3, kd) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
@@ -128,7 +132,7 @@ class BottleneckFn(torch.autograd.Function):
         # conv3 (input = relu(bn2(t2)), virtual)
         dw3 = K.conv_wgrad(t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
         dt2, dg2, db2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2)
-        dw2 = K.conv_wgrad(t1, dt2, 3, 3, stride, 1, pro=(s1, h1))
+        dw2 = K.conv_wgrad(a1, dt2, 3, 3, stride, 1)
         dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1)
         dw1 = K.conv_wgrad(x, dt1, 1, 1, 1, 0)
         if down:
@@ -154,7 +158,9 @@ class BasicBlockFn(torch.autograd.Function):
         w1, g1, b1, w2, g2, b2 = params[:6]
         k1, k2 = shadows[:2]
         t1, m1, i1, s1, h1 = _conv_bn(x, k1, stride, 1, None, training, (g1, b1), bufs[0:2], mom, eps)
-        t2, m2, i2, s2, h2 = _conv_bn(t1, k2, 1, 1, (s1, h1), training, (g2, b2), bufs[2:4], mom, eps)
+        C1 = t1.shape[-1]
+        a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)    # 3x3 consumer: materialise
+        t2, m2, i2, s2, h2 = _conv_bn(a1, k2, 1, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
         C2 = t2.shape[-1]
         if down:
             wd, gd, bd = params[6:]
@@ -164,14 +170,14 @@ class BasicBlockFn(torch.autograd.Function):
             td = md = idd = None
             out = K.bn_apply(t2.view(-1, C2), s2, h2, res=x.view(-1, C2), relu=True)
         out = out.view(t2.shape)
-        ctx.save_for_backward(x, t1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
+        ctx.save_for_backward(x, t1, a1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
                               params[7] if down else None, k1, k2, shadows[2] if down else None)
         ctx.conf = (stride, training, down)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        (x, t1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
+        (x, t1, a1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused BasicBlock backward requires training-mode BatchNorm")
@@ -189,7 +195,7 @@ class BasicBlockFn(torch.autograd.Function):
         else:
             dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, want_gm=True)
         dt2 = dt2.view(t2.shape)
-        dw2 = K.conv_wgrad(t1, dt2, 3, 3, 1, 1, pro=(s1, h1))
+        dw2 = K.conv_wgrad(a1, dt2, 3, 3, 1, 1)
         dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1)
         dw1 = K.conv_wgrad(x, dt1, 3, 3, stride, 1)
         if down:
