@@ -1,6 +1,6 @@
 """Headline benchmark (BASELINE.json): samples/sec of ResNet-50 DDP training on 1..8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model resnet50]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model resnet50|gpt2_small]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -10,6 +10,9 @@ One process per GPU (RCCL over xGMI for N > 1).  Model: ResNet-50, ImageNet layo
 fused SGD with momentum 0.9 + weight decay, full step timed (forward, backward, bucketed all-reduce,
 optimizer).  Per-GPU batch is fixed as N grows (weak scaling).  Rank 0 prints one JSON line with the
 WHOLE-JOB samples/sec (max step time over ranks).
+
+``--model gpt2_small`` benchmarks BASELINE.json config 4 instead: GPT-2 small (124M, T=1024, vocab
+50304), per-GPU batch 8 sequences, fused AdamW, metric tokens/sec (whole node).
 """
 from __future__ import annotations
 
@@ -32,7 +35,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (256 images / 8 sequences)")
+    ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
@@ -42,7 +46,7 @@ def main():
     from pytorch_distributed_nn_amd.parallel import runtime
     from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
     from pytorch_distributed_nn_amd.models import build_model
-    from pytorch_distributed_nn_amd.optim import SGD, flatten_module
+    from pytorch_distributed_nn_amd.optim import SGD, AdamW, flatten_module
     from pytorch_distributed_nn_amd.ops import functional as OF
 
     env = runtime.init_process_group()
@@ -50,22 +54,32 @@ def main():
     dev = runtime.device()
     torch.manual_seed(1234 + env.rank)
 
+    lm = a.model.lower().startswith("gpt2")
     model = build_model(a.model, num_classes=1000).to(dev)
     if world > 1:
         net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
     else:
         flatten_module(model)
         net = model
-    opt = SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5)
-
-    B, S = a.batch, a.image_size
-    xs = [torch.randn(B, 3, S, S, device=dev).to(torch.bfloat16) for _ in range(2)]
-    ys = [torch.randint(0, 1000, (B,), device=dev) for _ in range(2)]
+    if lm:
+        opt = AdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), weight_decay=0.1)
+        B, S = a.batch or 8, a.seq_len
+        V = model.config.vocab_size
+        toks = [torch.randint(0, 50257, (B, S + 1), device=dev) for _ in range(2)]
+        xs = [t[:, :-1].contiguous() for t in toks]
+        ys = [t[:, 1:].contiguous() for t in toks]
+    else:
+        opt = SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5)
+        B, S = a.batch or 256, a.image_size
+        xs = [torch.randn(B, 3, S, S, device=dev).to(torch.bfloat16) for _ in range(2)]
+        ys = [torch.randint(0, 1000, (B,), device=dev) for _ in range(2)]
 
     def step(i):
         opt.zero_grad()
-        out = net(xs[i % 2])
-        loss = OF.cross_entropy(out, ys[i % 2])
+        if lm:
+            loss = net(xs[i % 2], ys[i % 2])
+        else:
+            loss = OF.cross_entropy(net(xs[i % 2]), ys[i % 2])
         loss.backward()
         opt.step()
         return loss
@@ -86,7 +100,28 @@ def main():
     dt = t.item()
     ms = 1e3 * dt / a.steps
     value = B * world * a.steps / dt
-    if env.rank == 0:
+    if lm and env.rank == 0:
+        tok = value * S
+        print(json.dumps({
+            "metric": "tokens/sec (whole node) GPT-2-small DDP",
+            "value": round(tok, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (device-resident random token ids), random-init weights",
+            "final_loss": round(float(loss), 4),
+            "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
+            "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
+                       "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb},
+        }), flush=True)
+    elif env.rank == 0:
         print(json.dumps({
             "metric": "samples/sec (whole node) ResNet-50 DDP",
             "value": round(value, 2),

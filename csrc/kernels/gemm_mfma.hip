@@ -75,17 +75,36 @@ struct GemmArgs {
     void* C; long ldc;
     float alpha;
     const float* bias;        // per-column bias (E_BF16 / E_F32)
-    int relu;
+    int relu;                 // epilogue activation: 0 none, 1 ReLU, 2 GELU (tanh form)
     float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
     int ktiles_per_split;     // split-K (grid.z)
     int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
     int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
     int transC;               // E_ATOMIC: accumulate C^T (C[n * ldc + m])
+    // batched GEMM (grid.y = nb1 * nb2): operand offsets z1 * s*1 + z2 * s*2 (elements), z = z1 * nb2 + z2
+    int nb2;
+    long sA1, sA2, sB1, sB2, sC1, sC2;
+    // causal attention structure (square T x T operands, row = query, col = key):
+    //  1: C tiles strictly above the diagonal are skipped (S = Q K^T; never read by the softmax)
+    //  2: reduction limited to k < m0 + BM   (A = P or dS [q][k], lower triangular: P V, dS K)
+    //  3: reduction starts at k >= m0        (A = P^T / dS^T, upper triangular: P^T dO, dS^T Q)
+    int causal;
     // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
     const bf16_t* ep_res;
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
+    bf16_t* ep_aux;           // relu == 2: the pre-activation (bias added) is also stored here (ld = ldc)
+    const bf16_t* ep_dgelu;   // multiply the result by gelu'(u), u read from here (GELU backward)
 };
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+    const float t = tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 0.134145f * x * x);
+}
 
 // ---------------------------------------------------------------------------------------------
 // LDS image helpers
@@ -406,6 +425,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
+    if (gridDim.y > 1) {
+        const int z = blockIdx.y, z1 = z / a.nb2, z2 = z - z1 * a.nb2;
+        a.A += z1 * a.sA1 + z2 * a.sA2;
+        a.B += z1 * a.sB1 + z2 * a.sB2;
+        a.C = (void*)((char*)a.C + (z1 * a.sC1 + z2 * a.sC2) * (EM == E_BF16 ? 2 : 4));
+        if (a.ep_res) a.ep_res += z1 * a.sC1 + z2 * a.sC2;
+    }
     const int tiles_m = (a.M + BMt - 1) / BMt, tiles_n = (a.N + BNW - 1) / BNW;
     const int nwg = tiles_m * tiles_n;
     const int t = xcd_remap(blockIdx.x, nwg);
@@ -414,8 +440,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     const int m0 = tm * BMt, n0 = tn * BNW;
 
     const int ktiles = (a.K + BK - 1) / BK;
-    const int kt0 = blockIdx.z * a.ktiles_per_split;
-    const int kt1 = min(ktiles, kt0 + a.ktiles_per_split);
+    int kt0 = blockIdx.z * a.ktiles_per_split;
+    int kt1 = min(ktiles, kt0 + a.ktiles_per_split);
+    if (a.causal == 1 && n0 >= m0 + BMt) return;
+    if (a.causal == 2) kt1 = min(kt1, (m0 + BMt + BK - 1) / BK);
+    if (a.causal == 3) kt0 = max(kt0, m0 / BK);
     if (kt0 >= kt1) return;
 
     using LA = typename ASel<AM, PRO_A>::T;
@@ -558,7 +587,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                     const bool ok = mv[fm] && n + 4 <= a.N;
                     const long off = orow[fm] * a.ldc + n;
                     rv[fm][fn] = (a.ep_res && ok) ? *reinterpret_cast<const u16x4_t*>(a.ep_res + off) : u16x4_t{0, 0, 0, 0};
-                    tv[fm][fn] = (bnb && ok) ? *reinterpret_cast<const u16x4_t*>(a.ep_x + off) : u16x4_t{0, 0, 0, 0};
+                    const bf16_t* tsrc = bnb ? a.ep_x : a.ep_dgelu;
+                    tv[fm][fn] = (tsrc && ok) ? *reinterpret_cast<const u16x4_t*>(tsrc + off) : u16x4_t{0, 0, 0, 0};
                 }
         }
         uint32_t pk[4][FN][2];     // packed bf16 results (2 dwords = 4 columns per lane and fragment)
@@ -583,9 +613,25 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 for (int j = 0; j < 4; ++j) {
                     v[j] = acc[fm][fn][j] * a.alpha;
                     if (a.bias) v[j] += (n + j < a.N) ? a.bias[n + j] : 0.f;
-                    if (a.relu) v[j] = fmaxf(v[j], 0.f);
+                    if (a.relu == 1) v[j] = fmaxf(v[j], 0.f);
                 }
                 if constexpr (EM == E_BF16) {
+                    if (a.relu == 2) {
+                        if (a.ep_aux && ok) {
+                            u16x4_t pre;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
+                            bf16_t* ax = a.ep_aux + orow[fm] * a.ldc + n;
+                            if (n4) *reinterpret_cast<u16x4_t*>(ax) = pre;
+                            else for (int j = 0; j < 4 && n + j < a.N; ++j) ax[j] = pre[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(f2bf(v[j])));
+                    }
+                    if (a.ep_dgelu) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(tv[fm][fn][j]));
+                    }
                     if (a.ep_res) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) v[j] += bf2f(rv[fm][fn][j]);
@@ -676,7 +722,7 @@ FastDiv make_fdiv(uint32_t d) {
 }
 
 template <int AM, int BMODE, int EM, bool PA, bool PB, int BNW>
-int launch_w(const GemmArgs& a, int splits, hipStream_t st) {
+int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     static bool attr = false;
     constexpr int SM = smem_bytes<BNW, EM>();
     if (!attr) {
@@ -689,16 +735,16 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st) {
     int sm = SM;
     if (a.ktiles_per_split <= 1 && EM != E_ATOMIC) sm = (BMt + BNW) * BK * 2;
     const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW));
-    dim3 grid(tiles, 1, splits);
+    dim3 grid(tiles, batch, splits);
     hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), sm, st, a);
     PDNN_LAUNCH_RET;
 }
 
 // N <= 64: a 128x64 block tile; otherwise 128x128.
 template <int AM, int BMODE, int EM, bool PA, bool PB>
-int launch(const GemmArgs& a, int splits, hipStream_t st) {
-    if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st);
-    return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st);
+int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
+    if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
+    return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
 }
 
 template <int BNW>
@@ -729,6 +775,34 @@ static void ensure_attrs() {}
 // C API
 // ------------------------------------------------------------------------------------------------
 
+// Generic (batched) GEMM  C[M][N] = alpha * A . B  over nb1 x nb2 batches with two-level strides.
+//   amode: 0 = A row-major [M][K] (K-major), 1 = A stored [K][M] (reduction-major)
+//   bmode: 0 = B stored [N][K] (C = A.B^T),  1 = B stored [K][N]
+//   out:   0 = bf16, 1 = fp32;  res (bf16, laid out like C) is added in the epilogue when given
+//   causal: see GemmArgs::causal (0 for a dense GEMM)
+PDNN_API int pdnn_gemm_batched(int amode, int bmode, int out_f32, const bf16_t* A, long lda, long sA1, long sA2,
+                               const bf16_t* B, long ldb, long sB1, long sB2, void* C, long ldc, long sC1, long sC2,
+                               int M, int N, int K, int nb1, int nb2, float alpha, const bf16_t* res,
+                               int causal, hipStream_t st) {
+    GemmArgs a{};
+    a.causal = causal;
+    a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
+    a.alpha = alpha; a.ep_res = res; a.ktiles_per_split = (int)cdiv(K, BK);
+    a.nb2 = nb2 > 0 ? nb2 : 1;
+    a.sA1 = sA1; a.sA2 = sA2; a.sB1 = sB1; a.sB2 = sB2; a.sC1 = sC1; a.sC2 = sC2;
+    const int nb = (nb1 > 0 ? nb1 : 1) * a.nb2;
+    const int key = amode * 100 + bmode * 10 + out_f32;
+    switch (key) {
+        case 0: return launch<A_KMAJOR, B_KMAJOR, E_BF16, false, false>(a, 1, st, nb);
+        case 1: return launch<A_KMAJOR, B_KMAJOR, E_F32, false, false>(a, 1, st, nb);
+        case 10: return launch<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>(a, 1, st, nb);
+        case 11: return launch<A_KMAJOR, B_MNMAJOR, E_F32, false, false>(a, 1, st, nb);
+        case 110: return launch<A_MNMAJOR, B_MNMAJOR, E_BF16, false, false>(a, 1, st, nb);
+        case 111: return launch<A_MNMAJOR, B_MNMAJOR, E_F32, false, false>(a, 1, st, nb);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
 // Y[M][N] (bf16 or fp32) = alpha * X[M][K] . W[N][K]^T (+ bias) (relu)
 PDNN_API int pdnn_gemm_nt(const bf16_t* X, long ldx, const bf16_t* W, long ldw, void* Y, long ldy,
                           int M, int N, int K, float alpha, const float* bias, int relu, int out_f32,
@@ -739,6 +813,19 @@ PDNN_API int pdnn_gemm_nt(const bf16_t* X, long ldx, const bf16_t* W, long ldw, 
     a.alpha = alpha; a.bias = bias; a.relu = relu; a.ktiles_per_split = (int)cdiv(K, BK);
     return out_f32 ? launch<A_KMAJOR, B_KMAJOR, E_F32, false, false>(a, 1, st)
                    : launch<A_KMAJOR, B_KMAJOR, E_BF16, false, false>(a, 1, st);
+}
+
+// Y[M][N] = act(alpha * X[M][K] . W[N][K]^T + bias) (+ res); act 0/1/2 = none/ReLU/GELU; with GELU the
+// pre-activation is also written to aux (same ld) for the backward.  dgelu: Y *= gelu'(dgelu) instead.
+PDNN_API int pdnn_gemm_nt_ex(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t* Y, long ldy,
+                             int M, int N, int K, float alpha, const float* bias, int act, bf16_t* aux,
+                             const bf16_t* res, const bf16_t* dgelu, int w_kn, hipStream_t st) {
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = W; a.ldb = ldw; a.C = Y; a.ldc = ldy;
+    a.alpha = alpha; a.bias = bias; a.relu = act; a.ep_aux = aux; a.ep_res = res; a.ep_dgelu = dgelu;
+    a.ktiles_per_split = (int)cdiv(K, BK);
+    return w_kn ? launch<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>(a, 1, st)
+                : launch<A_KMAJOR, B_KMAJOR, E_BF16, false, false>(a, 1, st);
 }
 
 // Y[M][N] = alpha * X[M][K] . W[K][N]     (W row-major [K][N]: reduction-major B)

@@ -65,10 +65,15 @@ _SIGS = {
     "pdnn_nchw_to_nhwc": [P, I, P, I, I, I, I, P],
     "pdnn_nhwc_to_nchw_f32": [P, P, I, I, I, I, P],
     "pdnn_colsum": [P, L, I, P, I, P],
+    "pdnn_gemm_batched": [I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P, I, P],
+    "pdnn_gemm_nt_ex": [P, L, P, L, P, L, I, I, I, F, P, I, P, P, P, I, P],
     "pdnn_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
-    "pdnn_layernorm_bwd": [P, P, P, P, P, P, P, P, I, I, P, P],
-    "pdnn_attn_fwd": [P, P, P, P, P, I, I, I, I, L, L, F, I, P],
-    "pdnn_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, L, L, F, I, P],
+    "pdnn_layernorm_bwd_blocks": [I],
+    "pdnn_layernorm_bwd": [P, P, P, P, P, P, P, P, I, I, I, P],
+    "pdnn_attn_softmax_fwd": [P, L, P, L, P, I, I, F, I, P],
+    "pdnn_attn_softmax_bwd": [P, L, P, L, P, L, I, I, F, P],
+    "pdnn_embedding_fwd": [P, P, P, P, I, I, I, P],
+    "pdnn_embedding_bwd": [P, P, P, P, I, I, I, P],
     "pdnn_gemm_fp8_nt": [P, L, P, L, P, L, I, I, I, F, P, I, P],
     "pdnn_quant_fp8": [P, P, L, P, P, P],
     "pdnn_amax_f32": [P, L, P, I, P],

@@ -355,3 +355,86 @@ def axpy_(y, x, a):
 def sumsq(x, out):
     call("pdnn_sumsq_f32", ptr(x), x.numel(), ptr(out), stream())
     return out
+
+
+# ----------------------------------------------------------------------------------- transformer
+def gemm_batched(a, lda, sa, amode, b, ldb, sb, bmode, c, ldc, sc, M, N, K, nb, alpha=1.0, res=None, causal=0):
+    """Strided batched GEMM over nb = (nb1, nb2) batches: C = alpha * A . B (+res).
+
+    amode 0: A[M][K] row stride lda; 1: A stored [K][M].  bmode 0: B stored [N][K]; 1: B stored [K][N].
+    sa/sb/sc = (stride1, stride2) in elements.  ``c`` is a bf16 or fp32 tensor (base pointer)."""
+    _chk(lda % 8 == 0 and ldb % 8 == 0 and K % 8 == 0, "gemm_batched: 16-byte aligned leading dims")
+    _chk(all(s % 8 == 0 for s in (*sa, *sb)), "gemm_batched: 16-byte aligned batch strides")
+    _chk(c.dtype in (BF16, F32), "gemm_batched: bf16/fp32 output")
+    call("pdnn_gemm_batched", int(amode), int(bmode), int(c.dtype == F32), ptr(a), lda, sa[0], sa[1], ptr(b), ldb,
+         sb[0], sb[1], ptr(c), ldc, sc[0], sc[1], M, N, K, nb[0], nb[1], float(alpha), ptr(res), int(causal),
+         stream())
+    return c
+
+
+def gemm_nt_ex(x, w, bias=None, act=0, aux=None, res=None, dgelu=None, w_kn=False, out=None):
+    """y = act(x @ w^T + bias) (+res); act 0/1/2 = none/ReLU/GELU(tanh), GELU also stores the
+    pre-activation into ``aux``; ``dgelu``: y *= gelu'(dgelu).  ``w_kn``: w stored [K][N] (y = x @ w)."""
+    M, K = x.shape
+    N = w.shape[1] if w_kn else w.shape[0]
+    _chk((w.shape[0] if w_kn else w.shape[1]) == K and K % 8 == 0 and N % 8 == 0, f"gemm_nt_ex: {x.shape} {w.shape}")
+    _chk(x.stride(1) == 1 and w.is_contiguous() and x.stride(0) % 8 == 0, "gemm_nt_ex: row-major operands")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=BF16)
+    for t in (aux, res, dgelu):
+        _chk(t is None or (t.shape == out.shape and t.stride() == out.stride()), "gemm_nt_ex: epilogue operand shape")
+    call("pdnn_gemm_nt_ex", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), M, N, K, 1.0,
+         ptr(bias), int(act), ptr(aux), ptr(res), ptr(dgelu), int(w_kn), stream())
+    return out
+
+
+def layernorm_fwd(x, g, b, eps):
+    _bf16_c(x, "layernorm.x")
+    R, D = x.shape
+    _chk(D % 8 == 0 and D <= 2048, f"layernorm: D={D}")
+    y = torch.empty_like(x)
+    mean = torch.empty(R, device=x.device, dtype=F32)
+    rstd = torch.empty_like(mean)
+    call("pdnn_layernorm_fwd", ptr(x), ptr(g), ptr(b), ptr(y), ptr(mean), ptr(rstd), R, D, float(eps), stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, g, mean, rstd, dres=None):
+    """-> dx (+dres), dgamma, dbeta."""
+    R, D = x.shape
+    dy = dy.contiguous()
+    _chk(dy.shape == x.shape and (dres is None or dres.shape == x.shape), "layernorm_bwd: shapes")
+    nb = lib().pdnn_layernorm_bwd_blocks(R)
+    slab = torch.empty(2 * nb, D, device=x.device, dtype=F32)
+    dx = torch.empty_like(x)
+    call("pdnn_layernorm_bwd", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(slab), R, D,
+         nb, stream())
+    dg, db = bn_bwd_finalize(slab, nb)
+    return dx, dg, db
+
+
+def attn_softmax_fwd(S, P, lse, rows, T, scale, causal=True):
+    _chk(T % 4 == 0 and S.dtype == F32 and P.dtype == BF16 and S.numel() >= rows * T and P.numel() >= rows * T,
+         "attn_softmax_fwd: buffers")
+    call("pdnn_attn_softmax_fwd", ptr(S), T, ptr(P), T, ptr(lse), rows, T, float(scale), int(causal), stream())
+
+
+def attn_softmax_bwd(P, dP, dS, rows, T, scale):
+    _chk(T % 4 == 0 and dP.dtype == F32 and dS.dtype == BF16, "attn_softmax_bwd: buffers")
+    call("pdnn_attn_softmax_bwd", ptr(P), T, ptr(dP), T, ptr(dS), T, rows, T, float(scale), stream())
+
+
+def embedding_fwd(idx, wte, wpe, T):
+    R = idx.numel()
+    D = wte.shape[1]
+    _chk(idx.dtype == torch.int64 and idx.is_contiguous() and D % 8 == 0, "embedding: int64 ids, D % 8")
+    _chk(wpe is None or (wpe.shape[1] == D and wpe.shape[0] >= T), "embedding: wpe shape")
+    out = torch.empty(R, D, device=wte.device, dtype=BF16)
+    call("pdnn_embedding_fwd", ptr(idx), ptr(wte), ptr(wpe), ptr(out), R, T, D, stream())
+    return out
+
+
+def embedding_bwd(idx, g, dwte, dwpe, T):
+    R, D = g.shape
+    _chk(dwte.dtype == F32 and dwte.shape[1] == D and (dwpe is None or dwpe.shape[1] == D), "embedding_bwd")
+    call("pdnn_embedding_bwd", ptr(idx), ptr(g.contiguous()), ptr(dwte), ptr(dwpe), R, T, D, stream())

@@ -1,0 +1,220 @@
+"""Fused GPT-2 building blocks (BASELINE.json config 4: "GPT-2-small transformer DDP bf16 8xMI355X
+(LayerNorm + attention GEMM HIP kernels)").  The reference has no transformer (SURVEY.md §2 lists CNNs and
+MLPs only), so this is new capability exercising the same engine: every GEMM runs on the MFMA engine of
+``csrc/kernels/gemm_mfma.hip`` and every row op on ``csrc/kernels/transformer.hip``.
+
+A whole pre-LN block ``x + attn(ln_1(x))`` -> ``+ mlp(ln_2(.))`` is ONE autograd Function
+(:class:`GPT2BlockFn`) so the backward schedules its own kernels (fused epilogues, no autograd glue):
+
+forward                                              backward
+  ln1 = LN(x)                 layernorm_fwd            dh   = dx2 . Wfc2 * gelu'(u)   gemm_nt_ex (w_kn, dgelu epilogue)
+  qkv = ln1 Wqkv^T + b        gemm_nt_ex(bias)         dWfc2 += dx2^T h ; dbfc2 = colsum(dx2)
+  S   = Q K^T (per b, h)      gemm_batched(causal=1)   dln2 = dh . Wfc ; dWfc, dbfc
+  P   = softmax(S/sqrt(d))    attn_softmax_fwd         dx1  = LN2_bwd(dln2) + dx2     (residual fused)
+  y   = P V                   gemm_batched(causal=2)   dy   = dx1 . Wproj ; dWproj, dbproj
+  x1  = x + y Wproj^T + b     gemm_nt_ex(res=x)        attention bwd (dV, dP, dS, dQ, dK: 4 batched GEMMs
+  ln2 = LN(x1)                                               + attn_softmax_bwd), written into dqkv
+  h   = gelu(ln2 Wfc^T + b)   gemm_nt_ex(GELU, aux=u)  dln1 = dqkv . Wqkv ; dWqkv, dbqkv
+  x2  = x1 + h Wfc2^T + b     gemm_nt_ex(res=x1)       dx   = LN1_bwd(dln1) + dx1
+
+The residual stream is bf16 [B*T][D]; LayerNorm statistics, GEMM accumulation, softmax and all weight
+gradients are fp32.  Attention materialises the causal score matrix per (batch, head) — T=1024 fits
+easily in 288 GB of HBM — with tiles above the diagonal skipped (causal modes of the GEMM).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+# ------------------------------------------------------------------------------------------------
+# attention core on a packed qkv [B*T][3D] bf16 tensor
+# ------------------------------------------------------------------------------------------------
+def attention_fwd(qkv, B, T, H, causal=True):
+    """-> y [B*T][D] bf16, P [B*H*T][T] bf16 (saved for backward)."""
+    D = qkv.shape[1] // 3
+    d = D // H
+    ld = 3 * D
+    dev = qkv.device
+    S = torch.empty(B * H * T, T, device=dev, dtype=F32)
+    P = torch.empty(B * H * T, T, device=dev, dtype=BF16)
+    lse = torch.empty(B * H * T, device=dev, dtype=F32)
+    y = torch.empty(B * T, D, device=dev, dtype=BF16)
+    q, k, v = qkv, qkv[:, D:], qkv[:, 2 * D:]
+    # S[b,h] = Q K^T : A = Q [T][d] (K-major), B = K [T][d] (K-major)
+    K.gemm_batched(q, ld, (T * ld, d), 0, k, ld, (T * ld, d), 0, S, T, (H * T * T, T * T), T, T, d, (B, H),
+                   causal=1 if causal else 0)
+    K.attn_softmax_fwd(S, P, lse, B * H * T, T, 1.0 / math.sqrt(d), causal)
+    # y[b, :, h] = P V : A = P [T][T], B = V stored [T(k)][d]
+    K.gemm_batched(P, T, (H * T * T, T * T), 0, v, ld, (T * ld, d), 1, y, D, (T * D, d), T, d, T, (B, H),
+                   causal=2 if causal else 0)
+    return y, P, S
+
+
+def attention_bwd(dy, qkv, P, B, T, H, causal=True, dS_buf=None):
+    """dy [B*T][D] -> dqkv [B*T][3D].  ``dS_buf``: fp32 [B*H*T][T] scratch (the forward's S)."""
+    D = qkv.shape[1] // 3
+    d = D // H
+    ld = 3 * D
+    dev = qkv.device
+    dqkv = torch.empty(B * T, ld, device=dev, dtype=BF16)
+    q, k, v = qkv, qkv[:, D:], qkv[:, 2 * D:]
+    dq, dk, dv = dqkv, dqkv[:, D:], dqkv[:, 2 * D:]
+    sP = (H * T * T, T * T)
+    # dV = P^T dO : A = P stored [q][k] = [K][M] (amode 1), B = dO stored [q][d] = [K][N] (bmode 1)
+    K.gemm_batched(P, T, sP, 1, dy, D, (T * D, d), 1, dv, ld, (T * ld, d), T, d, T, (B, H),
+                   causal=3 if causal else 0)
+    # dP = dO V^T (fp32)
+    dP = dS_buf if dS_buf is not None else torch.empty(B * H * T, T, device=dev, dtype=F32)
+    K.gemm_batched(dy, D, (T * D, d), 0, v, ld, (T * ld, d), 0, dP, T, sP, T, T, d, (B, H),
+                   causal=1 if causal else 0)
+    # dS = P * (dP - rowsum(P dP)) / sqrt(d), written over P (row-local, read-before-write per element)
+    dS = P
+    K.attn_softmax_bwd(P, dP, dS, B * H * T, T, 1.0 / math.sqrt(d))
+    # dQ = dS K : B = K stored [k][d] = [K][N]
+    K.gemm_batched(dS, T, sP, 0, k, ld, (T * ld, d), 1, dq, ld, (T * ld, d), T, d, T, (B, H),
+                   causal=2 if causal else 0)
+    # dK = dS^T Q : A = dS stored [q][k] = [K][M], B = Q stored [q][d] = [K][N]
+    K.gemm_batched(dS, T, sP, 1, q, ld, (T * ld, d), 1, dk, ld, (T * ld, d), T, d, T, (B, H),
+                   causal=3 if causal else 0)
+    return dqkv
+
+
+def attention_reference(qkv, B, T, H, causal=True):
+    """fp32 PyTorch reference of :func:`attention_fwd` (tests, CPU path)."""
+    D = qkv.shape[1] // 3
+    q, k, v = qkv.float().view(B, T, 3, H, D // H).permute(2, 0, 3, 1, 4)
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=causal)
+    return y.transpose(1, 2).reshape(B * T, D)
+
+
+# ------------------------------------------------------------------------------------------------
+# LayerNorm
+# ------------------------------------------------------------------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2, weight, bias, eps):
+        y, mean, rstd = K.layernorm_fwd(x2, weight, bias, eps)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        dx, dg, db = K.layernorm_bwd(gy.to(BF16), x2, weight, mean, rstd)
+        return dx, dg, db, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    if not x.is_cuda:
+        return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1]).to(BF16).contiguous()
+    return _LayerNorm.apply(x2, weight, bias, eps).view(shp)
+
+
+# ------------------------------------------------------------------------------------------------
+# embedding (token + position)
+# ------------------------------------------------------------------------------------------------
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe):
+        ctx.save_for_backward(idx)
+        ctx.conf = (T, wte.shape, wpe.shape)
+        return K.embedding_fwd(idx, wte_k, wpe_k, T)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        T, s_te, s_pe = ctx.conf
+        dwte = torch.zeros(s_te, device=g.device, dtype=F32)
+        dwpe = torch.zeros(s_pe, device=g.device, dtype=F32)
+        K.embedding_bwd(idx, g, dwte, dwpe, T)
+        return None, None, None, None, dwte, dwpe
+
+
+# ------------------------------------------------------------------------------------------------
+# one transformer block
+# ------------------------------------------------------------------------------------------------
+def _wgrad(g, x, shape):
+    dw = torch.zeros(shape, device=g.device, dtype=F32)
+    K.gemm_tn_acc(g, x, dw)
+    return dw
+
+
+class GPT2BlockFn(torch.autograd.Function):
+    """params: ln1_w, ln1_b, attn_w, attn_b, proj_w, proj_b, ln2_w, ln2_b, fc_w, fc_b, fc2_w, fc2_b
+    shadows: bf16 copies of attn_w [3D][D], proj_w [D][D], fc_w [4D][D], fc2_w [D][4D]."""
+
+    @staticmethod
+    def forward(ctx, x, conf, shadows, *params):
+        B, T, H, eps = conf
+        ln1w, ln1b, _, attn_b, _, proj_b, ln2w, ln2b, _, fc_b, _, fc2_b = params
+        wqkv, wproj, wfc, wfc2 = shadows
+        ln1, m1, r1 = K.layernorm_fwd(x, ln1w, ln1b, eps)
+        qkv = K.gemm_nt_ex(ln1, wqkv, bias=attn_b)
+        y, P, S = attention_fwd(qkv, B, T, H)
+        x1 = K.gemm_nt_ex(y, wproj, bias=proj_b, res=x)
+        ln2, m2, r2 = K.layernorm_fwd(x1, ln2w, ln2b, eps)
+        u = torch.empty(x.shape[0], wfc.shape[0], device=x.device, dtype=BF16)
+        h = K.gemm_nt_ex(ln2, wfc, bias=fc_b, act=2, aux=u)
+        x2 = K.gemm_nt_ex(h, wfc2, bias=fc2_b, res=x1)
+        ctx.save_for_backward(x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, *shadows)
+        ctx.conf = conf
+        ctx.S = S          # reused as the fp32 dP scratch in backward
+        return x2
+
+    @staticmethod
+    def backward(ctx, g):
+        (x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, wqkv, wproj, wfc, wfc2) = ctx.saved_tensors
+        B, T, H, eps = ctx.conf
+        g = g.contiguous()
+        # MLP
+        du = K.gemm_nt_ex(g, wfc2, dgelu=u, w_kn=True)                 # (g . Wfc2) * gelu'(u)
+        dfc2_w, dfc2_b = _wgrad(g, h, wfc2.shape), K.colsum(g)
+        dln2 = K.gemm_nt_ex(du, wfc, w_kn=True)
+        dfc_w, dfc_b = _wgrad(du, ln2, wfc.shape), K.colsum(du)
+        dx1, dln2w, dln2b = K.layernorm_bwd(dln2, x1, ln2w, m2, r2, dres=g)
+        # attention
+        dy = K.gemm_nt_ex(dx1, wproj, w_kn=True)
+        dproj_w, dproj_b = _wgrad(dx1, y, wproj.shape), K.colsum(dx1)
+        dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
+        ctx.S = None
+        dln1 = K.gemm_nt_ex(dqkv, wqkv, w_kn=True)
+        dattn_w, dattn_b = _wgrad(dqkv, ln1, wqkv.shape), K.colsum(dqkv)
+        dx, dln1w, dln1b = K.layernorm_bwd(dln1, x, ln1w, m1, r1, dres=dx1)
+        return (dx, None, None, dln1w, dln1b, dattn_w, dattn_b, dproj_w, dproj_b, dln2w, dln2b, dfc_w, dfc_b,
+                dfc2_w, dfc2_b)
+
+
+# ------------------------------------------------------------------------------------------------
+# final LayerNorm + tied LM head + cross-entropy
+# ------------------------------------------------------------------------------------------------
+class LMHeadLossFn(torch.autograd.Function):
+    """loss = mean CE(LN_f(x) . Wte^T, targets); logits bf16 [B*T][V] live only inside this op."""
+
+    @staticmethod
+    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte):
+        xf, m, r = K.layernorm_fwd(x, lnw, lnb, eps)
+        logits = K.gemm_nt_ex(xf, wte_k)
+        _, lse, acc = K.xent_fwd(logits, targets)
+        ctx.save_for_backward(x, xf, m, r, logits, targets, lse, acc, lnw, wte_k)
+        ctx.eps = eps
+        return acc[0] / acc[1].clamp_min(1.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, xf, m, r, logits, targets, lse, acc, lnw, wte_k = ctx.saved_tensors
+        gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
+        dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
+        dxf = K.gemm_nt_ex(dlogits, wte_k, w_kn=True)
+        dwte = _wgrad(dlogits, xf, wte_k.shape)
+        dx, dlnw, dlnb = K.layernorm_bwd(dxf, x, lnw, m, r)
+        return dx, None, None, None, dlnw, dlnb, dwte
