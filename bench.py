@@ -115,7 +115,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (device-resident random token ids), random-init weights",
-            "final_loss": round(float(loss), 4),
+            "final_loss": round(float(loss.detach()), 4),
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
@@ -136,7 +136,7 @@ def main():
             "vs_stock_pytorch_rocm": round(value / (STOCK_PYTORCH_1GPU * world), 4),
             "dtype": "bf16",
             "data": "synthetic (device-resident random 224x224x3 images, random labels), random-init weights",
-            "final_loss": round(float(loss), 4),
+            "final_loss": round(float(loss.detach()), 4),
             "config": {"model": f"{a.model} (ImageNet layout, 224x224, 1000 classes)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
                        "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb},

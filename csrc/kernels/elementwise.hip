@@ -99,7 +99,47 @@ __global__ void __launch_bounds__(NT) colsum_kernel(const bf16_t* __restrict__ x
         out[c] = accumulate ? out[c] + t : t;
     }
 }
+
+// Two-level column sum for tall matrices (cols % 8 == 0): level 1 — block (column group of 512, row split
+// y) accumulates 8 columns per lane over its rows with 16-byte loads and writes one partial row;
+// level 2 sums the partial rows (deterministic, no atomics).
+__global__ void __launch_bounds__(NT) colsum_partial_kernel(const bf16_t* __restrict__ x, long rows, int cols,
+                                                            float* __restrict__ part) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = (blockIdx.x * 64 + lane) * 8;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < cols) {
+        for (long r = (long)blockIdx.y * 4 + w; r < rows; r += (long)gridDim.y * 4) {
+            float v[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(x + r * cols + c), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += v[j];
+        }
+    }
+    __shared__ float red[4][512];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = s[j];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 512; i += NT) {
+        const int cc = blockIdx.x * 512 + i;
+        if (cc < cols) part[(long)blockIdx.y * cols + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    }
+}
+
+__global__ void __launch_bounds__(NT) colsum_final_kernel(const float* __restrict__ part, int nrows, int cols,
+                                                          float* __restrict__ out, int accumulate) {
+    const int c = blockIdx.x * NT + threadIdx.x;
+    if (c >= cols) return;
+    float t = 0.f;
+    for (int r = 0; r < nrows; ++r) t += part[(long)r * cols + c];
+    out[c] = accumulate ? out[c] + t : t;
+}
 }  // namespace
+
+PDNN_API int pdnn_colsum_splits(long rows) {
+    const long s = (rows + 63) / 64;
+    return (int)(s < 1 ? 1 : (s > 64 ? 64 : s));
+}
 
 PDNN_API int pdnn_act_fwd(const bf16_t* x, bf16_t* y, long n, int op, hipStream_t st) {
     hipLaunchKernelGGL(act_fwd_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, x, y, n / 8, op);
@@ -127,7 +167,16 @@ PDNN_API int pdnn_nhwc_to_nchw_f32(const bf16_t* x, float* y, int N, int C, int 
                        HW, Cp);
     PDNN_LAUNCH_RET;
 }
-PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, x, rows, cols, out, accumulate);
+// work: pdnn_colsum_splits(rows) * cols floats (required when cols % 8 == 0 and rows > 256)
+PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int accumulate, float* work,
+                         hipStream_t st) {
+    if (work && cols % 8 == 0 && rows > 256) {
+        const int sp = pdnn_colsum_splits(rows);
+        hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 511) / 512, sp), dim3(NT), 0, st, x, rows, cols, work);
+        hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, work, sp, cols, out,
+                           accumulate);
+    } else {
+        hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, x, rows, cols, out, accumulate);
+    }
     PDNN_LAUNCH_RET;
 }

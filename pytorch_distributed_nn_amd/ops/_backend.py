@@ -64,7 +64,8 @@ _SIGS = {
     "pdnn_add": [P, P, P, L, F, F, P],
     "pdnn_nchw_to_nhwc": [P, I, P, I, I, I, I, P],
     "pdnn_nhwc_to_nchw_f32": [P, P, I, I, I, I, P],
-    "pdnn_colsum": [P, L, I, P, I, P],
+    "pdnn_colsum": [P, L, I, P, I, P, P],
+    "pdnn_colsum_splits": [L],
     "pdnn_gemm_batched": [I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P, I, P],
     "pdnn_gemm_nt_ex": [P, L, P, L, P, L, I, I, I, F, P, I, P, P, P, I, P],
     "pdnn_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],

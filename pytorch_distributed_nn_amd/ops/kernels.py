@@ -321,7 +321,10 @@ def colsum(x2d, out=None, accumulate=False):
     R, C = x2d.shape
     if out is None:
         out = torch.empty(C, device=x2d.device, dtype=F32)
-    call("pdnn_colsum", ptr(x2d), R, C, ptr(out), int(accumulate), stream())
+    work = None
+    if C % 8 == 0 and R > 256 and x2d.is_contiguous():
+        work = torch.empty(lib().pdnn_colsum_splits(R) * C, device=x2d.device, dtype=F32)
+    call("pdnn_colsum", ptr(x2d), R, C, ptr(out), int(accumulate), ptr(work), stream())
     return out
 
 

@@ -248,3 +248,28 @@ def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
     xh = (t.float() - mean) * inv
     assert torch.allclose(sums[0], gm_ref.reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
     assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("R,C", [(100, 10), (8192, 768), (8192, 3072), (3000, 2304), (513, 40)])
+def test_colsum(K, R, C):
+    x = rnd(R, C)
+    out = K.colsum(x)
+    ref = x.float().sum(0)
+    assert rel(out, ref) < 1e-4
+    K.colsum(x, out=out, accumulate=True)
+    assert rel(out, 2 * ref) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1000, 776, 1024), (2048, 2048, 64), (4104, 1032, 768), (8192, 3072, 768)])
+def test_gemm_large_tile_engine(K, M, N, Kd):
+    """Shapes routed to the 256x256 glds engine (K % 64 == 0, enough tiles), incl. ragged M/N edges."""
+    x, w = rnd(M, Kd), rnd(N, Kd)
+    b = torch.randn(N, device="cuda")
+    assert rel(K.gemm_nt(x, w, bias=b), x.float() @ w.float().t() + b) < 1e-2
+    assert rel(K.gemm_nt(x, w, out_f32=True), x.float() @ w.float().t()) < 2e-3
+    wt = w.t().contiguous()
+    assert rel(K.gemm_nn(x, wt), x.float() @ wt.float()) < 1e-2
+    g = rnd(M, N)
+    dw = torch.zeros(N, Kd, device="cuda")
+    K.gemm_tn_acc(g, x, dw)
+    assert rel(dw, g.float().t() @ x.float()) < 2e-3
