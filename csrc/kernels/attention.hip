@@ -1,0 +1,478 @@
+// Fused causal attention for head dim 64 (GPT-2; SURVEY.md §2.8 K-18 "flash-style attention"), bf16
+// operands, fp32 softmax/accumulation, on the gfx950 MFMA 16x16x32 bf16 instruction.
+//
+// Layout: q, k, v are column blocks of the packed c_attn output qkv[B*T][3D] (ld = 3D): head h of
+// token t of sequence b lives at row b*T + t, columns h*64 (q), D + h*64 (k), 2D + h*64 (v).  The output
+// o[B*T][D] and the gradient dqkv[B*T][3D] use the same packing, so no head split/merge copies exist.
+//
+// Forward (one block = 128 queries of one (b, h), 4 waves x 32 queries; K/V tiles of 64 keys
+// register-staged into double-buffered LDS, one barrier per tile):
+//   S^T = K Q^T  ->  lane holds S^T[key = 16f + 4g + r][query = lane & 15]  (g = lane >> 4)
+//   online softmax per query (= per lane; the 4 lane groups are combined by two xor-shuffles)
+//   O^T += V^T P^T: P^T is consumed straight from the accumulator registers as the B operand of the
+//   next MFMA (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"); the k order
+//   inside an MFMA step is permuted (element e of lane group g = key 4g + e or 16 + 4g + e - 4), and the
+//   V^T operand is read with ds_read_b64_tr_b16 from exactly those permuted key rows, so no LDS round trip
+//   of P is needed.
+// Saves lse2 = m + log2(sum) (base-2, scaled-score domain) per query for the backward.
+//
+// Backward (FlashAttention-2 split, both kernels recompute P from lse2):
+//   attn_bwd_dkdv: one block = 64 keys (4 waves x 16 keys), loop over query tiles q >= key:
+//       S = Q K^T, P, dV^T += dO^T P, dP = dO V^T, dS = P (dP - delta), dK^T += Q^T dS
+//   attn_bwd_dq:   one block = 64 queries (4 waves x 16 queries), loop over key tiles k <= query:
+//       S^T = K Q^T, P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T
+//   delta[q] = sum_d dO[q][d] O[q][d] comes from attn_bwd_delta.
+#include "common.h"
+
+namespace {
+constexpr int HD = 64;          // head dim
+constexpr int NTA = 256;
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// [64][64] bf16 tile image, 128-byte rows, 16-byte chunk c of row r at chunk c ^ ((r >> 1) & 7)
+__device__ __forceinline__ int toff(int row, int chunk) { return row * HD + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+// K-major fragment: lane -> row (row0 + (lane & 15)), k = 32 ks + 8 (lane >> 4) .. +7
+__device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int row0, int ks, int lane) {
+    const int row = row0 + (lane & 15);
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(img + toff(row, ks * 4 + (lane >> 4))));
+}
+
+// Transposed fragment for an MFMA step over 32 tile rows [32 kk, 32 kk + 32) in the permuted order of
+// an accumulator-sourced operand: lane (col = col0 + (lane & 15), group g) receives rows
+// 32kk + 4g + 0..3 (elements 0-3) and 32kk + 16 + 4g + 0..3 (elements 4-7) of column col.
+__device__ __forceinline__ bf16x8_t frag_tr_perm(const bf16_t* img, int col0, int kk, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = col0 + 4 * p;
+    const int r0 = 32 * kk + 4 * g + q;
+    const bf16_t* p0 = img + toff(r0, col >> 3) + (col & 7);
+    const bf16_t* p1 = img + toff(r0 + 16, col >> 3) + (col & 7);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// two fp32 accumulator fragments (rows 4g + r of fragment a and b) -> one bf16 B operand (permuted k)
+__device__ __forceinline__ bf16x8_t pack_acc(const f32x4_t& a, const f32x4_t& b) {
+    s16x8 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[r] = (short)f2bf(a[r]);
+        v[4 + r] = (short)f2bf(b[r]);
+    }
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__device__ __forceinline__ f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// global fragment load: row-major [rows][ld] source, lane -> row (lane & 15), 8 k at 32 ks + 8 g
+__device__ __forceinline__ bf16x8_t gfrag(const bf16_t* base, long ld, int ks, int lane) {
+    const bf16_t* p = base + (long)(lane & 15) * ld + ks * 32 + 8 * (lane >> 4);
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(p));
+}
+
+// 64 x 64 tile: 256 threads x 2 chunks
+struct TileLd {
+    u16x8_t r[2];
+    __device__ __forceinline__ void load(const bf16_t* src, long ld, int tid) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = (tid >> 3) + 32 * i, ch = tid & 7;
+            r[i] = *reinterpret_cast<const u16x8_t*>(src + (long)row * ld + ch * 8);
+        }
+    }
+    __device__ __forceinline__ void store(bf16_t* img, int tid) const {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = (tid >> 3) + 32 * i, ch = tid & 7;
+            *reinterpret_cast<u16x8_t*>(img + toff(row, ch)) = r[i];
+        }
+    }
+};
+
+__device__ __forceinline__ float xmax16(float v) {
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float xsum16(float v) {
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
+// ---------------------------------------------------------------------------------------------- forward
+__global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                       float* __restrict__ lse2, int T, int H, float scale, int causal) {
+    __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const int nqb = T / 128;
+    const int qb = nqb - 1 - blockIdx.x;             // heavy (late) query tiles first
+    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    const long ld = 3L * D;
+    const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
+    const bf16_t* Kp = Q + D;
+    const bf16_t* Vp = Q + 2 * D;
+    const int q0 = qb * 128 + 32 * w;                // this wave's 32 queries
+    const float c = scale * LOG2E;
+
+    bf16x8_t qf[2][2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[f][ks] = gfrag(Q + (long)(q0 + 16 * f) * ld, ld, ks, lane);
+
+    f32x4_t o[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) o[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+    const int nkb = causal ? (qb * 128 + 128) / 64 : T / 64;
+    TileLd tk, tv;
+    tk.load(Kp, ld, tid);
+    tv.load(Vp, ld, tid);
+    tk.store(smem[0][0], tid);
+    tv.store(smem[0][1], tid);
+    __syncthreads();
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int cur = kb & 1;
+        const bool more = kb + 1 < nkb;
+        if (more) {
+            tk.load(Kp + (long)(kb + 1) * 64 * ld, ld, tid);
+            tv.load(Vp + (long)(kb + 1) * 64 * ld, ld, tid);
+        }
+        const int k0 = kb * 64;
+        if (!causal || k0 <= q0 + 31) {              // wave-uniform: tile not entirely above the diagonal
+            const bf16_t* Ki = smem[cur][0];
+            const bf16_t* Vi = smem[cur][1];
+            f32x4_t s[4][2];
+#pragma unroll
+            for (int kf = 0; kf < 4; ++kf) {
+                const bf16x8_t a0 = frag_rows(Ki, 16 * kf, 0, lane), a1 = frag_rows(Ki, 16 * kf, 1, lane);
+#pragma unroll
+                for (int f = 0; f < 2; ++f) {
+                    f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                    z = mfma(a0, qf[f][0], z);
+                    s[kf][f] = mfma(a1, qf[f][1], z);
+                }
+            }
+            const bool diag = causal && k0 + 63 > q0;
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const int qi = q0 + 16 * f + (lane & 15);
+                float mx = -INFINITY;
+#pragma unroll
+                for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = s[kf][f][r] * c;
+                        if (diag && k0 + 16 * kf + 4 * g + r > qi) v = -INFINITY;
+                        s[kf][f][r] = v;
+                        mx = fmaxf(mx, v);
+                    }
+                mx = xmax16(mx);
+                const float mn = fmaxf(m[f], mx);
+                const float alpha = exp2f(m[f] - mn);
+                float rs = 0.f;
+#pragma unroll
+                for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float p = exp2f(s[kf][f][r] - mn);
+                        s[kf][f][r] = p;
+                        rs += p;
+                    }
+                l[f] = l[f] * alpha + xsum16(rs);
+                m[f] = mn;
+#pragma unroll
+                for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                bf16x8_t pb[2];
+#pragma unroll
+                for (int f = 0; f < 2; ++f) pb[f] = pack_acc(s[2 * kk][f], s[2 * kk + 1][f]);
+#pragma unroll
+                for (int df = 0; df < 4; ++df) {
+                    const bf16x8_t va = frag_tr_perm(Vi, 16 * df, kk, lane);
+#pragma unroll
+                    for (int f = 0; f < 2; ++f) o[df][f] = mfma(va, pb[f], o[df][f]);
+                }
+            }
+        }
+        if (more) {
+            tk.store(smem[cur ^ 1][0], tid);
+            tv.store(smem[cur ^ 1][1], tid);
+        }
+        __syncthreads();
+    }
+    // lane holds O^T[d = 16 df + 4 g + r][q = q0 + 16 f + (lane & 15)]
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int qi = q0 + 16 * f + (lane & 15);
+        const float inv = 1.f / l[f];
+        bf16_t* op = out + ((long)b * T + qi) * D + h * HD;
+#pragma unroll
+        for (int df = 0; df < 4; ++df) {
+            u16x4_t v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = f2bf(o[df][f][r] * inv);
+            *reinterpret_cast<u16x4_t*>(op + 16 * df + 4 * g) = v;
+        }
+        if (g == 0) lse2[((long)b * H + h) * T + qi] = m[f] + __log2f(l[f]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------- backward
+// delta[b][h][t] = sum_d dO . O   (one thread per (row, head), 8 x 16-byte loads each)
+__global__ void __launch_bounds__(NTA) attn_bwd_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dO,
+                                                             float* __restrict__ delta, int BT, int T, int H) {
+    const long i = (long)blockIdx.x * NTA + threadIdx.x;
+    if (i >= (long)BT * H) return;
+    const long row = i / H;
+    const int h = (int)(i - row * H);
+    const int D = H * HD;
+    const bf16_t* a = o + row * D + h * HD;
+    const bf16_t* bb = dO + row * D + h * HD;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float x[8], y[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(a + 8 * c), x);
+        unpack8(*reinterpret_cast<const u16x8_t*>(bb + 8 * c), y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+    }
+    const long bidx = row / T, t = row - bidx * T;
+    delta[(bidx * H + h) * T + t] = s;
+}
+
+// dK, dV for 64 keys per block (wave w: keys k0 + 16 w .. +15); loop over 64-query tiles
+__global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
+                                                            const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                            bf16_t* __restrict__ dqkv, int T, int H, float scale,
+                                                            int causal) {
+    __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][Q|dO]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const int nkb = T / 64;
+    const int kb = blockIdx.x;                       // early key tiles have the most work: launched first
+    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    const long ld = 3L * D;
+    const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
+    const bf16_t* Kp = Q + D;
+    const bf16_t* Vp = Q + 2 * D;
+    const bf16_t* dOp = dO + (long)b * T * D + h * HD;
+    const float* L2 = lse2 + ((long)b * H + h) * T;
+    const float* Dl = delta + ((long)b * H + h) * T;
+    const int k0 = kb * 64 + 16 * w;
+    const int kl = k0 + (lane & 15);                 // this lane's key
+    const float c = scale * LOG2E;
+
+    bf16x8_t kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        kf[ks] = gfrag(Kp + (long)k0 * ld, ld, ks, lane);
+        vf[ks] = gfrag(Vp + (long)k0 * ld, ld, ks, lane);
+    }
+    f32x4_t dv[4], dk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dv[i] = dk[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int qb0 = causal ? kb : 0;
+    const int nqb = T / 64;
+    TileLd tq, tdo;
+    tq.load(Q + (long)qb0 * 64 * ld, ld, tid);
+    tdo.load(dOp + (long)qb0 * 64 * D, D, tid);
+    tq.store(smem[0][0], tid);
+    tdo.store(smem[0][1], tid);
+    __syncthreads();
+    for (int qb = qb0; qb < nqb; ++qb) {
+        const int cur = (qb - qb0) & 1;
+        const bool more = qb + 1 < nqb;
+        if (more) {
+            tq.load(Q + (long)(qb + 1) * 64 * ld, ld, tid);
+            tdo.load(dOp + (long)(qb + 1) * 64 * D, D, tid);
+        }
+        const int qs = qb * 64;
+        if (!causal || qs + 63 >= k0) {
+            const bf16_t* Qi = smem[cur][0];
+            const bf16_t* Oi = smem[cur][1];
+            // S[q][key], dP[q][key]: lane holds rows q = qs + 16 qi + 4 g + r, column key = kl
+            f32x4_t s[4], dp[4];
+#pragma unroll
+            for (int qi = 0; qi < 4; ++qi) {
+                f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                z = mfma(frag_rows(Qi, 16 * qi, 0, lane), kf[0], z);
+                s[qi] = mfma(frag_rows(Qi, 16 * qi, 1, lane), kf[1], z);
+                f32x4_t y = {0.f, 0.f, 0.f, 0.f};
+                y = mfma(frag_rows(Oi, 16 * qi, 0, lane), vf[0], y);
+                dp[qi] = mfma(frag_rows(Oi, 16 * qi, 1, lane), vf[1], y);
+            }
+#pragma unroll
+            for (int qi = 0; qi < 4; ++qi) {
+                const int qr = qs + 16 * qi + 4 * g;
+                const float4 lv = *reinterpret_cast<const float4*>(L2 + qr);
+                const float4 dl = *reinterpret_cast<const float4*>(Dl + qr);
+                const float la[4] = {lv.x, lv.y, lv.z, lv.w}, da[4] = {dl.x, dl.y, dl.z, dl.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float p = exp2f(s[qi][r] * c - la[r]);
+                    if (causal && kl > qr + r) p = 0.f;
+                    s[qi][r] = p;
+                    dp[qi][r] = p * (dp[qi][r] - da[r]);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const bf16x8_t pb = pack_acc(s[2 * kk], s[2 * kk + 1]);
+                const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+#pragma unroll
+                for (int df = 0; df < 4; ++df) {
+                    dv[df] = mfma(frag_tr_perm(Oi, 16 * df, kk, lane), pb, dv[df]);
+                    dk[df] = mfma(frag_tr_perm(Qi, 16 * df, kk, lane), sb, dk[df]);
+                }
+            }
+        }
+        if (more) {
+            tq.store(smem[cur ^ 1][0], tid);
+            tdo.store(smem[cur ^ 1][1], tid);
+        }
+        __syncthreads();
+    }
+    // lane holds dK^T / dV^T [d = 16 df + 4 g + r][key = kl]
+    bf16_t* dkp = dqkv + ((long)b * T + kl) * ld + D + h * HD;
+    bf16_t* dvp = dkp + D;
+#pragma unroll
+    for (int df = 0; df < 4; ++df) {
+        u16x4_t a, v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            a[r] = f2bf(dk[df][r] * scale);
+            v[r] = f2bf(dv[df][r]);
+        }
+        *reinterpret_cast<u16x4_t*>(dkp + 16 * df + 4 * g) = a;
+        *reinterpret_cast<u16x4_t*>(dvp + 16 * df + 4 * g) = v;
+    }
+}
+
+// dQ for 64 queries per block (wave w: queries q0 + 16 w .. +15); loop over 64-key tiles
+__global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
+                                                          const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                          bf16_t* __restrict__ dqkv, int T, int H, float scale,
+                                                          int causal) {
+    __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const int nqb = T / 64;
+    const int qb = nqb - 1 - blockIdx.x;
+    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    const long ld = 3L * D;
+    const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
+    const bf16_t* Kp = Q + D;
+    const bf16_t* Vp = Q + 2 * D;
+    const bf16_t* dOp = dO + (long)b * T * D + h * HD;
+    const int q0 = qb * 64 + 16 * w;
+    const int ql = q0 + (lane & 15);
+    const float c = scale * LOG2E;
+    const float lq = lse2[((long)b * H + h) * T + ql];
+    const float dq_ = delta[((long)b * H + h) * T + ql];
+
+    bf16x8_t qf[2], of[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        qf[ks] = gfrag(Q + (long)q0 * ld, ld, ks, lane);
+        of[ks] = gfrag(dOp + (long)q0 * D, D, ks, lane);
+    }
+    f32x4_t dq[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dq[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int nkb = causal ? qb + 1 : T / 64;
+    TileLd tk, tv;
+    tk.load(Kp, ld, tid);
+    tv.load(Vp, ld, tid);
+    tk.store(smem[0][0], tid);
+    tv.store(smem[0][1], tid);
+    __syncthreads();
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int cur = kb & 1;
+        const bool more = kb + 1 < nkb;
+        if (more) {
+            tk.load(Kp + (long)(kb + 1) * 64 * ld, ld, tid);
+            tv.load(Vp + (long)(kb + 1) * 64 * ld, ld, tid);
+        }
+        const int k0 = kb * 64;
+        if (!causal || k0 <= q0 + 15) {
+            const bf16_t* Ki = smem[cur][0];
+            const bf16_t* Vi = smem[cur][1];
+            // S^T[key][q], dP^T[key][q]: lane holds rows key = k0 + 16 ki + 4 g + r, column q = ql
+            f32x4_t s[4], dp[4];
+#pragma unroll
+            for (int ki = 0; ki < 4; ++ki) {
+                f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                z = mfma(frag_rows(Ki, 16 * ki, 0, lane), qf[0], z);
+                s[ki] = mfma(frag_rows(Ki, 16 * ki, 1, lane), qf[1], z);
+                f32x4_t y = {0.f, 0.f, 0.f, 0.f};
+                y = mfma(frag_rows(Vi, 16 * ki, 0, lane), of[0], y);
+                dp[ki] = mfma(frag_rows(Vi, 16 * ki, 1, lane), of[1], y);
+            }
+#pragma unroll
+            for (int ki = 0; ki < 4; ++ki)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float p = exp2f(s[ki][r] * c - lq);
+                    if (causal && k0 + 16 * ki + 4 * g + r > ql) p = 0.f;
+                    dp[ki][r] = p * (dp[ki][r] - dq_);
+                }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+#pragma unroll
+                for (int df = 0; df < 4; ++df) dq[df] = mfma(frag_tr_perm(Ki, 16 * df, kk, lane), sb, dq[df]);
+            }
+        }
+        if (more) {
+            tk.store(smem[cur ^ 1][0], tid);
+            tv.store(smem[cur ^ 1][1], tid);
+        }
+        __syncthreads();
+    }
+    bf16_t* dqp = dqkv + ((long)b * T + ql) * ld + h * HD;
+#pragma unroll
+    for (int df = 0; df < 4; ++df) {
+        u16x4_t a;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = f2bf(dq[df][r] * scale);
+        *reinterpret_cast<u16x4_t*>(dqp + 16 * df + 4 * g) = a;
+    }
+}
+}  // namespace
+
+// qkv [B*T][3*H*64] bf16 -> out [B*T][H*64] bf16, lse2 [B][H][T] fp32.  T % 128 == 0.
+PDNN_API int pdnn_flash_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse2, int B, int T, int H, float scale,
+                                 int causal, hipStream_t st) {
+    if (T % 128) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3(T / 128, H, B), dim3(NTA), 0, st, qkv, out, lse2, T, H, scale, causal);
+    PDNN_LAUNCH_RET;
+}
+
+// dO [B*T][H*64], out/lse2 from the forward -> dqkv [B*T][3*H*64]; delta: fp32 [B][H][T] scratch.
+PDNN_API int pdnn_flash_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dO, const float* lse2,
+                                 float* delta, bf16_t* dqkv, int B, int T, int H, float scale, int causal,
+                                 hipStream_t st) {
+    if (T % 128) return (int)hipErrorInvalidValue;
+    const long n = (long)B * T * H;
+    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n + NTA - 1) / NTA)), dim3(NTA), 0, st, out, dO, delta,
+                       B * T, T, H);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
+                       scale, causal);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
+                       scale, causal);
+    PDNN_LAUNCH_RET;
+}

@@ -427,6 +427,26 @@ def attn_softmax_bwd(P, dP, dS, rows, T, scale):
     call("pdnn_attn_softmax_bwd", ptr(P), T, ptr(dP), T, ptr(dS), T, rows, T, float(scale), stream())
 
 
+def flash_attn_fwd(qkv, B, T, H, scale, causal=True):
+    """Fused attention, head dim 64: qkv [B*T][3*H*64] -> (out [B*T][H*64], lse2 [B][H][T])."""
+    _bf16_c(qkv, "flash_attn.qkv")
+    _chk(qkv.shape == (B * T, 3 * H * 64) and T % 128 == 0, f"flash_attn: qkv {tuple(qkv.shape)} B={B} T={T} H={H}")
+    out = torch.empty(B * T, H * 64, device=qkv.device, dtype=BF16)
+    lse2 = torch.empty(B, H, T, device=qkv.device, dtype=F32)
+    call("pdnn_flash_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), B, T, H, float(scale), int(causal), stream())
+    return out, lse2
+
+
+def flash_attn_bwd(qkv, out, dout, lse2, B, T, H, scale, causal=True):
+    dout = dout.contiguous()
+    _chk(dout.shape == out.shape and lse2.shape == (B, H, T), "flash_attn_bwd: shapes")
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, H, T, device=qkv.device, dtype=F32)
+    call("pdnn_flash_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(delta), ptr(dqkv), B, T, H, float(scale),
+         int(causal), stream())
+    return dqkv
+
+
 def embedding_fwd(idx, wte, wpe, T):
     R = idx.numel()
     D = wte.shape[1]

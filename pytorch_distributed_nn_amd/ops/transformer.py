@@ -18,8 +18,10 @@ forward                                              backward
   x2  = x1 + h Wfc2^T + b     gemm_nt_ex(res=x1)       dx   = LN1_bwd(dln1) + dx1
 
 The residual stream is bf16 [B*T][D]; LayerNorm statistics, GEMM accumulation, softmax and all weight
-gradients are fp32.  Attention materialises the causal score matrix per (batch, head) — T=1024 fits
-easily in 288 GB of HBM — with tiles above the diagonal skipped (causal modes of the GEMM).
+gradients are fp32.  Attention (head dim 64, T % 128 == 0) runs the fused flash kernels of
+``csrc/kernels/attention.hip`` (scores never leave registers; backward recomputes P from the saved
+log-sum-exp); other shapes fall back to the materialised path below (batched MFMA GEMMs with causal tile
+skipping + row-softmax kernels).
 """
 from __future__ import annotations
 
@@ -85,6 +87,10 @@ def attention_bwd(dy, qkv, P, B, T, H, causal=True, dS_buf=None):
     K.gemm_batched(dS, T, sP, 1, q, ld, (T * ld, d), 1, dk, ld, (T * ld, d), T, d, T, (B, H),
                    causal=3 if causal else 0)
     return dqkv
+
+
+def use_flash(T, D, H):
+    return D // H == 64 and T % 128 == 0
 
 
 def attention_reference(qkv, B, T, H, causal=True):
@@ -160,7 +166,13 @@ class GPT2BlockFn(torch.autograd.Function):
         wqkv, wproj, wfc, wfc2 = shadows
         ln1, m1, r1 = K.layernorm_fwd(x, ln1w, ln1b, eps)
         qkv = K.gemm_nt_ex(ln1, wqkv, bias=attn_b)
-        y, P, S = attention_fwd(qkv, B, T, H)
+        D = x.shape[1]
+        flash = use_flash(T, D, H)
+        if flash:
+            y, P = K.flash_attn_fwd(qkv, B, T, H, 1.0 / math.sqrt(D // H))     # P := lse2
+            S = None
+        else:
+            y, P, S = attention_fwd(qkv, B, T, H)
         x1 = K.gemm_nt_ex(y, wproj, bias=proj_b, res=x)
         ln2, m2, r2 = K.layernorm_fwd(x1, ln2w, ln2b, eps)
         u = torch.empty(x.shape[0], wfc.shape[0], device=x.device, dtype=BF16)
@@ -168,7 +180,8 @@ class GPT2BlockFn(torch.autograd.Function):
         x2 = K.gemm_nt_ex(h, wfc2, bias=fc2_b, res=x1)
         ctx.save_for_backward(x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, *shadows)
         ctx.conf = conf
-        ctx.S = S          # reused as the fp32 dP scratch in backward
+        ctx.flash = flash
+        ctx.S = S          # materialised path: reused as the fp32 dP scratch in backward
         return x2
 
     @staticmethod
@@ -185,7 +198,10 @@ class GPT2BlockFn(torch.autograd.Function):
         # attention
         dy = K.gemm_nt_ex(dx1, wproj, w_kn=True)
         dproj_w, dproj_b = _wgrad(dx1, y, wproj.shape), K.colsum(dx1)
-        dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
+        if ctx.flash:
+            dqkv = K.flash_attn_bwd(qkv, y, dy, P, B, T, H, 1.0 / math.sqrt(x.shape[1] // H))
+        else:
+            dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
         ctx.S = None
         dln1 = K.gemm_nt_ex(dqkv, wqkv, w_kn=True)
         dattn_w, dattn_b = _wgrad(dqkv, ln1, wqkv.shape), K.colsum(dqkv)

@@ -187,3 +187,27 @@ def test_gpt2_tiny_trains():
         opt.step()
         first = first if first is not None else loss.item()
     assert math.isfinite(loss.item()) and loss.item() < 0.7 * first
+
+
+@pytest.mark.parametrize("B,T,H,causal", [(2, 256, 3, True), (1, 128, 2, False), (2, 1024, 2, True), (1, 384, 1, False)])
+def test_flash_attention(K, B, T, H, causal):
+    from pytorch_distributed_nn_amd.ops import transformer as TX
+    D = 64 * H
+    qkv = rnd(B * T, 3 * D)
+    y, lse2 = K.flash_attn_fwd(qkv, B, T, H, 0.125, causal)
+    qr = qkv.float().requires_grad_(True)
+    ref = TX.attention_reference(qr, B, T, H, causal)
+    assert rel2(y, ref) < 1e-2
+    # log-sum-exp (base 2, scaled domain) vs reference
+    q, k, _ = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if causal:
+        s = s.masked_fill(torch.ones(T, T, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
+    assert rel(lse2, torch.logsumexp(s, -1) * 1.4426950408889634) < 1e-3
+    dy = rnd(B * T, D)
+    ref.backward(dy.float())
+    dqkv = K.flash_attn_bwd(qkv, y, dy, lse2, B, T, H, 0.125, causal)
+    for i, n in enumerate("qkv"):
+        a, b = dqkv[:, i * D:(i + 1) * D], qr.grad[:, i * D:(i + 1) * D]
+        assert rel2(a, b) < 3e-2, n
+        assert cos(a, b) > 0.999, n
