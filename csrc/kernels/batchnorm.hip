@@ -227,7 +227,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
 
 // sum partial rows -> dbeta (= sum gm), dgamma (= sum gm*xhat).  Optionally accumulate (+=).
 __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             float* dgamma, float* dbeta, int accumulate) {
+                                                             float* dgamma, float* dbeta, int accumulate,
+                                                             float* gacc, float* bacc) {
     const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
     __shared__ double red[2][4][64];
     double s = 0.0, q = 0.0;
@@ -245,6 +246,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __rest
     q = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
     if (accumulate) { dbeta[c] += (float)s; dgamma[c] += (float)q; }
     else { dbeta[c] = (float)s; dgamma[c] = (float)q; }
+    if (gacc) { gacc[c] += (float)q; bacc[c] += (float)s; }     // direct accumulation into param grads
 }
 
 // dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
@@ -364,8 +366,10 @@ PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C,
     PDNN_LAUNCH_RET;
 }
 
+// dgamma/dbeta of this backward (consumed by bn_bwd_apply); gacc/bacc (optional): also added into the
+// parameters' gradient accumulators.
 PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dgamma, float* dbeta,
-                                  int accumulate, float* work, hipStream_t st) {
+                                  int accumulate, float* work, float* gacc, float* bacc, hipStream_t st) {
     const float* src = slab;
     int r = rows;
     if (rows > 64) {
@@ -374,7 +378,7 @@ PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dga
         r = 64;
     }
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, st, src, r, C, dgamma,
-                       dbeta, accumulate);
+                       dbeta, accumulate, gacc, bacc);
     PDNN_LAUNCH_RET;
 }
 

@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..optim.flat import direct_grad, grad_ready
 from . import kernels as K
 
 BF16 = torch.bfloat16
@@ -164,6 +165,8 @@ class _Linear(torch.autograd.Function):
         y = K.gemm_nt(x2, wk, bias=bias, relu=relu)
         ctx.save_for_backward(x2, wk, y if relu else None)
         ctx.conf = (bias is not None, relu, weight.shape)
+        # unpadded weight/bias: their gradients can be accumulated straight into the flat arena
+        ctx.direct = (weight, bias) if wk.shape == weight.shape else None
         return y
 
     @staticmethod
@@ -175,12 +178,26 @@ class _Linear(torch.autograd.Function):
             gy = K.act_bwd(gy, y, "relu")
         dx = K.gemm_nn(gy, wk) if ctx.needs_input_grad[0] else None
         dw = db = None
+        direct, ctx.direct = ctx.direct, None
+        ready = []
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros(wk.shape, device=gy.device, dtype=torch.float32)
-            K.gemm_tn_acc(gy, x2, dw)
-            dw = dw[: wshape[0], : wshape[1]]
+            tw = direct_grad(direct[0]) if direct is not None else None
+            if tw is not None:
+                K.gemm_tn_acc(gy, x2, tw)
+                ready.append(direct[0])
+            else:
+                dw = torch.zeros(wk.shape, device=gy.device, dtype=torch.float32)
+                K.gemm_tn_acc(gy, x2, dw)
+                dw = dw[: wshape[0], : wshape[1]]
         if has_bias and ctx.needs_input_grad[2]:
-            db = K.colsum(gy)              # shape of the (possibly padded) bias input
+            tb = direct_grad(direct[1]) if direct is not None else None
+            if tb is not None:
+                K.colsum(gy, out=tb, accumulate=True)
+                ready.append(direct[1])
+            else:
+                db = K.colsum(gy)              # shape of the (possibly padded) bias input
+        for p in ready:
+            grad_ready(p)
         return dx, dw, db, None, None
 
 

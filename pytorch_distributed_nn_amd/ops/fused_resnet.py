@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import torch
 
+from ..optim.flat import direct_grad, grad_ready
 from . import kernels as K
 from .functional import weight_bf16
 
@@ -53,22 +54,60 @@ def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
     return t, mean, inv, sc, sh
 
 
-def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None):
+class _Sink:
+    """Parameter-gradient routing of one fused backward: gradients go straight into the flat arena
+    (optim.flat.direct_grad) when possible — the op then returns None for them and announces them with
+    grad_ready — otherwise they are returned to autograd."""
+
+    def __init__(self):
+        self.ready = []
+
+    def acc(self, *ps):
+        tg = [direct_grad(p) for p in ps]
+        if any(t is None for t in tg):
+            return None
+        self.ready += ps
+        return tg
+
+    def bn(self, slab, rows, gamma_p, beta_p):
+        """-> (dgamma, dbeta) for bn_bwd_apply, (returned grads of gamma, beta)"""
+        acc = self.acc(gamma_p, beta_p)
+        dg, db = K.bn_bwd_finalize(slab, rows, acc=acc)
+        return (dg, db), ((None, None) if acc is not None else (dg, db))
+
+    def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
+        acc = self.acc(w_p)
+        if acc is not None:
+            K.conv_wgrad(x, dy, R, S, st, pad, pro=pro, out=acc[0].permute(0, 2, 3, 1))
+            return None
+        return _krsc_grad(K.conv_wgrad(x, dy, R, S, st, pad, pro=pro))
+
+    def done(self):
+        for p in self.ready:
+            grad_ready(p)
+
+
+def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
     slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
+    if sink is not None:
+        (dgamma, dbeta), (rg, rb) = sink.bn(slab, rows, *bn_params)
+        dt, _, _ = K.bn_bwd_apply(g2d, t2d, mean, inv, gamma, dgamma, dbeta, mode=mode, msrc=msrc, mscale=msc,
+                                  mshift=msh)
+        return dt, rg, rb
     dgamma, dbeta = K.bn_bwd_finalize(slab, rows)
     dt, _, _ = K.bn_bwd_apply(g2d, t2d, mean, inv, gamma, dgamma, dbeta, mode=mode, msrc=msrc, mscale=msc,
                               mshift=msh)
     return dt, dgamma, dbeta
 
 
-def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma):
+def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p):
     """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
     one apply pass produces dt (the gradient w.r.t. the BN input t)."""
     gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh))
-    dgamma, dbeta = K.bn_bwd_finalize(slab, slab.shape[0] // 2)
+    (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     C = t.shape[-1]
     dt, _, _ = K.bn_bwd_apply(gm.view(-1, C), t.view(-1, C), mean, inv, gamma, dgamma, dbeta, mode=0)
-    return dt.view(t.shape), dgamma, dbeta
+    return dt.view(t.shape), ret[0], ret[1]
 
 
 def _krsc_grad(dw):
@@ -104,6 +143,7 @@ class BottleneckFn(torch.autograd.Function):
         ctx.save_for_backward(x, t1, a1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None)
         ctx.conf = (stride, training, down)
+        ctx.params = params
         return out
 
     @staticmethod
@@ -117,11 +157,14 @@ class BottleneckFn(torch.autograd.Function):
         C3 = t3.shape[-1]
         g2d, t3_2d, out2d = gout.view(-1, C3), t3.view(-1, C3), out.view(-1, C3)
         # block output BN3 (+BNd) with the ReLU mask of `out`
+        P = ctx.params
+        ctx.params = None
+        sink = _Sink()
         slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=1, msrc=out2d,
                                              x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
-        dg3, db3 = K.bn_bwd_finalize(slab3, rows)
+        (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
         if down:
-            dgd, dbd = K.bn_bwd_finalize(slabd, rows)
+            (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
             dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d,
                                          x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                          dbeta2=dbd)
@@ -130,21 +173,21 @@ class BottleneckFn(torch.autograd.Function):
             dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d, want_gm=True)
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
-        dw3 = K.conv_wgrad(t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
-        dt2, dg2, db2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2)
-        dw2 = K.conv_wgrad(a1, dt2, 3, 3, stride, 1)
-        dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1)
-        dw1 = K.conv_wgrad(x, dt1, 1, 1, 1, 0)
+        dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5])
+        dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
+        dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
+        dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)
         if down:
             dtd = dtd.view(td.shape)
-            dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
+            dwd = sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
             dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
             dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=dxd)          # residual add fused
-            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3,
-                     _krsc_grad(dwd), dgd, dbd)
+            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3, dwd, rgd, rbd)
         else:
             dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape))
-            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dw3), dg3, db3)
+            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3)
+        sink.done()
         return (dx, None, None, None) + grads
 
 
@@ -173,6 +216,7 @@ class BasicBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, t1, a1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
                               params[7] if down else None, k1, k2, shadows[2] if down else None)
         ctx.conf = (stride, training, down)
+        ctx.params = params
         return out
 
     @staticmethod
@@ -184,29 +228,33 @@ class BasicBlockFn(torch.autograd.Function):
         gout = gout.contiguous()
         C2 = t2.shape[-1]
         g2d, t2_2d, out2d = gout.view(-1, C2), t2.view(-1, C2), out.view(-1, C2)
+        P = ctx.params
+        ctx.params = None
+        sink = _Sink()
         slab2, slabd, rows = K.bn_bwd_reduce(g2d, t2_2d, m2, i2, mode=1, msrc=out2d,
                                              x2=td.view(-1, C2) if down else None, mean2=md, invstd2=idd)
-        dg2, db2 = K.bn_bwd_finalize(slab2, rows)
+        (dg2, db2), (rg2, rb2) = sink.bn(slab2, rows, P[4], P[5])
         if down:
-            dgd, dbd = K.bn_bwd_finalize(slabd, rows)
+            (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[7], P[8])
             dt2, dtd, _ = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, x2=td.view(-1, C2),
                                          mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd, dbeta2=dbd)
             gres = None
         else:
             dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, want_gm=True)
         dt2 = dt2.view(t2.shape)
-        dw2 = K.conv_wgrad(a1, dt2, 3, 3, 1, 1)
-        dt1, dg1, db1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1)
-        dw1 = K.conv_wgrad(x, dt1, 3, 3, stride, 1)
+        dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, 1, 1)
+        dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
+        dw1 = sink.wgrad(P[0], x, dt1, 3, 3, stride, 1)
         if down:
             dtd = dtd.view(td.shape)
-            dwd = K.conv_wgrad(x, dtd, 1, 1, stride, 0)
+            dwd = sink.wgrad(P[6], x, dtd, 1, 1, stride, 0)
             dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
             dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=dxd)
-            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2, _krsc_grad(dwd), dgd, dbd)
+            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dwd, rgd, rbd)
         else:
             dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape))
-            grads = (_krsc_grad(dw1), dg1, db1, _krsc_grad(dw2), dg2, db2)
+            grads = (dw1, rg1, rb1, dw2, rg2, rb2)
+        sink.done()
         return (dx, None, None, None) + grads
 
 
@@ -228,6 +276,7 @@ class StemFn(torch.autograd.Function):
             y, idx = a, None
         ctx.save_for_backward(x, t, a, idx, m, i, gamma)
         ctx.conf = (stride, pad, pool, w.shape, kpad.shape)
+        ctx.params = (w, gamma, beta)
         return y
 
     @staticmethod
@@ -237,10 +286,18 @@ class StemFn(torch.autograd.Function):
         gy = gy.contiguous()
         ga = K.maxpool_bwd(gy, idx, a.shape, 3, 2, 1) if pool else gy
         C = t.shape[-1]
-        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 1, msrc=a.view(-1, C))
+        P = ctx.params
+        ctx.params = None
+        sink = _Sink()
+        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 1, msrc=a.view(-1, C), sink=sink,
+                              bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
-        dwk = K.conv_wgrad(x, dt, kshape[1], kshape[2], stride, pad)     # [K][R][S][Cpad]
-        dw = dwk[:, :, :, : wshape[1]].permute(0, 3, 1, 2)
+        if kshape[3] == wshape[1]:
+            dw = sink.wgrad(P[0], x, dt, kshape[1], kshape[2], stride, pad)
+        else:
+            dwk = K.conv_wgrad(x, dt, kshape[1], kshape[2], stride, pad)     # [K][R][S][Cpad]
+            dw = dwk[:, :, :, : wshape[1]].permute(0, 3, 1, 2)
+        sink.done()
         # the stem input is the data batch: no input gradient is produced
         return None, None, None, None, dw, dg, db
 

@@ -138,6 +138,7 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     _, Ho, Wo, K = dy.shape
     if out is None:
         out = torch.zeros(K, R, S, C, device=x.device, dtype=F32)
+    _chk(out.shape == (K, R, S, C) and out.is_contiguous() and out.dtype == F32, "conv_wgrad: out [K][R][S][C] fp32")
     sc, sh = pro if pro is not None else (None, None)
     call("pdnn_conv_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
          stream())
@@ -195,13 +196,16 @@ def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=Non
     return slab, slab2, rows
 
 
-def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False):
+def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=None):
+    """-> (dgamma, dbeta) of this backward; ``acc`` = (gamma.grad, beta.grad) also receive them (+=)."""
     C = slab.shape[1]
     if dgamma is None:
         dgamma = torch.empty(C, device=slab.device, dtype=F32)
         dbeta = torch.empty_like(dgamma)
     work = torch.empty(2 * 64 * C, device=slab.device, dtype=F32) if rows > 64 else None
-    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), stream())
+    ga, ba = acc if acc is not None else (None, None)
+    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), ptr(ga),
+         ptr(ba), stream())
     return dgamma, dbeta
 
 
@@ -402,8 +406,9 @@ def layernorm_fwd(x, g, b, eps):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, g, mean, rstd, dres=None):
-    """-> dx (+dres), dgamma, dbeta."""
+def layernorm_bwd(dy, x, g, mean, rstd, dres=None, acc=None):
+    """-> dx (+dres), dgamma, dbeta; with ``acc`` = (gamma.grad, beta.grad) the parameter gradients are
+    accumulated there instead (returns dx, None, None)."""
     R, D = x.shape
     dy = dy.contiguous()
     _chk(dy.shape == x.shape and (dres is None or dres.shape == x.shape), "layernorm_bwd: shapes")
@@ -412,6 +417,9 @@ def layernorm_bwd(dy, x, g, mean, rstd, dres=None):
     dx = torch.empty_like(x)
     call("pdnn_layernorm_bwd", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(slab), R, D,
          nb, stream())
+    if acc is not None:
+        bn_bwd_finalize(slab, nb, dgamma=acc[0], dbeta=acc[1], accumulate=True)
+        return dx, None, None
     dg, db = bn_bwd_finalize(slab, nb)
     return dx, dg, db
 

@@ -30,6 +30,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from ..optim.flat import direct_grad, grad_ready
 from . import kernels as K
 
 BF16 = torch.bfloat16
@@ -134,15 +135,21 @@ class EmbeddingFn(torch.autograd.Function):
     def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe):
         ctx.save_for_backward(idx)
         ctx.conf = (T, wte.shape, wpe.shape)
+        ctx.wpe = wpe
         return K.embedding_fwd(idx, wte_k, wpe_k, T)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         T, s_te, s_pe = ctx.conf
-        dwte = torch.zeros(s_te, device=g.device, dtype=F32)
-        dwpe = torch.zeros(s_pe, device=g.device, dtype=F32)
+        dwte = torch.zeros(s_te, device=g.device, dtype=F32)       # tied with the LM head: returned
+        tpe = direct_grad(ctx.wpe)
+        dwpe = tpe if tpe is not None else torch.zeros(s_pe, device=g.device, dtype=F32)
         K.embedding_bwd(idx, g, dwte, dwpe, T)
+        if tpe is not None:
+            grad_ready(ctx.wpe)
+            dwpe = None
+        ctx.wpe = None
         return None, None, None, None, dwte, dwpe
 
 
@@ -153,6 +160,49 @@ def _wgrad(g, x, shape):
     dw = torch.zeros(shape, device=g.device, dtype=F32)
     K.gemm_tn_acc(g, x, dw)
     return dw
+
+
+class _Sink:
+    """Routes parameter gradients straight into the flat arena when possible (optim.flat.direct_grad):
+    the GEMM / column-sum / LayerNorm kernels accumulate in place, the op returns None for the parameter
+    and announces it with grad_ready.  Otherwise the gradient is returned to autograd."""
+
+    def __init__(self):
+        self.ready = []
+
+    def _tgt(self, p):
+        t = direct_grad(p)
+        if t is not None:
+            self.ready.append(p)
+        return t
+
+    def linear(self, p_w, p_b, g, x):
+        tw = self._tgt(p_w)
+        if tw is not None:
+            K.gemm_tn_acc(g, x, tw)
+            rw = None
+        else:
+            rw = _wgrad(g, x, p_w.shape)
+        rb = None
+        if p_b is not None:
+            tb = self._tgt(p_b)
+            if tb is not None:
+                K.colsum(g, out=tb, accumulate=True)
+            else:
+                rb = K.colsum(g)
+        return rw, rb
+
+    def layernorm(self, dy, x, w, m, r, dres, p_w, p_b):
+        tw, tb = direct_grad(p_w), direct_grad(p_b)
+        if tw is not None and tb is not None:
+            self.ready += [p_w, p_b]
+            dx, _, _ = K.layernorm_bwd(dy, x, w, m, r, dres=dres, acc=(tw, tb))
+            return dx, None, None
+        return K.layernorm_bwd(dy, x, w, m, r, dres=dres)
+
+    def done(self):
+        for p in self.ready:
+            grad_ready(p)
 
 
 class GPT2BlockFn(torch.autograd.Function):
@@ -182,30 +232,35 @@ class GPT2BlockFn(torch.autograd.Function):
         ctx.conf = conf
         ctx.flash = flash
         ctx.S = S          # materialised path: reused as the fp32 dP scratch in backward
+        ctx.params = params
         return x2
 
     @staticmethod
     def backward(ctx, g):
         (x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, wqkv, wproj, wfc, wfc2) = ctx.saved_tensors
         B, T, H, eps = ctx.conf
+        Pm = ctx.params
+        ctx.params = None
+        sink = _Sink()
         g = g.contiguous()
         # MLP
         du = K.gemm_nt_ex(g, wfc2, dgelu=u, w_kn=True)                 # (g . Wfc2) * gelu'(u)
-        dfc2_w, dfc2_b = _wgrad(g, h, wfc2.shape), K.colsum(g)
+        dfc2_w, dfc2_b = sink.linear(Pm[10], Pm[11], g, h)
         dln2 = K.gemm_nt_ex(du, wfc, w_kn=True)
-        dfc_w, dfc_b = _wgrad(du, ln2, wfc.shape), K.colsum(du)
-        dx1, dln2w, dln2b = K.layernorm_bwd(dln2, x1, ln2w, m2, r2, dres=g)
+        dfc_w, dfc_b = sink.linear(Pm[8], Pm[9], du, ln2)
+        dx1, dln2w, dln2b = sink.layernorm(dln2, x1, ln2w, m2, r2, g, Pm[6], Pm[7])
         # attention
         dy = K.gemm_nt_ex(dx1, wproj, w_kn=True)
-        dproj_w, dproj_b = _wgrad(dx1, y, wproj.shape), K.colsum(dx1)
+        dproj_w, dproj_b = sink.linear(Pm[4], Pm[5], dx1, y)
         if ctx.flash:
             dqkv = K.flash_attn_bwd(qkv, y, dy, P, B, T, H, 1.0 / math.sqrt(x.shape[1] // H))
         else:
             dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
         ctx.S = None
         dln1 = K.gemm_nt_ex(dqkv, wqkv, w_kn=True)
-        dattn_w, dattn_b = _wgrad(dqkv, ln1, wqkv.shape), K.colsum(dqkv)
-        dx, dln1w, dln1b = K.layernorm_bwd(dln1, x, ln1w, m1, r1, dres=dx1)
+        dattn_w, dattn_b = sink.linear(Pm[2], Pm[3], dqkv, ln1)
+        dx, dln1w, dln1b = sink.layernorm(dln1, x, ln1w, m1, r1, dx1, Pm[0], Pm[1])
+        sink.done()
         return (dx, None, None, dln1w, dln1b, dattn_w, dattn_b, dproj_w, dproj_b, dln2w, dln2b, dfc_w, dfc_b,
                 dfc2_w, dfc2_b)
 
@@ -223,6 +278,7 @@ class LMHeadLossFn(torch.autograd.Function):
         _, lse, acc = K.xent_fwd(logits, targets)
         ctx.save_for_backward(x, xf, m, r, logits, targets, lse, acc, lnw, wte_k)
         ctx.eps = eps
+        ctx.params = (lnw, lnb)
         return acc[0] / acc[1].clamp_min(1.0)
 
     @staticmethod
@@ -231,6 +287,9 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
         dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
         dxf = K.gemm_nt_ex(dlogits, wte_k, w_kn=True)
-        dwte = _wgrad(dlogits, xf, wte_k.shape)
-        dx, dlnw, dlnb = K.layernorm_bwd(dxf, x, lnw, m, r)
+        dwte = _wgrad(dlogits, xf, wte_k.shape)         # tied weight: summed by autograd (not direct)
+        sink = _Sink()
+        dx, dlnw, dlnb = sink.layernorm(dxf, x, lnw, m, r, None, *ctx.params)
+        ctx.params = None
+        sink.done()
         return dx, None, None, None, dlnw, dlnb, dwte

@@ -16,6 +16,8 @@ the implicit-GEMM kernels read.  ``p.data`` / ``p.grad`` become views into ``dat
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 ALIGN = 64
@@ -42,7 +44,8 @@ class FlatParams:
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
         use_shadow = (device.type == "cuda") if shadow is None else shadow
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device) if use_shadow else None
-        for p, o in zip(self.params, self.offsets):
+        for i, (p, o) in enumerate(zip(self.params, self.offsets)):
+            p._pdnn_flat_idx = i
             n = p.numel()
             if p.dim() == 4:
                 dv = torch.as_strided(self.data, p.shape, _cl_strides(p.shape), o)
@@ -114,3 +117,82 @@ def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatPar
         fp.refresh_shadow()
     module.register_load_state_dict_post_hook(_post_load)
     return fp
+
+
+# ------------------------------------------------------------------------------------------------
+# Direct gradient accumulation.  A fused backward op may write a parameter's gradient straight into
+# its slice of the flat arena (``p.grad`` is a view of it) instead of returning a fresh tensor that
+# autograd's AccumulateGrad then adds in a separate pass: one kernel instead of fill + GEMM + add.
+# Such a parameter returns ``None`` from the op's backward.  torch still runs the parameter's
+# AccumulateGrad node (a no-op for a None gradient) and its post-accumulate hooks right after the op's
+# backward returns, so DDP buckets / PS gradient streaming see it complete at the right time.  Should a
+# torch build skip those hooks for None gradients (probed once), :func:`grad_ready` runs them instead.
+# Only for parameters used ONCE per forward (a tied weight's contributions are summed by autograd).
+# ------------------------------------------------------------------------------------------------
+DIRECT_GRAD = os.environ.get("PDNN_DIRECT_GRAD", "1") == "1"
+
+
+def direct_grad(p):
+    """The arena gradient view of ``p`` if a fused op may accumulate into it directly, else None."""
+    if not DIRECT_GRAD or not p.requires_grad:
+        return None
+    fp = getattr(p, "_pdnn_flat", None)
+    g = p.grad
+    if fp is None or g is None or not g.is_cuda:
+        return None
+    if g.data_ptr() != fp.grad.data_ptr() + 4 * fp.offsets[p._pdnn_flat_idx]:
+        return None
+    return g
+
+
+_HOOK_ON_NONE = None
+
+
+def _torch_hooks_fire_on_none() -> bool:
+    global _HOOK_ON_NONE
+    if _HOOK_ON_NONE is None:
+        class _F(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, x, w):
+                return x * 1
+
+            @staticmethod
+            def backward(ctx, g):
+                return g, None
+        w = torch.nn.Parameter(torch.ones(1))
+        x = torch.ones(1, requires_grad=True)
+        calls = []
+        w.register_post_accumulate_grad_hook(lambda p: calls.append(1))
+        _F.apply(x, w).sum().backward()
+        _HOOK_ON_NONE = bool(calls)
+    return _HOOK_ON_NONE
+
+
+def grad_ready(p):
+    """Announce that a fused op accumulated ``p``'s gradient in place (returns None for it)."""
+    if _torch_hooks_fire_on_none():
+        return                       # AccumulateGrad will run the hooks after the op's backward
+    for fn in getattr(p, "_pdnn_grad_hooks", ()):
+        fn(p)
+
+
+class _GradHookHandle:
+    def __init__(self, h, lst, fn):
+        self.h, self.lst, self.fn = h, lst, fn
+
+    def remove(self):
+        self.h.remove()
+        if self.fn in self.lst:
+            self.lst.remove(self.fn)
+
+
+def register_grad_ready_hook(p, fn):
+    """``fn(p)`` runs once ``p``'s gradient of the current backward is complete: after AccumulateGrad
+    (torch post-accumulate hook) or after a fused op accumulated it in place (:func:`grad_ready`)."""
+    h = p.register_post_accumulate_grad_hook(fn)
+    lst = p.__dict__.setdefault("_pdnn_grad_hooks", [])
+    lst.append(fn)
+    return _GradHookHandle(h, lst, fn)
+
+
+_torch_hooks_fire_on_none()      # probe at import, never from inside a running backward

@@ -37,7 +37,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..optim.flat import flatten_module
+from ..optim.flat import flatten_module, register_grad_ready_hook
 
 
 def _is_nccl(pg):
@@ -69,7 +69,7 @@ class DistributedDataParallel(nn.Module):
         self._buffers_list = [b for b in module.buffers() if b is not None and b.numel() > 0]
         self._broadcast_init()
         self._build_buckets(bucket_cap_mb, first_bucket_cap_mb)
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.flat.params]
+        self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
         self._reset()
         self.step_comm_log = []
 

@@ -38,7 +38,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from ..optim.flat import flatten_module
+from ..optim.flat import flatten_module, register_grad_ready_hook
 from ..utils.native import PSCoordinator, Store, StoreServer
 
 
@@ -188,7 +188,7 @@ class PSWorker(_Base):
         self.loss_fn = loss_fn
         self.delay = cfg.inject_straggler.get(self.rank, 0) / 1e3
         self.cur = 0
-        self._hooks = [p.register_post_accumulate_grad_hook(self._layer_done) for p in self.flat.params]
+        self._hooks = [register_grad_ready_hook(p, self._layer_done) for p in self.flat.params]
         self.aborted_steps = 0
 
     def _should_abort(self):
