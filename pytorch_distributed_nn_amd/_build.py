@@ -97,8 +97,22 @@ def build_runtime(verbose=False, sanitize: str | None = None) -> Path:
     return _build_lib(srcs, CXX, flags, LIBDIR / name, objdir, deps, link_extra=["-pthread"])
 
 
+def build_tools() -> Path:
+    """``_lib/pdnn_mlp``: the native MLP command-line driver (csrc/tools), statically linking the runtime
+    objects."""
+    build_runtime()
+    rdir = ROOT / "csrc" / "runtime"
+    objs = sorted((BUILD / "runtime").glob("*.o"))
+    src = ROOT / "csrc" / "tools" / "pdnn_mlp.cpp"
+    out = LIBDIR / "pdnn_mlp"
+    deps = list(rdir.glob("*.h")) + objs
+    if _newer(src, out, deps):
+        _run([CXX, *CXX_FLAGS, str(src), *map(str, objs), "-o", str(out), "-pthread"])
+    return out
+
+
 def build_all():
-    return build_kernels(), build_runtime()
+    return build_kernels(), build_runtime(), build_tools()
 
 
 if __name__ == "__main__":
@@ -107,5 +121,7 @@ if __name__ == "__main__":
         print(build_kernels())
     if which in ("all", "runtime"):
         print(build_runtime())
+    if which in ("all", "tools"):
+        print(build_tools())
     if which.startswith("sanitize="):
         print(build_runtime(sanitize=which.split("=", 1)[1]))

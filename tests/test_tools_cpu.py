@@ -1,0 +1,45 @@
+"""Native CLI (CPP-11/12) and run-report tooling (CPP-14, TF-09) on the CPU box."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def binary():
+    from pytorch_distributed_nn_amd import _build
+    return str(_build.build_tools())
+
+
+def test_pdnn_mlp_single(binary):
+    r = subprocess.run([binary, "single", "--iters", "5"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "final loss" in r.stdout
+
+
+def test_pdnn_mlp_distributed_backup_workers(binary, tmp_path):
+    out = str(tmp_path) + "/"
+    r = subprocess.run([binary, "distributed", "--nprocs", "5", "--collect", "2", "--iters", "6", "--out", out],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    tl = [f for f in os.listdir(tmp_path) if f.startswith("timeline_out_")]
+    tlo = [f for f in os.listdir(tmp_path) if f.startswith("time_loss_out_")]
+    assert tl and tlo
+    rep = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "report.py"), "timeline",
+                          os.path.join(tmp_path, tl[0])], capture_output=True, text=True, timeout=60)
+    assert rep.returncode == 0 and "average gradients received per step 2.00" in rep.stdout
+
+
+def test_report_percentiles(tmp_path):
+    p = tmp_path / "m.jsonl"
+    with open(p, "w") as f:
+        for i in range(100):
+            f.write(json.dumps({"step": i, "backward_ms": float(i)}) + "\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "report.py"), "percentiles", str(p)],
+                       capture_output=True, text=True, timeout=60)
+    rec = json.loads(r.stdout.strip())
+    assert rec["n"] == 100 and abs(rec["p90"] - 89.1) < 1e-6

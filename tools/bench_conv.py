@@ -48,20 +48,27 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--json", default=None)
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--layers", default=None, help="comma-separated indices into SHAPES")
+    ap.add_argument("--only", default=None, choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     N = a.batch
     res = []
     tot = {"ours": [0.0, 0.0, 0.0], "miopen": [0.0, 0.0, 0.0]}
-    for (H, W, C, Ko, R, st, pad, cnt) in SHAPES:
+    sel = [int(i) for i in a.layers.split(",")] if a.layers else range(len(SHAPES))
+    for li in sel:
+        (H, W, C, Ko, R, st, pad, cnt) = SHAPES[li]
         x = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
         w = (torch.randn(Ko, R, R, C, device="cuda") * 0.05).to(torch.bfloat16)
         Ho, Wo = K.conv_out_hw(H, W, R, R, st, pad)
         dy = torch.randn(N, Ho, Wo, Ko, device="cuda").to(torch.bfloat16)
         flops = 2.0 * N * Ho * Wo * Ko * C * R * R
-        t_f = timeit(lambda: K.conv_fwd(x, w, st, pad, want_stats=True))
-        t_d = timeit(lambda: K.conv_dgrad(dy, w, x.shape, st, pad)) if not (R == 7) else 0.0
-        t_w = timeit(lambda: K.conv_wgrad(x, dy, R, R, st, pad))
+        on = lambda k: a.only in (None, k)
+        it = a.iters
+        t_f = timeit(lambda: K.conv_fwd(x, w, st, pad, want_stats=True), it) if on("fwd") else 1e-9
+        t_d = timeit(lambda: K.conv_dgrad(dy, w, x.shape, st, pad), it) if not (R == 7) and on("dgrad") else 1e-9
+        t_w = timeit(lambda: K.conv_wgrad(x, dy, R, R, st, pad), it) if on("wgrad") else 1e-9
         row = {"shape": [H, W, C, Ko, R, st, pad], "count": cnt, "ours_ms": [t_f, t_d, t_w],
                "ours_tflops": [flops / t_f / 1e9, flops / max(t_d, 1e-9) / 1e9, flops / t_w / 1e9]}
         for i, t in enumerate((t_f, t_d, t_w)):
