@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define PDNN_API extern "C" __attribute__((visibility("default")))
 #define PDNN_LAUNCH_RET return (int)hipGetLastError()
 

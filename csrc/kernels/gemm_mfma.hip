@@ -711,257 +711,30 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Large-tile engine for plain (non-gather) operands: block tile 256 x 256 x 64, 512 threads = 8 waves
-// in a 2 (M) x 4 (N) arrangement, wave tile 128 x 64 = 8 x 4 fragments (64 MFMAs per K-step per
-// wave).  Both operands are staged global -> LDS with `global_load_lds_dwordx4` (glds: no VGPR round
-// trip, no ds_write), 2 LDS buffers of 64 KiB, one barrier per K-step, the next tile's glds in flight
-// during this tile's MFMAs (cdna_hip_programming.md §5 "glds vs register staging": at ~1 block/CU
-// glds is the cheap way to a staging pipeline).  The LDS images are lane-linear per wave-instruction
-// (1 KiB = 8 K-major rows or 2 MN-major k-rows); the bank swizzle is applied on the GLOBAL source
-// address.  Fragment reads are the same as the 128-tile kernel's (ds_read_b128 / ds_read_b64_tr_b16).
-// Used when K % 64 == 0 and the problem has enough 256-tiles; rows/columns past M/N load clamped
-// (valid memory, results discarded by the masked epilogue).
-// ---------------------------------------------------------------------------------------------
-constexpr int BT = 256;
-constexpr int NTB = 512;
-constexpr int BIG_LDS = 2 * 2 * BT * BK * 2;                 // 128 KiB: 2 buffers x (A | B)
-constexpr int BIG_CST = 128 * (BT + CPAD) * 4;               // half-tile fp32 C stage (atomic epilogue)
-constexpr int BIG_SMEM = BIG_LDS > BIG_CST ? BIG_LDS : BIG_CST;
+#include "gemm_glds.h"
 
-typedef __attribute__((address_space(3))) void lds_void;
-
-template <bool KMAJ>
-struct GldsLoader {
-    const bf16_t* src[4];
-    long step;
-    __device__ __forceinline__ void init(const bf16_t* p, long ld, int rows_total, int row0, int wave, int lane,
-                                         int kt0) {
-        if constexpr (KMAJ) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int rr = 8 * (wave * 4 + i) + (lane >> 3);
-                const int c = (lane & 7) ^ ((rr >> 1) & 7);
-                const int row = min(row0 + rr, rows_total - 1);
-                src[i] = p + (long)row * ld + (long)kt0 * BK + 8 * c;
-            }
-            step = BK;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int kr = 2 * (wave * 4 + i) + (lane >> 5);
-                const int c = (lane & 31) ^ (((kr & 3) | ((kr >> 1) & 4)) << 1);
-                const int col = min(row0 + 8 * c, rows_total - 8);
-                src[i] = p + ((long)kt0 * BK + kr) * ld + col;
-            }
-            step = (long)BK * ld;
-        }
-    }
-    // 4 x 1 KiB pieces of this wave into the operand image `img` (wave-uniform destinations)
-    __device__ __forceinline__ void issue(bf16_t* img, int wave) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_global_load_lds((const void*)src[i], (lds_void*)(img + (wave * 4 + i) * 512), 16, 0, 0);
-            src[i] += step;
-        }
-    }
-};
-
-template <int AM, int BMODE, int EM>
-__global__ void __launch_bounds__(NTB) gemm_big_kernel(GemmArgs a) {
-    constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
-    constexpr int IMG = BT * BK;                           // bf16 elements per operand image
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* const sbase = reinterpret_cast<bf16_t*>(smem);  // [buf][A | B]
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    if (gridDim.y > 1) {
-        const int z = blockIdx.y, z1 = z / a.nb2, z2 = z - z1 * a.nb2;
-        a.A += z1 * a.sA1 + z2 * a.sA2;
-        a.B += z1 * a.sB1 + z2 * a.sB2;
-        a.C = (void*)((char*)a.C + (z1 * a.sC1 + z2 * a.sC2) * (EM == E_BF16 ? 2 : 4));
-        if (a.ep_res) a.ep_res += z1 * a.sC1 + z2 * a.sC2;
-    }
-    const int tiles_m = (a.M + BT - 1) / BT, tiles_n = (a.N + BT - 1) / BT;
-    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-    const int tm = t / tiles_n, tn = t % tiles_n;
-    const int m0 = tm * BT, n0 = tn * BT;
-
-    const int ktiles = a.K / BK;
-    int kt0 = blockIdx.z * a.ktiles_per_split;
-    int kt1 = min(ktiles, kt0 + a.ktiles_per_split);
-    if (a.causal == 1 && n0 >= m0 + BT) return;
-    if (a.causal == 2) kt1 = min(kt1, (m0 + BT + BK - 1) / BK);
-    if (a.causal == 3) kt0 = max(kt0, m0 / BK);
-    if (kt0 >= kt1) return;
-
-    GldsLoader<AK> la;
-    GldsLoader<BKm> lb;
-    la.init(a.A, a.lda, a.M, m0, wave, lane, kt0);
-    lb.init(a.B, a.ldb, a.N, n0, wave, lane, kt0);
-
-    f32x4_t acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    la.issue(sbase, wave);
-    lb.issue(sbase + IMG, wave);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        if (kt + 1 < kt1) {
-            bf16_t* nb = sbase + (cur ^ 1) * 2 * IMG;
-            la.issue(nb, wave);
-            lb.issue(nb + IMG, wave);
-        }
-        const bf16_t* A_ = sbase + cur * 2 * IMG;
-        const bf16_t* B_ = A_ + IMG;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8_t bfr[4];
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                if constexpr (BKm) bfr[f] = frag_kmajor(B_, wn * 64 + f * 16 + (lane & 15), ks, lane);
-                else bfr[f] = frag_mnmajor<BT>(B_, wn * 64 + f * 16, ks, lane);
-            }
-#pragma unroll
-            for (int fm = 0; fm < 8; ++fm) {
-                bf16x8_t af;
-                if constexpr (AK) af = frag_kmajor(A_, wm * 128 + fm * 16 + (lane & 15), ks, lane);
-                else af = frag_mnmajor<BT>(A_, wm * 128 + fm * 16, ks, lane);
-#pragma unroll
-                for (int fn = 0; fn < 4; ++fn)
-                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af, acc[fm][fn], 0, 0, 0);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        cur ^= 1;
-    }
-
-    // ---------------- epilogue: lane holds C[m0 + wm*128 + fm*16 + lm][n0 + wn*64 + fn*16 + 4*lg + j]
-    const int lm = lane & 15, lg = lane >> 4;
-    if constexpr (EM == E_ATOMIC) {
-        // two rounds (wm = 0, 1) through a 128 x 256 fp32 LDS stage -> 256-byte atomic rows
-        float* cs = reinterpret_cast<float*>(smem);
-        constexpr int LDC_S = BT + CPAD;
-        float* C = reinterpret_cast<float*>(a.C);
-#pragma unroll
-        for (int round = 0; round < 2; ++round) {
-            if (wm == round) {
-#pragma unroll
-                for (int fm = 0; fm < 8; ++fm)
-#pragma unroll
-                    for (int fn = 0; fn < 4; ++fn)
-                        *reinterpret_cast<f32x4_t*>(cs + (fm * 16 + lm) * LDC_S + wn * 64 + fn * 16 + 4 * lg) =
-                            acc[fm][fn];
-            }
-            __syncthreads();
-            for (int r = wave; r < 128; r += 8) {
-                const int m = m0 + round * 128 + r;
-                if (m >= a.M) break;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int c = q * 64 + lane;
-                    const int n = n0 + c;
-                    if (n < a.N) atomicAdd(C + (long)m * a.ldc + n, a.alpha * cs[r * LDC_S + c]);
-                }
-            }
-            __syncthreads();
-        }
-        return;
-    } else {
-#pragma unroll
-        for (int fm = 0; fm < 8; ++fm) {
-            const int m = m0 + wm * 128 + fm * 16 + lm;
-            const bool mv = m < a.M;
-            uint32_t pk[4][2];
-#pragma unroll
-            for (int fn = 0; fn < 4; ++fn) {
-                const int n = n0 + wn * 64 + fn * 16 + 4 * lg;
-                const bool n4 = n + 4 <= a.N, ok = mv && n4;
-                const long off = (long)m * a.ldc + n;
-                float v[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    v[j] = acc[fm][fn][j] * a.alpha;
-                    if (a.bias) v[j] += n4 ? a.bias[n + j] : 0.f;
-                    if (a.relu == 1) v[j] = fmaxf(v[j], 0.f);
-                }
-                if constexpr (EM == E_BF16) {
-                    if (a.relu == 2) {
-                        u16x4_t pre;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
-                        if (a.ep_aux && ok) *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
-                    }
-                    if (a.ep_dgelu && ok) {
-                        const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
-                    }
-                    if (a.ep_res && ok) {
-                        const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
-                    }
-                    pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                    pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                } else {
-                    if (!mv || n >= a.N) continue;
-                    float* C = reinterpret_cast<float*>(a.C) + off;
-                    if (n4 && (a.ldc & 3) == 0) *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
-                    else for (int j = 0; j < 4 && n + j < a.N; ++j) C[j] = v[j];
-                }
-            }
-            if constexpr (EM == E_BF16) {
-#pragma unroll
-                for (int fp = 0; fp < 2; ++fp) {
-                    const auto s0 = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
-                    const auto s1 = __builtin_amdgcn_permlane16_swap(pk[2 * fp][1], pk[2 * fp + 1][1], false, false);
-                    const int n = n0 + wn * 64 + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
-                    if (mv && n + 8 <= a.N) {
-                        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc + n) =
-                            make_uint4(s0[0], s1[0], s0[1], s1[1]);
-                    } else if (mv && n < a.N) {
-                        const uint32_t w4[4] = {s0[0], s1[0], s0[1], s1[1]};
-                        bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc + n;
-                        for (int j = 0; j < 8 && n + j < a.N; ++j) C[j] = (bf16_t)(w4[j >> 1] >> (16 * (j & 1)));
-                    }
-                }
-            }
-        }
-    }
+// glds engine selection: 1 = automatic (default), 0 = off, 2 = whenever the operands allow (tests).
+// Environment PDNN_GLDS or pdnn_set_glds_mode().
+int g_glds_mode = -1;
+int glds_mode() {
+    if (g_glds_mode < 0) { const char* e = getenv("PDNN_GLDS"); g_glds_mode = e ? atoi(e) : 1; }
+    return g_glds_mode;
 }
-
-template <int AM, int BMODE, int EM>
-int launch_big(const GemmArgs& a, int splits, hipStream_t st, int batch) {
-    static bool attr = false;
-    if (!attr) {
-        attr = true;
-        (void)hipFuncSetAttribute((const void*)gemm_big_kernel<AM, BMODE, EM>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, BIG_SMEM);
-    }
-    const int tiles = (int)(cdiv(a.M, BT) * cdiv(a.N, BT));
-    hipLaunchKernelGGL((gemm_big_kernel<AM, BMODE, EM>), dim3(tiles, batch, splits), dim3(NTB), BIG_SMEM, st, a);
-    PDNN_LAUNCH_RET;
-}
-
-// the 256-tile engine applies when the operands are plain matrices, K is a whole number of K-steps,
-// no BN-statistics / BN-backward / scatter epilogue is requested, and there are enough tiles.
-bool big_ok(const GemmArgs& a, int batch) {
-    if (a.K % BK || a.M < BT || a.N < BT || a.stats || a.ep_x || a.scatter || a.transC) return false;
-    if (a.M % 8 || a.N % 8 || a.lda % 8 || a.ldb % 8) return false;
-    // measured (tools/bench_gemm.py): the 256-tile engine wins once its grid fills most of the 256 CUs;
-    // with fewer tiles the 128-tile kernel's 4x finer grid (2 blocks/CU) has the better wave quantisation
-    return cdiv(a.M, BT) * cdiv(a.N, BT) * (long)batch >= 192;
+bool glds_enabled() { return glds_mode() != 0; }
+// measured (tools/bench_gemm.py, tools/bench_conv.py): the 256-row tiles win once the grid fills most of the
+// 256 CUs; with fewer tiles the 128-tile kernel's finer grid (2 blocks/CU) has better wave quantisation.
+// Per-layer conv measurements (profiles/conv_layers_glds_vs_reg_r1.json): the glds engine wins on the
+// implicit-GEMM forward once the reduction is long (K >= 512: 3x3 convs, wide 1x1s) and on the data
+// gradient unless both C and K are small; the low-K 1x1 convs are memory bound and prefer the 128-row
+// kernel's finer grid, and the weight gradient's split-K atomics are faster there too.
+template <int AM>
+bool glds_worth(const GemmArgs& a, int batch, int splits) {
+    if (glds_mode() == 2) return true;
+    const long tiles = cdiv(a.M, GBM) * cdiv(a.N, glds_bn(a.N)) * (long)batch * splits;
+    if (tiles < 192) return false;
+    if constexpr (AM == A_CONV) return a.K >= 512;
+    if constexpr (AM == A_CONVT) return a.N >= 128 || a.K >= 512;
+    return true;
 }
 
 FastDiv make_fdiv(uint32_t d) {
@@ -993,12 +766,19 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     PDNN_LAUNCH_RET;
 }
 
-// N <= 64: a 128x64 block tile; otherwise 128x128.
+// the register-staged 128-row kernel: N <= 64 -> 128x64 tile, otherwise 128x128
+template <int AM, int BMODE, int EM, bool PA, bool PB>
+int launch_old(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
+    if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
+    return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
+}
+
+// glds engine when the operands allow it and the grid is big enough, else the 128-row kernel
 template <int AM, int BMODE, int EM, bool PA, bool PB>
 int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
-    if constexpr ((AM == A_KMAJOR || AM == A_MNMAJOR) && (BMODE == B_KMAJOR || BMODE == B_MNMAJOR) && !PA && !PB) {
-        if (big_ok(a, batch)) {
-            return launch_big<AM, BMODE, EM>(a, splits, st, batch);
+    if constexpr (!PA && !PB) {
+        if (glds_enabled() && glds_operands_ok<AM, BMODE>(a) && glds_worth<AM>(a, batch, splits)) {
+            return launch_glds<AM, BMODE, EM>(a, splits, st, batch, glds_bn(a.N));
         }
     }
     if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
@@ -1032,6 +812,12 @@ static void ensure_attrs() {}
 // ------------------------------------------------------------------------------------------------
 // C API
 // ------------------------------------------------------------------------------------------------
+
+PDNN_API int pdnn_set_glds_mode(int mode) {
+    const int old = glds_mode();
+    g_glds_mode = mode;
+    return old;
+}
 
 // Generic (batched) GEMM  C[M][N] = alpha * A . B  over nb1 x nb2 batches with two-level strides.
 //   amode: 0 = A row-major [M][K] (K-major), 1 = A stored [K][M] (reduction-major)
@@ -1107,18 +893,21 @@ PDNN_API int pdnn_gemm_tn_acc(const bf16_t* X, long ldx, const bf16_t* Y, long l
     a.alpha = alpha;
     const int ktiles = (int)cdiv(K, BK);
     a.ktiles_per_split = ktiles;
-    if (big_ok(a, 1)) {   // 256-tiles: split K until the grid covers the 256 CUs once
-        const int tiles = (int)(cdiv(M, BT) * cdiv(N, BT));
-        int s = (256 + tiles - 1) / tiles;
-        s = s < ktiles / 4 ? s : ktiles / 4;
-        s = s < 1 ? 1 : s;
-        a.ktiles_per_split = (int)cdiv(ktiles, s);
-        return launch_big<A_MNMAJOR, B_MNMAJOR, E_ATOMIC>(a, (int)cdiv(ktiles, a.ktiles_per_split), st, 1);
+    if (glds_enabled() && glds_operands_ok<A_MNMAJOR, B_MNMAJOR>(a)) {
+        const int bn = glds_bn(N);
+        const int tiles = (int)(cdiv(M, GBM) * cdiv(N, bn));
+        if (tiles >= 192 || glds_mode() == 2) {   // enough output tiles: split K only until the grid covers the CUs once
+            int s = (256 + tiles - 1) / tiles;
+            s = s < ktiles / 4 ? s : ktiles / 4;
+            s = s < 1 ? 1 : s;
+            a.ktiles_per_split = (int)cdiv(ktiles, s);
+            return launch_glds<A_MNMAJOR, B_MNMAJOR, E_ATOMIC>(a, (int)cdiv(ktiles, a.ktiles_per_split), st, 1, bn);
+        }
     }
     const int tiles = N <= 64 ? tiles_of<64>(a) : tiles_of<128>(a);
     const int splits = pick_splits(a, ktiles, tiles, 256);
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
-    return launch<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false>(a, (int)cdiv(ktiles, a.ktiles_per_split), st);
+    return launch_w<A_MNMAJOR, B_MNMAJOR, E_ATOMIC, false, false, 128>(a, (int)cdiv(ktiles, a.ktiles_per_split), st);
 }
 
 // Convolution forward, NHWC bf16 activations, weight [Ko][R][S][C] bf16 (== torch channels_last).
@@ -1233,16 +1022,30 @@ PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int N
     fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift;
-    const int ktiles = (int)cdiv(a.K, BK), tiles = a.N <= 64 ? tiles_of<64>(a) : tiles_of<128>(a);
+    const int ktiles = (int)cdiv(a.K, BK);
+    if (!pro_scale && glds_mode() == 2 &&      // measured slower than the 128-row kernel: forced mode only
+        (swap ? glds_operands_ok<A_IM2COL, B_MNMAJOR>(a) : glds_operands_ok<A_MNMAJOR, B_IM2COL>(a))) {
+        // glds engine: split the pixel reduction so ~1.5 blocks per CU run, >= 8 K-steps each
+        const int bn = glds_bn(a.N);
+        const int tiles = (int)(cdiv(a.M, GBM) * cdiv(a.N, bn));
+        int sp = (384 + tiles - 1) / tiles;
+        sp = sp < ktiles / 8 ? sp : ktiles / 8;
+        sp = sp < 1 ? 1 : sp;
+        a.ktiles_per_split = (int)cdiv(ktiles, sp);
+        const int nz = (int)cdiv(ktiles, a.ktiles_per_split);
+        if (swap) return launch_glds<A_IM2COL, B_MNMAJOR, E_ATOMIC>(a, nz, stream, 1, bn);
+        return launch_glds<A_MNMAJOR, B_IM2COL, E_ATOMIC>(a, nz, stream, 1, bn);
+    }
+    const int tiles = a.N <= 64 ? tiles_of<64>(a) : tiles_of<128>(a);
     const int splits = pick_splits(a, ktiles, tiles, 1024);
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
     const int nz = (int)cdiv(ktiles, a.ktiles_per_split);
     if (swap) {
-        if (pro_scale) return launch<A_IM2COL, B_MNMAJOR, E_ATOMIC, true, false>(a, nz, stream);
-        return launch<A_IM2COL, B_MNMAJOR, E_ATOMIC, false, false>(a, nz, stream);
+        if (pro_scale) return launch_old<A_IM2COL, B_MNMAJOR, E_ATOMIC, true, false>(a, nz, stream);
+        return launch_old<A_IM2COL, B_MNMAJOR, E_ATOMIC, false, false>(a, nz, stream);
     }
-    if (pro_scale) return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
-    return launch<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
+    if (pro_scale) return launch_old<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
+    return launch_old<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
 }
 
 // Number of stats rows the fused epilogue writes for M output rows (2 wave-rows per 128-row tile).

@@ -32,6 +32,12 @@ def _bf16_c(t, name):
 
 
 # ----------------------------------------------------------------------------------- GEMM / conv
+def set_glds_mode(mode: int) -> int:
+    """GEMM engine selection: 1 automatic (default), 0 register-staged 128-tile kernel only, 2 the glds
+    256-row engine whenever the operands allow it.  Returns the previous mode."""
+    return lib().pdnn_set_glds_mode(int(mode))
+
+
 def gemm_nt(x, w, bias=None, relu=False, out_f32=False, alpha=1.0, out=None):
     """y[M][N] = alpha * x[M][K] @ w[N][K]^T (+bias)(relu).  x, w bf16 row-major."""
     M, K = x.shape

@@ -22,6 +22,15 @@ def K():
     return kernels
 
 
+@pytest.fixture(autouse=True, params=[1, 0, 2], ids=["auto", "reg128", "glds"])
+def engine(request, K):
+    """Every GEMM/conv test runs with automatic engine choice, the register-staged 128-tile kernel only,
+    and the glds 256-row engine forced wherever its operand conditions hold."""
+    old = K.set_glds_mode(request.param)
+    yield request.param
+    K.set_glds_mode(old)
+
+
 def rnd(*s, scale=1.0):
     return (torch.randn(*s, device="cuda") * scale).to(BF)
 
@@ -63,6 +72,8 @@ CONV_SHAPES = [
     (2, 56, 56, 64, 256, 1, 1, 0),
     (2, 15, 15, 64, 64, 3, 2, 1),
     (2, 15, 15, 64, 128, 1, 2, 0),
+    (3, 10, 10, 64, 128, 3, 1, 1),       # M = 300: ragged 256-row tiles, partial stats groups
+    (2, 12, 12, 128, 64, 3, 2, 1),
 ]
 
 
