@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -56,6 +57,11 @@ def main():
 
     lm = a.model.lower().startswith("gpt2")
     model = build_model(a.model, num_classes=1000).to(dev)
+    if a.fp8:
+        if lm:
+            model.config.fp8 = True
+        else:
+            model.enable_fp8()
     if world > 1:
         net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
     else:
@@ -113,7 +119,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8(e4m3) fwd GEMMs + bf16" if a.fp8 else "bf16",
             "data": "synthetic (device-resident random token ids), random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
@@ -123,7 +129,8 @@ def main():
         }), flush=True)
     elif env.rank == 0:
         print(json.dumps({
-            "metric": "samples/sec (whole node) ResNet-50 DDP",
+            "metric": "samples/sec (whole node) ResNet-50 DDP" if a.model == "resnet50"
+                      else f"samples/sec (whole node) {a.model} DDP",
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": world,
@@ -133,8 +140,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "vs_stock_pytorch_rocm": round(value / (STOCK_PYTORCH_1GPU * world), 4),
-            "dtype": "bf16",
+            "vs_stock_pytorch_rocm": (round(value / (STOCK_PYTORCH_1GPU * world), 4)
+                                      if a.model == "resnet50" and B == 256 and not a.fp8 else None),
+            "dtype": "fp8(e4m3) 1x1-conv fwd GEMMs + bf16" if a.fp8 else "bf16",
             "data": "synthetic (device-resident random 224x224x3 images, random labels), random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "config": {"model": f"{a.model} (ImageNet layout, 224x224, 1000 classes)", "global_batch": B * world,

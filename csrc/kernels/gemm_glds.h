@@ -237,7 +237,22 @@ template <> struct GWaves<256> { static constexpr int WM = 2, WN = 4; };
 template <> struct GWaves<128> { static constexpr int WM = 4, WN = 2; };
 template <> struct GWaves<64> { static constexpr int WM = 4, WN = 1; };
 
-template <int AM, int BMODE, int EM, int BN>
+// fp8 fragment of the block-scaled 16x16x128 MFMA: lane l holds 32 consecutive k bytes
+// [32 (l >> 4), +32) of row (row0 + (l & 15)) = 16-byte chunks 2g, 2g+1 of the 128-byte image row
+typedef __attribute__((ext_vector_type(8))) int v8i_t;
+__device__ __forceinline__ v8i_t frag_fp8(const bf16_t* img, int row, int lane) {
+    const int g = lane >> 4;
+    const u16x8_t lo = *reinterpret_cast<const u16x8_t*>(img + kimg_off(row, 2 * g));
+    const u16x8_t hi = *reinterpret_cast<const u16x8_t*>(img + kimg_off(row, 2 * g + 1));
+    typedef __attribute__((ext_vector_type(4))) int v4i_t;
+    const v4i_t a = __builtin_bit_cast(v4i_t, lo), b = __builtin_bit_cast(v4i_t, hi);
+    return v8i_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// DT = 1: fp8 (OCP e4m3) operands, both K-major; the caller passes every K / ld in units of 2 fp8
+// (the loaders move bytes), so one 64-"element" K-step is 128 fp8 = one block-scaled MFMA step
+// (unit block scales: per-tensor scales are applied in the epilogue through alpha_ptr).
+template <int AM, int BMODE, int EM, int BN, int DT = 0>
 __global__ void __launch_bounds__(GWaves<BN>::WM * GWaves<BN>::WN * 64)
 gemm_glds_kernel(GemmArgs a) {
     constexpr int WM = GWaves<BN>::WM, WN = GWaves<BN>::WN, NWAVE = WM * WN, NTH = NWAVE * 64;
@@ -296,8 +311,21 @@ gemm_glds_kernel(GemmArgs a) {
         }
         const bf16_t* A_ = sbase + cur * (IMA + IMB);
         const bf16_t* B_ = A_ + IMA;
+        if constexpr (DT == 1) {
+            v8i_t bq[FN];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+            for (int f = 0; f < FN; ++f) bq[f] = frag_fp8(B_, wn * WTN + f * 16 + (lane & 15), lane);
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) {
+                const v8i_t aq = frag_fp8(A_, wm * WTM + fm * 16 + (lane & 15), lane);
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                        bq[fn], aq, acc[fm][fn], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < (DT == 1 ? 0 : 2); ++ks) {
             bf16x8_t bfr[FN];
 #pragma unroll
             for (int f = 0; f < FN; ++f) {
@@ -321,6 +349,7 @@ gemm_glds_kernel(GemmArgs a) {
 
     // ---------------- epilogue: lane holds C[m0 + wm*WTM + fm*16 + lm][n0 + wn*WTN + fn*16 + 4*lg + j]
     const int lm = lane & 15, lg = lane >> 4;
+    if (a.alpha_ptr) a.alpha *= *a.alpha_ptr;      // device-side scale (fp8 dequantisation)
     if constexpr (EM == E_ATOMIC) {
         // rounds of GCST_ROWS rows through an fp32 LDS stage -> 256-byte contiguous atomic wave-instructions
         float* cs = reinterpret_cast<float*>(smem);
@@ -510,18 +539,18 @@ gemm_glds_kernel(GemmArgs a) {
     }
 }
 
-template <int AM, int BMODE, int EM, int BN>
+template <int AM, int BMODE, int EM, int BN, int DT = 0>
 int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {
     constexpr int NTH = GWaves<BN>::WM * GWaves<BN>::WN * 64;
     constexpr int SM = glds_smem<BN>();
     static bool attr = false;
     if (!attr) {
         attr = true;
-        (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<AM, BMODE, EM, BN>,
+        (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<AM, BMODE, EM, BN, DT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, SM);
     }
     const int tiles = (int)(cdiv(a.M, GBM) * cdiv(a.N, BN));
-    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN>), dim3(tiles, batch, splits), dim3(NTH), SM, st, a);
+    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN, DT>), dim3(tiles, batch, splits), dim3(NTH), SM, st, a);
     PDNN_LAUNCH_RET;
 }
 

@@ -93,6 +93,7 @@ struct GemmArgs {
     const bf16_t* ep_res;
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
+    const float* alpha_ptr;   // optional device scalar multiplying alpha (fp8 per-tensor dequantisation)
     bf16_t* ep_aux;           // relu == 2: the pre-activation (bias added) is also stored here (ld = ldc)
     const bf16_t* ep_dgelu;   // multiply the result by gelu'(u), u read from here (GELU backward)
 };
@@ -870,6 +871,32 @@ PDNN_API int pdnn_gemm_nt_ex(const bf16_t* X, long ldx, const bf16_t* W, long ld
     a.ktiles_per_split = (int)cdiv(K, BK);
     return w_kn ? launch<A_KMAJOR, B_MNMAJOR, E_BF16, false, false>(a, 1, st)
                 : launch<A_KMAJOR, B_KMAJOR, E_BF16, false, false>(a, 1, st);
+}
+
+// FP8 GEMM (OCP e4m3 operands, both K-major [rows][K] bytes, K % 128 == 0, lda/ldb % 16 == 0):
+// Y[M][N] = act(scale[0] * X . W^T + bias) (+ res), bf16 output (or fp32 with out_f32), optional BN
+// statistics of the output.  Runs the glds engine on the block-scaled 16x16x128 MFMA (2x the bf16 rate)
+// with unit block scales; `scale` (device) = 1 / (scale_x * scale_w).
+PDNN_API int pdnn_gemm_fp8(const uint8_t* X, long ldx, const uint8_t* W, long ldw, void* Y, long ldy, int M, int N,
+                           int K, const float* scale, const float* bias, int act, bf16_t* aux, const bf16_t* res,
+                           float* stats, int out_f32, hipStream_t st) {
+    if (K % 128 || ldx % 16 || ldw % 16 || N % 8 || M < 1) return (int)hipErrorInvalidValue;
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K / 2;
+    a.A = reinterpret_cast<const bf16_t*>(X); a.lda = ldx / 2;
+    a.B = reinterpret_cast<const bf16_t*>(W); a.ldb = ldw / 2;
+    a.C = Y; a.ldc = ldy; a.alpha = 1.f; a.alpha_ptr = scale;
+    a.bias = bias; a.relu = act; a.ep_aux = aux; a.ep_res = res; a.stats = stats;
+    a.ktiles_per_split = (int)cdiv(a.K, BK);
+    const int bn = glds_bn(N);
+    if (out_f32) {
+        if (bn == 256) return launch_glds_w<A_KMAJOR, B_KMAJOR, E_F32, 256, 1>(a, 1, st, 1);
+        if (bn == 128) return launch_glds_w<A_KMAJOR, B_KMAJOR, E_F32, 128, 1>(a, 1, st, 1);
+        return launch_glds_w<A_KMAJOR, B_KMAJOR, E_F32, 64, 1>(a, 1, st, 1);
+    }
+    if (bn == 256) return launch_glds_w<A_KMAJOR, B_KMAJOR, E_BF16, 256, 1>(a, 1, st, 1);
+    if (bn == 128) return launch_glds_w<A_KMAJOR, B_KMAJOR, E_BF16, 128, 1>(a, 1, st, 1);
+    return launch_glds_w<A_KMAJOR, B_KMAJOR, E_BF16, 64, 1>(a, 1, st, 1);
 }
 
 // Y[M][N] = alpha * X[M][K] . W[K][N]     (W row-major [K][N]: reduction-major B)

@@ -34,6 +34,7 @@ class GPT2Config:
     n_head: int = 12
     n_embd: int = 768
     eps: float = 1e-5
+    fp8: bool = False          # block linears' forward GEMMs in fp8 (e4m3, delayed scaling); bwd bf16
 
 
 CONFIGS = {
@@ -81,6 +82,13 @@ class Block(nn.Module):
     def forward(self, x):
         x = x + self.attn(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
+
+    def fp8_metas(self, device):
+        metas = getattr(self, "_fp8_metas", None)
+        if metas is None:
+            from ..ops.fp8 import Fp8Meta
+            metas = self._fp8_metas = tuple(Fp8Meta(device) for _ in range(4))
+        return metas
 
     def fused_params(self):
         p = (self.ln_1.weight, self.ln_1.bias, self.attn.c_attn.weight, self.attn.c_attn.bias,
@@ -138,7 +146,8 @@ class GPT2(nn.Module):
         x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, wte, wpe)
         for blk in tr.h:
             params, shadows = blk.fused_params()
-            x = TX.GPT2BlockFn.apply(x, (B, T, c.n_head, c.eps), shadows, *params)
+            metas = blk.fp8_metas(x.device) if c.fp8 else None
+            x = TX.GPT2BlockFn.apply(x, (B, T, c.n_head, c.eps, metas), shadows, *params)
         if targets is None:
             xf = TX.layer_norm(x, tr.ln_f.weight, tr.ln_f.bias, c.eps)
             return OF.linear(xf, wte).view(B, T, -1)

@@ -110,10 +110,18 @@ class Bottleneck(_FusedBlockMixin, nn.Module):
         out = out + getattr(self, self.ds_name)(x)
         return F.relu(out)
 
+    fp8 = False                    # conv1 (1x1, stride 1) forward on the fp8 GEMM engine (enable_fp8)
+
     def forward_nhwc(self, x):
         params, bufs, shadows, bns = self._block_params()
         mom, eps = _bn_conf(self.bn1)
-        return BottleneckFn.apply(x, (self.stride, self.training, mom, eps), bufs, shadows, *params)
+        meta = None
+        if self.fp8 and x.shape[-1] % 128 == 0:
+            meta = getattr(self, "_fp8_meta", None)
+            if meta is None:
+                from ..ops.fp8 import Fp8Meta
+                meta = self._fp8_meta = Fp8Meta(x.device)
+        return BottleneckFn.apply(x, (self.stride, self.training, mom, eps, meta), bufs, shadows, *params)
 
 
 class _ResNetBase(nn.Module):
@@ -163,6 +171,14 @@ class ResNet(_ResNetBase):
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
         out = F.avg_pool2d(out, 4)
         return self.linear(out.reshape(out.size(0), -1))
+
+    def enable_fp8(self, on: bool = True):
+        """BASELINE.json config 5: run the 1x1 stride-1 bottleneck convs' forward GEMMs on the fp8 (e4m3,
+        per-tensor delayed scaling) MFMA path; backward stays bf16."""
+        for m in self.modules():
+            if isinstance(m, Bottleneck):
+                m.fp8 = on
+        return self
 
     def forward_nhwc(self, x):
         xin = OF.nchw_to_nhwc_input(x)
@@ -216,6 +232,14 @@ class ResNetImageNet(_ResNetBase):
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def enable_fp8(self, on: bool = True):
+        """BASELINE.json config 5: run the 1x1 stride-1 bottleneck convs' forward GEMMs on the fp8 (e4m3,
+        per-tensor delayed scaling) MFMA path; backward stays bf16."""
+        for m in self.modules():
+            if isinstance(m, Bottleneck):
+                m.fp8 = on
+        return self
 
     def forward_nhwc(self, x):
         xin = OF.nchw_to_nhwc_input(x)

@@ -78,9 +78,15 @@ _SIGS = {
     "pdnn_flash_attn_bwd": [P, P, P, P, P, P, I, I, I, F, I, P],
     "pdnn_embedding_fwd": [P, P, P, P, I, I, I, P],
     "pdnn_embedding_bwd": [P, P, P, P, I, I, I, P],
-    "pdnn_gemm_fp8_nt": [P, L, P, L, P, L, I, I, I, F, P, I, P],
-    "pdnn_quant_fp8": [P, P, L, P, P, P],
-    "pdnn_amax_f32": [P, L, P, I, P],
+    "pdnn_gemm_fp8": [P, L, P, L, P, L, I, I, I, P, P, I, P, P, P, I, P],
+    "pdnn_fp8_probe": [P, P, P, I, P],
+    "pdnn_amax_bf16": [P, L, P, P],
+    "pdnn_amax_f32": [P, L, P, P],
+    "pdnn_fp8_scale": [P, P, P, I, P],
+    "pdnn_fp8_scale_step": [P, P, P, P, P, I, P],
+    "pdnn_quant_fp8": [P, L, P, P, P, P],
+    "pdnn_quant_fp8_f32": [P, L, P, P, P],
+    "pdnn_dequant_fp8": [P, L, P, P, P],
 }
 
 

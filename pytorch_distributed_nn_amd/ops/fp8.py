@@ -1,0 +1,82 @@
+"""FP8 (OCP e4m3) forward GEMMs with per-tensor delayed scaling (SURVEY.md §2.8 K-18 "fp8 MFMA GEMM with
+per-tensor scaling"; BASELINE.json config 5 "ResNet-152 fp8 weights").
+
+Recipe (the usual fp8-training split): forward GEMMs read fp8 operands on the block-scaled
+``v_mfma_scale_f32_16x16x128_f8f6f4`` path (2x the bf16 MFMA rate, ``csrc/kernels/gemm_mfma.hip``
+``pdnn_gemm_fp8``); backward GEMMs stay bf16 on the saved bf16 activations and the bf16 weight shadow.
+
+* **Weights** are quantised with *current* scaling once per optimizer step (amax pass -> scale -> quant,
+  three tiny launches), cached against the parameter's version counter like the bf16 shadow.
+* **Activations** use *delayed* scaling: the quantisation kernel records the tensor's amax while it
+  converts with the scale derived from the previous step's amax; one single-thread kernel then forms the
+  GEMM's dequantisation factor (1 / (s_x s_w)) and rolls the scale forward.  No host synchronisation.
+  The very first call primes the scale with a real amax pass.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .functional import weight_bf16
+
+F32 = torch.float32
+
+
+class Fp8Meta:
+    """Device-side scaling state of one fp8 GEMM input."""
+
+    def __init__(self, device, margin: int = 0):
+        self.amax = torch.zeros(1, device=device, dtype=F32)
+        self.scale = torch.ones(1, device=device, dtype=F32)
+        self.inv = torch.ones(1, device=device, dtype=F32)
+        self.gemm_scale = torch.ones(1, device=device, dtype=F32)
+        self.margin = margin
+        self.primed = False
+
+    def quantize(self, x, inv_w):
+        """-> (e4m3 bytes of x, device scalar 1 / (s_x * s_w) for the GEMM epilogue)."""
+        if not self.primed:
+            K.amax_(x, self.amax)
+            K.fp8_scale(self.amax, self.scale, self.inv, self.margin)
+            self.amax.zero_()
+            self.primed = True
+        q = K.quant_fp8(x, self.scale, amax=self.amax)
+        K.fp8_scale_step(self.amax, self.scale, self.inv, inv_w, self.gemm_scale, self.margin)
+        return q, self.gemm_scale
+
+
+def _weight_version(p):
+    # flat-arena parameters are updated in place by the fused optimizer (no autograd version bump):
+    # key on the arena's update generation as well
+    fp = getattr(p, "_pdnn_flat", None)
+    return (p._version, fp.generation if fp is not None else 0)
+
+
+def weight_fp8(p: torch.Tensor, krsc: bool = False):
+    """(e4m3 weight [N][K] (conv: [K][R*S*C]), device inverse scale) cached per parameter version."""
+    st = getattr(p, "_pdnn_fp8", None)
+    ver = _weight_version(p)
+    if st is not None and st[0] == ver:
+        return st[1], st[2]
+    wb = weight_bf16(p, krsc=krsc)
+    w2 = wb.reshape(wb.shape[0], -1)
+    dev = p.device
+    amax = torch.zeros(1, device=dev, dtype=F32)
+    scale = torch.empty(1, device=dev, dtype=F32)
+    inv = torch.empty(1, device=dev, dtype=F32)
+    K.amax_(w2, amax)
+    K.fp8_scale(amax, scale, inv)
+    q = K.quant_fp8(w2.contiguous(), scale)
+    p._pdnn_fp8 = (ver, q, inv)
+    return q, inv
+
+
+def fp8_ok(M, N, Kd):
+    return Kd % 128 == 0 and N % 8 == 0 and M >= 1
+
+
+def linear_fp8_fwd(x2, p_w, meta: Fp8Meta, bias=None, act=0, aux=None, res=None, stats=None):
+    """y = act(x2 @ W^T + bias) (+res) with x2 and W in e4m3 (bf16 output)."""
+    wq, winv = weight_fp8(p_w)
+    xq, gs = meta.quantize(x2, winv)
+    return K.gemm_fp8(xq, wq, gs, bias=bias, act=act, aux=aux, res=res, stats=stats)

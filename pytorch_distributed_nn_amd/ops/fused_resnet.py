@@ -87,6 +87,23 @@ class _Sink:
             grad_ready(p)
 
 
+def _conv1x1_bn_fp8(x, w_param, meta, training, bn_params, bufs, mom, eps):
+    """1x1 stride-1 conv as an fp8 GEMM (x and W in e4m3, per-tensor delayed scaling, fused BN stats)."""
+    from .fp8 import weight_fp8
+    N, H, W, C = x.shape
+    M = N * H * W
+    wq, winv = weight_fp8(w_param, krsc=True)
+    xq, gs = meta.quantize(x.view(M, C), winv)
+    Ko = wq.shape[0]
+    slab = torch.empty(2 * K.stats_rows(M), Ko, device=x.device, dtype=F32) if training else None
+    t = K.gemm_fp8(xq, wq, gs, stats=slab).view(N, H, W, Ko)
+    if training:
+        mean, inv, sc, sh = _bn_train(slab, M, bn_params, bufs, mom, eps)
+    else:
+        mean, inv, sc, sh = _bn_eval(bn_params, bufs, eps)
+    return t, mean, inv, sc, sh
+
+
 def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
     slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
     if sink is not None:
@@ -120,11 +137,15 @@ class BottleneckFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, conf, bufs, shadows, *params):
-        stride, training, mom, eps = conf
+        stride, training, mom, eps = conf[:4]
+        fp8_meta = conf[4] if len(conf) > 4 else None
         down = len(params) == 12
         w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
         k1, k2, k3 = shadows[:3]
-        t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
+        if fp8_meta is not None:
+            t1, m1, i1, s1, h1 = _conv1x1_bn_fp8(x, w1, fp8_meta, training, (g1, b1), bufs[0:2], mom, eps)
+        else:
+            t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
         # a1 = relu(bn1(t1)) is materialised once: the 3x3 conv gathers every element 9 times, so applying
         # the BN affine in its operand loader would cost 9x the VALU work (fwd and wgrad)
         C1 = t1.shape[-1]

@@ -475,3 +475,65 @@ def embedding_bwd(idx, g, dwte, dwpe, T):
     R, D = g.shape
     _chk(dwte.dtype == F32 and dwte.shape[1] == D and (dwpe is None or dwpe.shape[1] == D), "embedding_bwd")
     call("pdnn_embedding_bwd", ptr(idx), ptr(g.contiguous()), ptr(dwte), ptr(dwpe), R, T, D, stream())
+
+
+# ----------------------------------------------------------------------------------- fp8 (OCP e4m3)
+U8 = torch.uint8
+
+
+def fp8_probe(A, Bt, layout):
+    D = torch.empty(16, 16, device=A.device, dtype=F32)
+    call("pdnn_fp8_probe", ptr(A), ptr(Bt), ptr(D), int(layout), stream())
+    return D
+
+
+def amax_(x, out):
+    """out (fp32 [1], device) = max(out, max|x|)."""
+    if x.dtype == BF16:
+        call("pdnn_amax_bf16", ptr(x), x.numel(), ptr(out), stream())
+    else:
+        call("pdnn_amax_f32", ptr(x), x.numel(), ptr(out), stream())
+    return out
+
+
+def fp8_scale(amax, scale, inv, margin=0):
+    """scale = 448 / amax * 2^-margin (device scalars, no host sync)."""
+    call("pdnn_fp8_scale", ptr(amax), ptr(scale), ptr(inv), int(margin), stream())
+
+
+def fp8_scale_step(amax, scale, inv, inv_w, gemm_scale, margin=0):
+    call("pdnn_fp8_scale_step", ptr(amax), ptr(scale), ptr(inv), ptr(inv_w), ptr(gemm_scale), int(margin), stream())
+
+
+def quant_fp8(x, scale, out=None, amax=None):
+    """e4m3(x * scale) as uint8; bf16 input may also record its amax (delayed scaling)."""
+    _chk(x.is_contiguous() and x.numel() % 8 == 0, "quant_fp8: contiguous, numel % 8")
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=U8)
+    if x.dtype == BF16:
+        call("pdnn_quant_fp8", ptr(x), x.numel(), ptr(scale), ptr(out), ptr(amax), stream())
+    else:
+        _chk(x.dtype == F32 and amax is None, "quant_fp8: fp32 input without amax")
+        call("pdnn_quant_fp8_f32", ptr(x), x.numel(), ptr(scale), ptr(out), stream())
+    return out
+
+
+def dequant_fp8(q, inv):
+    out = torch.empty(q.shape, device=q.device, dtype=BF16)
+    call("pdnn_dequant_fp8", ptr(q), q.numel(), ptr(inv), ptr(out), stream())
+    return out
+
+
+def gemm_fp8(xq, wq, scale, bias=None, act=0, aux=None, res=None, stats=None, out_f32=False, out=None):
+    """y[M][N] = act(scale * xq[M][K] . wq[N][K]^T + bias) (+res); xq, wq e4m3 (uint8), K % 128 == 0."""
+    M, Kd = xq.shape
+    N, K2 = wq.shape
+    _chk(xq.dtype == U8 and wq.dtype == U8 and K2 == Kd and Kd % 128 == 0 and N % 8 == 0,
+         f"gemm_fp8: {tuple(xq.shape)} {tuple(wq.shape)}")
+    _chk(xq.stride(1) == 1 and wq.stride(1) == 1 and xq.stride(0) % 16 == 0 and wq.stride(0) % 16 == 0,
+         "gemm_fp8: K-contiguous rows, 16-byte aligned")
+    if out is None:
+        out = torch.empty(M, N, device=xq.device, dtype=F32 if out_f32 else BF16)
+    call("pdnn_gemm_fp8", ptr(xq), xq.stride(0), ptr(wq), wq.stride(0), ptr(out), out.stride(0), M, N, Kd,
+         ptr(scale), ptr(bias), int(act), ptr(aux), ptr(res), ptr(stats), int(out_f32), stream())
+    return out

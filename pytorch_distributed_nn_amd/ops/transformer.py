@@ -211,11 +211,20 @@ class GPT2BlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, conf, shadows, *params):
-        B, T, H, eps = conf
+        B, T, H, eps = conf[:4]
+        metas = conf[4] if len(conf) > 4 else None
         ln1w, ln1b, _, attn_b, _, proj_b, ln2w, ln2b, _, fc_b, _, fc2_b = params
         wqkv, wproj, wfc, wfc2 = shadows
+        if metas is not None:
+            from .fp8 import linear_fp8_fwd
+
+            def lin(inp, i, wk, **kw):      # forward GEMM on the fp8 engine (weights: params[2/4/8/10])
+                return linear_fp8_fwd(inp, params[i], metas[(i - 2) // 2 if i < 6 else (i - 4) // 2], **kw)
+        else:
+            def lin(inp, i, wk, **kw):
+                return K.gemm_nt_ex(inp, wk, **kw)
         ln1, m1, r1 = K.layernorm_fwd(x, ln1w, ln1b, eps)
-        qkv = K.gemm_nt_ex(ln1, wqkv, bias=attn_b)
+        qkv = lin(ln1, 2, wqkv, bias=attn_b)
         D = x.shape[1]
         flash = use_flash(T, D, H)
         if flash:
@@ -223,11 +232,11 @@ class GPT2BlockFn(torch.autograd.Function):
             S = None
         else:
             y, P, S = attention_fwd(qkv, B, T, H)
-        x1 = K.gemm_nt_ex(y, wproj, bias=proj_b, res=x)
+        x1 = lin(y, 4, wproj, bias=proj_b, res=x)
         ln2, m2, r2 = K.layernorm_fwd(x1, ln2w, ln2b, eps)
         u = torch.empty(x.shape[0], wfc.shape[0], device=x.device, dtype=BF16)
-        h = K.gemm_nt_ex(ln2, wfc, bias=fc_b, act=2, aux=u)
-        x2 = K.gemm_nt_ex(h, wfc2, bias=fc2_b, res=x1)
+        h = lin(ln2, 8, wfc, bias=fc_b, act=2, aux=u)
+        x2 = lin(h, 10, wfc2, bias=fc2_b, res=x1)
         ctx.save_for_backward(x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, *shadows)
         ctx.conf = conf
         ctx.flash = flash
@@ -238,7 +247,7 @@ class GPT2BlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (x, ln1, m1, r1, qkv, P, y, x1, ln2, m2, r2, u, h, ln1w, ln2w, wqkv, wproj, wfc, wfc2) = ctx.saved_tensors
-        B, T, H, eps = ctx.conf
+        B, T, H, eps = ctx.conf[:4]
         Pm = ctx.params
         ctx.params = None
         sink = _Sink()

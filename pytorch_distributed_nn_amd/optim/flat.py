@@ -40,6 +40,7 @@ class FlatParams:
             self.offsets.append(off)
             off += (p.numel() + align - 1) // align * align
         self.numel = off
+        self.generation = 0          # bumped by every in-place update of `data` (optimizer step, reload)
         self.data = torch.zeros(off, dtype=torch.float32, device=device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
         use_shadow = (device.type == "cuda") if shadow is None else shadow
@@ -78,6 +79,7 @@ class FlatParams:
         self.mark_shadow_fresh()
 
     def mark_shadow_fresh(self):
+        self.generation += 1
         for p in self.params:
             p._pdnn_shadow_ver = p._version
 

@@ -90,6 +90,7 @@ class SGD(_FusedBase):
                 buf = st.get("momentum_buffer")
                 K.sgd_step(fp.data[s:e], fp.grad[s:e], buf, fp.shadow[s:e] if fp.shadow is not None else None,
                            lr, mom, damp, wd, nest, self.grad_scale_dev, self.grad_scale, first)
+                fp.generation += 1
                 continue
             for p in group["params"]:
                 if p.grad is None:
@@ -141,6 +142,7 @@ class Adam(_FusedBase):
                 K.adam_step(fp.data[s:e], fp.grad[s:e], st["exp_avg"], st["exp_avg_sq"],
                             fp.shadow[s:e] if fp.shadow is not None else None, lr, b1, b2, eps, wd,
                             self.decoupled, 1 - b1 ** t, 1 - b2 ** t, self.grad_scale_dev, self.grad_scale)
+                fp.generation += 1
                 continue
             for p in group["params"]:
                 if p.grad is None:

@@ -1,0 +1,117 @@
+"""FP8 (OCP e4m3) kernels: MFMA lane layout, quantisation, fp8 GEMM (BASELINE config 5)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+E4M3 = torch.float8_e4m3fn
+
+
+@pytest.fixture(scope="module")
+def K():
+    from pytorch_distributed_nn_amd.ops import _backend, kernels
+    assert _backend.available(), "HIP kernel library must load on a GPU box"
+    return kernels
+
+
+def as_bytes(t):
+    return t.to(E4M3).view(torch.uint8)
+
+
+def test_block_scaled_mfma_lane_layout(K):
+    """Exact small-integer data, asymmetric operands: layout 0 (32 consecutive k per lane) is the one the
+    fp8 GEMM engine assumes."""
+    g = torch.Generator().manual_seed(0)
+    A = torch.randint(-4, 5, (16, 128), generator=g).float()
+    B = torch.randint(-4, 5, (128, 16), generator=g).float()
+    ref = (A @ B).cuda()
+    Ab, Btb = as_bytes(A).cuda(), as_bytes(B.t().contiguous()).cuda()
+    d0 = K.fp8_probe(Ab, Btb, 0)
+    d1 = K.fp8_probe(Ab, Btb, 1)
+    assert torch.equal(d0, ref), f"layout 0 mismatch (layout 1 matches: {torch.equal(d1, ref)})"
+
+
+def test_quant_dequant_roundtrip(K):
+    x = (torch.randn(4096, device="cuda") * 3).to(torch.bfloat16)
+    amax = torch.zeros(1, device="cuda")
+    K.amax_(x, amax)
+    assert torch.allclose(amax, x.float().abs().max().reshape(1))
+    scale, inv = torch.empty(1, device="cuda"), torch.empty(1, device="cuda")
+    K.fp8_scale(amax, scale, inv)
+    q = K.quant_fp8(x, scale)
+    ref = (x.float() * scale).to(E4M3).view(torch.uint8)
+    assert (q == ref).float().mean() > 0.999          # identical rounding except rare ties
+    back = K.dequant_fp8(q, inv).float()
+    assert ((back - x.float()).abs() <= x.float().abs() * 0.07 + 1e-3).all()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(512, 256, 256), (1000, 776, 512), (4096, 3072, 768), (300, 64, 128)])
+def test_gemm_fp8(K, M, N, Kd):
+    x = torch.randn(M, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    sx, sw = 448 / x.abs().max(), 448 / w.abs().max()
+    xq, wq = as_bytes(x * sx), as_bytes(w * sw)
+    scale = (1.0 / (sx * sw)).reshape(1).float()
+    xd = xq.view(E4M3).float() / sx
+    wd = wq.view(E4M3).float() / sw
+    ref = xd @ wd.t()
+    b = torch.randn(N, device="cuda")
+    y = K.gemm_fp8(xq, wq, scale, bias=b)
+    assert ((y.float() - (ref + b)).norm() / (ref + b).norm()) < 1e-2
+    y32 = K.gemm_fp8(xq, wq, scale, out_f32=True)
+    assert ((y32 - ref).norm() / ref.norm()) < 1e-4
+
+
+def test_gpt2_tiny_fp8_close_to_bf16_and_trains():
+    import copy
+    from pytorch_distributed_nn_amd.models.gpt2 import build_gpt2
+    from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
+    torch.manual_seed(0)
+    m = build_gpt2("gpt2_tiny").cuda()
+    m8 = copy.deepcopy(m)
+    m8.config.fp8 = True
+    idx = torch.randint(0, 64, (4, 129), device="cuda")
+    x, y = idx[:, :-1].contiguous(), idx[:, 1:].contiguous()
+    l16, l8 = m(x, y), m8(x, y)
+    assert abs(l8.item() - l16.item()) / l16.item() < 0.02
+    flatten_module(m8)
+    opt = AdamW(m8.parameters(), lr=3e-3, weight_decay=0.0)
+    first = None
+    for _ in range(30):
+        opt.zero_grad()
+        loss = m8(x, y)
+        loss.backward()
+        opt.step()
+        first = first if first is not None else loss.item()
+    assert loss.item() < 0.7 * first
+
+
+def test_bottleneck_fp8_forward_and_resnet_trains():
+    """One bottleneck: the fp8 conv1 path matches the bf16 block closely (a whole random-init ResNet-50
+    amplifies any per-layer perturbation chaotically, see test_models_gpu); the fp8 model trains."""
+    import copy
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.models.resnet import Bottleneck
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD, flatten_module
+    torch.manual_seed(0)
+    blk = Bottleneck(256, 64, 1, "downsample").cuda()
+    blk8 = copy.deepcopy(blk)
+    blk8.fp8 = True
+    x = torch.relu(torch.randn(8, 14, 14, 256, device="cuda")).to(torch.bfloat16)
+    y16, y8 = blk.forward_nhwc(x), blk8.forward_nhwc(x)
+    rel = ((y8.float() - y16.float()).norm() / y16.float().norm()).item()
+    assert rel < 0.08, rel
+    m = build_model("resnet50").cuda().enable_fp8()
+    flatten_module(m)
+    opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
+    xin = torch.randn(16, 3, 64, 64, device="cuda")
+    yl = torch.randint(0, 10, (16,), device="cuda")
+    first = None
+    for _ in range(12):
+        opt.zero_grad()
+        loss = OF.cross_entropy(m(xin), yl)
+        loss.backward()
+        opt.step()
+        first = first if first is not None else loss.item()
+    assert torch.isfinite(loss) and loss.item() < 0.6 * first

@@ -59,6 +59,11 @@ def main():
         r["torch_nn"] = fl / timeit(lambda: x @ wt) / 1e9
         r["ours_tn"] = fl / timeit(lambda: K.gemm_tn_acc(g, x, dw)) / 1e9
         r["torch_tn"] = fl / timeit(lambda: g.t() @ x) / 1e9
+        if Kd % 128 == 0:
+            xq = x.to(torch.float8_e4m3fn).view(torch.uint8)
+            wq = w.to(torch.float8_e4m3fn).view(torch.uint8)
+            one = torch.ones(1, device="cuda")
+            r["ours_fp8_nt"] = fl / timeit(lambda: K.gemm_fp8(xq, wq, one)) / 1e9
         print(" ".join(f"{k}={v:.0f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
         res.append(r)
         del x, w, wt, g, dw
