@@ -100,7 +100,10 @@ struct Server {
                 auto pred = [&] { return stop.load() || kv.count(key) > 0; };
                 bool ok;
                 if (tmo < 0) { cv.wait(lk, pred); ok = kv.count(key) > 0; }
-                else ok = cv.wait_for(lk, std::chrono::milliseconds(tmo), pred) && kv.count(key) > 0;
+                // system_clock deadline: pthread_cond_timedwait (libstdc++'s steady_clock wait_for uses
+                // pthread_cond_clockwait, which this toolchain's ThreadSanitizer cannot see through)
+                else ok = cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(tmo), pred) &&
+                          kv.count(key) > 0;
                 if (!ok) { lk.unlock(); reply(fd, TIMEOUT, nullptr, 0); continue; }
                 if (op == WAIT) { lk.unlock(); reply(fd, OK, nullptr, 0); continue; }
                 std::vector<char> out = kv[key];
@@ -227,8 +230,9 @@ struct Client {
         }
     }
 
-    // returns status, response in `last`
-    int rpc(uint8_t op, const std::string& key, const void* val, uint64_t vl) {
+    // returns status, response in `last`; with `out` the response is also copied out while the handle's
+    // lock is still held, so one handle may be shared by threads for the single-call ops (add / check)
+    int rpc(uint8_t op, const std::string& key, const void* val, uint64_t vl, std::vector<char>* out = nullptr) {
         std::lock_guard<std::mutex> g(mu);
         uint32_t kl = (uint32_t)key.size();
         if (!send_all(fd, &op, 1) || !send_all(fd, &kl, 4) || (kl && !send_all(fd, key.data(), kl)) ||
@@ -239,6 +243,7 @@ struct Client {
         if (!recv_all(fd, &st, 1) || !recv_all(fd, &n, 8)) return -1;
         last.resize(n);
         if (n && !recv_all(fd, last.data(), n)) return -1;
+        if (out) *out = last;
         return st;
     }
 };
@@ -288,15 +293,17 @@ RT_API int pdnn_store_wait(void* h, const char* key, int64_t timeout_ms) {
 }
 RT_API int64_t pdnn_store_add(void* h, const char* key, int64_t delta) {
     auto* c = static_cast<Client*>(h);
-    if (c->rpc(ADD, key, &delta, 8) != 0 || c->last.size() != 8) return INT64_MIN;
+    std::vector<char> r;
+    if (c->rpc(ADD, key, &delta, 8, &r) != 0 || r.size() != 8) return INT64_MIN;
     int64_t v;
-    memcpy(&v, c->last.data(), 8);
+    memcpy(&v, r.data(), 8);
     return v;
 }
 RT_API int pdnn_store_check(void* h, const char* key) {
     auto* c = static_cast<Client*>(h);
-    if (c->rpc(CHECK, key, nullptr, 0) != 0 || c->last.empty()) return -1;
-    return c->last[0];
+    std::vector<char> r;
+    if (c->rpc(CHECK, key, nullptr, 0, &r) != 0 || r.empty()) return -1;
+    return r[0];
 }
 RT_API int pdnn_store_del(void* h, const char* key) { return static_cast<Client*>(h)->rpc(DEL, key, nullptr, 0); }
 RT_API int pdnn_store_keys(void* h, const char* prefix) { return static_cast<Client*>(h)->rpc(KEYS, prefix, nullptr, 0); }

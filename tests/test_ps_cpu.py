@@ -67,3 +67,46 @@ def test_ps_k_of_n_kill_with_straggler():
     assert all(r["count"] == 1 for r in master_log)
     assert sum(2 in r["arrived"] for r in master_log) >= 6          # the fast worker wins most steps
     assert aborted_rank3 >= 4                                       # straggler was short-circuited
+
+
+def _ps_job_cfg(rank, world, cfg_kw, out_dir, steps):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    model = build_model("mlp2", 10)
+    x, y = _data()
+    cfg = PSConfig(lr=0.05, max_steps=steps, out_dir=out_dir, **cfg_kw)
+
+    def batches():
+        i = 0
+        while True:
+            sl = slice((i * 32) % 512, (i * 32) % 512 + 32)
+            yield x[sl], y[sl]
+            i += 1
+
+    res = run_ps(model, cfg, torch.device("cpu"), loss_fn=OF.cross_entropy, batches=batches())
+    w = torch.cat([p.detach().flatten() for p in model.parameters()])
+    return res, w
+
+
+def test_ps_backup_workers_drop_stragglers():
+    """PAR-DP-BACKUP: collect the first 2 of 3 workers' gradients each step; the slow worker's late
+    gradients are dropped as stale and it short-circuits its backward."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_job_cfg, 4, ({"n_to_collect": 2, "inject_straggler": {3: 25}}, out, 8))
+    master_log = res[0][0]
+    assert all(r["count"] == 2 for r in master_log)
+    assert sum(3 in r["arrived"] for r in master_log) <= 2          # the straggler rarely makes the cut
+    for r in res[1:]:
+        assert torch.equal(r[1], res[0][1])                         # consistent final weights
+
+
+def test_ps_interval_mode_closes_steps_on_timer():
+    """PAR-DP-INTERVAL (TF TimeoutReplicasOptimizer): a step closes interval_ms after its first gradient
+    with whatever arrived; a worker slower than the interval is left out."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_job_cfg, 3, ({"interval_ms": 5.0, "inject_straggler": {2: 60}}, out, 6))
+    master_log = res[0][0]
+    assert all(1 <= r["count"] <= 2 for r in master_log)
+    assert sum(r["count"] == 1 for r in master_log) >= 4            # the timer closed most steps early
