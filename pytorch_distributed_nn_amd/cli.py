@@ -55,7 +55,29 @@ def add_fit_args(p: argparse.ArgumentParser):
     p.add_argument("--trace", type=str, default=None)
     p.add_argument("--metrics", type=str, default=None)
     p.add_argument("--out-dir", type=str, default="outfiles")
+    p.add_argument("--config", type=str, default=None,
+                   help="YAML file of flag defaults (keys = flag names without '--'); explicit flags win")
     return p
+
+
+def parse_args(argv=None):
+    """Flags, with defaults optionally taken from a YAML experiment config (TF-11 cfg files).
+    The YAML is read with ``yaml.safe_load``."""
+    p = add_fit_args(argparse.ArgumentParser(description="pytorch_distributed_nn_amd trainer"))
+    pre, _ = p.parse_known_args(argv)
+    if pre.config:
+        import yaml
+        with open(pre.config) as f:
+            cfg = yaml.safe_load(f) or {}
+        known = {a.dest for a in p._actions}
+        defaults = {}
+        for k, v in cfg.items():
+            dest = k.replace("-", "_")
+            if dest not in known:
+                raise SystemExit(f"{pre.config}: unknown option {k!r}")
+            defaults[dest] = v
+        p.set_defaults(**defaults)
+    return p.parse_args(argv)
 
 
 def parse_stragglers(s: str) -> dict:
@@ -67,7 +89,7 @@ def parse_stragglers(s: str) -> dict:
 
 
 def main(argv=None):
-    args = add_fit_args(argparse.ArgumentParser(description="pytorch_distributed_nn_amd trainer")).parse_args(argv)
+    args = parse_args(argv)
     from .data.datasets import DataLoader, dataset_from_args
     from .models import build_model
     from .ops import functional as OF

