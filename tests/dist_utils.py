@@ -37,14 +37,14 @@ def _from_np(obj):
     return obj
 
 
-def _entry(rank, world, port, fn, args, q):
+def _entry(rank, world, port, fn, args, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
         import torch
         torch.set_num_threads(1)
         from pytorch_distributed_nn_amd.parallel import runtime
-        runtime.init_process_group(backend="gloo", device="cpu")
+        runtime.init_process_group(backend="gloo", device=device)
         res = fn(rank, world, *args)
         q.put((rank, "ok", _to_np(res)))
     except Exception:
@@ -57,11 +57,13 @@ def _entry(rank, world, port, fn, args, q):
             pass
 
 
-def run_world(fn, world=2, args=(), timeout=180):
+def run_world(fn, world=2, args=(), timeout=180, device="cpu"):
+    """device="cpu": CPU tensors over gloo; device=None: every rank uses the (single) GPU, still over gloo
+    (RCCL needs one GPU per rank; gloo moves GPU tensors through the host)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
