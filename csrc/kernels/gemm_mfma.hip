@@ -89,6 +89,7 @@ struct GemmArgs {
     //  2: reduction limited to k < m0 + BM   (A = P or dS [q][k], lower triangular: P V, dS K)
     //  3: reduction starts at k >= m0        (A = P^T / dS^T, upper triangular: P^T dO, dS^T Q)
     int causal;
+    int stage_store;          // 128-row kernel: bf16 epilogue stores staged through LDS (full-row writes)
     // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
     const bf16_t* ep_res;
     const bf16_t* ep_x;
@@ -687,6 +688,44 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
             }
         }
         if constexpr (EM == E_BF16) {
+          if (a.stage_store) {
+            // Stage the bf16 tile through LDS ([128][BNW], 16-byte chunk c of row r at c ^ (r & 15): both
+            // the 8-byte fragment writes and the 16-byte row reads are conflict-free), then every 16 (8)
+            // threads write one full 256 (128)-byte row segment: whole cache lines per wave-instruction
+            // instead of 64-byte pieces of 16 rows.
+            constexpr int CPR = BNW / 8;                     // 16-byte chunks per tile row
+            bf16_t* st = reinterpret_cast<bf16_t*>(smem);
+            __syncthreads();                                 // operand images no longer read
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) {
+                    const int r = wm * 64 + fm * 16 + lm;
+                    const int c = wn * WTN + fn * 16 + 4 * lg;
+                    const int ch = (c >> 3) ^ (r & (CPR - 1));
+                    *reinterpret_cast<uint2*>(st + r * BNW + ch * 8 + (c & 7)) = make_uint2(pk[fm][fn][0], pk[fm][fn][1]);
+                }
+            __syncthreads();
+            constexpr int RPI = NT / CPR;                    // rows per pass
+#pragma unroll
+            for (int it = 0; it < BMt / RPI; ++it) {
+                const int r = it * RPI + tid / CPR, j = tid % CPR;
+                const int m = m0 + r;
+                const int n = n0 + j * 8;
+                if (m < a.M && n < a.N) {
+                    long orw = m;
+                    if (a.scatter) {
+                        const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
+                        const uint32_t rem = (uint32_t)m - nn * a.g.dHW.d;
+                        const uint32_t hc = fdiv(rem, a.g.dW);
+                        const uint32_t wc = rem - hc * a.g.dW.d;
+                        orw = ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
+                    }
+                    const uint4 v = *reinterpret_cast<const uint4*>(st + r * BNW + ((j ^ (r & (CPR - 1))) << 3));
+                    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + orw * a.ldc + n) = v;
+                }
+            }
+          } else {
             // Lanes l, l+16, l+32, l+48 hold columns 0-3 / 4-7 / 8-11 / 12-15 of the same row.  One
             // permlane16_swap per dword between fragments (fn, fn+1) gives every lane 16 contiguous bytes:
             // 16-lane row g of the wave then holds fragment fn + (g & 1), columns 8*(g >> 1) .. +7.
@@ -708,6 +747,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                     }
                 }
             }
+          }
         }
     }
 }
@@ -748,6 +788,12 @@ FastDiv make_fdiv(uint32_t d) {
     return f;
 }
 
+int g_stage_store = -1;
+int stage_store_mode() {
+    if (g_stage_store < 0) { const char* e = getenv("PDNN_STAGED_STORE"); g_stage_store = e ? atoi(e) : 1; }
+    return g_stage_store;
+}
+
 template <int AM, int BMODE, int EM, bool PA, bool PB, int BNW>
 int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     static bool attr = false;
@@ -763,7 +809,9 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     if (a.ktiles_per_split <= 1 && EM != E_ATOMIC) sm = (BMt + BNW) * BK * 2;
     const int tiles = (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW));
     dim3 grid(tiles, batch, splits);
-    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), sm, st, a);
+    GemmArgs b = a;
+    b.stage_store = stage_store_mode();
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE, EM, PA, PB, BNW>), grid, dim3(NT), sm, st, b);
     PDNN_LAUNCH_RET;
 }
 
@@ -813,6 +861,12 @@ static void ensure_attrs() {}
 // ------------------------------------------------------------------------------------------------
 // C API
 // ------------------------------------------------------------------------------------------------
+
+PDNN_API int pdnn_set_staged_store(int mode) {
+    const int old = stage_store_mode();
+    g_stage_store = mode;
+    return old;
+}
 
 PDNN_API int pdnn_set_glds_mode(int mode) {
     const int old = glds_mode();

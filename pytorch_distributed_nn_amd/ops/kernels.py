@@ -32,6 +32,11 @@ def _bf16_c(t, name):
 
 
 # ----------------------------------------------------------------------------------- GEMM / conv
+def set_staged_store(mode: int) -> int:
+    """128-row kernel bf16 epilogue: 1 = stores staged through LDS (full rows), 0 = direct fragment stores."""
+    return lib().pdnn_set_staged_store(int(mode))
+
+
 def set_glds_mode(mode: int) -> int:
     """GEMM engine selection: 1 automatic (default), 0 register-staged 128-tile kernel only, 2 the glds
     256-row engine whenever the operands allow it.  Returns the previous mode."""

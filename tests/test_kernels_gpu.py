@@ -22,13 +22,17 @@ def K():
     return kernels
 
 
-@pytest.fixture(autouse=True, params=[1, 0, 2], ids=["auto", "reg128", "glds"])
+@pytest.fixture(autouse=True, params=[(1, 1), (0, 1), (0, 0), (2, 1)],
+                ids=["auto", "reg128", "reg128-direct-store", "glds"])
 def engine(request, K):
-    """Every GEMM/conv test runs with automatic engine choice, the register-staged 128-tile kernel only,
-    and the glds 256-row engine forced wherever its operand conditions hold."""
-    old = K.set_glds_mode(request.param)
+    """Every GEMM/conv test runs with automatic engine choice, the register-staged 128-tile kernel only
+    (LDS-staged and direct epilogue stores), and the glds 256-row engine forced wherever it applies."""
+    glds, staged = request.param
+    old = K.set_glds_mode(glds)
+    old_s = K.set_staged_store(staged)
     yield request.param
     K.set_glds_mode(old)
+    K.set_staged_store(old_s)
 
 
 def rnd(*s, scale=1.0):
