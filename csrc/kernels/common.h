@@ -45,15 +45,39 @@ template <> struct Ld<bf16_t> {
     static __device__ __forceinline__ void put(bf16_t* p, long i, float v) { p[i] = f2bf(v); }
 };
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// DPP lane moves (VALU, no LDS round trip like ds_bpermute-based __shfl_xor)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Sum over each 16-lane row; every lane of the row receives the row total.
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);    // row_half_mirror: quads 0<->1, 2<->3
+    v += dpp_f<0x140>(v);    // row_mirror: half-rows swap
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    v = fmaxf(v, dpp_f<0x140>(v));
     return v;
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// Whole-wave reductions (all 64 lanes active): DPP within 16-lane rows, then the 4 row results via
+// v_readlane (scalar) -- no LDS traffic.
+__device__ __forceinline__ float wave_sum(float v) {
+    v = row16_sum(v);
+    return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = row16_max(v);
+    return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
 }
 
 // Block-wide sum for blockDim.x == NT (multiple of 64).  `red` must hold NT/64 floats.

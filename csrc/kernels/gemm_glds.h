@@ -509,11 +509,8 @@ gemm_glds_kernel(GemmArgs a) {
                     for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                            for (int o = 1; o < 16; o <<= 1) {
-                                s_[fn][j] += __shfl_xor(s_[fn][j], o, 64);
-                                q_[fn][j] += __shfl_xor(q_[fn][j], o, 64);
-                            }
+                            s_[fn][j] = row16_sum(s_[fn][j]);
+                            q_[fn][j] = row16_sum(q_[fn][j]);
                         }
                     const int grp = m0 + wm * WTM + (fm / 4) * 64;           // first row of these 64
                     const int slab_row = a.stats_row0 + grp / 64;

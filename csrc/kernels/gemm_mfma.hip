@@ -669,12 +669,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
             }
             if (want_stats) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        s[j] += __shfl_xor(s[j], o, 64);
-                        q[j] += __shfl_xor(q[j], o, 64);
-                    }
+                for (int j = 0; j < 4; ++j) {      // sum over the 16 rows (lanes l & 15) of the fragment column
+                    s[j] = row16_sum(s[j]);
+                    q[j] = row16_sum(q[j]);
                 }
                 if (lm == 0 && nv) {
                     const long row = (long)(a.stats_row0 + tm * 2 + wm) * 2;
