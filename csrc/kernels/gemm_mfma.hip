@@ -812,10 +812,20 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     PDNN_LAUNCH_RET;
 }
 
+int g_lowk_bn64 = -1;
+int lowk_bn64_mode() {
+    if (g_lowk_bn64 < 0) { const char* e = getenv("PDNN_LOWK_BN64"); g_lowk_bn64 = e ? atoi(e) : 0; }
+    return g_lowk_bn64;
+}
+
 // the register-staged 128-row kernel: N <= 64 -> 128x64 tile, otherwise 128x128
 template <int AM, int BMODE, int EM, bool PA, bool PB>
 int launch_old(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
+    // one K-step: the block's life is load -> 32 MFMAs -> store; the 64-wide tile needs 128 VGPRs
+    // (4 blocks/CU instead of 2), which hides the memory latency better
+    if (lowk_bn64_mode() && EM != E_ATOMIC && a.ktiles_per_split <= 1)
+        return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
     return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
 }
 
