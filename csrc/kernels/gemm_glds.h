@@ -274,22 +274,35 @@ gemm_glds_kernel(GemmArgs a) {
         if (a.ep_res) a.ep_res += z1 * a.sC1 + z2 * a.sC2;
     }
     const int tiles_m = (a.M + GBM - 1) / GBM, tiles_n = (a.N + BN - 1) / BN;
-    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int ntiles = tiles_m * tiles_n;
+    const int ktiles = (a.K + BK - 1) / BK;
+    // Optionally persistent over output tiles (PDNN_GLDS_PERSISTENT=1; measured slower than the hardware
+    // dispatcher on every shape tried, so off by default): block b takes tiles
+    // b, b + G, ... (same XCD when G % 8 == 0), and issues the next tile's first K-step into the free LDS
+    // buffer before running this tile's epilogue, so short-K tiles overlap loads with stores.
+    int cur = 0;
+    bool pre = false;
+    LA la;
+    LB lb;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int t = xcd_remap(tile, ntiles);
     const int tm = t / tiles_n, tn = t % tiles_n;
     const int m0 = tm * GBM, n0 = tn * BN;
 
-    const int ktiles = (a.K + BK - 1) / BK;
     int kt0 = blockIdx.z * a.ktiles_per_split;
     int kt1 = min(ktiles, kt0 + a.ktiles_per_split);
-    if (a.causal == 1 && n0 >= m0 + GBM) return;
+    if (a.causal == 1 && n0 >= m0 + GBM) continue;
     if (a.causal == 2) kt1 = min(kt1, (m0 + GBM + BK - 1) / BK);
     if (a.causal == 3) kt0 = max(kt0, m0 / BK);
-    if (kt0 >= kt1) return;
+    if (kt0 >= kt1) continue;
 
-    LA la;
-    LB lb;
-    la.init(a, a.A, a.lda, a.M, m0, wave, lane, kt0);
-    lb.init(a, a.B, a.ldb, a.N, n0, wave, lane, kt0);
+    if (!pre) {
+        la.init(a, a.A, a.lda, a.M, m0, wave, lane, kt0);
+        lb.init(a, a.B, a.ldb, a.N, n0, wave, lane, kt0);
+        gissue<AK>(la, a, sbase + cur * (IMA + IMB), wave, lane, a.M);
+        gissue<BKm>(lb, a, sbase + cur * (IMA + IMB) + IMA, wave, lane, a.N);
+    }
+    pre = false;
 
     f32x4_t acc[FM][FN];
 #pragma unroll
@@ -297,12 +310,9 @@ gemm_glds_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    gissue<AK>(la, a, sbase, wave, lane, a.M);
-    gissue<BKm>(lb, a, sbase + IMA, wave, lane, a.N);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
         if (kt + 1 < kt1) {
             bf16_t* nb = sbase + (cur ^ 1) * (IMA + IMB);
@@ -345,6 +355,18 @@ gemm_glds_kernel(GemmArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         cur ^= 1;
+    }
+    if constexpr (EM != E_ATOMIC) {     // (the atomic epilogue stages C through the LDS buffers)
+        const int nt = tile + gridDim.x;
+        if (nt < ntiles && a.causal == 0) {
+            const int t2 = xcd_remap(nt, ntiles);
+            const int kt0n = blockIdx.z * a.ktiles_per_split;
+            la.init(a, a.A, a.lda, a.M, (t2 / tiles_n) * GBM, wave, lane, kt0n);
+            lb.init(a, a.B, a.ldb, a.N, (t2 % tiles_n) * BN, wave, lane, kt0n);
+            gissue<AK>(la, a, sbase + cur * (IMA + IMB), wave, lane, a.M);
+            gissue<BKm>(lb, a, sbase + cur * (IMA + IMB) + IMA, wave, lane, a.N);
+            pre = true;
+        }
     }
 
     // ---------------- epilogue: lane holds C[m0 + wm*WTM + fm*16 + lm][n0 + wn*WTN + fn*16 + 4*lg + j]
@@ -389,7 +411,7 @@ gemm_glds_kernel(GemmArgs a) {
             }
             __syncthreads();
         }
-        return;
+        continue;
     } else {
         const bool bnb = a.ep_x != nullptr;
         const bool want_stats = EM == E_BF16 && a.stats != nullptr;
@@ -534,6 +556,22 @@ gemm_glds_kernel(GemmArgs a) {
             }
         });
     }
+    }   // tile loop
+}
+
+inline int device_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+int g_glds_persistent = -1;
+inline int glds_persistent() {
+    if (g_glds_persistent < 0) { const char* e = getenv("PDNN_GLDS_PERSISTENT"); g_glds_persistent = e ? atoi(e) : 0; }
+    return g_glds_persistent;
 }
 
 template <int AM, int BMODE, int EM, int BN, int DT = 0>
@@ -547,7 +585,12 @@ int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, SM);
     }
     const int tiles = (int)(cdiv(a.M, GBM) * cdiv(a.N, BN));
-    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN, DT>), dim3(tiles, batch, splits), dim3(NTH), SM, st, a);
+    int gx = tiles;
+    if (batch * splits == 1 && a.causal == 0 && glds_persistent()) {
+        const int slots = device_cus();                   // 1 block per CU (128 KiB LDS)
+        if (tiles > slots) gx = slots;
+    }
+    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN, DT>), dim3(gx, batch, splits), dim3(NTH), SM, st, a);
     PDNN_LAUNCH_RET;
 }
 

@@ -78,6 +78,7 @@ CONV_SHAPES = [
     (2, 15, 15, 64, 128, 1, 2, 0),
     (3, 10, 10, 64, 128, 3, 1, 1),       # M = 300: ragged 256-row tiles, partial stats groups
     (2, 12, 12, 128, 64, 3, 2, 1),
+    (32, 56, 56, 64, 64, 3, 1, 1),       # 392 row tiles: the persistent glds grid loops over tiles
 ]
 
 
