@@ -121,40 +121,54 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
 
 // y = act(x*scale + shift + residual'), residual' = res (identity) or res*rscale + rshift.
 // Each thread owns one fixed group of 8 channels (coefficients in registers) and strides over rows.
+template <bool RES, bool RSC, bool RELU>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ x, long L, int C,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
                                                       const bf16_t* __restrict__ res,
                                                       const float* __restrict__ rscale,
-                                                      const float* __restrict__ rshift, int relu,
+                                                      const float* __restrict__ rshift,
                                                       bf16_t* __restrict__ y) {
     const int CG = C >> 3, RPI = NT / CG;
     const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
     if (rr >= RPI) return;
-    float sc[8], sh[8], rs[8], rh[8];
+    float sc[8], sh[8], rs_[RSC ? 8 : 1];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        sc[j] = scale[c + j]; sh[j] = shift[c + j];
-        rs[j] = rscale ? rscale[c + j] : 1.f; rh[j] = rscale ? rshift[c + j] : 0.f;
+        sc[j] = scale[c + j];
+        sh[j] = shift[c + j] + (RSC ? rshift[c + j] : 0.f);
+        if constexpr (RSC) rs_[j] = rscale[c + j];
     }
-    for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
-        const long off = r * C + c;
-        float v[8];
-        unpack8(*reinterpret_cast<const u16x8_t*>(x + off), v);
-        if (res) {
-            float rv[8];
-            unpack8(*reinterpret_cast<const u16x8_t*>(res + off), rv);
+    const long step = (long)gridDim.x * RPI;
+    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
+        const long rws[2] = {r0, r0 + step};
+        u16x8_t xv[2], rv[2];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], fmaf(rv[j], rs[j], sh[j] + rh[j]));
-        } else {
+        for (int u = 0; u < 2; ++u)
+            if (rws[u] < L) {
+                xv[u] = *reinterpret_cast<const u16x8_t*>(x + rws[u] * C + c);
+                if constexpr (RES) rv[u] = *reinterpret_cast<const u16x8_t*>(res + rws[u] * C + c);
+            }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+        for (int u = 0; u < 2; ++u) {
+            if (rws[u] >= L) break;
+            float v[8];
+            unpack8(xv[u], v);
+            if constexpr (RES) {
+                float r[8];
+                unpack8(rv[u], r);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], fmaf(r[j], RSC ? rs_[j] : 1.f, sh[j]));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+            }
+            if constexpr (RELU) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
+            *reinterpret_cast<u16x8_t*>(y + rws[u] * C + c) = pack8(v);
         }
-        if (relu) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        *reinterpret_cast<u16x8_t*>(y + off) = pack8(v);
     }
 }
 
@@ -193,16 +207,43 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
         mu2[j] = x2 ? mean2[c + j] : 0.f; is2[j] = x2 ? invstd2[c + j] : 0.f;
     }
     if (rr < RPI) {
-        for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
-            float gm[8], xv[8];
-            masked_grad(g, x, msrc, mscale, mshift, mode, r * C + c, c, gm, xv);
+        const long step = (long)gridDim.x * RPI;
+        for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
+            const long rs[2] = {r0, r0 + step};
+            u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { s[j] += gm[j]; q[j] += gm[j] * (xv[j] - mu[j]) * is[j]; }
-            if (x2) {
-                float x2v[8];
-                unpack8(*reinterpret_cast<const u16x8_t*>(x2 + r * C + c), x2v);
+            for (int u = 0; u < 2; ++u) {      // both rows' loads in flight together
+                if (rs[u] < L) {
+                    const long off = rs[u] * C + c;
+                    gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
+                    xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
+                    if (mode == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
+                    if (x2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
+                }
+            }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) q2[j] += gm[j] * (x2v[j] - mu2[j]) * is2[j];
+            for (int u = 0; u < 2; ++u) {
+                if (rs[u] >= L) break;
+                float gm[8], xv[8];
+                unpack8(gv[u], gm);
+                unpack8(xv8[u], xv);
+                if (mode == 1) {
+                    float m[8];
+                    unpack8(mv[u], m);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
+                } else if (mode == 2) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], mscale[c + j], mshift[c + j]) > 0.f ? gm[j] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { s[j] += gm[j]; q[j] += gm[j] * (xv[j] - mu[j]) * is[j]; }
+                if (x2) {
+                    float x2v[8];
+                    unpack8(x2v8[u], x2v);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) q2[j] += gm[j] * (x2v[j] - mu2[j]) * is2[j];
+                }
             }
         }
     }
@@ -251,10 +292,13 @@ __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __rest
 
 // dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
 // registers; optionally also a second BN's dx2 (shared gm) and/or gm itself.
+// Specialised on the mask mode / second BN / outputs so unused coefficient arrays take no registers
+// (occupancy), and two rows per thread per iteration so twice the loads are in flight.
+template <int MODE, bool X2, bool DX, bool GMO>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
-    const float* __restrict__ dgamma, const float* __restrict__ dbeta, int mode,
+    const float* __restrict__ dgamma, const float* __restrict__ dbeta,
     const bf16_t* __restrict__ msrc, const float* __restrict__ mscale, const float* __restrict__ mshift,
     bf16_t* __restrict__ dx, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
     const float* __restrict__ invstd2, const float* __restrict__ gamma2, const float* __restrict__ dgamma2,
@@ -263,49 +307,64 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
     if (rr >= RPI) return;
     const float invL = (float)(1.0 / (double)L);
-    float k1[8], A1[8], B1[8], k2[8], A2[8], B2[8], ms[8], mh[8];
+    float k1[8], A1[8], B1[8];
+    float k2[X2 ? 8 : 1], A2[X2 ? 8 : 1], B2[X2 ? 8 : 1], ms[MODE == 2 ? 8 : 1], mh[MODE == 2 ? 8 : 1];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float is = invstd[c + j], k = (gamma ? gamma[c + j] : 1.f) * is;
         const float dg = dgamma[c + j] * invL, db = dbeta[c + j] * invL;
         k1[j] = k; A1[j] = -k * is * dg; B1[j] = k * (mean[c + j] * is * dg - db);
-        if (x2) {
+        if constexpr (X2) {
             const float is2 = invstd2[c + j], kk = (gamma2 ? gamma2[c + j] : 1.f) * is2;
             const float dg2 = dgamma2[c + j] * invL, db2 = dbeta2[c + j] * invL;
             k2[j] = kk; A2[j] = -kk * is2 * dg2; B2[j] = kk * (mean2[c + j] * is2 * dg2 - db2);
-        } else {
-            k2[j] = A2[j] = B2[j] = 0.f;
         }
-        ms[j] = mode == 2 ? mscale[c + j] : 0.f;
-        mh[j] = mode == 2 ? mshift[c + j] : 0.f;
+        if constexpr (MODE == 2) { ms[j] = mscale[c + j]; mh[j] = mshift[c + j]; }
     }
-    for (long r = (long)blockIdx.x * RPI + rr; r < L; r += (long)gridDim.x * RPI) {
-        const long off = r * C + c;
-        float gm[8], xv[8], o[8];
-        unpack8(*reinterpret_cast<const u16x8_t*>(g + off), gm);
-        unpack8(*reinterpret_cast<const u16x8_t*>(x + off), xv);
-        if (mode == 1) {
-            float m[8];
-            unpack8(*reinterpret_cast<const u16x8_t*>(msrc + off), m);
+    const long step = (long)gridDim.x * RPI;
+    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
+        const long rs[2] = {r0, r0 + step};
+        u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
-        } else if (mode == 2) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+        for (int u = 0; u < 2; ++u) {          // issue every load of both rows first
+            if (rs[u] < L) {
+                const long off = rs[u] * C + c;
+                gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
+                xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
+                if constexpr (MODE == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
+                if constexpr (X2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
+            }
         }
-        if (dx) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gm[j], fmaf(xv[j], A1[j], B1[j]));
-            *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
-        }
-        if (x2) {
-            float x2v[8];
-            unpack8(*reinterpret_cast<const u16x8_t*>(x2 + off), x2v);
+        for (int u = 0; u < 2; ++u) {
+            if (rs[u] >= L) break;
+            const long off = rs[u] * C + c;
+            float gm[8], xv[8], o[8];
+            unpack8(gv[u], gm);
+            unpack8(xv8[u], xv);
+            if constexpr (MODE == 1) {
+                float m[8];
+                unpack8(mv[u], m);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = fmaf(k2[j], gm[j], fmaf(x2v[j], A2[j], B2[j]));
-            *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
+                for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
+            } else if constexpr (MODE == 2) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+            }
+            if constexpr (DX) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gm[j], fmaf(xv[j], A1[j], B1[j]));
+                *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
+            }
+            if constexpr (X2) {
+                float x2v[8];
+                unpack8(x2v8[u], x2v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = fmaf(k2[j], gm[j], fmaf(x2v[j], A2[j], B2[j]));
+                *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
+            }
+            if constexpr (GMO) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
         }
-        if (gm_out) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
     }
 }
 
@@ -352,8 +411,13 @@ PDNN_API int pdnn_bn_stats(const bf16_t* x, long L, int C, float* slab, hipStrea
 PDNN_API int pdnn_bn_apply(const bf16_t* x, long L, int C, const float* scale, const float* shift,
                            const bf16_t* res, const float* rscale, const float* rshift, int relu, bf16_t* y,
                            hipStream_t st) {
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(L * (C / 8), NT)), dim3(NT), 0, st, x, L, C, scale,
-                       shift, res, rscale, rshift, relu, y);
+    const dim3 grid(stream_grid(L * (C / 8), NT));
+#define PDNN_BA(RES, RSC, RELU) \
+    hipLaunchKernelGGL((bn_apply_kernel<RES, RSC, RELU>), grid, dim3(NT), 0, st, x, L, C, scale, shift, res, rscale, rshift, y)
+    if (res && rscale) { if (relu) PDNN_BA(true, true, true); else PDNN_BA(true, true, false); }
+    else if (res) { if (relu) PDNN_BA(true, false, true); else PDNN_BA(true, false, false); }
+    else { if (relu) PDNN_BA(false, false, true); else PDNN_BA(false, false, false); }
+#undef PDNN_BA
     PDNN_LAUNCH_RET;
 }
 
@@ -388,8 +452,21 @@ PDNN_API int pdnn_bn_bwd_apply(const bf16_t* g, const bf16_t* x, long L, int C, 
                                const float* mshift, bf16_t* dx, const bf16_t* x2, const float* mean2,
                                const float* invstd2, const float* gamma2, const float* dgamma2,
                                const float* dbeta2, bf16_t* dx2, bf16_t* gm_out, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(L * (C / 8), NT)), dim3(NT), 0, st, g, x, L, C,
-                       mean, invstd, gamma, dgamma, dbeta, mode, msrc, mscale, mshift, dx, x2, mean2, invstd2,
-                       gamma2, dgamma2, dbeta2, dx2, gm_out);
+    const dim3 grid(stream_grid(L * (C / 8), NT));
+#define PDNN_BWA(MODE, X2, DX, GMO)                                                                              \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MODE, X2, DX, GMO>), grid, dim3(NT), 0, st, g, x, L, C, mean, invstd, \
+                       gamma, dgamma, dbeta, msrc, mscale, mshift, dx, x2, mean2, invstd2, gamma2, dgamma2,      \
+                       dbeta2, dx2, gm_out)
+    const bool hx2 = x2 != nullptr, hdx = dx != nullptr, hgm = gm_out != nullptr;
+    if (mode == 1) {
+        if (hx2) { if (hgm) PDNN_BWA(1, true, true, true); else PDNN_BWA(1, true, true, false); }
+        else if (hgm) { if (hdx) PDNN_BWA(1, false, true, true); else PDNN_BWA(1, false, false, true); }
+        else PDNN_BWA(1, false, true, false);
+    } else if (mode == 2) {
+        if (hgm) PDNN_BWA(2, false, true, true); else PDNN_BWA(2, false, true, false);
+    } else {
+        if (hx2) PDNN_BWA(0, true, true, false); else PDNN_BWA(0, false, true, false);
+    }
+#undef PDNN_BWA
     PDNN_LAUNCH_RET;
 }
