@@ -1,4 +1,7 @@
-"""Summarise a rocprofv3 kernel trace: per-kernel time over the last `--window-ms` of the trace (steady state)."""
+"""Summarise a rocprofv3 kernel trace: per-kernel time over the last `--window-ms` of the trace (steady state).
+
+``--by-grid`` splits each kernel by its launch grid, so one GEMM kernel template is reported per problem
+shape (which tile count / occupancy each call site gets)."""
 import argparse
 import collections
 import csv
@@ -9,6 +12,7 @@ ap.add_argument("trace")
 ap.add_argument("--window-ms", type=float, default=0, help="0 = whole trace")
 ap.add_argument("--steps", type=int, default=1, help="divide totals by this many steps")
 ap.add_argument("--top", type=int, default=30)
+ap.add_argument("--by-grid", action="store_true")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -18,6 +22,10 @@ if a.window_ms:
 tot, cnt = collections.Counter(), collections.Counter()
 for r in rows:
     n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:90]
+    if a.by_grid:
+        g = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+        w = r.get("Workgroup_Size_X", "?")
+        n = f"{n} grid={g} wg={w}"
     d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     tot[n] += d
     cnt[n] += 1
@@ -25,4 +33,5 @@ busy = sum(tot.values())
 span = (end - int(rows[0]["Start_Timestamp"])) / 1e6
 print(f"kernels={len(rows)} busy={busy/1e6/a.steps:.2f} ms/step span={span/a.steps:.2f} ms/step")
 for n, d in tot.most_common(a.top):
-    print(f"{d/1e6/a.steps:8.3f} ms {cnt[n]//a.steps:5d}x  {100*d/busy:5.1f}%  {n}")
+    c = cnt[n] / a.steps
+    print(f"{d/1e6/a.steps:8.3f} ms {c:6.1f}x {1e3*d/1e6/max(cnt[n],1):8.1f} us/call {100*d/busy:5.1f}%  {n}")
