@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
+    ap.add_argument("--graph", default="off", choices=["off", "on", "auto", "collectives"],
+                    help="replay each step as one captured hipGraph (auto: single-GPU runs only)")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -56,7 +58,12 @@ def main():
     torch.manual_seed(1234 + env.rank)
 
     lm = a.model.lower().startswith("gpt2")
-    model = build_model(a.model, num_classes=1000).to(dev)
+    # the reference's own configs: LeNet on MNIST, CIFAR-stem ResNets, batch 128 per worker, 10 classes
+    # (pytorch_code/distributed_nn.py:42,58-63; model_ops/resnet.py:72,94)
+    small = a.model.lower() == "lenet" or a.model.lower().endswith("_cifar")
+    nc = 10 if small else 1000
+    in_chw = (1, 28, 28) if a.model.lower() == "lenet" else (3, 32, 32) if small else (3, a.image_size, a.image_size)
+    model = build_model(a.model, num_classes=nc).to(dev)
     if a.fp8:
         if lm:
             model.config.fp8 = True
@@ -76,11 +83,21 @@ def main():
         ys = [t[:, 1:].contiguous() for t in toks]
     else:
         opt = SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5)
-        B, S = a.batch or 256, a.image_size
-        xs = [torch.randn(B, 3, S, S, device=dev).to(torch.bfloat16) for _ in range(2)]
-        ys = [torch.randint(0, 1000, (B,), device=dev) for _ in range(2)]
+        B, S = a.batch or (128 if small else 256), in_chw[-1]
+        xs = [torch.randn(B, *in_chw, device=dev).to(torch.bfloat16) for _ in range(2)]
+        ys = [torch.randint(0, nc, (B,), device=dev) for _ in range(2)]
+
+    use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1)
+    if use_graph:
+        # whole step (fwd + bwd + optimizer [+ RCCL buckets if 'collectives']) replayed as one hipGraph
+        from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
+        gstep = GraphedStep(net, opt, loss_fn=OF.cross_entropy, warmup=2,
+                            forward=(lambda m, x, y: m(x, y)) if lm else None,
+                            allow_collectives=a.graph == "collectives")
 
     def step(i):
+        if use_graph:
+            return gstep(xs[i % 2], ys[i % 2])
         opt.zero_grad()
         if lm:
             loss = net(xs[i % 2], ys[i % 2])
@@ -125,7 +142,7 @@ def main():
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
-                       "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb},
+                       "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
         }), flush=True)
     elif env.rank == 0:
         print(json.dumps({
@@ -143,11 +160,13 @@ def main():
             "vs_stock_pytorch_rocm": (round(value / (STOCK_PYTORCH_1GPU * world), 4)
                                       if a.model == "resnet50" and B == 256 and not a.fp8 else None),
             "dtype": "fp8(e4m3) 1x1-conv fwd GEMMs + bf16" if a.fp8 else "bf16",
-            "data": "synthetic (device-resident random 224x224x3 images, random labels), random-init weights",
+            "data": f"synthetic (device-resident random {in_chw[1]}x{in_chw[2]}x{in_chw[0]} images, random labels), "
+                    "random-init weights",
             "final_loss": round(float(loss.detach()), 4),
-            "config": {"model": f"{a.model} (ImageNet layout, 224x224, 1000 classes)", "global_batch": B * world,
+            "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
+                                 f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
-                       "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb},
+                       "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
         }), flush=True)
     runtime.destroy()
 

@@ -861,6 +861,21 @@ void fill_geom(ConvGeom& g, int Nimg, int H, int W, int C, int Ho, int Wo, int R
     g.ph = g.pw = g.r0 = g.s0 = 0; g.Sc = S; g.dSc = make_fdiv(S);
 }
 
+// dst := src (or zeros when src is null), bf16 elements.  Used where a conv dgrad must pre-initialise
+// dx before the parity-class GEMMs scatter into it: a kernel rather than hipMemsetAsync/hipMemcpyAsync
+// keeps a training step a pure kernel sequence, which is what a captured hipGraph replays reliably
+// (memset/memcpy graph nodes broke the second replay of a captured ResNet step).
+__global__ void __launch_bounds__(256) copy_or_zero_kernel(bf16_t* __restrict__ dst, const bf16_t* __restrict__ src,
+                                                           long n) {
+    const long n8 = n >> 3;
+    uint4* d8 = reinterpret_cast<uint4*>(dst);
+    const uint4* s8 = reinterpret_cast<const uint4*>(src);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256)
+        d8[i] = src ? s8[i] : make_uint4(0u, 0u, 0u, 0u);
+    for (long i = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        dst[i] = src ? src[i] : (bf16_t)0;
+}
+
 }  // namespace
 
 static void ensure_attrs() {}
@@ -1065,9 +1080,10 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
     bool any_empty;
     const int ncl = dgrad_classes(H, W, R, S, st, pad, cl, &any_empty);
     if (any_empty) {   // pixels no tap reaches: zero (or the residual)
-        const size_t bytes = (size_t)Nimg * H * W * C * sizeof(bf16_t);
-        hipError_t e = (res && !bn_x) ? hipMemcpyAsync(dx, res, bytes, hipMemcpyDeviceToDevice, stream)
-                                      : hipMemsetAsync(dx, 0, bytes, stream);
+        const long n = (long)Nimg * H * W * C;         // C % 8 == 0: 16-B aligned rows
+        hipLaunchKernelGGL(copy_or_zero_kernel, dim3(stream_grid(n / 8 + 1, 256)), dim3(256), 0, stream, dx,
+                           (res && !bn_x) ? res : nullptr, n);
+        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
     int row0 = 0;

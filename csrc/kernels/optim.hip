@@ -11,6 +11,12 @@
 // factor (1/world, or 1/alive-count for k-of-n straggler mode) in as `gscale` read from device memory.
 #include "common.h"
 
+//
+// Graph replay: a captured hipGraph bakes kernel arguments in, so the per-step hyper-parameters that
+// change between replays (learning rate, Adam's bias corrections) can instead be read from a small
+// device buffer `hyper` that the host refreshes (stream-ordered H2D copy) before each replay:
+//   SGD:  hyper[0] = lr               Adam: hyper[0] = lr, hyper[1] = 1 - b1^t, hyper[2] = 1 - b2^t
+// hyper == nullptr keeps the by-value arguments (eager mode).
 namespace {
 constexpr int NT = 256;
 
@@ -18,8 +24,9 @@ __global__ void __launch_bounds__(NT) sgd_kernel(float* __restrict__ p, const fl
                                                  float* __restrict__ buf, bf16_t* __restrict__ shadow, long n,
                                                  float lr, float momentum, float dampening, float wd,
                                                  int nesterov, const float* __restrict__ gscale_ptr,
-                                                 float gscale, int first) {
+                                                 float gscale, int first, const float* __restrict__ hyper) {
     const float gs = gscale_ptr ? gscale * (*gscale_ptr) : gscale;
+    if (hyper) lr = hyper[0];
     const long n4 = n >> 2;
     for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
         float4 pv = reinterpret_cast<float4*>(p)[i];
@@ -60,26 +67,59 @@ __global__ void __launch_bounds__(NT) sgd_kernel(float* __restrict__ p, const fl
     }
 }
 
-// Adam / AdamW (decoupled=1).  bc1 = 1 - beta1^t, bc2 = 1 - beta2^t computed on the host.
+// Adam / AdamW (decoupled=1).  bc1 = 1 - beta1^t, bc2 = 1 - beta2^t (by value, or hyper[1..2]).
+// Memory bound (16 B read + 14 B written per parameter): float4 loads/stores over the 16-B aligned
+// body (`vec`, checked by the launcher), scalar tail.
+struct AdamCoef {
+    float lr, b1, b2, eps, wd, step, rbc2, gs;
+    int decoupled;
+    __device__ __forceinline__ void upd(float& pi, float gi, float& mi, float& vi) const {
+        gi *= gs;
+        if (decoupled) pi -= lr * wd * pi;
+        else gi += wd * pi;
+        mi = b1 * mi + (1.f - b1) * gi;
+        vi = b2 * vi + (1.f - b2) * gi * gi;
+        pi -= step * mi / (sqrtf(vi) * rbc2 + eps);
+    }
+};
+
 __global__ void __launch_bounds__(NT) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ m, float* __restrict__ v,
                                                   bf16_t* __restrict__ shadow, long n, float lr, float b1,
                                                   float b2, float eps, float wd, int decoupled, float bc1,
                                                   float bc2, const float* __restrict__ gscale_ptr,
-                                                  float gscale) {
-    const float gs = gscale_ptr ? gscale * (*gscale_ptr) : gscale;
-    const float step = lr / bc1, rbc2 = rsqrtf(bc2);
-    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
-        float pi = p[i];
-        float gi = g[i] * gs;
-        if (decoupled) pi -= lr * wd * pi;
-        else gi += wd * pi;
-        const float mi = b1 * m[i] + (1.f - b1) * gi;
-        const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+                                                  float gscale, const float* __restrict__ hyper, int vec) {
+    if (hyper) {
+        lr = hyper[0];
+        bc1 = hyper[1];
+        bc2 = hyper[2];
+    }
+    const AdamCoef c{lr, b1, b2, eps, wd, lr / bc1, rsqrtf(bc2), gscale_ptr ? gscale * (*gscale_ptr) : gscale,
+                     decoupled};
+    const long n4 = vec ? (n >> 2) : 0;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+        float4 pv = reinterpret_cast<float4*>(p)[i];
+        const float4 gv = reinterpret_cast<const float4*>(g)[i];
+        float4 mv = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        c.upd(pv.x, gv.x, mv.x, vv.x);
+        c.upd(pv.y, gv.y, mv.y, vv.y);
+        c.upd(pv.z, gv.z, mv.z, vv.z);
+        c.upd(pv.w, gv.w, mv.w, vv.w);
+        reinterpret_cast<float4*>(p)[i] = pv;
+        reinterpret_cast<float4*>(m)[i] = mv;
+        reinterpret_cast<float4*>(v)[i] = vv;
+        if (shadow) {
+            u16x4_t s = {f2bf(pv.x), f2bf(pv.y), f2bf(pv.z), f2bf(pv.w)};
+            reinterpret_cast<u16x4_t*>(shadow)[i] = s;
+        }
+    }
+    for (long i = n4 * 4 + (long)blockIdx.x * NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        c.upd(pi, g[i], mi, vi);
+        p[i] = pi;
         m[i] = mi;
         v[i] = vi;
-        pi -= step * mi / (sqrtf(vi) * rbc2 + eps);
-        p[i] = pi;
         if (shadow) shadow[i] = f2bf(pi);
     }
 }
@@ -118,17 +158,20 @@ __global__ void __launch_bounds__(NT) sumsq_kernel(const float* __restrict__ x, 
 
 PDNN_API int pdnn_sgd_step(float* p, const float* g, float* buf, bf16_t* shadow, long n, float lr, float momentum,
                            float dampening, float wd, int nesterov, const float* gscale_ptr, float gscale, int first,
-                           hipStream_t st) {
+                           const float* hyper, hipStream_t st) {
     hipLaunchKernelGGL(sgd_kernel, dim3(stream_grid(n / 4 + 1, NT)), dim3(NT), 0, st, p, g, buf, shadow, n, lr,
-                       momentum, dampening, wd, nesterov, gscale_ptr, gscale, first);
+                       momentum, dampening, wd, nesterov, gscale_ptr, gscale, first, hyper);
     PDNN_LAUNCH_RET;
 }
 
 PDNN_API int pdnn_adam_step(float* p, const float* g, float* m, float* v, bf16_t* shadow, long n, float lr, float b1,
                             float b2, float eps, float wd, int decoupled, float bc1, float bc2,
-                            const float* gscale_ptr, float gscale, hipStream_t st) {
-    hipLaunchKernelGGL(adam_kernel, dim3(stream_grid(n, NT)), dim3(NT), 0, st, p, g, m, v, shadow, n, lr, b1, b2, eps,
-                       wd, decoupled, bc1, bc2, gscale_ptr, gscale);
+                            const float* gscale_ptr, float gscale, const float* hyper, hipStream_t st) {
+    const uintptr_t a16 = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                          reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
+    const int vec = (a16 & 15) == 0 && (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
+    hipLaunchKernelGGL(adam_kernel, dim3(stream_grid(vec ? n / 4 + 1 : n, NT)), dim3(NT), 0, st, p, g, m, v, shadow,
+                       n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale_ptr, gscale, hyper, vec);
     PDNN_LAUNCH_RET;
 }
 

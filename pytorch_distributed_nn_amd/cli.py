@@ -53,6 +53,9 @@ def add_fit_args(p: argparse.ArgumentParser):
     p.add_argument("--checkpoint-dir", type=str, default=None)
     p.add_argument("--resume", type=str, default=None)
     p.add_argument("--trace", type=str, default=None)
+    p.add_argument("--graph", type=str, default="off", choices=["off", "on", "collectives"],
+                   help="replay each training step as one captured hipGraph (utils/graphs.py); 'on' applies to "
+                        "single-GPU runs, 'collectives' also captures the DDP all-reduces (every rank)")
     p.add_argument("--metrics", type=str, default=None)
     p.add_argument("--out-dir", type=str, default="outfiles")
     p.add_argument("--config", type=str, default=None,
@@ -173,8 +176,12 @@ def main(argv=None):
         def __len__(self):
             return len(loader)
 
+    graph = {"off": False, "on": world == 1, "collectives": "collectives"}[args.graph]
+    if strag:                      # per-step host sleeps in grad hooks cannot be replayed from a graph
+        graph = False
     tr = Trainer(net, opt, OF.cross_entropy, dev, rank, world, args.log_interval, args.metrics,
-                 args.trace, args.checkpoint_dir, arch=args.network, printer=print if rank == 0 else (lambda *a: None))
+                 args.trace, args.checkpoint_dir, arch=args.network, printer=print if rank == 0 else (lambda *a: None),
+                 graph=graph)
     if args.resume:
         tr.resume(args.resume)
     hist = tr.train(_DevLoader(), epochs=args.epochs, max_steps=args.max_steps, batch_size=args.batch_size,

@@ -54,8 +54,8 @@ _SIGS = {
     "pdnn_avgpool_bwd": [P, P, I, I, I, P],
     "pdnn_xent_fwd": [P, L, I, I, P, I, P, P, P, P, I, P],
     "pdnn_xent_bwd": [P, L, I, I, P, I, P, P, F, P, L, I, P],
-    "pdnn_sgd_step": [P, P, P, P, L, F, F, F, F, I, P, F, I, P],
-    "pdnn_adam_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, F, P, F, P],
+    "pdnn_sgd_step": [P, P, P, P, L, F, F, F, F, I, P, F, I, P, P],
+    "pdnn_adam_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, F, P, F, P, P],
     "pdnn_cast_f32_bf16": [P, P, L, F, P],
     "pdnn_cast_bf16_f32": [P, P, L, F, I, P],
     "pdnn_scale_f32": [P, L, F, P, I, P],

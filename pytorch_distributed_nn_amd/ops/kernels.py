@@ -344,14 +344,18 @@ def colsum(x2d, out=None, accumulate=False):
 
 
 # ----------------------------------------------------------------------------------- optim / buckets
-def sgd_step(p, g, buf, shadow, lr, momentum, dampening, wd, nesterov, gscale_dev=None, gscale=1.0, first=False):
+def sgd_step(p, g, buf, shadow, lr, momentum, dampening, wd, nesterov, gscale_dev=None, gscale=1.0, first=False,
+             hyper=None):
+    """``hyper`` (optional fp32 device tensor [lr]) overrides ``lr`` at run time (graph replay)."""
     call("pdnn_sgd_step", ptr(p), ptr(g), ptr(buf), ptr(shadow), p.numel(), float(lr), float(momentum),
-         float(dampening), float(wd), int(nesterov), ptr(gscale_dev), float(gscale), int(first), stream())
+         float(dampening), float(wd), int(nesterov), ptr(gscale_dev), float(gscale), int(first), ptr(hyper), stream())
 
 
-def adam_step(p, g, m, v, shadow, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale_dev=None, gscale=1.0):
+def adam_step(p, g, m, v, shadow, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale_dev=None, gscale=1.0, hyper=None):
+    """``hyper`` (optional fp32 device tensor [lr, 1-b1^t, 1-b2^t]) overrides lr/bc1/bc2 (graph replay)."""
     call("pdnn_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(b1), float(b2),
-         float(eps), float(wd), int(decoupled), float(bc1), float(bc2), ptr(gscale_dev), float(gscale), stream())
+         float(eps), float(wd), int(decoupled), float(bc1), float(bc2), ptr(gscale_dev), float(gscale), ptr(hyper),
+         stream())
 
 
 def cast_f32_bf16(x, y, scale=1.0):

@@ -40,11 +40,56 @@ class _FusedBase(torch.optim.Optimizer):
         self.grad_scale = 1.0          # host-side factor (e.g. 1/world_size when grads are summed)
         self.grad_scale_dev = None     # optional device scalar (e.g. 1/alive for k-of-n)
         self._flat_cache = {}
+        self._graph = False            # graph mode: per-step hyper-parameters live in device memory
+        self._hyper = {}
 
     def _group_flat(self, gi, group):
         if gi not in self._flat_cache:
             self._flat_cache[gi] = _flat_of(group["params"])
         return self._flat_cache[gi]
+
+    # ---------------------------------------------------------------------------------- graph mode
+    # A hipGraph captured around ``step()`` replays the kernels with the arguments they had at capture.
+    # In graph mode the fused kernels read the values that change between steps (lr; Adam's bias
+    # corrections) from a per-group device buffer instead, and :meth:`pre_replay` — called on the host
+    # before every replay — advances the host-side state and refreshes that buffer with stream-ordered
+    # fills (no host<->device sync, so the CPU can run ahead of the GPU as in eager mode).
+    _HYPER_LEN = 1
+
+    def graph_mode(self, on: bool = True):
+        if on:
+            for gi, group in enumerate(self.param_groups):
+                fp, _ = self._group_flat(gi, group)
+                if fp is None or not fp.data.is_cuda:
+                    raise RuntimeError("graph mode needs every param group on a flat CUDA arena")
+                self._check_graphable(gi)
+                # allocated (and filled) OUTSIDE any capture: a buffer created inside the capture would
+                # come from the graph pool and its initialising fill would be replayed over pre_replay's
+                if gi not in self._hyper:
+                    self._hyper[gi] = torch.zeros(self._HYPER_LEN, dtype=torch.float32, device=fp.data.device)
+                    self._fill_hyper(gi, group, advance=False)
+        self._graph = bool(on)
+
+    def _check_graphable(self, gi):
+        pass
+
+    def _hyper_buf(self, gi, n, device):
+        return self._hyper[gi]
+
+    def _hyper_values(self, gi, group, advance=True):    # one step's values, in the kernel's hyper[] order
+        return [group["lr"]]
+
+    @torch.no_grad()
+    def _fill_hyper(self, gi, group, advance=True):
+        h = self._hyper[gi]
+        for j, v in enumerate(self._hyper_values(gi, group, advance)):
+            h[j:j + 1].fill_(float(v))
+
+    @torch.no_grad()
+    def pre_replay(self):
+        for gi, group in enumerate(self.param_groups):
+            if gi in self._hyper:
+                self._fill_hyper(gi, group)
 
     def zero_grad(self, set_to_none: bool = False):
         done = set()
@@ -70,6 +115,11 @@ class SGD(_FusedBase):
         super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                                       nesterov=nesterov))
 
+    def _check_graphable(self, gi):
+        # the first momentum step initialises the buffer (a different kernel branch): run it eagerly
+        if self.param_groups[gi]["momentum"] != 0 and "momentum_buffer" not in self.state.get(f"flat{gi}", {}):
+            raise RuntimeError("SGD graph mode: run one eager step before capture (momentum buffer init)")
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -88,8 +138,9 @@ class SGD(_FusedBase):
                 if mom != 0 and first:
                     st["momentum_buffer"] = torch.zeros(e - s, device=fp.data.device)
                 buf = st.get("momentum_buffer")
+                hyper = self._hyper_buf(gi, 1, fp.data.device) if self._graph else None
                 K.sgd_step(fp.data[s:e], fp.grad[s:e], buf, fp.shadow[s:e] if fp.shadow is not None else None,
-                           lr, mom, damp, wd, nest, self.grad_scale_dev, self.grad_scale, first)
+                           lr, mom, damp, wd, nest, self.grad_scale_dev, self.grad_scale, first, hyper=hyper)
                 fp.generation += 1
                 continue
             for p in group["params"]:
@@ -120,6 +171,16 @@ class Adam(_FusedBase):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
 
+    _HYPER_LEN = 3
+
+    def _hyper_values(self, gi, group, advance=True):
+        st = self.state.setdefault(f"flat{gi}", {})
+        if advance:
+            st["step"] = st.get("step", 0) + 1       # this replay is step t
+        t = max(st.get("step", 0), 1)
+        b1, b2 = group["betas"]
+        return [group["lr"], 1 - b1 ** t, 1 - b2 ** t]
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -137,11 +198,16 @@ class Adam(_FusedBase):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros(e - s, device=fp.data.device)
                     st["exp_avg_sq"] = torch.zeros(e - s, device=fp.data.device)
-                st["step"] += 1
-                t = st["step"]
+                hyper = None
+                if self._graph:                  # t advances in pre_replay(); kernel reads hyper[]
+                    hyper = self._hyper_buf(gi, 3, fp.data.device)
+                else:
+                    st["step"] += 1
+                t = max(st["step"], 1)
                 K.adam_step(fp.data[s:e], fp.grad[s:e], st["exp_avg"], st["exp_avg_sq"],
                             fp.shadow[s:e] if fp.shadow is not None else None, lr, b1, b2, eps, wd,
-                            self.decoupled, 1 - b1 ** t, 1 - b2 ** t, self.grad_scale_dev, self.grad_scale)
+                            self.decoupled, 1 - b1 ** t, 1 - b2 ** t, self.grad_scale_dev, self.grad_scale,
+                            hyper=hyper)
                 fp.generation += 1
                 continue
             for p in group["params"]:

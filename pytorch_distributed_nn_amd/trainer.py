@@ -23,7 +23,7 @@ from .utils.observability import MetricsSink, Tracer, accuracy, load_checkpoint,
 class Trainer:
     def __init__(self, model, optimizer, loss_fn=None, device=None, rank=0, world=1, log_interval=10,
                  metrics_path=None, trace_path=None, checkpoint_dir=None, arch="", timing=True, printer=print,
-                 lr_schedule=None, grad_clip=None):
+                 lr_schedule=None, grad_clip=None, graph=False, graph_warmup=2):
         self.model = model
         self.opt = optimizer
         self.loss_fn = loss_fn or OF.cross_entropy
@@ -41,6 +41,12 @@ class Trainer:
         self.step_no = 0
         self.epoch = 0
         self.history = []
+        # hipGraph-captured step (utils/graphs.py): one replay per iteration instead of ~1000 launches
+        self.graph_step = None
+        if graph and self.device.type == "cuda":
+            from .utils.graphs import GraphedStep
+            self.graph_step = GraphedStep(model, optimizer, self.loss_fn, warmup=graph_warmup, grad_clip=grad_clip,
+                                          allow_collectives=graph == "collectives")
 
     # ----------------------------------------------------------------------------------------- step
     def _sync(self):
@@ -59,6 +65,12 @@ class Trainer:
         if self.lr_schedule is not None:
             for g in self.opt.param_groups:
                 g["lr"] = self.lr_schedule(self.step_no)
+        if self.graph_step is not None:       # whole step is one graph: no per-phase split
+            with self._span("graph_step"):
+                loss = self.graph_step(x, y)
+            self._sync()
+            self.step_no += 1
+            return loss, self.graph_step.output, (0.0, time.perf_counter() - t0, 0.0)
         self.opt.zero_grad()
         with self._span("forward"):
             out = self.model(x)

@@ -1,0 +1,179 @@
+"""hipGraph-captured training step (utils/graphs.py) vs the eager step: same model, same data, same
+optimizer schedule -> same trajectory.  Covers SGD+momentum with a changing learning rate (device lr read
+at replay) and AdamW (bias corrections advanced at replay), the fused ResNet path, the Trainer wiring and
+the eager fallback for a batch of a different shape."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _delta_rel(pg, pe, p0):
+    """|| (pg - p0) - (pe - p0) || / || pe - p0 ||: how far the graph trajectory is from the eager one."""
+    return ((pg - pe).norm() / (pe - p0).norm().clamp_min(1e-12)).item()
+
+
+def _pair(name, opt_name, lr):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.optim import SGD, AdamW, flatten_module
+    torch.manual_seed(0)
+    m0 = build_model(name, 10) if not name.startswith("gpt2") else build_model(name)
+    ms = [copy.deepcopy(m0).cuda() for _ in range(2)]
+    opts = []
+    for m in ms:
+        flatten_module(m)
+        opts.append(SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4) if opt_name == "sgd"
+                    else AdamW(m.parameters(), lr=lr, weight_decay=0.1))
+    return ms, opts
+
+
+# ResNet-18 at batch 16: even two EAGER runs drift apart (split-K fp32 atomics reorder sums and 16 BN layers
+# amplify it), so its bounds are looser and its learning rate smaller
+@pytest.mark.parametrize("name,opt_name,shape,lr,tol", [("LeNet", "sgd", (32, 1, 28, 28), 0.05, 2e-2),
+                                                        ("ResNet18", "sgd", (16, 3, 32, 32), 0.005, 1e-1),
+                                                        ("gpt2_tiny", "adamw", (2, 64), 1e-3, 2e-2)])
+def test_graph_step_matches_eager(name, opt_name, shape, lr, tol):
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
+    lm = name.startswith("gpt2")
+    (me, mg), (oe, og) = _pair(name, opt_name, lr)
+    p0 = me._pdnn_flat.data.clone()
+    g = torch.Generator().manual_seed(1)
+    if lm:
+        data = [torch.randint(0, 512, (shape[0], shape[1] + 1), generator=g).cuda() for _ in range(6)]
+        batches = [(d[:, :-1].contiguous(), d[:, 1:].contiguous()) for d in data]
+        fwd = lambda m, x, y: m(x, y)  # noqa: E731
+    else:
+        batches = [(torch.randn(*shape, generator=g).cuda(), torch.randint(0, 10, (shape[0],), generator=g).cuda())
+                   for _ in range(6)]
+        fwd = lambda m, x, y: OF.cross_entropy(m(x), y)  # noqa: E731
+    sched = [1.0, 0.5, 0.8, 0.3, 0.6, 0.2]          # per-step lr multipliers: must reach the graph
+    base = oe.param_groups[0]["lr"]
+    gs = GraphedStep(mg, og, forward=fwd, warmup=2)
+    losses_e, losses_g = [], []
+    for i, (x, y) in enumerate(batches):
+        for o in (oe, og):
+            o.param_groups[0]["lr"] = base * sched[i]
+        oe.zero_grad()
+        le = fwd(me, x, y)
+        le.backward()
+        oe.step()
+        losses_e.append(float(le.detach()))
+        losses_g.append(float(gs(x, y)))
+    torch.cuda.synchronize()
+    assert gs.graph is not None and gs.replays == 4
+    for a, b in zip(losses_e, losses_g):
+        assert abs(a - b) < tol * max(1.0, abs(a)), (losses_e, losses_g)
+    d = _delta_rel(mg._pdnn_flat.data, me._pdnn_flat.data, p0)
+    assert d < 2.5 * tol, d
+    # bf16 shadow refreshed by the replayed optimizer kernel
+    fp = mg._pdnn_flat
+    assert ((fp.shadow.float() - fp.data).norm() / fp.data.norm()).item() < 5e-3
+    if opt_name == "adamw":
+        assert og.state["flat0"]["step"] == oe.state["flat0"]["step"] == 6
+
+
+def _copy_state(dst_m, dst_o, src_m, src_o):
+    """dst := src (flat weights + bf16 shadow, BN buffers, optimizer state)."""
+    dst_m._pdnn_flat.data.copy_(src_m._pdnn_flat.data)
+    dst_m._pdnn_flat.refresh_shadow()
+    for bd, bs in zip(dst_m.buffers(), src_m.buffers()):
+        bd.copy_(bs)
+    dst = dst_o.state.setdefault("flat0", {})
+    for k, v in src_o.state.get("flat0", {}).items():
+        if torch.is_tensor(v) and k in dst:
+            dst[k].copy_(v)
+        else:
+            dst[k] = v.clone() if torch.is_tensor(v) else v
+
+
+@pytest.mark.parametrize("name,opt_name,shape,lr", [("ResNet18", "sgd", (64, 3, 32, 32), 0.1),
+                                                    ("ResNet50", "sgd", (32, 3, 32, 32), 0.1),
+                                                    ("resnet50", "sgd", (8, 3, 96, 96), 0.02),
+                                                    ("gpt2_tiny", "adamw", (4, 128), 1e-3)])
+def test_graph_replay_lockstep(name, opt_name, shape, lr):
+    """Every replay == one eager step from the SAME state, at the bench learning rate.  Two eager copies are
+    re-synced to the graph model before each step: their disagreement is the one-step nondeterminism
+    (fp32 atomics) floor, and the replay must sit within it — a replay that reads a stale value or skips
+    work cannot hide behind trajectory chaos."""
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
+    lm = name.startswith("gpt2")
+    (me, mg), (oe, og) = _pair(name, opt_name, lr)
+    (me2, _), (oe2, _) = _pair(name, opt_name, lr)
+    g = torch.Generator().manual_seed(2)
+    if lm:
+        fwd = lambda m, x, y: m(x, y)  # noqa: E731
+
+        def batch():
+            d = torch.randint(0, 512, (shape[0], shape[1] + 1), generator=g).cuda()
+            return d[:, :-1].contiguous(), d[:, 1:].contiguous()
+    else:
+        fwd = lambda m, x, y: OF.cross_entropy(m(x), y)  # noqa: E731
+        nc = 1000 if name == "resnet50" else 10
+
+        def batch():
+            return torch.randn(*shape, generator=g).cuda(), torch.randint(0, nc, (shape[0],), generator=g).cuda()
+
+    def eager(m, o, x, y):
+        o.zero_grad()
+        loss = fwd(m, x, y)
+        loss.backward()
+        o.step()
+        return float(loss.detach())
+
+    gs = GraphedStep(mg, og, forward=fwd, warmup=2)
+    for i in range(8):
+        x, y = batch()
+        if i >= 2:
+            _copy_state(me, oe, mg, og)
+            _copy_state(me2, oe2, mg, og)
+        p_before = mg._pdnn_flat.data.clone()
+        le = eager(me, oe, x, y)
+        if i >= 2:
+            eager(me2, oe2, x, y)
+        lg = float(gs(x, y))
+        torch.cuda.synchronize()
+        if i >= 2:
+            de = me._pdnn_flat.data - p_before
+            noise = ((me2._pdnn_flat.data - me._pdnn_flat.data).norm() / de.norm()).item()
+            err = ((mg._pdnn_flat.data - me._pdnn_flat.data).norm() / de.norm()).item()
+            print(f"step {i}: replay-vs-eager {err:.2e}, eager-vs-eager {noise:.2e}, loss {le:.4f} / {lg:.4f}")
+            assert err < 3 * noise + 2e-3, (i, err, noise)
+            assert abs(le - lg) < 1e-2 * max(1.0, abs(lg)), (i, le, lg)
+    assert gs.replays == 6
+
+
+def test_graph_step_shape_change_runs_eager():
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
+    (_, m), (_, o) = _pair("LeNet", "sgd", 0.05)
+    gs = GraphedStep(m, o, loss_fn=OF.cross_entropy, warmup=1)
+    x, y = torch.randn(16, 1, 28, 28).cuda(), torch.randint(0, 10, (16,)).cuda()
+    for _ in range(3):
+        gs(x, y)
+    assert gs.replays == 2
+    l_small = gs(x[:5], y[:5])                    # partial batch: eager, graph untouched
+    assert gs.replays == 2 and torch.isfinite(l_small)
+    gs(x, y)
+    assert gs.replays == 3 and o._graph
+
+
+def test_trainer_graph_mode():
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.trainer import Trainer
+    (_, m), (_, o) = _pair("LeNet", "sgd", 0.05)
+    tr = Trainer(m, o, OF.cross_entropy, torch.device("cuda"), log_interval=2, printer=lambda *a: None, graph=True,
+                 lr_schedule=lambda s: 0.05 / (1 + s))
+    g = torch.Generator().manual_seed(3)
+    x, y = torch.randn(64, 1, 28, 28, generator=g).cuda(), torch.randint(0, 10, (64,), generator=g).cuda()
+
+    def loader():
+        while True:
+            yield x, y
+    hist = tr.train(loader(), epochs=1, max_steps=8, steps_per_epoch=8)
+    assert tr.graph_step.replays == 6
+    losses = [h["loss"] for h in hist if h["loss"] is not None]
+    assert losses[-1] < losses[0]                 # memorising one batch

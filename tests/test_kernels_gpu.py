@@ -226,6 +226,37 @@ def test_sgd_adam(K):
     assert torch.allclose(p2, pr2.detach(), atol=1e-6)
 
 
+@pytest.mark.parametrize("offset", [0, 1])          # 16-B aligned float4 body + tail / scalar-only path
+def test_adam_vec_and_device_hyper(K, offset):
+    """Adam over an (un)aligned slice with bf16 shadow, hyper-parameters read from device memory
+    (graph-replay mode) vs torch.optim.Adam; SGD lr from device memory vs by value."""
+    n = 4099
+    base = torch.randn(n + offset, device="cuda")
+    p = base[offset:]
+    g = torch.randn(n, device="cuda")
+    m, v = torch.zeros(n + offset, device="cuda")[offset:], torch.zeros(n + offset, device="cuda")[offset:]
+    sh = torch.empty(n + offset, device="cuda", dtype=BF)[offset:]
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=2e-3, weight_decay=0.01)
+    hyper = torch.zeros(3, device="cuda")
+    for t in (1, 2, 3):
+        pr.grad = g.clone()
+        opt.step()
+        hyper.copy_(torch.tensor([2e-3, 1 - 0.9 ** t, 1 - 0.999 ** t]))
+        # by-value lr/bc deliberately wrong: the device values must win
+        K.adam_step(p, g, m, v, sh, 9.0, 0.9, 0.999, 1e-8, 0.01, False, 0.5, 0.5, hyper=hyper)
+    assert torch.allclose(p, pr.detach(), atol=1e-6)
+    assert rel(sh, p) < 5e-3
+    q1, q2 = torch.randn(n, device="cuda"), None
+    q2 = q1.clone()
+    b1, b2 = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    lr_dev = torch.tensor([0.05], device="cuda")
+    for first in (True, False):
+        K.sgd_step(q1, g, b1, None, 0.05, 0.9, 0.0, 0.0, False, first=first)
+        K.sgd_step(q2, g, b2, None, 7.0, 0.9, 0.0, 0.0, False, first=first, hyper=lr_dev)
+    assert torch.equal(q1, q2)
+
+
 @pytest.mark.parametrize("op", ["relu", "sigmoid", "gelu"])
 def test_act(K, op):
     x = rnd(4096)
