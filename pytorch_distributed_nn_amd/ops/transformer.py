@@ -31,6 +31,7 @@ import torch
 import torch.nn.functional as F
 
 from ..optim.flat import direct_grad, grad_ready
+from . import blas as BL
 from . import kernels as K
 
 BF16 = torch.bfloat16
@@ -158,7 +159,7 @@ class EmbeddingFn(torch.autograd.Function):
 # ------------------------------------------------------------------------------------------------
 def _wgrad(g, x, shape):
     dw = torch.zeros(shape, device=g.device, dtype=F32)
-    K.gemm_tn_acc(g, x, dw)
+    BL.wgrad_acc(g, x, dw)
     return dw
 
 
@@ -179,7 +180,7 @@ class _Sink:
     def linear(self, p_w, p_b, g, x):
         tw = self._tgt(p_w)
         if tw is not None:
-            K.gemm_tn_acc(g, x, tw)
+            BL.wgrad_acc(g, x, tw)
             rw = None
         else:
             rw = _wgrad(g, x, p_w.shape)
@@ -222,7 +223,7 @@ class GPT2BlockFn(torch.autograd.Function):
                 return linear_fp8_fwd(inp, params[i], metas[(i - 2) // 2 if i < 6 else (i - 4) // 2], **kw)
         else:
             def lin(inp, i, wk, **kw):
-                return K.gemm_nt_ex(inp, wk, **kw)
+                return BL.linear_fwd(inp, wk, **kw)
         ln1, m1, r1 = K.layernorm_fwd(x, ln1w, ln1b, eps)
         qkv = lin(ln1, 2, wqkv, bias=attn_b)
         D = x.shape[1]
@@ -253,20 +254,20 @@ class GPT2BlockFn(torch.autograd.Function):
         sink = _Sink()
         g = g.contiguous()
         # MLP
-        du = K.gemm_nt_ex(g, wfc2, dgelu=u, w_kn=True)                 # (g . Wfc2) * gelu'(u)
+        du = BL.linear_dgrad(g, wfc2, dgelu=u)                         # (g . Wfc2) * gelu'(u)
         dfc2_w, dfc2_b = sink.linear(Pm[10], Pm[11], g, h)
-        dln2 = K.gemm_nt_ex(du, wfc, w_kn=True)
+        dln2 = BL.linear_dgrad(du, wfc)
         dfc_w, dfc_b = sink.linear(Pm[8], Pm[9], du, ln2)
         dx1, dln2w, dln2b = sink.layernorm(dln2, x1, ln2w, m2, r2, g, Pm[6], Pm[7])
         # attention
-        dy = K.gemm_nt_ex(dx1, wproj, w_kn=True)
+        dy = BL.linear_dgrad(dx1, wproj)
         dproj_w, dproj_b = sink.linear(Pm[4], Pm[5], dx1, y)
         if ctx.flash:
             dqkv = K.flash_attn_bwd(qkv, y, dy, P, B, T, H, 1.0 / math.sqrt(x.shape[1] // H))
         else:
             dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
         ctx.S = None
-        dln1 = K.gemm_nt_ex(dqkv, wqkv, w_kn=True)
+        dln1 = BL.linear_dgrad(dqkv, wqkv)
         dattn_w, dattn_b = sink.linear(Pm[2], Pm[3], dqkv, ln1)
         dx, dln1w, dln1b = sink.layernorm(dln1, x, ln1w, m1, r1, dx1, Pm[0], Pm[1])
         sink.done()
@@ -283,7 +284,7 @@ class LMHeadLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte):
         xf, m, r = K.layernorm_fwd(x, lnw, lnb, eps)
-        logits = K.gemm_nt_ex(xf, wte_k)
+        logits = BL.linear_fwd(xf, wte_k)
         _, lse, acc = K.xent_fwd(logits, targets)
         ctx.save_for_backward(x, xf, m, r, logits, targets, lse, acc, lnw, wte_k)
         ctx.eps = eps
@@ -295,7 +296,7 @@ class LMHeadLossFn(torch.autograd.Function):
         x, xf, m, r, logits, targets, lse, acc, lnw, wte_k = ctx.saved_tensors
         gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
         dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
-        dxf = K.gemm_nt_ex(dlogits, wte_k, w_kn=True)
+        dxf = BL.linear_dgrad(dlogits, wte_k)
         dwte = _wgrad(dlogits, xf, wte_k.shape)         # tied weight: summed by autograd (not direct)
         sink = _Sink()
         dx, dlnw, dlnb = sink.layernorm(dxf, x, lnw, m, r, None, *ctx.params)
