@@ -102,14 +102,25 @@ __global__ void __launch_bounds__(NT) colsum_kernel(const bf16_t* __restrict__ x
 
 // Two-level column sum for tall matrices (cols % 8 == 0): level 1 — block (column group of 512, row split
 // y) accumulates 8 columns per lane over its rows with 16-byte loads and writes one partial row;
-// level 2 sums the partial rows (deterministic, no atomics).
+// level 2 sums the partial rows (deterministic, no atomics).  Sized so level 1 fills the chip (>= ~256
+// blocks even for 768 columns: up to 128 row splits of >= 64 rows) and level 2 is a short unrolled
+// reduction spread over 64-column blocks (bias gradients of a GPT-2 step are 60+ of these calls).
 __global__ void __launch_bounds__(NT) colsum_partial_kernel(const bf16_t* __restrict__ x, long rows, int cols,
                                                             float* __restrict__ part) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = (blockIdx.x * 64 + lane) * 8;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (c < cols) {
-        for (long r = (long)blockIdx.y * 4 + w; r < rows; r += (long)gridDim.y * 4) {
+        const long r0 = (long)blockIdx.y * 4 + w, rs = (long)gridDim.y * 4;
+        long r = r0;
+        for (; r + rs < rows; r += 2 * rs) {          // two rows in flight per lane
+            float v[8], u[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(x + r * cols + c), v);
+            unpack8(*reinterpret_cast<const u16x8_t*>(x + (r + rs) * cols + c), u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += v[j] + u[j];
+        }
+        if (r < rows) {
             float v[8];
             unpack8(*reinterpret_cast<const u16x8_t*>(x + r * cols + c), v);
 #pragma unroll
@@ -126,19 +137,35 @@ __global__ void __launch_bounds__(NT) colsum_partial_kernel(const bf16_t* __rest
     }
 }
 
+// level 2: block = 64 columns x 4 row groups, 4 independent accumulators per lane
 __global__ void __launch_bounds__(NT) colsum_final_kernel(const float* __restrict__ part, int nrows, int cols,
                                                           float* __restrict__ out, int accumulate) {
-    const int c = blockIdx.x * NT + threadIdx.x;
-    if (c >= cols) return;
-    float t = 0.f;
-    for (int r = 0; r < nrows; ++r) t += part[(long)r * cols + c];
-    out[c] = accumulate ? out[c] + t : t;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (c < cols) {
+        int r = w;
+        for (; r + 12 < nrows; r += 16) {
+            a0 += part[(long)r * cols + c];
+            a1 += part[(long)(r + 4) * cols + c];
+            a2 += part[(long)(r + 8) * cols + c];
+            a3 += part[(long)(r + 12) * cols + c];
+        }
+        for (; r < nrows; r += 4) a0 += part[(long)r * cols + c];
+    }
+    __shared__ float red[4][64];
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && c < cols) {
+        const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        out[c] = accumulate ? out[c] + t : t;
+    }
 }
 }  // namespace
 
 PDNN_API int pdnn_colsum_splits(long rows) {
-    const long s = (rows + 63) / 64;
-    return (int)(s < 1 ? 1 : (s > 64 ? 64 : s));
+    const long s = rows / 64;                    // >= 64 rows (16 per wave) per split, at most 128 splits
+    return (int)(s < 1 ? 1 : (s > 128 ? 128 : s));
 }
 
 PDNN_API int pdnn_act_fwd(const bf16_t* x, bf16_t* y, long n, int op, hipStream_t st) {
@@ -173,7 +200,7 @@ PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int a
     if (work && cols % 8 == 0 && rows > 256) {
         const int sp = pdnn_colsum_splits(rows);
         hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 511) / 512, sp), dim3(NT), 0, st, x, rows, cols, work);
-        hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, work, sp, cols, out,
+        hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, work, sp, cols, out,
                            accumulate);
     } else {
         hipLaunchKernelGGL(colsum_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, x, rows, cols, out, accumulate);

@@ -6,7 +6,8 @@
 // block -> per-row loss = lse - x[label] and the row's log-sum-exp saved for backward.
 // Backward: one more pass writing dlogits = (softmax - onehot) * scale, scale = grad_out / rows read from
 // a DEVICE pointer (no host sync; graph-capturable).  Rows with label == ignore_index get zero grad.
-// Works for 10-class heads and the 50257-way GPT-2 vocabulary alike (16-byte vector loads for bf16).
+// Works for 10-class heads and the 50257-way GPT-2 vocabulary alike; bf16 rows whose length and stride
+// are multiples of 8 take 16-byte vector loads/stores (the 50304-padded GPT-2 head: HBM-speed passes).
 #include "common.h"
 
 namespace {
@@ -18,7 +19,7 @@ __device__ __forceinline__ void online(float& m, float& s, float v) {
     else s += __expf(v - m);
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ void __launch_bounds__(NT) xent_fwd_kernel(const T* __restrict__ logits, long ld, int V,
                                                       const int64_t* __restrict__ labels, int ignore,
                                                       float* __restrict__ loss, float* __restrict__ lse,
@@ -26,7 +27,36 @@ __global__ void __launch_bounds__(NT) xent_fwd_kernel(const T* __restrict__ logi
     const long row = blockIdx.x;
     const T* x = logits + row * ld;
     float m = -INFINITY, s = 0.f;
-    for (int i = threadIdx.x; i < V; i += NT) online<T>(m, s, Ld<T>::get(x, i));
+    if (VEC) {
+        // 16-byte loads (8 bf16 per lane), one rescale per chunk: the row is read at HBM speed
+        const u16x8_t* x8 = reinterpret_cast<const u16x8_t*>(x);
+        const int n8 = V / 8;
+        for (int i = threadIdx.x; i < n8; i += 2 * NT) {       // two 16-byte loads in flight per lane
+            const bool two = i + NT < n8;
+            const u16x8_t a = x8[i];
+            const u16x8_t b = two ? x8[i + NT] : a;
+            float v[16];
+            unpack8(a, v);
+            unpack8(b, v + 8);
+            float cm = v[0];
+#pragma unroll
+            for (int j = 1; j < 16; ++j) cm = fmaxf(cm, v[j]);
+            if (cm > m) {
+                s = (m == -INFINITY) ? 0.f : s * __expf(m - cm);
+                m = cm;
+            }
+            float t = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t += __expf(v[j] - m);
+            if (two) {
+#pragma unroll
+                for (int j = 8; j < 16; ++j) t += __expf(v[j] - m);
+            }
+            s += t;
+        }
+    } else {
+        for (int i = threadIdx.x; i < V; i += NT) online<T>(m, s, Ld<T>::get(x, i));
+    }
     // merge (m, s) across the block
     __shared__ float sm[NT / 64], ss[NT / 64];
 #pragma unroll
@@ -58,7 +88,7 @@ __global__ void __launch_bounds__(NT) xent_fwd_kernel(const T* __restrict__ logi
     }
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ void __launch_bounds__(NT) xent_bwd_kernel(const T* __restrict__ logits, long ld, int V,
                                                       const int64_t* __restrict__ labels, int ignore,
                                                       const float* __restrict__ lse,
@@ -71,6 +101,27 @@ __global__ void __launch_bounds__(NT) xent_bwd_kernel(const T* __restrict__ logi
     const bool ign = (y == ignore || y < 0 || y >= V);
     const float sc = ign ? 0.f : (*gscale) / denom;
     const float l = lse[row];
+    if (VEC) {
+        const u16x8_t* x8 = reinterpret_cast<const u16x8_t*>(x);
+        u16x8_t* d8 = reinterpret_cast<u16x8_t*>(d);
+        const int n8 = V / 8;
+        for (int i = threadIdx.x; i < n8; i += 2 * NT) {       // two 16-byte loads in flight per lane
+            const bool two = i + NT < n8;
+            const u16x8_t a = x8[i];
+            const u16x8_t b = two ? x8[i + NT] : a;
+            float v[8], u[8];
+            unpack8(a, v);
+            unpack8(b, u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[j] = sc * (__expf(v[j] - l) - (8 * i + j == y ? 1.f : 0.f));
+                u[j] = sc * (__expf(u[j] - l) - (8 * (i + NT) + j == y ? 1.f : 0.f));
+            }
+            d8[i] = pack8(v);
+            if (two) d8[i + NT] = pack8(u);
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < V; i += NT) {
         const float p = __expf(Ld<T>::get(x, i) - l);
         Ld<T>::put(d, i, sc * (p - (i == y ? 1.f : 0.f)));
@@ -81,11 +132,15 @@ __global__ void __launch_bounds__(NT) xent_bwd_kernel(const T* __restrict__ logi
 // dtype: 0 = fp32 logits, 1 = bf16 logits
 PDNN_API int pdnn_xent_fwd(const void* logits, long ld, int rows, int V, const int64_t* labels, int ignore,
                            float* loss, float* lse, float* loss_sum, float* count, int dtype, hipStream_t st) {
-    if (dtype == 1)
-        hipLaunchKernelGGL(xent_fwd_kernel<bf16_t>, dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld, V,
-                           labels, ignore, loss, lse, loss_sum, count);
+    const bool vec = dtype == 1 && V % 8 == 0 && ld % 8 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL((xent_fwd_kernel<bf16_t, true>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
+                           V, labels, ignore, loss, lse, loss_sum, count);
+    else if (dtype == 1)
+        hipLaunchKernelGGL((xent_fwd_kernel<bf16_t, false>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
+                           V, labels, ignore, loss, lse, loss_sum, count);
     else
-        hipLaunchKernelGGL(xent_fwd_kernel<float>, dim3(rows), dim3(NT), 0, st, (const float*)logits, ld, V,
+        hipLaunchKernelGGL((xent_fwd_kernel<float, false>), dim3(rows), dim3(NT), 0, st, (const float*)logits, ld, V,
                            labels, ignore, loss, lse, loss_sum, count);
     PDNN_LAUNCH_RET;
 }
@@ -93,11 +148,16 @@ PDNN_API int pdnn_xent_fwd(const void* logits, long ld, int rows, int V, const i
 PDNN_API int pdnn_xent_bwd(const void* logits, long ld, int rows, int V, const int64_t* labels, int ignore,
                            const float* lse, const float* gscale, float denom, void* dlogits, long ldd, int dtype,
                            hipStream_t st) {
-    if (dtype == 1)
-        hipLaunchKernelGGL(xent_bwd_kernel<bf16_t>, dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld, V,
-                           labels, ignore, lse, gscale, denom, (bf16_t*)dlogits, ldd);
+    const bool vec = dtype == 1 && V % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL((xent_bwd_kernel<bf16_t, true>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
+                           V, labels, ignore, lse, gscale, denom, (bf16_t*)dlogits, ldd);
+    else if (dtype == 1)
+        hipLaunchKernelGGL((xent_bwd_kernel<bf16_t, false>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
+                           V, labels, ignore, lse, gscale, denom, (bf16_t*)dlogits, ldd);
     else
-        hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), dim3(NT), 0, st, (const float*)logits, ld, V,
-                           labels, ignore, lse, gscale, denom, (float*)dlogits, ldd);
+        hipLaunchKernelGGL((xent_bwd_kernel<float, false>), dim3(rows), dim3(NT), 0, st, (const float*)logits, ld,
+                           V, labels, ignore, lse, gscale, denom, (float*)dlogits, ldd);
     PDNN_LAUNCH_RET;
 }

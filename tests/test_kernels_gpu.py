@@ -186,7 +186,7 @@ def test_avgpool(K):
     assert rel(dx, (g.float() / 49)[:, None, None, :].expand(4, 7, 7, 2048)) < 1e-2
 
 
-@pytest.mark.parametrize("V", [10, 1000, 50257])
+@pytest.mark.parametrize("V", [10, 1000, 50257, 50304, 8])
 def test_xent(K, V):
     R = 64
     lg = rnd(R, V, scale=3.0)
@@ -297,7 +297,8 @@ def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
     assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("R,C", [(100, 10), (8192, 768), (8192, 3072), (3000, 2304), (513, 40)])
+@pytest.mark.parametrize("R,C", [(100, 10), (8192, 768), (8192, 3072), (3000, 2304), (513, 40), (260, 1032), (100000, 64),
+                                 (8191, 2312)])
 def test_colsum(K, R, C):
     x = rnd(R, C)
     out = K.colsum(x)
