@@ -51,7 +51,14 @@ def add_fit_args(p: argparse.ArgumentParser):
     p.add_argument("--inject-straggler", type=str, default="")
     p.add_argument("--straggler-mode", action="store_true")
     p.add_argument("--checkpoint-dir", type=str, default=None)
-    p.add_argument("--resume", type=str, default=None)
+    p.add_argument("--resume", type=str, default=None, help="checkpoint path, or 'auto' (newest in --checkpoint-dir)")
+    p.add_argument("--checkpoint-interval", type=int, default=0, help="rank 0 saves every N steps (0: per epoch)")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="seconds without a completed step before the rank aborts the communicator and exits "
+                        "(code 75) for a torchrun --max-restarts restart; 0 = off")
+    p.add_argument("--inject-hang", type=str, default="",
+                   help="RANK:STEP - that rank stops making progress before step STEP on the FIRST attempt only "
+                        "(fault injection for the watchdog + restart path; TORCHELASTIC_RESTART_COUNT == 0)")
     p.add_argument("--trace", type=str, default=None)
     p.add_argument("--graph", type=str, default="off", choices=["off", "on", "collectives"],
                    help="replay each training step as one captured hipGraph (utils/graphs.py); 'on' applies to "
@@ -168,9 +175,20 @@ def main(argv=None):
 
     loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world)
 
+    hang_at = None
+    if args.inject_hang and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0":
+        hr, hs = (int(v) for v in args.inject_hang.split(":"))
+        hang_at = hs if hr == rank else None
+
     class _DevLoader:
         def __iter__(self):
+            n = 0
             while True:
+                n += 1
+                if hang_at is not None and n >= hang_at:      # a wedged rank: peers block in the all-reduce
+                    import time as _t
+                    while True:
+                        _t.sleep(60)
                 yield to_dev(loader.next_batch())
 
         def __len__(self):
@@ -179,11 +197,17 @@ def main(argv=None):
     graph = {"off": False, "on": world == 1, "collectives": "collectives"}[args.graph]
     if strag:                      # per-step host sleeps in grad hooks cannot be replayed from a graph
         graph = False
+    wd = None
+    if args.watchdog_timeout > 0:
+        from .parallel.watchdog import CommWatchdog
+        wd = CommWatchdog(args.watchdog_timeout, out_dir=args.out_dir, rank=rank).start()
     tr = Trainer(net, opt, OF.cross_entropy, dev, rank, world, args.log_interval, args.metrics,
                  args.trace, args.checkpoint_dir, arch=args.network, printer=print if rank == 0 else (lambda *a: None),
-                 graph=graph)
+                 graph=graph, checkpoint_interval=args.checkpoint_interval, watchdog=wd)
     if args.resume:
-        tr.resume(args.resume)
+        ck = tr.resume(args.resume)
+        if ck is not None and rank == 0:
+            print(f"resumed from step {tr.step_no} (epoch {tr.epoch})")
     hist = tr.train(_DevLoader(), epochs=args.epochs, max_steps=args.max_steps, batch_size=args.batch_size,
                     dataset_size=len(train_ds))
     test_loader = DataLoader(test_ds, min(args.test_batch_size, len(test_ds)), "cpu")
@@ -195,6 +219,8 @@ def main(argv=None):
 
     if rank == 0:
         tr.evaluate(_TestLoader(), 1)
+    if wd is not None:
+        wd.stop()
     runtime.destroy()
     return hist
 

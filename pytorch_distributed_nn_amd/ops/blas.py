@@ -29,6 +29,7 @@ import os
 import torch
 
 from . import kernels as K
+from .functional import weight_bf16
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -61,7 +62,9 @@ def linear_fwd(x, wk, bias=None, act=0, aux=None, res=None):
     N = wk.shape[0]
     if not _blas(M, N, Kd, "fwd"):
         return K.gemm_nt_ex(x, wk, bias=bias, act=act, aux=aux, res=res)
-    b = bias.to(BF16) if bias is not None else None
+    # bf16 bias for the library epilogue: the flat arena's bf16 shadow of the parameter (refreshed by the
+    # fused optimizer) instead of a per-call fp32 -> bf16 conversion kernel
+    b = weight_bf16(bias) if bias is not None else None
     if act:
         u = aux if aux is not None else torch.empty(M, N, device=x.device, dtype=BF16)
         if b is not None:

@@ -71,6 +71,13 @@ def init_process_group(backend: str | None = None, device: str | None = None, ti
                   timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart not in (None, "", "0"):
+            # a restarted worker group (parallel/watchdog.py) may share the launcher's store with the failed
+            # attempt: namespace this attempt's keys so no rank reads a dead peer's address
+            store, _, _ = next(dist.rendezvous("env://", env.rank, env.world_size,
+                                               timeout=datetime.timedelta(seconds=timeout_s)))
+            kw["store"] = dist.PrefixStore(f"pdnn_attempt{restart}", store)
         dist.init_process_group(**kw)
     _ENV = env
     return env

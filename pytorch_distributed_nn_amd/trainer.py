@@ -23,7 +23,8 @@ from .utils.observability import MetricsSink, Tracer, accuracy, load_checkpoint,
 class Trainer:
     def __init__(self, model, optimizer, loss_fn=None, device=None, rank=0, world=1, log_interval=10,
                  metrics_path=None, trace_path=None, checkpoint_dir=None, arch="", timing=True, printer=print,
-                 lr_schedule=None, grad_clip=None, graph=False, graph_warmup=2):
+                 lr_schedule=None, grad_clip=None, graph=False, graph_warmup=2, checkpoint_interval=0,
+                 watchdog=None):
         self.model = model
         self.opt = optimizer
         self.loss_fn = loss_fn or OF.cross_entropy
@@ -41,6 +42,8 @@ class Trainer:
         self.step_no = 0
         self.epoch = 0
         self.history = []
+        self.checkpoint_interval = checkpoint_interval     # steps between rank-0 checkpoints (0: epoch ends)
+        self.watchdog = watchdog                           # parallel.watchdog.CommWatchdog, fed every step
         # hipGraph-captured step (utils/graphs.py): one replay per iteration instead of ~1000 launches
         self.graph_step = None
         if graph and self.device.type == "cuda":
@@ -96,7 +99,7 @@ class Trainer:
         n_per_epoch = steps_per_epoch or (len(loader) if hasattr(loader, "__len__") else 100)
         it = iter(loader)
         done = False
-        for ep in range(epochs):
+        for ep in range(self.epoch, epochs):          # a resumed run continues from its checkpoint's epoch
             self.epoch = ep
             for i in range(n_per_epoch):
                 tf = time.perf_counter()
@@ -122,6 +125,11 @@ class Trainer:
                                f"Samples/s: {rec['samples_per_s']:.1f}, Prec@1: {p1:.2f}")
                 self.metrics.log(**rec)
                 self.history.append(rec)
+                if self.watchdog is not None:
+                    self.watchdog.beat(self.step_no)
+                if (self.checkpoint_dir and self.checkpoint_interval and self.rank == 0
+                        and self.step_no % self.checkpoint_interval == 0):
+                    self.save(f"{self.checkpoint_dir}/checkpoint_step{self.step_no}.pt")
                 if max_steps and self.step_no >= max_steps:
                     done = True
                     break
@@ -159,6 +167,13 @@ class Trainer:
                                best_prec1=best_prec1)
 
     def resume(self, path):
+        """Restore model / optimizer / step / RNG from ``path`` (``"auto"``: the newest checkpoint in
+        ``checkpoint_dir``, no-op when there is none — the restart-after-hang path of parallel/watchdog.py)."""
+        if path == "auto":
+            from .parallel.watchdog import latest_checkpoint
+            path = latest_checkpoint(self.checkpoint_dir)
+            if path is None:
+                return None
         ck = load_checkpoint(path, self.model, self.opt, map_location=self.device)
         self.epoch, self.step_no = ck.get("epoch", 0), ck.get("step", 0)
         return ck
