@@ -135,18 +135,25 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
     const int nkb = causal ? (qb * 128 + 128) / 64 : T / 64;
-    TileLd tk, tv;
-    tk.load(Kp, ld, tid);
-    tv.load(Vp, ld, tid);
-    tk.store(smem[0][0], tid);
-    tv.store(smem[0][1], tid);
+    // K/V tiles: prefetch distance 2 (two register stages + two LDS buffers).  The per-tile compute of a
+    // d=64 head is short, so with distance 1 every iteration waited out most of a global-load round trip
+    // (causal and full attention took the same time: latency-, not throughput-bound).
+    TileLd ka, va, kn, vn;
+    ka.load(Kp, ld, tid);
+    va.load(Vp, ld, tid);
+    ka.store(smem[0][0], tid);
+    va.store(smem[0][1], tid);
+    if (nkb > 1) {
+        kn.load(Kp + 64L * ld, ld, tid);
+        vn.load(Vp + 64L * ld, ld, tid);
+    }
     __syncthreads();
-    for (int kb = 0; kb < nkb; ++kb) {
+    // tile kb is in LDS buffer kb & 1; (hk, hv) hold tile kb + 1 in flight; (fk, fv) are free for kb + 2
+    auto step = [&](const int kb, TileLd& hk, TileLd& hv, TileLd& fk, TileLd& fv) {
         const int cur = kb & 1;
-        const bool more = kb + 1 < nkb;
-        if (more) {
-            tk.load(Kp + (long)(kb + 1) * 64 * ld, ld, tid);
-            tv.load(Vp + (long)(kb + 1) * 64 * ld, ld, tid);
+        if (kb + 2 < nkb) {
+            fk.load(Kp + (long)(kb + 2) * 64 * ld, ld, tid);
+            fv.load(Vp + (long)(kb + 2) * 64 * ld, ld, tid);
         }
         const int k0 = kb * 64;
         if (!causal || k0 <= q0 + 31) {              // wave-uniform: tile not entirely above the diagonal
@@ -163,36 +170,47 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
                     s[kf][f] = mfma(a1, qf[f][1], z);
                 }
             }
+            // VALU budget per tile is what bounds a d=64 head (32 MFMAs vs ~32 softmax elements per lane):
+            // the causal mask runs only on diagonal tiles (wave-uniform branch), the softmax scale is folded
+            // into the exponent's FMA, exp2 is the raw v_exp_f32 (arguments <= 0; underflow to 0 is
+            // exactly what softmax wants), and O is rescaled only when some row maximum moved.
             const bool diag = causal && k0 + 63 > q0;
+            if (diag) {
+#pragma unroll
+                for (int f = 0; f < 2; ++f) {
+                    const int qi = q0 + 16 * f + (lane & 15);
+#pragma unroll
+                    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (k0 + 16 * kf + 4 * g + r > qi) s[kf][f][r] = -INFINITY;
+                }
+            }
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
-                const int qi = q0 + 16 * f + (lane & 15);
                 float mx = -INFINITY;
 #pragma unroll
                 for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = s[kf][f][r] * c;
-                        if (diag && k0 + 16 * kf + 4 * g + r > qi) v = -INFINITY;
-                        s[kf][f][r] = v;
-                        mx = fmaxf(mx, v);
-                    }
-                mx = xmax16(mx);
-                const float mn = fmaxf(m[f], mx);
-                const float alpha = exp2f(m[f] - mn);
+                    for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kf][f][r]);
+                const float mn = fmaxf(m[f], xmax16(mx) * c);      // scaled-score domain (c > 0)
+                const bool moved = __any(mn != m[f]);
+                const float alpha = moved ? __builtin_amdgcn_exp2f(m[f] - mn) : 1.f;
                 float rs = 0.f;
 #pragma unroll
                 for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float p = exp2f(s[kf][f][r] - mn);
+                        const float p = __builtin_amdgcn_exp2f(fmaf(s[kf][f][r], c, -mn));
                         s[kf][f][r] = p;
                         rs += p;
                     }
                 l[f] = l[f] * alpha + xsum16(rs);
                 m[f] = mn;
+                if (moved) {
 #pragma unroll
-                for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
+                    for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
+                }
             }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -201,17 +219,21 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
                 for (int f = 0; f < 2; ++f) pb[f] = pack_acc(s[2 * kk][f], s[2 * kk + 1][f]);
 #pragma unroll
                 for (int df = 0; df < 4; ++df) {
-                    const bf16x8_t va = frag_tr_perm(Vi, 16 * df, kk, lane);
+                    const bf16x8_t vfr = frag_tr_perm(Vi, 16 * df, kk, lane);
 #pragma unroll
-                    for (int f = 0; f < 2; ++f) o[df][f] = mfma(va, pb[f], o[df][f]);
+                    for (int f = 0; f < 2; ++f) o[df][f] = mfma(vfr, pb[f], o[df][f]);
                 }
             }
         }
-        if (more) {
-            tk.store(smem[cur ^ 1][0], tid);
-            tv.store(smem[cur ^ 1][1], tid);
+        if (kb + 1 < nkb) {
+            hk.store(smem[cur ^ 1][0], tid);
+            hv.store(smem[cur ^ 1][1], tid);
         }
         __syncthreads();
+    };
+    for (int kb = 0; kb < nkb; kb += 2) {            // unrolled by 2: register stages are compile-time
+        step(kb, kn, vn, ka, va);
+        if (kb + 1 < nkb) step(kb + 1, ka, va, kn, vn);
     }
     // lane holds O^T[d = 16 df + 4 g + r][q = q0 + 16 f + (lane & 15)]
 #pragma unroll
@@ -315,6 +337,7 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
                 y = mfma(frag_rows(Oi, 16 * qi, 0, lane), vf[0], y);
                 dp[qi] = mfma(frag_rows(Oi, 16 * qi, 1, lane), vf[1], y);
             }
+            const bool diag = causal && qs < k0 + 16;    // wave-uniform: only these tiles need the mask
 #pragma unroll
             for (int qi = 0; qi < 4; ++qi) {
                 const int qr = qs + 16 * qi + 4 * g;
@@ -322,12 +345,14 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
                 const float4 dl = *reinterpret_cast<const float4*>(Dl + qr);
                 const float la[4] = {lv.x, lv.y, lv.z, lv.w}, da[4] = {dl.x, dl.y, dl.z, dl.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float p = exp2f(s[qi][r] * c - la[r]);
-                    if (causal && kl > qr + r) p = 0.f;
-                    s[qi][r] = p;
-                    dp[qi][r] = p * (dp[qi][r] - da[r]);
+                for (int r = 0; r < 4; ++r) s[qi][r] = __builtin_amdgcn_exp2f(fmaf(s[qi][r], c, -la[r]));
+                if (diag) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kl > qr + r) s[qi][r] = 0.f;
                 }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dp[qi][r] = s[qi][r] * (dp[qi][r] - da[r]);
             }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -422,14 +447,19 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
                 y = mfma(frag_rows(Vi, 16 * ki, 0, lane), of[0], y);
                 dp[ki] = mfma(frag_rows(Vi, 16 * ki, 1, lane), of[1], y);
             }
+            const bool diag = causal && k0 + 63 > q0;     // wave-uniform: only these tiles need the mask
 #pragma unroll
-            for (int ki = 0; ki < 4; ++ki)
+            for (int ki = 0; ki < 4; ++ki) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float p = exp2f(s[ki][r] * c - lq);
-                    if (causal && k0 + 16 * ki + 4 * g + r > ql) p = 0.f;
-                    dp[ki][r] = p * (dp[ki][r] - dq_);
+                for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(fmaf(s[ki][r], c, -lq));
+                if (diag) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (k0 + 16 * ki + 4 * g + r > ql) s[ki][r] = 0.f;
                 }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dp[ki][r] = s[ki][r] * (dp[ki][r] - dq_);
+            }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
                 const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);

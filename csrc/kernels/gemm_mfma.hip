@@ -1079,7 +1079,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
     DgradClass cl[16];
     bool any_empty;
     const int ncl = dgrad_classes(H, W, R, S, st, pad, cl, &any_empty);
-    if (any_empty) {   // pixels no tap reaches: zero (or the residual)
+    if (any_empty && !(res == dx && !bn_x)) {   // pixels no tap reaches: zero (or the residual, unless in place)
         const long n = (long)Nimg * H * W * C;         // C % 8 == 0: 16-B aligned rows
         hipLaunchKernelGGL(copy_or_zero_kernel, dim3(stream_grid(n / 8 + 1, 256)), dim3(256), 0, stream, dx,
                            (res && !bn_x) ? res : nullptr, n);

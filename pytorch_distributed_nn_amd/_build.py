@@ -37,6 +37,12 @@ HIP_FLAGS = [
     "-Wno-unused-but-set-variable", "-Werror=return-type",
     f"-I{ROOT / 'csrc' / 'include'}", f"-I{ROOT / 'csrc' / 'kernels'}",
 ]
+# Per-file extra flags.  MFMA accumulators in plain VGPRs (no AGPR copies): the attention kernels mix
+# every MFMA result with VALU work (softmax, masking, bf16 packing), and in AGPR form the compiler spent
+# ~400 v_accvgpr_read/write per two key tiles; VGPR form cut the forward's vector instruction count by 30%
+# and raised occupancy (fwd 2 -> 3 waves/SIMD, dq 3 -> 4).
+VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+KERNEL_FILE_FLAGS = {"attention.hip": VGPR_FORM}
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
              "-pthread", f"-I{ROOT / 'csrc' / 'include'}", f"-I{ROOT / 'csrc' / 'runtime'}"]
 
@@ -55,7 +61,7 @@ def _run(cmd):
     return r.stdout
 
 
-def _build_lib(srcs, compiler, flags, out: Path, objdir: Path, deps, link_extra=(), jobs=None):
+def _build_lib(srcs, compiler, flags, out: Path, objdir: Path, deps, link_extra=(), jobs=None, file_flags=None):
     objdir.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     objs, todo = [], []
@@ -66,7 +72,8 @@ def _build_lib(srcs, compiler, flags, out: Path, objdir: Path, deps, link_extra=
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_run, [compiler, *flags, "-c", str(s), "-o", str(o)]) for s, o in todo]
+        ff = file_flags or {}
+        futs = [ex.submit(_run, [compiler, *flags, *ff.get(s.name, []), "-c", str(s), "-o", str(o)]) for s, o in todo]
         for f in futs:
             f.result()
     if todo or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
@@ -80,7 +87,8 @@ def build_kernels(verbose=False) -> Path:
     kdir = ROOT / "csrc" / "kernels"
     srcs = sorted(kdir.glob("*.hip"))
     deps = list(kdir.glob("*.h")) + list((ROOT / "csrc" / "include").glob("*.h"))
-    return _build_lib(srcs, HIPCC, HIP_FLAGS, LIBDIR / "libpdnn_kernels.so", BUILD / "kernels", deps)
+    return _build_lib(srcs, HIPCC, HIP_FLAGS, LIBDIR / "libpdnn_kernels.so", BUILD / "kernels", deps,
+                      file_flags=KERNEL_FILE_FLAGS)
 
 
 def build_runtime(verbose=False, sanitize: str | None = None) -> Path:

@@ -202,8 +202,10 @@ class BottleneckFn(torch.autograd.Function):
         if down:
             dtd = dtd.view(td.shape)
             dwd = sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
-            dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
-            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=dxd)          # residual add fused
+            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0)
+            # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
+            # reach, so no zero-filled full-size buffer and no extra full read/write pass
+            dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
             grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3, dwd, rgd, rbd)
         else:
             dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape))
@@ -269,8 +271,8 @@ class BasicBlockFn(torch.autograd.Function):
         if down:
             dtd = dtd.view(td.shape)
             dwd = sink.wgrad(P[6], x, dtd, 1, 1, stride, 0)
-            dxd = K.conv_dgrad(dtd, kd, x.shape, stride, 0)
-            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=dxd)
+            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1)
+            dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)      # shortcut, in place
             grads = (dw1, rg1, rb1, dw2, rg2, rb2, dwd, rgd, rbd)
         else:
             dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape))

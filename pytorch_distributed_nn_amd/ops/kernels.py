@@ -111,8 +111,9 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     return y, stats
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None):
-    """dx = conv_transpose(dy, w) (+ res).
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None):
+    """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
+    conv only the pixels its taps reach are touched, the others keep ``res``).
 
     bn = (t, mean, invstd, mscale, mshift): fuse the BatchNorm backward of the layer that produced t:
     returns (gm, slab) where gm = dx * [t*mscale + mshift > 0] and slab holds the partial sums of gm and
@@ -124,7 +125,10 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None):
     _chk(C2 == C, "conv_dgrad: weight [K][R][S][C]")
     _, Ho, Wo, K2 = dy.shape
     _chk(K2 == K and C % 8 == 0 and K % 8 == 0, "conv_dgrad: channel mismatch")
-    dx = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    if out is not None:
+        _chk(tuple(out.shape) == (N, H, W, C) and out.dtype == BF16 and out.is_contiguous(), "conv_dgrad: out")
+        _chk(bn is None, "conv_dgrad: out with a fused BN backward")
+    dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
     slab = None
     t = mean = inv = msc = msh = None
     if bn is not None:

@@ -119,6 +119,12 @@ def test_conv_dgrad(K, shape):
     y.backward(dy.float().permute(0, 3, 1, 2))
     dx = K.conv_dgrad(dy, w, (N, H, W, C), st, pad)
     assert rel(dx, x.grad.permute(0, 2, 3, 1)) < 1.5e-2
+    # in-place accumulation (shortcut branch of a residual block): out aliases res; a strided conv only
+    # touches the pixels its taps reach, every other pixel must keep res
+    base = rnd(N, H, W, C)
+    acc = base.clone()
+    K.conv_dgrad(dy, w, (N, H, W, C), st, pad, res=acc, out=acc)
+    assert rel(acc, base.float() + x.grad.permute(0, 2, 3, 1)) < 1.5e-2
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
