@@ -92,7 +92,8 @@ _SIGS = {
 
 
 def lib_path() -> Path:
-    return _LIBDIR / "libpdnn_kernels.so"
+    alt = os.environ.get("PDNN_KERNEL_LIB")        # experiments: an alternative build of the same kernels
+    return Path(alt) if alt else _LIBDIR / "libpdnn_kernels.so"
 
 
 def _load():
