@@ -121,14 +121,16 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
 
 // y = act(x*scale + shift + residual'), residual' = res (identity) or res*rscale + rshift.
 // Each thread owns one fixed group of 8 channels (coefficients in registers) and strides over rows.
-template <bool RES, bool RSC, bool RELU>
+// MASK: also write the sign bits of y (bit j of byte [row][c/8] = y[row][c + j] > 0, 1/16 of y's bytes), so
+// the backward's ReLU mask (mask mode 3) does not re-read the whole bf16 output.
+template <bool RES, bool RSC, bool RELU, bool MASK>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ x, long L, int C,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
                                                       const bf16_t* __restrict__ res,
                                                       const float* __restrict__ rscale,
                                                       const float* __restrict__ rshift,
-                                                      bf16_t* __restrict__ y) {
+                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ mbits) {
     const int CG = C >> 3, RPI = NT / CG;
     const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
     if (rr >= RPI) return;
@@ -167,12 +169,19 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
             }
+            if constexpr (MASK) {
+                unsigned bits = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bits |= (v[j] > 0.f ? 1u : 0u) << j;
+                mbits[rws[u] * CG + cg] = (uint8_t)bits;
+            }
             *reinterpret_cast<u16x8_t*>(y + rws[u] * C + c) = pack8(v);
         }
     }
 }
 
-// mask modes for the backward: 0 none, 1 mask = (msrc > 0), 2 mask = (x*mscale + mshift > 0)
+// mask modes for the backward: 0 none, 1 mask = (msrc > 0), 2 mask = (x*mscale + mshift > 0),
+// 3 mask = bit j of byte msrc[row][c/8] (written by bn_apply's MASK variant)
 __device__ __forceinline__ void masked_grad(const bf16_t* g, const bf16_t* x, const bf16_t* msrc,
                                             const float* mscale, const float* mshift, int mode, long off,
                                             int c, float* gm, float* xv) {
@@ -211,6 +220,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
         for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
             const long rs[2] = {r0, r0 + step};
             u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
+            unsigned mb[2] = {0u, 0u};
 #pragma unroll
             for (int u = 0; u < 2; ++u) {      // both rows' loads in flight together
                 if (rs[u] < L) {
@@ -218,6 +228,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
                     gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
                     xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
                     if (mode == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
+                    if (mode == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[rs[u] * CG + cg];
                     if (x2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
                 }
             }
@@ -235,6 +246,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
                 } else if (mode == 2) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], mscale[c + j], mshift[c + j]) > 0.f ? gm[j] : 0.f;
+                } else if (mode == 3) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gm[j] = ((mb[u] >> j) & 1u) ? gm[j] : 0.f;
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { s[j] += gm[j]; q[j] += gm[j] * (xv[j] - mu[j]) * is[j]; }
@@ -325,6 +339,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
         const long rs[2] = {r0, r0 + step};
         u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
+        unsigned mb[2] = {0u, 0u};
 #pragma unroll
         for (int u = 0; u < 2; ++u) {          // issue every load of both rows first
             if (rs[u] < L) {
@@ -332,6 +347,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
                 gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
                 xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
                 if constexpr (MODE == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
+                if constexpr (MODE == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[rs[u] * CG + cg];
                 if constexpr (X2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
             }
         }
@@ -350,6 +366,9 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
             } else if constexpr (MODE == 2) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+            } else if constexpr (MODE == 3) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gm[j] = ((mb[u] >> j) & 1u) ? gm[j] : 0.f;
             }
             if constexpr (DX) {
 #pragma unroll
@@ -408,15 +427,21 @@ PDNN_API int pdnn_bn_stats(const bf16_t* x, long L, int C, float* slab, hipStrea
     PDNN_LAUNCH_RET;
 }
 
+// mbits (optional, [L][C/8] bytes): sign bits of y for a mask-mode-3 backward
 PDNN_API int pdnn_bn_apply(const bf16_t* x, long L, int C, const float* scale, const float* shift,
                            const bf16_t* res, const float* rscale, const float* rshift, int relu, bf16_t* y,
-                           hipStream_t st) {
+                           uint8_t* mbits, hipStream_t st) {
     const dim3 grid(stream_grid(L * (C / 8), NT));
-#define PDNN_BA(RES, RSC, RELU) \
-    hipLaunchKernelGGL((bn_apply_kernel<RES, RSC, RELU>), grid, dim3(NT), 0, st, x, L, C, scale, shift, res, rscale, rshift, y)
-    if (res && rscale) { if (relu) PDNN_BA(true, true, true); else PDNN_BA(true, true, false); }
-    else if (res) { if (relu) PDNN_BA(true, false, true); else PDNN_BA(true, false, false); }
-    else { if (relu) PDNN_BA(false, false, true); else PDNN_BA(false, false, false); }
+#define PDNN_BA(RES, RSC, RELU, MASK)                                                                  \
+    hipLaunchKernelGGL((bn_apply_kernel<RES, RSC, RELU, MASK>), grid, dim3(NT), 0, st, x, L, C, scale, shift, res, \
+                       rscale, rshift, y, mbits)
+    if (mbits && relu) {
+        if (res && rscale) PDNN_BA(true, true, true, true);
+        else if (res) PDNN_BA(true, false, true, true);
+        else PDNN_BA(false, false, true, true);
+    } else if (res && rscale) { if (relu) PDNN_BA(true, true, true, false); else PDNN_BA(true, true, false, false); }
+    else if (res) { if (relu) PDNN_BA(true, false, true, false); else PDNN_BA(true, false, false, false); }
+    else { if (relu) PDNN_BA(false, false, true, false); else PDNN_BA(false, false, false, false); }
 #undef PDNN_BA
     PDNN_LAUNCH_RET;
 }
@@ -462,6 +487,10 @@ PDNN_API int pdnn_bn_bwd_apply(const bf16_t* g, const bf16_t* x, long L, int C, 
         if (hx2) { if (hgm) PDNN_BWA(1, true, true, true); else PDNN_BWA(1, true, true, false); }
         else if (hgm) { if (hdx) PDNN_BWA(1, false, true, true); else PDNN_BWA(1, false, false, true); }
         else PDNN_BWA(1, false, true, false);
+    } else if (mode == 3) {
+        if (hx2) { if (hgm) PDNN_BWA(3, true, true, true); else PDNN_BWA(3, true, true, false); }
+        else if (hgm) { if (hdx) PDNN_BWA(3, false, true, true); else PDNN_BWA(3, false, false, true); }
+        else PDNN_BWA(3, false, true, false);
     } else if (mode == 2) {
         if (hgm) PDNN_BWA(2, false, true, true); else PDNN_BWA(2, false, true, false);
     } else {

@@ -44,7 +44,7 @@ _SIGS = {
     "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P, P],
     "pdnn_bn_eval_coeff": [I, F, P, P, P, P, P, P, P],
     "pdnn_bn_stats": [P, L, I, P, P],
-    "pdnn_bn_apply": [P, L, I, P, P, P, P, P, I, P, P],
+    "pdnn_bn_apply": [P, L, I, P, P, P, P, P, I, P, P, P],
     "pdnn_bn_bwd_reduce": [P, P, L, I, P, P, I, P, P, P, P, P, P, P, P, P],
     "pdnn_bn_bwd_finalize": [P, I, I, P, P, I, P, P, P, P],
     "pdnn_bn_bwd_apply": [P, P, L, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],

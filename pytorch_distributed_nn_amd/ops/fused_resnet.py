@@ -156,12 +156,14 @@ class BottleneckFn(torch.autograd.Function):
         if down:
             wd, gd, bd = params[9:]
             td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (gd, bd), bufs[6:8], mom, eps)
-            out = K.bn_apply(t3.view(-1, C3), s3, h3, res=td.view(-1, C3), rscale=sd, rshift=hd, relu=True)
+            out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=td.view(-1, C3), rscale=sd, rshift=hd, relu=True,
+                                 want_mask=training)
         else:
             td = md = idd = None
-            out = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True)
+            out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True, want_mask=training)
         out = out.view(t3.shape)
-        ctx.save_for_backward(x, t1, a1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+        # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
+        ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None)
         ctx.conf = (stride, training, down)
         ctx.params = params
@@ -169,29 +171,29 @@ class BottleneckFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        (x, t1, a1, t2, t3, td, out, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
+        (x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
          g1, g2, g3, gd, k1, k2, k3, kd) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused Bottleneck backward requires training-mode BatchNorm")
         gout = gout.contiguous()
         C3 = t3.shape[-1]
-        g2d, t3_2d, out2d = gout.view(-1, C3), t3.view(-1, C3), out.view(-1, C3)
+        g2d, t3_2d = gout.view(-1, C3), t3.view(-1, C3)
         # block output BN3 (+BNd) with the ReLU mask of `out`
         P = ctx.params
         ctx.params = None
         sink = _Sink()
-        slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=1, msrc=out2d,
+        slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
                                              x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
         (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
         if down:
             (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
-            dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d,
+            dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
                                          x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                          dbeta2=dbd)
             gres = None
         else:
-            dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=1, msrc=out2d, want_gm=True)
+            dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
         dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
@@ -231,12 +233,13 @@ class BasicBlockFn(torch.autograd.Function):
         if down:
             wd, gd, bd = params[6:]
             td, md, idd, sd, hd = _conv_bn(x, shadows[2], stride, 0, None, training, (gd, bd), bufs[4:6], mom, eps)
-            out = K.bn_apply(t2.view(-1, C2), s2, h2, res=td.view(-1, C2), rscale=sd, rshift=hd, relu=True)
+            out, mb = K.bn_apply(t2.view(-1, C2), s2, h2, res=td.view(-1, C2), rscale=sd, rshift=hd, relu=True,
+                                 want_mask=training)
         else:
             td = md = idd = None
-            out = K.bn_apply(t2.view(-1, C2), s2, h2, res=x.view(-1, C2), relu=True)
+            out, mb = K.bn_apply(t2.view(-1, C2), s2, h2, res=x.view(-1, C2), relu=True, want_mask=training)
         out = out.view(t2.shape)
-        ctx.save_for_backward(x, t1, a1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
+        ctx.save_for_backward(x, t1, a1, t2, td, mb, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
                               params[7] if down else None, k1, k2, shadows[2] if down else None)
         ctx.conf = (stride, training, down)
         ctx.params = params
@@ -244,26 +247,26 @@ class BasicBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        (x, t1, a1, t2, td, out, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
+        (x, t1, a1, t2, td, mb, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused BasicBlock backward requires training-mode BatchNorm")
         gout = gout.contiguous()
         C2 = t2.shape[-1]
-        g2d, t2_2d, out2d = gout.view(-1, C2), t2.view(-1, C2), out.view(-1, C2)
+        g2d, t2_2d = gout.view(-1, C2), t2.view(-1, C2)
         P = ctx.params
         ctx.params = None
         sink = _Sink()
-        slab2, slabd, rows = K.bn_bwd_reduce(g2d, t2_2d, m2, i2, mode=1, msrc=out2d,
+        slab2, slabd, rows = K.bn_bwd_reduce(g2d, t2_2d, m2, i2, mode=3, msrc=mb,
                                              x2=td.view(-1, C2) if down else None, mean2=md, invstd2=idd)
         (dg2, db2), (rg2, rb2) = sink.bn(slab2, rows, P[4], P[5])
         if down:
             (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[7], P[8])
-            dt2, dtd, _ = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, x2=td.view(-1, C2),
+            dt2, dtd, _ = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=3, msrc=mb, x2=td.view(-1, C2),
                                          mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd, dbeta2=dbd)
             gres = None
         else:
-            dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=1, msrc=out2d, want_gm=True)
+            dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=3, msrc=mb, want_gm=True)
         dt2 = dt2.view(t2.shape)
         dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, 1, 1)
         dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
@@ -292,27 +295,28 @@ class StemFn(torch.autograd.Function):
         kpad = shadows[0]
         t, m, i, s, h = _conv_bn(x, kpad, stride, pad, None, training, (gamma, beta), bufs, mom, eps)
         C = t.shape[-1]
-        a = K.bn_apply(t.view(-1, C), s, h, relu=True).view(t.shape)
+        a, mb = K.bn_apply(t.view(-1, C), s, h, relu=True, want_mask=training)
+        a = a.view(t.shape)
         if pool:
             y, idx = K.maxpool_fwd(a, 3, 2, 1)
         else:
             y, idx = a, None
-        ctx.save_for_backward(x, t, a, idx, m, i, gamma)
+        ctx.save_for_backward(x, t, mb, idx, m, i, gamma)      # ReLU mask bits, not the activation
         ctx.conf = (stride, pad, pool, w.shape, kpad.shape)
         ctx.params = (w, gamma, beta)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, t, a, idx, m, i, gamma = ctx.saved_tensors
+        x, t, mb, idx, m, i, gamma = ctx.saved_tensors
         stride, pad, pool, wshape, kshape = ctx.conf
         gy = gy.contiguous()
-        ga = K.maxpool_bwd(gy, idx, a.shape, 3, 2, 1) if pool else gy
+        ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy
         C = t.shape[-1]
         P = ctx.params
         ctx.params = None
         sink = _Sink()
-        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 1, msrc=a.view(-1, C), sink=sink,
+        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
                               bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
         if kshape[3] == wshape[1]:

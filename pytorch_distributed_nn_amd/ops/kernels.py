@@ -191,13 +191,20 @@ def bn_stats(x2d):
     return slab, rows
 
 
-def bn_apply(x2d, scale, shift, res=None, rscale=None, rshift=None, relu=True, out=None):
+def bn_apply(x2d, scale, shift, res=None, rscale=None, rshift=None, relu=True, out=None, want_mask=None):
+    """y = act(x*scale + shift (+ res | res*rscale + rshift)).  With ``want_mask`` given the result is a
+    pair (y, bits): bits = the sign bits of y, uint8 [L][C/8], when want_mask is true (ReLU only; the
+    backward's mask mode 3 reads them instead of y), else None."""
     L, C = x2d.shape
     if out is None:
         out = torch.empty_like(x2d)
+    mbits = None
+    if want_mask:
+        _chk(relu and C % 8 == 0, "bn_apply: mask bits need ReLU and C % 8 == 0")
+        mbits = torch.empty(L, C // 8, device=x2d.device, dtype=torch.uint8)
     call("pdnn_bn_apply", ptr(x2d), L, C, ptr(scale), ptr(shift), ptr(res), ptr(rscale), ptr(rshift), int(relu),
-         ptr(out), stream())
-    return out
+         ptr(out), ptr(mbits), stream())
+    return out if want_mask is None else (out, mbits)
 
 
 def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=None, x2=None, mean2=None,

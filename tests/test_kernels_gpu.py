@@ -169,6 +169,15 @@ def test_bn_train_fwd_bwd(K):
     dx, _, _ = K.bn_bwd_apply(gy, x, mean, inv, gamma, dg, db, mode=1, msrc=y)
     assert rel(dg, g_.grad) < 2e-2 and rel(db, b_.grad) < 2e-2
     assert rel(dx, xr.grad) < 3e-2
+    # mask mode 3: the ReLU mask as sign bits written by bn_apply, bit-exact with mode 1 on y
+    y3, bits = K.bn_apply(x, sc, sh, relu=True, want_mask=True)
+    assert torch.equal(y3, y) and bits.shape == (L, C // 8) and bits.dtype == torch.uint8
+    ref_bits = ((y.view(L, C // 8, 8) > 0).to(torch.int32) << torch.arange(8, device="cuda")).sum(-1)
+    assert torch.equal(bits.to(torch.int32), ref_bits)
+    slab3, _, rows3 = K.bn_bwd_reduce(gy, x, mean, inv, mode=3, msrc=bits)
+    assert torch.equal(slab3, slab)
+    dx3, _, _ = K.bn_bwd_apply(gy, x, mean, inv, gamma, dg, db, mode=3, msrc=bits)
+    assert torch.equal(dx3, dx)
 
 
 def test_maxpool(K):
