@@ -18,6 +18,25 @@
 namespace {
 constexpr int NT = 256;
 
+// Rows per thread per iteration of the streaming kernels: all U rows' loads are issued before any is
+// consumed.  Measured on the ResNet-50 bs256 step (tools/gpu_runs/gpu_run44.sh, gpu_run45.sh), img/s:
+// U=2 everywhere 7530-7556, U=4 7508, U=8 7400 (VGPR pressure costs more occupancy than the extra loads
+// in flight buy); reduce U=1/2/4 and 16 vs 64 rows per thread-row all within noise; apply U=1 7553.
+// The templated reduce kernel itself (mode / second-BN specialisations) was the +2% (7385 -> 7530+).
+// A/B builds override them with -DPDNN_BN_UR=n (backward reduce) / -DPDNN_BN_UA=n (apply kernels).
+#ifndef PDNN_BN_UR
+#define PDNN_BN_UR 2
+#endif
+#ifndef PDNN_BN_UA
+#define PDNN_BN_UA 1
+#endif
+// Minimum rows per thread-row of a statistics reduction (more blocks for the narrow, short late layers:
+// ResNet-50 layer4 has only 12544 rows of 2048 channels at bs256).
+#ifndef PDNN_BN_RMIN
+#define PDNN_BN_RMIN 64
+#endif
+constexpr int BN_UR = PDNN_BN_UR, BN_UA = PDNN_BN_UA, BN_RMIN = PDNN_BN_RMIN;
+
 // Level-1 reduction of a partial-statistics slab [rows][2][C] -> [RB][2][C]: block (cx, ry) sums the
 // rows ry, ry+RB, ... for 64 channels with 4 row lanes (coalesced 256-byte row segments).
 __global__ void __launch_bounds__(NT) slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
@@ -142,17 +161,19 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
         if constexpr (RSC) rs_[j] = rscale[c + j];
     }
     const long step = (long)gridDim.x * RPI;
-    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
-        const long rws[2] = {r0, r0 + step};
-        u16x8_t xv[2], rv[2];
+    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += BN_UA * step) {
+        long rws[BN_UA];
+        u16x8_t xv[BN_UA], rv[RES ? BN_UA : 1];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < BN_UA; ++u) {
+            rws[u] = r0 + u * step;
             if (rws[u] < L) {
                 xv[u] = *reinterpret_cast<const u16x8_t*>(x + rws[u] * C + c);
                 if constexpr (RES) rv[u] = *reinterpret_cast<const u16x8_t*>(res + rws[u] * C + c);
             }
+        }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < BN_UA; ++u) {
             if (rws[u] >= L) break;
             float v[8];
             unpack8(xv[u], v);
@@ -182,77 +203,64 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
 
 // mask modes for the backward: 0 none, 1 mask = (msrc > 0), 2 mask = (x*mscale + mshift > 0),
 // 3 mask = bit j of byte msrc[row][c/8] (written by bn_apply's MASK variant)
-__device__ __forceinline__ void masked_grad(const bf16_t* g, const bf16_t* x, const bf16_t* msrc,
-                                            const float* mscale, const float* mshift, int mode, long off,
-                                            int c, float* gm, float* xv) {
-    unpack8(*reinterpret_cast<const u16x8_t*>(g + off), gm);
-    unpack8(*reinterpret_cast<const u16x8_t*>(x + off), xv);
-    if (mode == 1) {
-        float m[8];
-        unpack8(*reinterpret_cast<const u16x8_t*>(msrc + off), m);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
-    } else if (mode == 2) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], mscale[c + j], mshift[c + j]) > 0.f ? gm[j] : 0.f;
-    }
-}
-
 // partial sums of gm and gm*xhat (xhat = (x-mean)*invstd) for one or two BNs sharing gm.
+// Specialised on the mask mode and the second BN so unused operands take no registers.
+template <int MODE, bool X2>
 __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int mode,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
     const bf16_t* __restrict__ msrc, const float* __restrict__ mscale, const float* __restrict__ mshift,
     float* __restrict__ slab, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
     const float* __restrict__ invstd2, float* __restrict__ slab2) {
     __shared__ float red[2][NT * 8];
     const int CG = C >> 3, RPI = NT / CG;
     const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
-    float s[8] = {0}, q[8] = {0}, s2[8] = {0}, q2[8] = {0};
-    float mu[8], is[8], mu2[8], is2[8];
+    float s[8] = {0}, q[8] = {0}, q2[X2 ? 8 : 1] = {0};
+    float mu[8], is[8], mu2[X2 ? 8 : 1], is2[X2 ? 8 : 1], ms[MODE == 2 ? 8 : 1], mh[MODE == 2 ? 8 : 1];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         mu[j] = mean[c + j]; is[j] = invstd[c + j];
-        mu2[j] = x2 ? mean2[c + j] : 0.f; is2[j] = x2 ? invstd2[c + j] : 0.f;
+        if constexpr (X2) { mu2[j] = mean2[c + j]; is2[j] = invstd2[c + j]; }
+        if constexpr (MODE == 2) { ms[j] = mscale[c + j]; mh[j] = mshift[c + j]; }
     }
     if (rr < RPI) {
         const long step = (long)gridDim.x * RPI;
-        for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
-            const long rs[2] = {r0, r0 + step};
-            u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
-            unsigned mb[2] = {0u, 0u};
+        for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += BN_UR * step) {
+            u16x8_t gv[BN_UR], xv8[BN_UR], mv[MODE == 1 ? BN_UR : 1], x2v8[X2 ? BN_UR : 1];
+            unsigned mb[MODE == 3 ? BN_UR : 1];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {      // both rows' loads in flight together
-                if (rs[u] < L) {
-                    const long off = rs[u] * C + c;
+            for (int u = 0; u < BN_UR; ++u) {      // every row's loads in flight together
+                const long r = r0 + u * step;
+                if (r < L) {
+                    const long off = r * C + c;
                     gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
                     xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
-                    if (mode == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
-                    if (mode == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[rs[u] * CG + cg];
-                    if (x2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
+                    if constexpr (MODE == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
+                    if constexpr (MODE == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[r * CG + cg];
+                    if constexpr (X2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (rs[u] >= L) break;
+            for (int u = 0; u < BN_UR; ++u) {
+                if (r0 + u * step >= L) break;
                 float gm[8], xv[8];
                 unpack8(gv[u], gm);
                 unpack8(xv8[u], xv);
-                if (mode == 1) {
+                if constexpr (MODE == 1) {
                     float m[8];
                     unpack8(mv[u], m);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
-                } else if (mode == 2) {
+                } else if constexpr (MODE == 2) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], mscale[c + j], mshift[c + j]) > 0.f ? gm[j] : 0.f;
-                } else if (mode == 3) {
+                    for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+                } else if constexpr (MODE == 3) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) gm[j] = ((mb[u] >> j) & 1u) ? gm[j] : 0.f;
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { s[j] += gm[j]; q[j] += gm[j] * (xv[j] - mu[j]) * is[j]; }
-                if (x2) {
+                if constexpr (X2) {
                     float x2v[8];
                     unpack8(x2v8[u], x2v);
 #pragma unroll
@@ -261,12 +269,13 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
             }
         }
     }
-    for (int pass = 0; pass < (x2 ? 2 : 1); ++pass) {
+    for (int pass = 0; pass < (X2 ? 2 : 1); ++pass) {
         float* out = pass ? slab2 : slab;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             red[0][t * 8 + j] = s[j];
-            red[1][t * 8 + j] = pass ? q2[j] : q[j];
+            if constexpr (X2) red[1][t * 8 + j] = pass ? q2[j] : q[j];
+            else red[1][t * 8 + j] = q[j];
         }
         __syncthreads();
         for (int cc = t; cc < C; cc += NT) {
@@ -307,7 +316,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __rest
 // dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
 // registers; optionally also a second BN's dx2 (shared gm) and/or gm itself.
 // Specialised on the mask mode / second BN / outputs so unused coefficient arrays take no registers
-// (occupancy), and two rows per thread per iteration so twice the loads are in flight.
+// (occupancy), and BN_UA rows per thread per iteration so U times the loads are in flight.
 template <int MODE, bool X2, bool DX, bool GMO>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
@@ -336,25 +345,26 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
         if constexpr (MODE == 2) { ms[j] = mscale[c + j]; mh[j] = mshift[c + j]; }
     }
     const long step = (long)gridDim.x * RPI;
-    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += 2 * step) {
-        const long rs[2] = {r0, r0 + step};
-        u16x8_t gv[2], xv8[2], mv[2], x2v8[2];
-        unsigned mb[2] = {0u, 0u};
+    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += BN_UA * step) {
+        u16x8_t gv[BN_UA], xv8[BN_UA], mv[MODE == 1 ? BN_UA : 1], x2v8[X2 ? BN_UA : 1];
+        unsigned mb[MODE == 3 ? BN_UA : 1];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {          // issue every load of both rows first
-            if (rs[u] < L) {
-                const long off = rs[u] * C + c;
+        for (int u = 0; u < BN_UA; ++u) {       // issue every load of all U rows first
+            const long r = r0 + u * step;
+            if (r < L) {
+                const long off = r * C + c;
                 gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
                 xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
                 if constexpr (MODE == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
-                if constexpr (MODE == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[rs[u] * CG + cg];
+                if constexpr (MODE == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[r * CG + cg];
                 if constexpr (X2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
             }
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (rs[u] >= L) break;
-            const long off = rs[u] * C + c;
+        for (int u = 0; u < BN_UA; ++u) {
+            const long r = r0 + u * step;
+            if (r >= L) break;
+            const long off = r * C + c;
             float gm[8], xv[8], o[8];
             unpack8(gv[u], gm);
             unpack8(xv8[u], xv);
@@ -389,7 +399,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
 
 inline unsigned reduce_grid(long L, int C) {
     const int rpi = NT / (C / 8);
-    long g = (L + rpi * 64 - 1) / (rpi * 64);   // >= 64 rows per thread-row
+    long g = (L + rpi * BN_RMIN - 1) / (rpi * BN_RMIN);   // >= BN_RMIN rows per thread-row
     if (g > 1024) g = 1024;
     if (g < 1) g = 1;
     return (unsigned)g;
@@ -450,8 +460,17 @@ PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C,
                                 const float* invstd, int mode, const bf16_t* msrc, const float* mscale,
                                 const float* mshift, float* slab, const bf16_t* x2, const float* mean2,
                                 const float* invstd2, float* slab2, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(reduce_grid(L, C)), dim3(NT), 0, st, g, x, L, C, mean,
-                       invstd, mode, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2);
+#define PDNN_BWR(MODE, X2)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<MODE, X2>), dim3(reduce_grid(L, C)), dim3(NT), 0, st, g, x, L, C, \
+                       mean, invstd, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2)
+    const bool hx2 = x2 != nullptr;
+    switch (mode) {
+        case 1: if (hx2) PDNN_BWR(1, true); else PDNN_BWR(1, false); break;
+        case 2: if (hx2) PDNN_BWR(2, true); else PDNN_BWR(2, false); break;
+        case 3: if (hx2) PDNN_BWR(3, true); else PDNN_BWR(3, false); break;
+        default: if (hx2) PDNN_BWR(0, true); else PDNN_BWR(0, false); break;
+    }
+#undef PDNN_BWR
     PDNN_LAUNCH_RET;
 }
 
