@@ -41,6 +41,7 @@ _SIGS = {
     "pdnn_set_glds_mode": [I],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
+    "pdnn_bn_fin_work": [I, I],
     "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P, P],
     "pdnn_bn_eval_coeff": [I, F, P, P, P, P, P, P, P],
     "pdnn_bn_stats": [P, L, I, P, P],

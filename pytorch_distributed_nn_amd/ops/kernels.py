@@ -161,13 +161,18 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
 
 
 # ----------------------------------------------------------------------------------- BatchNorm
+def _fin_work(rows, C, device):
+    n = lib().pdnn_bn_fin_work(rows, C)
+    return torch.empty(n, device=device, dtype=F32) if n > 0 else None
+
+
 def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
     C = slab.shape[1]
     mean = torch.empty(C, device=slab.device, dtype=F32)
     invstd = torch.empty_like(mean)
     scale = torch.empty_like(mean)
     shift = torch.empty_like(mean)
-    work = torch.empty(2 * 64 * C, device=slab.device, dtype=F32) if rows > 64 else None
+    work = _fin_work(rows, C, slab.device)
     call("pdnn_bn_finalize", ptr(slab), rows, C, float(L), float(eps), float(momentum), ptr(gamma), ptr(beta),
          ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(work), stream())
     return mean, invstd, scale, shift
@@ -224,7 +229,7 @@ def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=N
     if dgamma is None:
         dgamma = torch.empty(C, device=slab.device, dtype=F32)
         dbeta = torch.empty_like(dgamma)
-    work = torch.empty(2 * 64 * C, device=slab.device, dtype=F32) if rows > 64 else None
+    work = _fin_work(rows, C, slab.device)
     ga, ba = acc if acc is not None else (None, None)
     call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), ptr(ga),
          ptr(ba), stream())

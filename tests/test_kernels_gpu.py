@@ -146,6 +146,33 @@ def test_conv_wgrad(K, shape, pro):
     assert rel(dw, w.grad.permute(0, 2, 3, 1)) < 5e-3
 
 
+@pytest.mark.parametrize("rows,C", [(1, 64), (7, 8), (64, 200), (65, 64), (1000, 2048), (12544, 64), (3137, 1024)])
+def test_bn_slab_finalize(K, rows, C):
+    """Wide-grid slab finalize (level-1 pass + per-column fp64 epilogue) against fp64 torch sums;
+    three calls in a row (no state carried between calls)."""
+    L = float(rows * 64)
+    for it in range(3):
+        slab = torch.rand(rows, 2, C, device="cuda") * 64
+        slab[:, 1] += slab[:, 0] ** 2 / 64 + 1.0            # sum of squares consistent with a positive var
+        slab = slab.reshape(rows * 2, C)
+        gamma, beta = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        mean, inv, sc, sh = K.bn_finalize(slab, rows, L, 1e-5, 0.1, gamma, beta, rm, rv)
+        sd = slab.view(rows, 2, C).double().sum(0)
+        m_ref = sd[0] / L
+        v_ref = (sd[1] / L - m_ref ** 2).clamp_min(0)
+        assert torch.allclose(mean.double(), m_ref, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(inv.double(), torch.rsqrt(v_ref + 1e-5), rtol=1e-4)
+        assert torch.allclose(sc.double(), gamma.double() * torch.rsqrt(v_ref + 1e-5), rtol=1e-4)
+        assert torch.allclose(rm.double(), 0.1 * m_ref, rtol=1e-5, atol=1e-6)
+        dg, db = torch.full((C,), 1.0, device="cuda"), torch.full((C,), 2.0, device="cuda")
+        acc = (torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda"))
+        K.bn_bwd_finalize(slab, rows, dg, db, accumulate=True, acc=acc)
+        assert torch.allclose(db.double(), sd[0] + 2.0, rtol=1e-5)
+        assert torch.allclose(dg.double(), sd[1] + 1.0, rtol=1e-5)
+        assert torch.allclose(acc[0].double(), sd[1], rtol=1e-5) and torch.allclose(acc[1].double(), sd[0], rtol=1e-5)
+
+
 def test_bn_train_fwd_bwd(K):
     L, C = 4096, 256
     x = rnd(L, C, scale=2.0) + 0.5

@@ -1,0 +1,7 @@
+#!/bin/bash
+# kernel trace of the one-launch BN finalize build
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/run48
+mkdir -p $O
+export TMPDIR=/tmp
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o ours --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 3 > $O/prof.log 2>&1
