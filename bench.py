@@ -69,7 +69,8 @@ def main():
             model.config.fp8 = True
         else:
             model.enable_fp8()
-    if world > 1:
+    use_ddp = world > 1 or os.environ.get("PDNN_DDP_FORCE_COMM") == "1"     # 1-GPU rehearsal of the DDP path
+    if use_ddp:
         net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
     else:
         flatten_module(model)

@@ -31,6 +31,7 @@ What it does, and how it differs from the reference's design:
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 
 import torch
@@ -63,6 +64,9 @@ class DistributedDataParallel(nn.Module):
         self.straggler_mode = straggler_mode
         self.tracer = tracer
         self.nccl = _is_nccl(process_group)
+        # communicate even at world size 1 (PDNN_DDP_FORCE_COMM=1 with a 1-rank process group): exercises the
+        # bucket hooks and RCCL launches on a single GPU exactly as at world size 8
+        self._comm = self.world > 1 or (dist.is_initialized() and os.environ.get("PDNN_DDP_FORCE_COMM") == "1")
         self._sync = True
         self.alive = True
         self.grad_scale_dev = None
@@ -76,7 +80,7 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ init broadcast (C-13)
     @torch.no_grad()
     def _broadcast_init(self):
-        if self.world == 1:
+        if not self._comm:
             return
         dist.broadcast(self.flat.data, 0, group=self.pg)
         self._broadcast_buffers()
@@ -84,7 +88,7 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _broadcast_buffers(self):
-        if self.world == 1 or not self._buffers_list:
+        if not self._comm or not self._buffers_list:
             return
         by_dtype = {}
         for b in self._buffers_list:
@@ -136,7 +140,7 @@ class DistributedDataParallel(nn.Module):
         self._armed = False
 
     def _on_grad(self, p):
-        if not self._sync or self.world == 1:
+        if not self._sync or not self._comm:
             return
         if not self._armed:
             self._armed = True
@@ -204,7 +208,7 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ public API
     def forward(self, *args, **kwargs):
-        if self.broadcast_buffers and self.world > 1 and self.module.training:
+        if self.broadcast_buffers and self._comm and self.module.training:
             self._broadcast_buffers()
         return self.module(*args, **kwargs)
 

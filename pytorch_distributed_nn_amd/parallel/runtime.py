@@ -61,7 +61,10 @@ def init_process_group(backend: str | None = None, device: str | None = None, ti
     use_gpu = (device != "cpu") and torch.cuda.is_available()
     if use_gpu:
         torch.cuda.set_device(env.local_rank % max(1, torch.cuda.device_count()))
-    if env.world_size > 1 and not dist.is_initialized():
+    # PDNN_FORCE_PG=1: build the (RCCL) process group even for one rank, so a 1-GPU box can rehearse the
+    # multi-GPU code path (DDP hooks + RCCL kernels on their stream) that the 8-GPU node runs
+    force = os.environ.get("PDNN_FORCE_PG") == "1"
+    if (env.world_size > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", env.master_addr)
         os.environ.setdefault("MASTER_PORT", str(env.master_port))
         # dmabuf IPC is the only mode the box's driver supports (see task environment notes)

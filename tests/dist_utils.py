@@ -37,14 +37,14 @@ def _from_np(obj):
     return obj
 
 
-def _entry(rank, world, port, fn, args, q, device="cpu"):
+def _entry(rank, world, port, fn, args, q, device="cpu", backend="gloo", env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), **(env or {}))
     try:
         import torch
         torch.set_num_threads(1)
         from pytorch_distributed_nn_amd.parallel import runtime
-        runtime.init_process_group(backend="gloo", device=device)
+        runtime.init_process_group(backend=backend, device=device)
         res = fn(rank, world, *args)
         q.put((rank, "ok", _to_np(res)))
     except Exception:
@@ -57,13 +57,14 @@ def _entry(rank, world, port, fn, args, q, device="cpu"):
             pass
 
 
-def run_world(fn, world=2, args=(), timeout=180, device="cpu"):
+def run_world(fn, world=2, args=(), timeout=180, device="cpu", backend="gloo", env=None):
     """device="cpu": CPU tensors over gloo; device=None: every rank uses the (single) GPU, still over gloo
-    (RCCL needs one GPU per rank; gloo moves GPU tensors through the host)."""
+    (RCCL needs one GPU per rank; gloo moves GPU tensors through the host).  backend="nccl" with world=1
+    and env={"PDNN_FORCE_PG": "1", ...} runs the RCCL path on a one-GPU box."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device, backend, env)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
