@@ -63,15 +63,22 @@ __global__ void __launch_bounds__(NT) add_kernel(const bf16_t* __restrict__ a, c
         reinterpret_cast<u16x8_t*>(y)[i] = pack8(av);
     }
 }
-// NCHW (fp32 or bf16) -> NHWC bf16 with the channel dim zero-padded to Cp (stem input, K-17)
+// NCHW (fp32 or bf16) -> NHWC bf16 with the channel dim zero-padded to Cp (stem input, K-17).
+// One thread per pixel; reads are coalesced along the pixel index, each group of 8 output channels is
+// one 16-byte store (Cp % 8 == 0, checked on the host), index math in 32 bits per image.
 template <typename T>
 __global__ void __launch_bounds__(NT) nchw_to_nhwc_kernel(const T* __restrict__ x, bf16_t* __restrict__ y, int N,
                                                           int C, int HW, int Cp) {
     const long total = (long)N * HW;
     for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-        const long n = i / HW, p = i - n * HW;
-        for (int c = 0; c < Cp; ++c)
-            y[i * Cp + c] = c < C ? f2bf(Ld<T>::get(x, (n * C + c) * HW + p)) : (bf16_t)0;
+        const int n = (int)(i / HW), p = (int)(i - (long)n * HW);
+        const T* xs = x + (long)n * C * HW + p;
+        for (int c0 = 0; c0 < Cp; c0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = c0 + j < C ? Ld<T>::get(xs, (long)(c0 + j) * HW) : 0.f;
+            *reinterpret_cast<u16x8_t*>(y + i * Cp + c0) = pack8(v);
+        }
     }
 }
 // NHWC bf16 (channels Cp) -> NCHW fp32 gradient of the first C channels
@@ -181,6 +188,7 @@ PDNN_API int pdnn_add(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, float
     PDNN_LAUNCH_RET;
 }
 PDNN_API int pdnn_nchw_to_nhwc(const void* x, int x_bf16, bf16_t* y, int N, int C, int HW, int Cp, hipStream_t st) {
+    if (Cp % 8 != 0 || C > Cp) return 1;                 // hipErrorInvalidValue: 16-byte channel groups
     if (x_bf16)
         hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(stream_grid((long)N * HW, NT)), dim3(NT), 0, st,
                            (const bf16_t*)x, y, N, C, HW, Cp);

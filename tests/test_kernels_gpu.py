@@ -207,15 +207,16 @@ def test_bn_train_fwd_bwd(K):
     assert torch.equal(dx3, dx)
 
 
-def test_maxpool(K):
+@pytest.mark.parametrize("k,st,pad", [(3, 2, 1), (2, 2, 0), (3, 1, 1), (5, 2, 2)])
+def test_maxpool(K, k, st, pad):
     x = torch.randn(2, 17, 17, 64, device="cuda").to(BF).requires_grad_(False)
-    y, idx = K.maxpool_fwd(x, 3, 2, 1)
+    y, idx = K.maxpool_fwd(x, k, st, pad)
     xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
-    ref = F.max_pool2d(xr, 3, 2, 1)
+    ref = F.max_pool2d(xr, k, st, pad)
     assert rel(y, ref.permute(0, 2, 3, 1)) < 1e-6
     g = rnd(*y.shape)
     ref.backward(g.float().permute(0, 3, 1, 2))
-    dx = K.maxpool_bwd(g, idx, x.shape, 3, 2, 1)
+    dx = K.maxpool_bwd(g, idx, x.shape, k, st, pad)
     assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
@@ -363,3 +364,13 @@ def test_gemm_large_tile_engine(K, M, N, Kd):
     dw = torch.zeros(N, Kd, device="cuda")
     K.gemm_tn_acc(g, x, dw)
     assert rel(dw, g.float().t() @ x.float()) < 2e-3
+
+
+@pytest.mark.parametrize("C,dt", [(3, torch.float32), (1, BF), (10, torch.float32), (16, BF)])
+def test_nchw_to_nhwc_pad(K, C, dt):
+    x = torch.randn(3, C, 13, 11, device="cuda").to(dt)
+    cp = (C + 7) // 8 * 8
+    y = K.nchw_to_nhwc(x, cp)
+    ref = torch.zeros(3, 13, 11, cp, device="cuda", dtype=BF)
+    ref[..., :C] = x.permute(0, 2, 3, 1).to(BF)
+    assert torch.equal(y, ref)
