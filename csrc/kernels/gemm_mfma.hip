@@ -765,11 +765,17 @@ bool glds_enabled() { return glds_mode() != 0; }
 // implicit-GEMM forward once the reduction is long (K >= 512: 3x3 convs, wide 1x1s) and on the data
 // gradient unless both C and K are small; the low-K 1x1 convs are memory bound and prefer the 128-row
 // kernel's finer grid, and the weight gradient's split-K atomics are faster there too.
+// PDNN_GLDS_MIN_TILES: the grid-size threshold (A/B experiments; default 192)
+int g_glds_min_tiles = -1;
+int glds_min_tiles() {
+    if (g_glds_min_tiles < 0) { const char* e = getenv("PDNN_GLDS_MIN_TILES"); g_glds_min_tiles = e ? atoi(e) : 192; }
+    return g_glds_min_tiles;
+}
 template <int AM>
 bool glds_worth(const GemmArgs& a, int batch, int splits) {
     if (glds_mode() == 2) return true;
     const long tiles = cdiv(a.M, GBM) * cdiv(a.N, glds_bn(a.N)) * (long)batch * splits;
-    if (tiles < 192) return false;
+    if (tiles < glds_min_tiles()) return false;
     if constexpr (AM == A_CONV) return a.K >= 512;
     if constexpr (AM == A_CONVT) return a.N >= 128 || a.K >= 512;
     return true;
