@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
-    ap.add_argument("--graph", default="off", choices=["off", "on", "auto", "collectives"],
+    ap.add_argument("--graph", default="auto", choices=["off", "on", "auto", "collectives"],
                     help="replay each step as one captured hipGraph (auto: single-GPU runs only)")
     a = ap.parse_args()
 
