@@ -771,13 +771,29 @@ int glds_min_tiles() {
     if (g_glds_min_tiles < 0) { const char* e = getenv("PDNN_GLDS_MIN_TILES"); g_glds_min_tiles = e ? atoi(e) : 192; }
     return g_glds_min_tiles;
 }
+// Per-operand-mode shape thresholds (A/B knobs): PDNN_GLDS_FWD_K (forward reduction length) and
+// PDNN_GLDS_DGRAD_N / PDNN_GLDS_DGRAD_K (data gradient: input channels / reduction length).
+// Whole-step A/B on ResNet-50 bs256 (tools/gpu_runs/gpu_run62.sh, gpu_run63.sh): the per-layer wins of the
+// glds data gradient do not survive inside the step (its BN-backward epilogue tiles at 256 rows run
+// 2.3% slower in aggregate than the 128-tile kernel), so dgrad stays on the register-staged kernel by
+// default (7,790 -> 7,970 img/s); forward K >= 1024 is within noise of 512 and of "never".
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+int g_glds_fwd_k = -1, g_glds_dgrad_n = -1, g_glds_dgrad_k = -1;
 template <int AM>
 bool glds_worth(const GemmArgs& a, int batch, int splits) {
     if (glds_mode() == 2) return true;
     const long tiles = cdiv(a.M, GBM) * cdiv(a.N, glds_bn(a.N)) * (long)batch * splits;
     if (tiles < glds_min_tiles()) return false;
-    if constexpr (AM == A_CONV) return a.K >= 512;
-    if constexpr (AM == A_CONVT) return a.N >= 128 || a.K >= 512;
+    if (g_glds_fwd_k < 0) {
+        g_glds_fwd_k = env_int("PDNN_GLDS_FWD_K", 1024);
+        g_glds_dgrad_n = env_int("PDNN_GLDS_DGRAD_N", 1 << 30);
+        g_glds_dgrad_k = env_int("PDNN_GLDS_DGRAD_K", 1 << 30);
+    }
+    if constexpr (AM == A_CONV) return a.K >= g_glds_fwd_k;
+    if constexpr (AM == A_CONVT) return a.N >= g_glds_dgrad_n || a.K >= g_glds_dgrad_k;
     return true;
 }
 
