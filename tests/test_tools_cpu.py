@@ -53,3 +53,22 @@ def test_cli_yaml_config_defaults(tmp_path):
         parse_args(["--config", os.path.join(ROOT, "configs", f)])      # every shipped config parses
     a = parse_args(["--config", os.path.join(ROOT, "configs", "ps_mlp_backup_workers.yaml"), "--lr", "0.5"])
     assert a.network == "mlp_cpp" and a.n_to_collect == 2 and a.evaluator and a.lr == 0.5
+
+
+def test_pmc_summary_flops_and_bytes(tmp_path):
+    """tools/pmc_summary.py: 512 FLOPs per MFMA MOP, doubled FETCH_SIZE, per-dispatch timestamps."""
+    hdr = "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n"
+    with open(tmp_path / "q1_counters.csv", "w") as f:
+        f.write(hdr)
+        for c, v in (("SQ_INSTS_VALU_MFMA_MOPS_BF16", 1e6), ("SQ_LDS_BANK_CONFLICT", 1), ("SQ_LDS_IDX_ACTIVE", 4)):
+            f.write(f"1,gemm,{c},{v},0,1000000\n")
+    with open(tmp_path / "q2_counters.csv", "w") as f:
+        f.write(hdr + "1,gemm,FETCH_SIZE,1000,0,1000000\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(tmp_path), "--steps", "1"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    row = [ln for ln in r.stdout.splitlines() if ln.endswith("gemm")][0].split()
+    # 5.12e8 FLOP in 1 ms = 0.512 TFLOP/s; conflicts 1/4; read 2 x 1000 KiB in 1 ms = 2 GB/s
+    assert float(row[2]) == pytest.approx(0.5, abs=0.05)
+    assert float(row[4]) == pytest.approx(0.25)
+    assert float(row[5]) == pytest.approx(2, abs=1)
