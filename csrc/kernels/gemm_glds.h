@@ -33,18 +33,6 @@ constexpr int glds_smem() {
     return ops > cst ? ops : cst;
 }
 
-typedef __attribute__((address_space(3))) void lds_void;
-
-// compile-time loop: the epilogue body is too large for `#pragma unroll` to be honoured, and a rolled
-// fragment loop indexes the accumulator array dynamically, which moves it to scratch memory
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
 __device__ __forceinline__ void glds16(const void* src, bf16_t* dst) {
     __builtin_amdgcn_global_load_lds(src, (lds_void*)dst, 16, 0, 0);
 }

@@ -35,121 +35,10 @@
 //    squares of the bf16-rounded outputs, one slab row per 64-row wave tile), or fp32 atomic
 //    accumulation for split-K weight gradients.
 //  * XCD-aware bijective block remap (T1) so neighbouring tiles share an XCD's L2.
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
-
-constexpr int BK = 64;
-constexpr int NT = 256;
-
-enum AMode { A_KMAJOR = 0, A_MNMAJOR = 1, A_CONV = 2, A_CONVT = 3, A_IM2COL = 4 };
-enum BMode { B_KMAJOR = 0, B_MNMAJOR = 1, B_WT = 2, B_IM2COL = 3 };
-enum EMode { E_BF16 = 0, E_F32 = 1, E_ATOMIC = 2 };
-
-// Granlund-Montgomery unsigned division by a runtime-invariant divisor (valid for n < 2^31).
-struct FastDiv {
-    uint32_t d, m, s;
-};
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-    return (__umulhi(n, f.m) + n) >> f.s;
-}
-
-struct ConvGeom {
-    int Nimg, H, W, C;      // activation tensor of the gather (NHWC)
-    int Ho, Wo, R, S;       // the "other" spatial extent and filter size
-    int st, pad;
-    int Ko;                 // output channels (for A_CONVT / B_WT reduction index)
-    // transposed-conv parity class (dgrad with stride > 1 is split into st*st dense sub-problems):
-    // output pixels h = hc*st + ph, taps r = r0 + st*ir (ir < Rc); identical to a plain conv when st == 1
-    int ph, pw, r0, s0, Sc;
-    FastDiv dHW, dW, dC, dS, dKo, dSc;  // divisors used by the gathers
-};
-
-struct GemmArgs {
-    int M, N, K;
-    const bf16_t* A; long lda;
-    const bf16_t* B; long ldb;
-    ConvGeom g;
-    const float* pro_scale;   // optional fused prologue  x -> relu(x*scale[c] + shift[c])
-    const float* pro_shift;
-    void* C; long ldc;
-    float alpha;
-    const float* bias;        // per-column bias (E_BF16 / E_F32)
-    int relu;                 // epilogue activation: 0 none, 1 ReLU, 2 GELU (tanh form)
-    float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
-    int ktiles_per_split;     // split-K (grid.z)
-    int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
-    int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
-    int transC;               // E_ATOMIC: accumulate C^T (C[n * ldc + m])
-    // batched GEMM (grid.y = nb1 * nb2): operand offsets z1 * s*1 + z2 * s*2 (elements), z = z1 * nb2 + z2
-    int nb2;
-    long sA1, sA2, sB1, sB2, sC1, sC2;
-    // causal attention structure (square T x T operands, row = query, col = key):
-    //  1: C tiles strictly above the diagonal are skipped (S = Q K^T; never read by the softmax)
-    //  2: reduction limited to k < m0 + BM   (A = P or dS [q][k], lower triangular: P V, dS K)
-    //  3: reduction starts at k >= m0        (A = P^T / dS^T, upper triangular: P^T dO, dS^T Q)
-    int causal;
-    int stage_store;          // 128-row kernel: bf16 epilogue stores staged through LDS (full-row writes)
-    // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
-    const bf16_t* ep_res;
-    const bf16_t* ep_x;
-    const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
-    const float* alpha_ptr;   // optional device scalar multiplying alpha (fp8 per-tensor dequantisation)
-    bf16_t* ep_aux;           // relu == 2: the pre-activation (bias added) is also stored here (ld = ldc)
-    const bf16_t* ep_dgelu;   // multiply the result by gelu'(u), u read from here (GELU backward)
-};
-
-__device__ __forceinline__ float gelu_tanh(float x) {
-    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
-}
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-    const float t = tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 0.134145f * x * x);
-}
-
-// ---------------------------------------------------------------------------------------------
-// LDS image helpers
-// ---------------------------------------------------------------------------------------------
-// K-major image: [rows][64] bf16, 128-byte rows, 16-byte chunk c of row r stored at chunk c^((r>>1)&7).
-__device__ __forceinline__ int kimg_off(int row, int chunk) {   // in bf16 elements
-    return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
-}
-// MN-major image: [64 k-rows][W] bf16, W in {64,128,256}; chunk XOR with an even, row-dependent value.
-template <int W>
-__device__ __forceinline__ int mimg_off(int krow, int chunk) {
-    int sw;
-    if constexpr (W >= 128) sw = ((krow & 3) | ((krow >> 1) & 4)) << 1;     // 16 (32) chunks / row
-    else sw = (((krow >> 1) & 1) | ((krow >> 2) & 2)) << 1;                 // 8 chunks / row
-    return krow * W + ((chunk ^ sw) << 3);
-}
-
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__device__ __forceinline__ bf16x8_t frag_kmajor(const bf16_t* img, int row, int ks, int lane) {
-    const int chunk = ks * 4 + (lane >> 4);
-    u16x8_t v = *reinterpret_cast<const u16x8_t*>(img + kimg_off(row, chunk));
-    return __builtin_bit_cast(bf16x8_t, v);
-}
-
-// Fragment of 16 columns [col0, col0+16) x 32 k (k0 = 32*ks) from an MN-major image via two
-// transpose reads: lane 4q+p of each 16-lane group addresses row (k0 + 8g + q [+4]), columns
-// col0 + 4p .. +3; lane i receives column col0+i of the four rows.
-template <int W>
-__device__ __forceinline__ bf16x8_t frag_mnmajor(const bf16_t* img, int col0, int ks, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int col = col0 + 4 * p;
-    const int chunk = col >> 3, within = col & 7;
-    const int r0 = ks * 32 + 8 * g + q;
-    const bf16_t* p0 = img + mimg_off<W>(r0, chunk) + within;
-    const bf16_t* p1 = img + mimg_off<W>(r0 + 4, chunk) + within;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-}
+using namespace pg;
 
 __device__ __forceinline__ u16x8_t zero8() {
     u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -411,11 +300,6 @@ constexpr int smem_bytes() {
     return ops > cst ? ops : cst;
 }
 
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-    // Bijective: blocks b, b+8, b+16... (same XCD under round-robin dispatch) get consecutive tiles.
-    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
 
 // BNW = block tile width (128, or 64 for the N <= 64 layers so no half-empty tiles are computed).
 template <int AM, int BMODE, int EM, bool PRO_A, bool PRO_B, int BNW>
@@ -854,6 +738,9 @@ int launch_old(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
 // glds engine when the operands allow it and the grid is big enough, else the 128-row kernel
 template <int AM, int BMODE, int EM, bool PA, bool PB>
 int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
+    if constexpr (!PA && !PB && (AM == A_KMAJOR || AM == A_MNMAJOR) && (BMODE == B_KMAJOR || BMODE == B_MNMAJOR)) {
+        if (pp_supported(a, AM, BMODE, EM, batch, splits)) return pp_launch(a, AM, BMODE, EM, st);
+    }
     if constexpr (!PA && !PB) {
         if (glds_enabled() && glds_operands_ok<AM, BMODE>(a) && glds_worth<AM>(a, batch, splits)) {
             return launch_glds<AM, BMODE, EM>(a, splits, st, batch, glds_bn(a.N));
@@ -909,6 +796,13 @@ static void ensure_attrs() {}
 PDNN_API int pdnn_set_staged_store(int mode) {
     const int old = stage_store_mode();
     g_stage_store = mode;
+    return old;
+}
+
+PDNN_API int pdnn_set_pp_mode(int mode) {
+    int& m = pg::pp_mode_ref();
+    const int old = m;
+    m = mode;
     return old;
 }
 

@@ -1,0 +1,598 @@
+// Ping-pong GEMM engine ("pp") for gfx950: the plain-GEMM kernel of the transformer linears and other
+// large dense GEMMs (reference GEMM sites MPI_code/src/util/util.h:35-81,
+// MPI_code/src/nn/nn_layer.h:111-175).
+//
+//  * Block tile 256 x BN, 512 threads = 8 waves in two GROUPS of four: group g owns output rows
+//    [128 g, 128 g + 128); its four waves form a WR x WC grid over that 128 x BN block.  Waves w and w + 4
+//    share a SIMD, so every SIMD holds one wave of each group.
+//  * The groups run the same program shifted by one barrier (group 1 executes one extra s_barrier before
+//    its loop, group 0 one after): while a wave of one group issues its MFMAs, its partner on the same
+//    SIMD reads the fragments of the next K-slice from LDS and issues global->LDS copies further ahead,
+//    so one wave's matrix work covers its partner's load latency (cdna_hip_programming.md §5 "256²
+//    8-phase template", MI355X_MICROARCH.md "Two waves per SIMD").
+//  * K is consumed in slices of 32.  A slice of both operands ((256 + BN) x 32 bf16) is staged by
+//    `global_load_lds_dwordx4` (glds) into a ring of NB slots; each group copies its half of every slice.
+//    A slice is issued NB-1 slices ahead and retired with a COUNTED `s_waitcnt vmcnt(N)` in the load
+//    segment before its first reader (never vmcnt(0) in the steady state); only raw `s_barrier`s are
+//    used, so the copies stay in flight across barriers ("Pipelining across barriers"; all LDS is the
+//    one dynamic array, so hipcc inserts no vmcnt(0) of its own — checked in the .s).
+//      RAW: slice s+1 is retired by each group in its load segment of slice s, one barrier before the
+//           other group's first read of it.
+//      WAR: slot (s-1) mod NB is refilled in the load segment of slice s; both groups read slice s-1 in
+//           earlier load segments that end with `s_waitcnt lgkmcnt(0)` before their barrier.
+//  * LDS images: K-major operands [rows][32] bf16 (64-byte rows, 16-byte chunk c of row r stored at
+//    c ^ t[(r >> 2) & 3], t = {0, 2, 3, 1}: conflict-free for the four 16-lane groups of ds_read_b128);
+//    MN-major operands (BN = 128 / 256 only) [32 k-rows][W] read with `ds_read_b64_tr_b16`.  glds writes
+//    lane-linear images, so the swizzle is applied to the per-lane GLOBAL source address (rule 21).
+//  * Tile widths 96 / 128 / 192 / 256 / 288 so that the grid fills the 256 CUs in whole rounds for the
+//    GPT-2 shapes (M = 8192 tokens: N = 768 -> 256x96 = 256 tiles, 2304 -> 256x288 = 256, 3072 -> 256x192
+//    = 512); the host picks the width with the smallest rounds x tile-time estimate.
+//  * Tile order: XCD-aware bijective remap (T1), then groups of 4 tile rows so the 32 tiles an XCD runs
+//    at once share 4 A row-blocks and 8 B column-blocks in its L2.
+//  * MFMA v_mfma_f32_16x16x32_bf16 with swapped operands, so each lane ends with 4 consecutive output
+//    columns; bf16 epilogues pair fragments with permlane16 swaps into 16-byte stores (T21).
+//  * Epilogues: alpha, bias, ReLU / GELU (+ pre-activation to ep_aux), dGELU, residual add (bf16);
+//    fp32 store / in-place accumulate (acc_c) / split-K partial slabs (slab reduction kernel below).
+#include "gemm_common.h"
+
+namespace pg {
+namespace {
+
+constexpr int PP_BM = 256;
+constexpr int PP_SK = 32;                 // K depth of one slice
+constexpr int PP_GROUP = 4;               // tile rows per L2 group
+
+template <int BN_, int WR_, int NB_>
+struct PPC {
+    static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_;
+    static constexpr int WTM = 128 / WR, WTN = BN / WC;
+    static constexpr int FM = WTM / 16, FN = WTN / 16;
+    static constexpr int IMA = PP_BM * PP_SK, IMB = BN * PP_SK, SLOT = IMA + IMB;
+    static constexpr int SMEM = NB * SLOT * 2;
+    static_assert(WTN % 16 == 0 && WTM % 16 == 0, "wave tile");
+    static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+__device__ __forceinline__ int pp_swz(int row) { return (0x78 >> (((row >> 2) & 3) << 1)) & 3; }
+__device__ __forceinline__ int pp_koff(int row, int chunk) { return row * PP_SK + ((chunk ^ pp_swz(row)) << 3); }
+
+// One operand's copies: NR = ROWS/16 wave-instructions of 1 KiB per slice, spread over the 8 waves
+// (NI each; instructions past NR duplicate the last one: identical bytes to identical LDS addresses).
+//   K-major  [rows][K]: instruction j covers rows 16 j .. 16 j + 15 (lane: row 16 j + lane / 4, chunk lane & 3)
+//   MN-major [K][cols]: instruction j covers k-rows RPI j .. RPI j + RPI - 1, RPI = 512 / ROWS
+template <int ROWS, bool KMAJ>
+struct PPLoader {
+    static constexpr int NR = ROWS / 16;
+    static constexpr int NI = (NR + 7) / 8;
+    const bf16_t* src[NI];
+    int dst[NI];
+    long step;
+
+    __device__ __forceinline__ void init(const bf16_t* p, long ld, int extent, int base, int wave, int lane) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            int j = wave * NI + i;
+            j = j < NR ? j : NR - 1;
+            dst[i] = j * 512;
+            if constexpr (KMAJ) {
+                const int row = 16 * j + (lane >> 2);
+                const int g = min(base + row, extent - 1);
+                src[i] = p + (long)g * ld + (((lane & 3) ^ pp_swz(row)) << 3);
+            } else {
+                constexpr int CPR = ROWS / 8, RPI = 64 / CPR;
+                const int kr = RPI * j + lane / CPR;
+                const int c = (lane % CPR) ^ ((mimg_off<ROWS>(kr, 0) - kr * ROWS) >> 3);
+                const int col = min(base + 8 * c, extent - 8);
+                src[i] = p + (long)kr * ld + col;
+            }
+        }
+        step = KMAJ ? PP_SK : PP_SK * ld;
+    }
+    __device__ __forceinline__ void skip(int slices) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) src[i] += slices * step;
+    }
+    __device__ __forceinline__ void issue(bf16_t* img, int s) const {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            __builtin_amdgcn_global_load_lds(src[i] + s * step, (lds_void*)(img + dst[i]), 16, 0, 0);
+    }
+    // copy the next slice and advance (the hot-loop form: one 64-bit add per instruction, no multiply)
+    __device__ __forceinline__ void issue_next(bf16_t* img) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            __builtin_amdgcn_global_load_lds(src[i], (lds_void*)(img + dst[i]), 16, 0, 0);
+            src[i] += step;
+        }
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void pp_vmwait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// retire all but `keep` slices of this wave's copies (keep = slices allowed to stay in flight)
+template <int NIT, int DMAX>
+__device__ __forceinline__ void pp_retire(int keep) {
+    if constexpr (DMAX >= 5) { if (keep >= 5) { pp_vmwait<5 * NIT>(); return; } }
+    if constexpr (DMAX >= 4) { if (keep == 4) { pp_vmwait<4 * NIT>(); return; } }
+    if constexpr (DMAX >= 3) { if (keep == 3) { pp_vmwait<3 * NIT>(); return; } }
+    if constexpr (DMAX >= 2) { if (keep == 2) { pp_vmwait<2 * NIT>(); return; } }
+    if (keep == 1) { pp_vmwait<NIT>(); return; }
+    if (keep == 0) pp_vmwait<0>();
+}
+
+// Persistent over work items (tile, K-split): block b takes items b, b + G, ... (G = gridDim.x, a
+// multiple of 8, so an item keeps its block's XCD label).  The K-slices of consecutive items form one
+// continuous stream through the ring: the copies of the next item's first slices are in flight while the
+// current item finishes and stores its tile, so a tile boundary costs only the epilogue.
+// ABL (timing ablations, PDNN_PP_ABLATE with tools/pp_one.py; results are garbage): bit 0 = no MFMA,
+// bit 1 = no global->LDS copies in the loop, bit 2 = no LDS fragment reads (1..7)
+template <class C, int AM, int BMODE, int EM, int ABL = 0>
+__global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
+    constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
+    constexpr int NB = C::NB, D = NB - 1;
+    using LA = PPLoader<PP_BM, AK>;
+    using LB = PPLoader<C::BN, BKm>;
+    constexpr int NIT = LA::NI + LB::NI;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const sb = reinterpret_cast<bf16_t*>(smem);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave >> 2, wr = (wave & 3) / C::WC, wc = (wave & 3) % C::WC;
+    const int tiles_m = (a.M + PP_BM - 1) / PP_BM, tiles_n = (a.N + C::BN - 1) / C::BN;
+    const int ntiles = tiles_m * tiles_n;
+    const int splits = a.nb2 > 0 ? a.nb2 : 1;                  // K-splits (slab epilogue when > 1)
+    const int nsl = a.ktiles_per_split;                          // slices per work item (divides K / 32)
+    const int G = gridDim.x, b = blockIdx.x;
+    const int nitems = (ntiles * splits - b + G - 1) / G;
+    if (nitems <= 0 || nsl <= 0) return;                         // uniform over the block
+    const int Q = nitems * nsl;                                  // slices this block consumes
+
+    // work item i of this block -> (m0, n0, first slice, split)
+    auto item = [&](int i, int& m0, int& n0, int& z) {
+        const int w = b + i * G;
+        z = w / ntiles;
+        const int t = xcd_remap(w - z * ntiles, ntiles);
+        const int gsz = PP_GROUP * tiles_n, gid = t / gsz, first = gid * PP_GROUP;
+        const int gm = min(tiles_m - first, PP_GROUP), r = t - gid * gsz;
+        m0 = (first + r % gm) * PP_BM;
+        n0 = (r / gm) * C::BN;
+    };
+
+    LA la;
+    LB lb;
+    // issue cursor (slices run ahead of the compute cursor by up to D): loaders point at the next slice
+    int iss_item = 0, iss_s = 0, wr_off = 0;
+    auto load_item = [&](int i) {
+        int m0, n0, z;
+        item(i, m0, n0, z);
+        la.init(a.A, a.lda, a.M, m0, wave, lane);
+        lb.init(a.B, a.ldb, a.N, n0, wave, lane);
+        la.skip(z * nsl);
+        lb.skip(z * nsl);
+    };
+    auto issue_next = [&]() {                                    // copy the next stream slice into its slot
+        bf16_t* img = sb + wr_off;
+        la.issue_next(img);
+        lb.issue_next(img + C::IMA);
+        wr_off = wr_off + C::SLOT == NB * C::SLOT ? 0 : wr_off + C::SLOT;
+        if (++iss_s == nsl) {
+            iss_s = 0;
+            if (++iss_item < nitems) load_item(iss_item);
+        }
+    };
+
+    f32x4_t acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // optional phase trace: [block][wave 0 / 4][0 start, 1 prologue done, 2 + 2i item i computed, 3 + 2i stored]
+    long long* const dbg = (a.dbg && lane == 0 && (wave & 3) == 0) ? a.dbg + ((long)b * 2 + grp) * 64 : nullptr;
+    if (dbg) dbg[0] = wall_clock64();
+    // prologue: stream slices 0 .. D-1, then retire slice 0
+    load_item(0);
+    for (int q = 0; q < D && q < Q; ++q) issue_next();
+    pp_retire<NIT, D>(min(Q, D) - 1);
+    if (dbg) dbg[1] = wall_clock64();
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();          // stagger: group 1 runs one barrier behind
+
+    const int koffl = pp_koff(lane & 15, lane >> 4);     // K-major fragment offset (row & 15 == lane & 15)
+    const int arow = grp * 128 + wr * C::WTM, bcol = wc * C::WTN;
+    const int lm = lane & 15, lg = lane >> 4;
+    float alpha = a.alpha;
+    if (a.alpha_ptr) alpha *= *a.alpha_ptr;
+
+    int s = 0, cur = 0, rd_off = 0;                      // slice within the current item, item index, read slot
+    for (int q = 0; q < Q; ++q) {
+        // ---------------- load segment ----------------
+        const bool more = q + D < Q;
+        if (more) pp_vmwait<(D - 2) * NIT>();            // stream slice q+1 landed (this wave's copies)
+        else pp_retire<NIT, D>(Q - q - 2);
+        const bf16_t* A_ = sb + rd_off;
+        const bf16_t* B_ = A_ + C::IMA;
+        rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
+        bf16x8_t af[C::FM], bfr[C::FN];
+        if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+            for (int f = 0; f < C::FN; ++f) bfr[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)q, 1, 2, 3, 4, 5, 6, 7});
+#pragma unroll
+            for (int f = 0; f < C::FM; ++f) af[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)f, 1, 2, 3, 4, 5, 6, 7});
+        } else {
+#pragma unroll
+        for (int f = 0; f < C::FN; ++f) {
+            if constexpr (BKm) bfr[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
+                                           B_ + (bcol + f * 16) * PP_SK + koffl));
+            else bfr[f] = frag_mnmajor<C::BN>(B_, bcol + f * 16, 0, lane);
+        }
+#pragma unroll
+        for (int f = 0; f < C::FM; ++f) {
+            if constexpr (AK) af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
+                                          A_ + (arow + f * 16) * PP_SK + koffl));
+            else af[f] = frag_mnmajor<PP_BM>(A_, arow + f * 16, 0, lane);
+        }
+        }
+        if (!(ABL & 2) && more) issue_next();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // ---------------- compute segment ----------------
+        __builtin_amdgcn_s_setprio(1);
+        if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+            for (int f = 0; f < C::FM; ++f) asm volatile("" ::"v"(af[f]));
+#pragma unroll
+            for (int f = 0; f < C::FN; ++f) asm volatile("" ::"v"(bfr[f]));
+        } else {
+#pragma unroll
+        for (int fm = 0; fm < C::FM; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < C::FN; ++fn)
+                acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        if (++s < nsl) continue;
+
+        // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
+        if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
+        s = 0;
+        int m0, n0, z;
+        item(cur++, m0, n0, z);
+        static_for<0, C::FM>([&](auto FMC) {
+            constexpr int fm = decltype(FMC)::value;
+            const int m = m0 + arow + fm * 16 + lm;
+            const bool mv = m < a.M;
+            if constexpr (EM == E_BF16) {
+                uint32_t pk[C::FN][2];
+#pragma unroll
+                for (int fn = 0; fn < C::FN; ++fn) {
+                    const int n = n0 + bcol + fn * 16 + 4 * lg;
+                    const bool ok = mv && n + 4 <= a.N;
+                    const long off = (long)m * a.ldc + n;
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
+                    if (a.bias && n + 4 <= a.N) {
+                        const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+                        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                    }
+                    if (a.relu == 1) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+                    } else if (a.relu == 2) {
+                        u16x4_t pre;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
+                        if (a.ep_aux && ok) *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
+                    }
+                    if (a.ep_dgelu && ok) {
+                        const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
+                    }
+                    if (a.ep_res && ok) {
+                        const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
+                    }
+                    pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                    pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                }
+                bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc;
+#pragma unroll
+                for (int fp = 0; fp < C::FN / 2; ++fp) {   // 16-byte stores: permlane16 swap pairs fragments
+                    const auto s0_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
+                    const auto s1_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][1], pk[2 * fp + 1][1], false, false);
+                    const int n = n0 + bcol + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
+                    if (mv && n + 8 <= a.N) {
+                        *reinterpret_cast<uint4*>(Crow + n) = make_uint4(s0_[0], s1_[0], s0_[1], s1_[1]);
+                    } else if (mv && n < a.N) {
+                        const uint32_t w4[4] = {s0_[0], s1_[0], s0_[1], s1_[1]};
+                        for (int j = 0; j < 8 && n + j < a.N; ++j) Crow[n + j] = (bf16_t)(w4[j >> 1] >> (16 * (j & 1)));
+                    }
+                }
+                if constexpr (C::FN % 2) {                 // odd fragment count: 8-byte stores for the last one
+                    const int n = n0 + bcol + (C::FN - 1) * 16 + 4 * lg;
+                    if (mv && n + 4 <= a.N)
+                        *reinterpret_cast<uint2*>(Crow + n) = make_uint2(pk[C::FN - 1][0], pk[C::FN - 1][1]);
+                }
+            } else {
+                // fp32: K-split items write partial slabs at C + z * sC1 (pp_slab_reduce_kernel sums them),
+                // otherwise store / accumulate (acc_c) into C
+                const bool slab = splits > 1;
+                float* const Cb = reinterpret_cast<float*>(a.C) + (slab ? z * a.sC1 : 0);
+#pragma unroll
+                for (int fn = 0; fn < C::FN; ++fn) {
+                    const int n = n0 + bcol + fn * 16 + 4 * lg;
+                    if (!mv || n >= a.N) continue;
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
+                    float* Cp = Cb + (long)m * a.ldc + n;
+                    const bool n4 = n + 4 <= a.N;
+                    if (!slab && a.bias && n4) {
+                        const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+                        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                    }
+                    if (!slab && a.relu == 1) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+                    } else if (!slab && a.relu == 2) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
+                    }
+                    if (n4 && (a.ldc & 3) == 0) {
+                        float4* C4 = reinterpret_cast<float4*>(Cp);
+                        if (a.acc_c && !slab) {
+                            const float4 o = *C4;
+                            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+                        }
+                        *C4 = make_float4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        for (int j = 0; j < 4 && n + j < a.N; ++j) Cp[j] = v[j] + ((a.acc_c && !slab) ? Cp[j] : 0.f);
+                    }
+                }
+            }
+        });
+        if (dbg && cur <= 31) dbg[1 + 2 * cur] = wall_clock64();
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();          // balance the stagger
+}
+
+// out[m][n] (+)= sum_z slab[z][m][n]  (fp32, ld = ldc, slab stride sz).  float4 per thread.
+__global__ void __launch_bounds__(256) pp_slab_reduce_kernel(const float* __restrict__ slab, long sz, int splits,
+                                                             float* __restrict__ out, int M, int N, long ldc,
+                                                             int accumulate) {
+    const int n4 = N >> 2;
+    const long total = (long)M * n4;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int m = (int)(i / n4), c = (int)(i - (long)m * n4) * 4;
+        const long off = (long)m * ldc + c;
+        float4 s = accumulate ? *reinterpret_cast<const float4*>(out + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int z = 0; z < splits; ++z) {
+            const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + off);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(out + off) = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+using C96 = PPC<96, 2, 7>;
+using C128 = PPC<128, 2, 5>;
+using C192 = PPC<192, 2, 5>;
+using C256 = PPC<256, 1, 4>;
+using C288 = PPC<288, 2, 4>;
+using C256b = PPC<256, 1, 5>;        // 160 KiB ring (A/B: PDNN_PP_BN=257)
+
+int g_pp_mode = -1;
+int g_pp_force_bn = -1;
+long long* g_pp_trace = nullptr;
+
+int device_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+int g_pp_ablate = -1;
+
+template <class C, int AM, int BMODE, int EM, int ABL>
+void set_attr() {
+    static bool attr = false;
+    if (!attr) {
+        attr = true;
+        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<C, AM, BMODE, EM, ABL>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+    }
+}
+
+template <class C, int AM, int BMODE, int EM>
+int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
+    if (g_pp_ablate < 0) { const char* e = getenv("PDNN_PP_ABLATE"); g_pp_ablate = e ? atoi(e) : 0; }
+    const long items = cdiv(a.M, PP_BM) * cdiv(a.N, C::BN) * splits;
+    const int cus = device_cus();
+    const int grid = items <= cus ? (int)items : (cus / 8) * 8;     // persistent: one block per CU
+    GemmArgs b = a;
+    b.nb2 = splits;
+    b.dbg = g_pp_trace;
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16) {
+#define PP_ABL_CASE(X) if (g_pp_ablate == X) { set_attr<C, AM, BMODE, EM, X>(); hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, X>), dim3(grid), dim3(512), C::SMEM, st, b); PDNN_LAUNCH_RET; }
+        PP_ABL_CASE(1) PP_ABL_CASE(2) PP_ABL_CASE(3) PP_ABL_CASE(4) PP_ABL_CASE(5) PP_ABL_CASE(6) PP_ABL_CASE(7)
+#undef PP_ABL_CASE
+    }
+    set_attr<C, AM, BMODE, EM, 0>();
+    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM>), dim3(grid), dim3(512), C::SMEM, st, b);
+    PDNN_LAUNCH_RET;
+}
+
+template <int AM, int BMODE, int EM>
+int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR) {
+        switch (bn) {
+            case 96: return launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
+            case 192: return launch_cfg<C192, AM, BMODE, EM>(a, splits, st);
+            case 288: return launch_cfg<C288, AM, BMODE, EM>(a, splits, st);
+            case 257: return launch_cfg<C256b, AM, BMODE, EM>(a, splits, st);
+            default: break;
+        }
+    }
+    if (bn == 128) return launch_cfg<C128, AM, BMODE, EM>(a, splits, st);
+    return launch_cfg<C256, AM, BMODE, EM>(a, splits, st);
+}
+
+// relative per-CU throughput of the tile widths (A/B measured, tools/pp_check.py)
+double bn_eff(int bn) {
+    switch (bn) {
+        case 96: return 0.78;
+        case 128: return 0.86;
+        case 192: return 0.93;
+        default: return 1.0;
+    }
+}
+
+int pick_bn(const GemmArgs& a, bool kk) {
+    if (g_pp_force_bn < 0) { const char* e = getenv("PDNN_PP_BN"); g_pp_force_bn = e ? atoi(e) : 0; }
+    const int cus = device_cus();
+    static const int kk_opts[] = {256, 288, 192, 128, 96};
+    static const int mn_opts[] = {256, 128};
+    const int* opts = kk ? kk_opts : mn_opts;
+    const int nopt = kk ? 5 : 2;
+    if (g_pp_force_bn > 0) {
+        if (kk && g_pp_force_bn == 257) return 257;
+        for (int i = 0; i < nopt; ++i)
+            if (opts[i] == g_pp_force_bn) return g_pp_force_bn;
+    }
+    int best = 256;
+    double bt = 1e300;
+    for (int i = 0; i < nopt; ++i) {
+        const int bn = opts[i];
+        const long tiles = cdiv(a.M, PP_BM) * cdiv(a.N, bn);
+        const long rounds = cdiv(tiles, cus);
+        const double t = (double)rounds * bn / bn_eff(bn);
+        if (t < bt * 0.999) { bt = t; best = bn; }
+    }
+    return best;
+}
+
+}  // namespace
+
+int& pp_mode_ref() {
+    if (g_pp_mode < 0) { const char* e = getenv("PDNN_PP"); g_pp_mode = e ? atoi(e) : 1; }
+    return g_pp_mode;
+}
+
+bool pp_supported(const GemmArgs& a, int amode, int bmode, int em, int batch, int splits) {
+    const int mode = pp_mode_ref();
+    if (!mode || batch != 1 || splits != 1 || em == E_ATOMIC) return false;
+    if (a.causal || a.scatter || a.stats || a.ep_x || a.transC || a.pro_scale) return false;
+    if (a.K % PP_SK || a.M < 16 || a.N < 16 || a.N % 8 || a.lda % 8 || a.ldb % 8) return false;
+    if (!((amode == A_KMAJOR && (bmode == B_KMAJOR || bmode == B_MNMAJOR)) ||
+          (amode == A_MNMAJOR && bmode == B_MNMAJOR)))
+        return false;
+    if (amode == A_MNMAJOR && a.M % 8) return false;
+    if (mode == 2) return true;
+    return cdiv(a.M, PP_BM) * cdiv(a.N, 256) >= 48 || (long)a.M * a.N >= (1L << 22);
+}
+
+int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) {
+    GemmArgs a = a0;
+    a.ktiles_per_split = a.K / PP_SK;
+    const int bn = pick_bn(a, amode == A_KMAJOR && bmode == B_KMAJOR);
+    const int key = amode * 100 + bmode * 10 + em;
+    switch (key) {
+        case 0: return launch_bn<A_KMAJOR, B_KMAJOR, E_BF16>(a, bn, 1, st);
+        case 1: return launch_bn<A_KMAJOR, B_KMAJOR, E_F32>(a, bn, 1, st);
+        case 10: return launch_bn<A_KMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
+        case 11: return launch_bn<A_KMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+        case 110: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
+        case 111: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+}  // namespace pg
+
+// hipcc (ROCm 7.2) emits the host launch stub of only the first implicitly instantiated specialisation of
+// a kernel template in an anonymous namespace: instantiate every specialisation used explicitly.
+#define PP_I(CFG, AM, BM_, EM) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::AM, pg::BM_, pg::EM, 0>(pg::GemmArgs);
+#define PP_A(CFG, X) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, X>(pg::GemmArgs);
+#define PP_A3(CFG) PP_A(CFG, 1) PP_A(CFG, 2) PP_A(CFG, 3) PP_A(CFG, 4) PP_A(CFG, 5) PP_A(CFG, 6) PP_A(CFG, 7)
+PP_A3(C96) PP_A3(C256) PP_A3(C256b)
+#undef PP_A3
+#undef PP_A
+#define PP_I2(CFG, AM, BM_) PP_I(CFG, AM, BM_, E_BF16) PP_I(CFG, AM, BM_, E_F32)
+PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR) PP_I2(C288, A_KMAJOR, B_KMAJOR)
+PP_I2(C128, A_KMAJOR, B_KMAJOR) PP_I2(C256, A_KMAJOR, B_KMAJOR) PP_I2(C256b, A_KMAJOR, B_KMAJOR)
+PP_I2(C128, A_KMAJOR, B_MNMAJOR) PP_I2(C256, A_KMAJOR, B_MNMAJOR)
+PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)
+#undef PP_I2
+#undef PP_I
+
+// pp_wgrad: out[M][N] (fp32) += alpha * A[K][M]^T . B[K][N] with split-K partial slabs in `ws`
+// (>= splits * M * N floats) reduced by a second kernel; splits == 1 accumulates in place.
+PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* out, long ldc, int M, int N,
+                           int K, float alpha, float* ws, int splits, hipStream_t st) {
+    using namespace pg;
+    if (K % PP_SK || M % 8 || N % 8 || splits < 1) return (int)hipErrorInvalidValue;
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.alpha = alpha;
+    const int nsl = K / PP_SK;
+    while (nsl % splits) --splits;                 // work items have equal slice counts
+    a.ktiles_per_split = nsl / splits;
+    const int bn = pick_bn(a, false);
+    if (splits == 1) {
+        a.C = out; a.ldc = ldc; a.acc_c = 1;
+        return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+    }
+    if (!ws) return (int)hipErrorInvalidValue;
+    a.C = ws; a.ldc = N; a.sC1 = (long)M * N;
+    int e = launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, splits, st);
+    if (e) return e;
+    hipLaunchKernelGGL(pp_slab_reduce_kernel, dim3(stream_grid((long)M * N / 4, 256)), dim3(256), 0, st,
+                       (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
+    using namespace pg;
+    // enough blocks to cover the CUs once, each with >= 16 slices; capped by the slab workspace volume
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K;
+    const int bn = pick_bn(a, false);
+    const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
+    const int cus = device_cus();
+    if (tiles >= cus / 2) return 1;
+    int s = (int)cdiv(cus, tiles);
+    const int nsl = K / PP_SK;
+    while (s > 1 && (nsl / s < 16 || nsl % s)) --s;
+    return s < 1 ? 1 : s;
+}
+
+// phase trace buffer for the next pp launches (null = off): 2 * grid * 64 int64 timestamps (100 MHz)
+PDNN_API void pdnn_set_pp_trace(long long* buf) { pg::g_pp_trace = buf; }
+
+// force a tile width (0 = automatic); returns the previous setting.  A/B experiments and tests.
+PDNN_API int pdnn_set_pp_bn(int bn) {
+    const int old = pg::g_pp_force_bn < 0 ? 0 : pg::g_pp_force_bn;
+    pg::g_pp_force_bn = bn;
+    return old;
+}

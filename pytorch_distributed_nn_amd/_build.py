@@ -43,7 +43,7 @@ HIP_FLAGS = [
 # and raised occupancy (fwd 2 -> 3 waves/SIMD, dq 3 -> 4).  In the GEMM engines only the 64-column glds
 # tiles held AGPRs; VGPR form there measured +1.9% on the ResNet-50 step (7142/7199 -> 7312/7293 img/s).
 VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
-KERNEL_FILE_FLAGS = {"attention.hip": VGPR_FORM, "gemm_mfma.hip": VGPR_FORM}   # gemm: +1.9% ResNet-50
+KERNEL_FILE_FLAGS = {"attention.hip": VGPR_FORM, "gemm_mfma.hip": VGPR_FORM, "gemm_pp.hip": VGPR_FORM}   # gemm: +1.9% ResNet-50
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
              "-pthread", f"-I{ROOT / 'csrc' / 'include'}", f"-I{ROOT / 'csrc' / 'runtime'}"]
 

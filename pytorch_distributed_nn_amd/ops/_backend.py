@@ -39,6 +39,11 @@ _SIGS = {
     "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "pdnn_gemm_stats_rows": [I],
     "pdnn_set_glds_mode": [I],
+    "pdnn_set_pp_mode": [I],
+    "pdnn_set_pp_bn": [I],
+    "pdnn_set_pp_trace": [P],
+    "pdnn_pp_wgrad": [P, L, P, L, P, L, I, I, I, F, P, I, P],
+    "pdnn_pp_wgrad_splits": [I, I, I],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
     "pdnn_bn_fin_work": [I, I],

@@ -75,47 +75,9 @@ def fp8_ok(M, N, Kd):
     return Kd % 128 == 0 and N % 8 == 0 and M >= 1
 
 
-_ONE = {}
-
-
-def _one(dev):
-    t = _ONE.get(dev)
-    if t is None:
-        t = _ONE[dev] = torch.ones(1, device=dev, dtype=F32)
-    return t
-
-
-def _scaled_mm_linear(xq, wq, gs, bias, act, aux, res):
-    """Library fp8 GEMM core (hipBLASLt via torch._scaled_mm, OCP e4m3 = torch.float8_e4m3fn) with the
-    dequantisation factor as a device scalar; GELU / ReLU / residual on the in-tree kernels (same split as
-    ops/blas.py for bf16)."""
-    f8 = torch.float8_e4m3fn
-    M, N = xq.shape[0], wq.shape[0]
-    b = weight_bf16(bias) if bias is not None else None
-    a_, b_ = xq.view(f8), wq.view(f8).t()
-    if act:
-        u = aux if aux is not None else torch.empty(M, N, device=xq.device, dtype=torch.bfloat16)
-        try:
-            torch._scaled_mm(a_, b_, scale_a=gs, scale_b=_one(xq.device), bias=b, out_dtype=torch.bfloat16, out=u)
-        except (TypeError, RuntimeError):
-            u.copy_(torch._scaled_mm(a_, b_, scale_a=gs, scale_b=_one(xq.device), bias=b, out_dtype=torch.bfloat16))
-        y = K.act_fwd(u, "gelu" if act == 2 else "relu")
-    else:
-        y = torch._scaled_mm(a_, b_, scale_a=gs, scale_b=_one(xq.device), bias=b, out_dtype=torch.bfloat16)
-    if res is not None:
-        y.add_(res)
-    return y
-
-
 def linear_fp8_fwd(x2, p_w, meta: Fp8Meta, bias=None, act=0, aux=None, res=None, stats=None):
-    """y = act(x2 @ W^T + bias) (+res) with x2 and W in e4m3 (bf16 output).  The e4m3 GEMM core runs on
-    the in-tree block-scaled MFMA engine, or — for large plain GEMMs where it measures faster, same rule
-    as the bf16 linears (ops/blas.py) — on hipBLASLt's fp8 kernels; fused BN statistics stay in-tree."""
-    from . import blas
+    """y = act(x2 @ W^T + bias) (+res) with x2 and W in e4m3 (bf16 output) on the in-tree block-scaled
+    MFMA engine (``pdnn_gemm_fp8``), optional fused BN statistics of the output."""
     wq, winv = weight_fp8(p_w)
     xq, gs = meta.quantize(x2, winv)
-    M, Kd = x2.shape
-    N = wq.shape[0]
-    if stats is None and N % 16 == 0 and Kd % 16 == 0 and blas._blas(M, N, Kd, "fwd"):
-        return _scaled_mm_linear(xq, wq, gs, bias, act, aux, res)
     return K.gemm_fp8(xq, wq, gs, bias=bias, act=act, aux=aux, res=res, stats=stats)

@@ -43,6 +43,34 @@ def set_glds_mode(mode: int) -> int:
     return lib().pdnn_set_glds_mode(int(mode))
 
 
+def set_pp_mode(mode: int) -> int:
+    """Ping-pong GEMM engine (csrc/kernels/gemm_pp.h) for plain GEMMs: 1 automatic (default), 0 off, 2 whenever
+    the operands allow it.  Returns the previous mode."""
+    return lib().pdnn_set_pp_mode(int(mode))
+
+
+def set_pp_bn(bn: int) -> int:
+    """Force the ping-pong engine's tile width (96/128/192/256/288; 0 = automatic).  Returns the previous."""
+    return lib().pdnn_set_pp_bn(int(bn))
+
+
+def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None):
+    """out[M][N] (fp32) += alpha * x[K][M]^T @ y[K][N] on the ping-pong engine: split-K partial slabs in a
+    workspace (``ws``, allocated when not given) reduced by a second kernel, or in place when one split
+    covers the CUs."""
+    K_, M = x.shape
+    K2, N = y.shape
+    _chk(K_ == K2 and K_ % 32 == 0 and M % 8 == 0 and N % 8 == 0, f"pp_wgrad: bad shapes {x.shape} {y.shape}")
+    _chk(out.dtype == F32 and out.shape == (M, N) and out.stride(1) == 1, "pp_wgrad: fp32 [M][N] output")
+    if splits is None:
+        splits = lib().pdnn_pp_wgrad_splits(M, N, K_)
+    if splits > 1 and ws is None:
+        ws = torch.empty(splits * M * N, device=x.device, dtype=F32)
+    call("pdnn_pp_wgrad", ptr(x), x.stride(0), ptr(y), y.stride(0), ptr(out), out.stride(0), M, N, K_,
+         float(alpha), ptr(ws), int(splits), stream())
+    return out
+
+
 def gemm_nt(x, w, bias=None, relu=False, out_f32=False, alpha=1.0, out=None):
     """y[M][N] = alpha * x[M][K] @ w[N][K]^T (+bias)(relu).  x, w bf16 row-major."""
     M, K = x.shape

@@ -1,0 +1,43 @@
+"""Transformer linear layers on the in-tree GEMM engines (no vendor BLAS on any path).
+
+Every call lands in ``csrc/kernels``:
+
+* forward ``y = act(x W^T + b) (+ res)`` and data gradient ``dX = g W (* gelu'(u))`` go through
+  ``kernels.gemm_nt_ex``; large shapes run the ping-pong engine (``csrc/kernels/gemm_pp.hip``: 256-row
+  tiles, tile width chosen from 96/128/192/256/288 so the grid fills the 256 CUs in whole rounds, glds ring
+  with counted vmcnt, fused bias / GELU (+ pre-activation) / dGELU / residual epilogues), small ones the
+  128-row register-staged kernel;
+* the weight gradient ``dW += g^T x`` (fp32, in place in the flat gradient arena) runs the ping-pong
+  engine with both operands reduction-major and split-K partial slabs reduced by a second kernel
+  (``kernels.pp_wgrad``), or the glds engine's split-K atomics for shapes it does not take.
+
+Reference GEMM sites this replaces: MPI_code/src/util/util.h:35-81 (cblas_dgemm),
+MPI_code/src/nn/nn_layer.h:111-175 (forward, dgrad, wgrad of the bias-folded dense layer).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+F32 = torch.float32
+
+
+def linear_fwd(x, wk, bias=None, act=0, aux=None, res=None):
+    """y = act(x @ wk^T + bias) (+ res), bf16 [M][N]; with act == 2 (GELU) ``aux`` receives the
+    pre-activation.  Same contract as :func:`kernels.gemm_nt_ex`."""
+    return K.gemm_nt_ex(x, wk, bias=bias, act=act, aux=aux, res=res)
+
+
+def linear_dgrad(g, wk, dgelu=None):
+    """dX = g @ wk (wk stored [N][K] as in the forward); with ``dgelu`` = pre-activation u: dX *= gelu'(u)."""
+    return K.gemm_nt_ex(g, wk, dgelu=dgelu, w_kn=True)
+
+
+def wgrad_acc(g, x, out):
+    """out[N][K] (fp32) += g[M][N]^T @ x[M][K]."""
+    M, N = g.shape
+    Kd = x.shape[1]
+    if M % 32 == 0 and N % 8 == 0 and Kd % 8 == 0 and out.is_contiguous() and M * N * Kd >= (1 << 24):
+        return K.pp_wgrad(g, x, out)
+    return K.gemm_tn_acc(g, x, out)

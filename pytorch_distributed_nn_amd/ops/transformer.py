@@ -31,7 +31,7 @@ import torch
 import torch.nn.functional as F
 
 from ..optim.flat import direct_grad, grad_ready
-from . import blas as BL
+from . import linear as BL
 from . import kernels as K
 
 BF16 = torch.bfloat16

@@ -157,14 +157,12 @@ def test_gpt2_block_matches_reference():
         assert rel2(p.grad, pr.grad) < 0.08, n
 
 
-@pytest.mark.parametrize("engine", ["mfma", "blas", "auto"])
-def test_gpt2_engines_match_reference(engine):
-    """GPT-2 (d=256, 4 heads, T=512, B=4: 2048 tokens, so 'auto' takes the hipBLASLt GEMM cores) loss and
-    every gradient against the fp32 CPU reference, with the linears on the in-tree MFMA kernels, on
-    hipBLASLt (+ our GELU/dGELU/residual kernels), or auto-selected (ops/blas.py)."""
-    from pytorch_distributed_nn_amd.ops import blas
-    old = blas.MODE
-    blas.set_mode(engine)
+@pytest.mark.parametrize("pp", [0, 2])
+def test_gpt2_engines_match_reference(K, pp):
+    """GPT-2 (d=256, 4 heads, T=512, B=4: 2048 tokens) loss and every gradient against the fp32 CPU
+    reference, with the linears on the ping-pong engine wherever it takes the shape (pp=2) or on the
+    register-staged / glds engines only (pp=0)."""
+    old = K.set_pp_mode(pp)
     try:
         m = _tiny(n_embd=256, n_head=4, block_size=512).cuda()
         ref = copy.deepcopy(m).float().cpu()
@@ -177,10 +175,10 @@ def test_gpt2_engines_match_reference(engine):
         loss.backward()
         lref.backward()
         for (n, p), (_, pr) in zip(m.named_parameters(), ref.named_parameters()):
-            assert cos(p.grad.cpu(), pr.grad) > 0.99, (engine, n)
-            assert rel2(p.grad.cpu(), pr.grad) < 0.1, (engine, n)
+            assert cos(p.grad.cpu(), pr.grad) > 0.99, (pp, n)
+            assert rel2(p.grad.cpu(), pr.grad) < 0.1, (pp, n)
     finally:
-        blas.set_mode(old)
+        K.set_pp_mode(old)
 
 
 def test_gpt2_tiny_loss_and_grads():
