@@ -215,3 +215,43 @@ PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int a
     }
     PDNN_LAUNCH_RET;
 }
+
+// ------------------------------------------------------------------------------------------------
+// bf16 matrix transpose dst[c][r] = src[r][c] (row strides lds / ldd): 64 x 64 tiles through LDS,
+// 16-byte global loads and stores (8 bf16 per lane), LDS rows padded by 2 elements (odd word stride)
+// so the column reads of the transposed pass hit distinct banks.  Used for the reduction-major copies of
+// the transformer weights (ops/functional.weight_bf16_t): the data-gradient GEMM then reads K-major B.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src, long lds, bf16_t* __restrict__ dst,
+                                                             long ldd, int R, int C) {
+    __shared__ bf16_t t[64][66];
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {                     // 64 rows x 8 chunks = 512 loads
+        const int k = tid + 256 * i, rr = k >> 3, cc = (k & 7) * 8;
+        const int r = r0 + rr, c = c0 + cc;
+        u16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (r < R && c + 8 <= C) v = *reinterpret_cast<const u16x8_t*>(src + (long)r * lds + c);
+        else if (r < R) for (int j = 0; j < 8 && c + j < C; ++j) v[j] = src[(long)r * lds + c + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[rr][cc + j] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int k = tid + 256 * i, cr = k >> 3, rc = (k & 7) * 8;    // output row = source column
+        const int c = c0 + cr, r = r0 + rc;
+        if (c >= C) continue;
+        u16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = t[rc + j][cr];
+        if (r + 8 <= R) *reinterpret_cast<u16x8_t*>(dst + (long)c * ldd + r) = v;
+        else for (int j = 0; j < 8 && r + j < R; ++j) dst[(long)c * ldd + r + j] = v[j];
+    }
+}
+
+PDNN_API int pdnn_transpose_bf16(const bf16_t* src, long lds, bf16_t* dst, long ldd, int R, int C, hipStream_t st) {
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, st, src, lds, dst, ldd, R, C);
+    PDNN_LAUNCH_RET;
+}

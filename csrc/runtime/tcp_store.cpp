@@ -31,6 +31,11 @@
 #include <vector>
 
 namespace {
+constexpr uint32_t kMaxKey = 1u << 20;            // 1 MiB keys
+constexpr uint64_t kMaxValue = 1ull << 30;        // 1 GiB values (the native MLP moves weight blobs)
+}  // namespace
+
+namespace {
 
 enum Op : uint8_t { SET = 1, GET = 2, ADD = 3, CHECK = 4, DEL = 5, WAIT = 6, KEYS = 7, PING = 8 };
 enum Status : uint8_t { OK = 0, TIMEOUT = 1, MISSING = 2, ERR = 3 };
@@ -81,9 +86,12 @@ struct Server {
             uint32_t kl;
             uint64_t vl;
             if (!recv_all(fd, &op, 1) || !recv_all(fd, &kl, 4)) break;
+            // lengths come from the wire: a stray or malformed peer must not make the detached serve
+            // thread throw bad_alloc (std::terminate would take the whole master down) -> drop it
+            if (kl > kMaxKey) break;
             std::string key(kl, '\0');
             if (kl && !recv_all(fd, &key[0], kl)) break;
-            if (!recv_all(fd, &vl, 8)) break;
+            if (!recv_all(fd, &vl, 8) || vl > kMaxValue) break;
             std::vector<char> val(vl);
             if (vl && !recv_all(fd, val.data(), vl)) break;
             if (op == SET) {

@@ -16,6 +16,8 @@ pytorch_distributed_nn_amd._build`` builds both.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import contextlib
+import fcntl
 import os
 import shutil
 import subprocess
@@ -55,6 +57,31 @@ def _newer(src: Path, dst: Path, deps) -> bool:
     return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
 
 
+@contextlib.contextmanager
+def build_lock():
+    """Exclusive inter-process lock around a build: torchrun ranks that all find the library missing
+    serialise here instead of compiling into the same object files."""
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    with open(LIBDIR / ".build.lock", "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
+def stale_sources(kind: str = "kernels"):
+    """Sources (or headers) newer than the built library, [] when it is up to date (or missing)."""
+    if kind == "kernels":
+        d, out, pats = ROOT / "csrc" / "kernels", LIBDIR / "libpdnn_kernels.so", ("*.hip", "*.h")
+    else:
+        d, out, pats = ROOT / "csrc" / "runtime", LIBDIR / "libpdnn_runtime.so", ("*.cpp", "*.h")
+    if not out.exists() or not d.exists():
+        return []
+    t = out.stat().st_mtime
+    return [str(f) for pat in pats for f in d.glob(pat) if f.stat().st_mtime > t + 1.0]
+
+
 def _run(cmd):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
@@ -72,19 +99,31 @@ def _build_lib(srcs, compiler, flags, out: Path, objdir: Path, deps, link_extra=
         if _newer(s, o, deps):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4)
+    pid = os.getpid()
+    ff = file_flags or {}
+
+    def compile_one(s, o):      # private temp object, renamed into place: readers never see a partial file
+        tmp = o.with_name(f"{o.stem}.{pid}.tmp.o")
+        _run([compiler, *flags, *ff.get(s.name, []), "-c", str(s), "-o", str(tmp)])
+        os.replace(tmp, o)
+
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        ff = file_flags or {}
-        futs = [ex.submit(_run, [compiler, *flags, *ff.get(s.name, []), "-c", str(s), "-o", str(o)]) for s, o in todo]
+        futs = [ex.submit(compile_one, s, o) for s, o in todo]
         for f in futs:
             f.result()
     if todo or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
-        tmp = out.with_suffix(".so.tmp")
+        tmp = out.with_name(f"{out.name}.{pid}.tmp")
         _run([compiler, *flags, "-shared", *map(str, objs), "-o", str(tmp), *link_extra])
         os.replace(tmp, out)
     return out
 
 
 def build_kernels(verbose=False) -> Path:
+    with build_lock():
+        return _build_kernels()
+
+
+def _build_kernels() -> Path:
     kdir = ROOT / "csrc" / "kernels"
     srcs = sorted(kdir.glob("*.hip"))
     deps = list(kdir.glob("*.h")) + list((ROOT / "csrc" / "include").glob("*.h"))
@@ -93,6 +132,11 @@ def build_kernels(verbose=False) -> Path:
 
 
 def build_runtime(verbose=False, sanitize: str | None = None) -> Path:
+    with build_lock():
+        return _build_runtime(sanitize)
+
+
+def _build_runtime(sanitize: str | None = None) -> Path:
     rdir = ROOT / "csrc" / "runtime"
     srcs = sorted(rdir.glob("*.cpp"))
     deps = list(rdir.glob("*.h")) + list((ROOT / "csrc" / "include").glob("*.h"))
@@ -111,7 +155,7 @@ def build_tools() -> Path:
     objects."""
     build_runtime()
     rdir = ROOT / "csrc" / "runtime"
-    objs = sorted((BUILD / "runtime").glob("*.o"))
+    objs = sorted(o for o in (BUILD / "runtime").glob("*.o") if ".tmp" not in o.name)
     src = ROOT / "csrc" / "tools" / "pdnn_mlp.cpp"
     out = LIBDIR / "pdnn_mlp"
     deps = list(rdir.glob("*.h")) + objs

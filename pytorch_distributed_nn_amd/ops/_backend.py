@@ -44,6 +44,9 @@ _SIGS = {
     "pdnn_set_pp_trace": [P],
     "pdnn_pp_wgrad": [P, L, P, L, P, L, I, I, I, F, P, I, P],
     "pdnn_pp_wgrad_splits": [I, I, I],
+    "pdnn_pp_gemm_nt_splitk": [P, L, P, L, P, L, I, I, I, P, I, P],
+    "pdnn_pp_splitk_splits": [I, I, I],
+    "pdnn_transpose_bf16": [P, L, P, L, I, I, P],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
     "pdnn_bn_fin_work": [I, I],
@@ -107,13 +110,19 @@ def _load():
     if _LIB is not None or _ERR is not None:
         return _LIB
     p = lib_path()
+    from .. import _build
     if not p.exists() and os.environ.get("PDNN_AUTOBUILD", "1") == "1":
         try:
-            from .. import _build
-            _build.build_kernels()
+            _build.build_kernels()          # under an inter-process lock; objects renamed into place
         except Exception as e:  # pragma: no cover - reported via _ERR
             _ERR = f"could not build {p}: {e}"
             return None
+    elif "PDNN_KERNEL_LIB" not in os.environ:
+        stale = _build.stale_sources("kernels")
+        if stale:
+            import warnings
+            warnings.warn(f"{p} is older than {len(stale)} kernel source(s) (e.g. {stale[0]}); "
+                          "rebuild with `python -m pytorch_distributed_nn_amd._build`", stacklevel=2)
     try:
         lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
     except OSError as e:

@@ -40,6 +40,24 @@ def weight_bf16(p: torch.Tensor, krsc: bool = False) -> torch.Tensor:
     return out
 
 
+def weight_bf16_t(p: torch.Tensor) -> torch.Tensor:
+    """bf16 transposed copy W^T [K][N] of a 2-D weight W [N][K] (the data-gradient GEMM's K-major B operand),
+    cached per parameter version / flat-arena update generation, rebuilt by the in-tree transpose kernel."""
+    fp = getattr(p, "_pdnn_flat", None)
+    ver = (p._version, fp.generation if fp is not None else 0)
+    st = getattr(p, "_pdnn_shadow_t", None)
+    if st is not None and st[0] == ver:
+        return st[1]
+    wb = weight_bf16(p)
+    if wb.is_cuda:
+        out = st[1] if st is not None and st[1].shape == (wb.shape[1], wb.shape[0]) else None
+        wt = K.transpose_bf16(wb, out=out)
+    else:
+        wt = wb.t().contiguous()
+    p._pdnn_shadow_t = (ver, wt)
+    return wt
+
+
 def _pad_last(t, mult=8):
     c = t.shape[-1]
     pc = (c + mult - 1) // mult * mult

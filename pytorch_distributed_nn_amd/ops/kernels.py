@@ -71,6 +71,33 @@ def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None):
     return out
 
 
+def gemm_nt_splitk(x, w, splits=None, ws=None):
+    """y[M][N] (bf16) = x[M][K] @ w[N][K]^T with the reduction split over work items writing fp32 slabs
+    (for K >> M, N: e.g. the tied LM head's data gradient, K = vocabulary)."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == Kd and Kd % 32 == 0 and N % 8 == 0, f"gemm_nt_splitk: bad shapes {x.shape} {w.shape}")
+    _chk(x.stride(1) == 1 and w.stride(1) == 1, "gemm_nt_splitk: K-contiguous operands")
+    if splits is None:
+        splits = lib().pdnn_pp_splitk_splits(M, N, Kd)
+    if ws is None:
+        ws = torch.empty(splits * M * N, device=x.device, dtype=F32)
+    out = torch.empty(M, N, device=x.device, dtype=BF16)
+    call("pdnn_pp_gemm_nt_splitk", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), M, N, Kd,
+         ptr(ws), int(splits), stream())
+    return out
+
+
+def transpose_bf16(x, out=None):
+    """out[C][R] = x[R][C] (bf16, 2-D, unit column stride)."""
+    _chk(x.dtype == BF16 and x.dim() == 2 and x.stride(1) == 1, "transpose_bf16: 2-D bf16 with unit column stride")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty(C, R, device=x.device, dtype=BF16)
+    call("pdnn_transpose_bf16", ptr(x), x.stride(0), ptr(out), out.stride(0), R, C, stream())
+    return out
+
+
 def gemm_nt(x, w, bias=None, relu=False, out_f32=False, alpha=1.0, out=None):
     """y[M][N] = alpha * x[M][K] @ w[N][K]^T (+bias)(relu).  x, w bf16 row-major."""
     M, K = x.shape

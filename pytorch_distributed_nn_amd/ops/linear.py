@@ -19,6 +19,7 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
+from .functional import weight_bf16_t
 
 F32 = torch.float32
 
@@ -29,9 +30,20 @@ def linear_fwd(x, wk, bias=None, act=0, aux=None, res=None):
     return K.gemm_nt_ex(x, wk, bias=bias, act=act, aux=aux, res=res)
 
 
-def linear_dgrad(g, wk, dgelu=None):
-    """dX = g @ wk (wk stored [N][K] as in the forward); with ``dgelu`` = pre-activation u: dX *= gelu'(u)."""
-    return K.gemm_nt_ex(g, wk, dgelu=dgelu, w_kn=True)
+def linear_dgrad(g, wk, dgelu=None, p=None):
+    """dX = g @ wk (wk stored [N][K] as in the forward); with ``dgelu`` = pre-activation u: dX *= gelu'(u).
+
+    With the parameter ``p`` given, the GEMM reads the cached transposed copy W^T [K][N] (K-major B: every
+    tile width of the ping-pong engine is available, measured faster than the reduction-major B form at
+    all GPT-2 shapes), and a reduction much longer than the output (the tied LM head: N = vocabulary)
+    splits K over work items with fp32 partial slabs."""
+    if p is None or not g.is_cuda:
+        return K.gemm_nt_ex(g, wk, dgelu=dgelu, w_kn=True)
+    wt = weight_bf16_t(p)
+    M, N = g.shape
+    if dgelu is None and N >= 16384 and N % 32 == 0 and N >= 8 * wt.shape[0]:
+        return K.gemm_nt_splitk(g, wt)
+    return K.gemm_nt_ex(g, wt, dgelu=dgelu)
 
 
 def wgrad_acc(g, x, out):

@@ -254,20 +254,20 @@ class GPT2BlockFn(torch.autograd.Function):
         sink = _Sink()
         g = g.contiguous()
         # MLP
-        du = BL.linear_dgrad(g, wfc2, dgelu=u)                         # (g . Wfc2) * gelu'(u)
+        du = BL.linear_dgrad(g, wfc2, dgelu=u, p=Pm[10])                       # (g . Wfc2) * gelu'(u)
         dfc2_w, dfc2_b = sink.linear(Pm[10], Pm[11], g, h)
-        dln2 = BL.linear_dgrad(du, wfc)
+        dln2 = BL.linear_dgrad(du, wfc, p=Pm[8])
         dfc_w, dfc_b = sink.linear(Pm[8], Pm[9], du, ln2)
         dx1, dln2w, dln2b = sink.layernorm(dln2, x1, ln2w, m2, r2, g, Pm[6], Pm[7])
         # attention
-        dy = BL.linear_dgrad(dx1, wproj)
+        dy = BL.linear_dgrad(dx1, wproj, p=Pm[4])
         dproj_w, dproj_b = sink.linear(Pm[4], Pm[5], dx1, y)
         if ctx.flash:
             dqkv = K.flash_attn_bwd(qkv, y, dy, P, B, T, H, 1.0 / math.sqrt(x.shape[1] // H))
         else:
             dqkv = attention_bwd(dy, qkv, P, B, T, H, dS_buf=ctx.S)
         ctx.S = None
-        dln1 = BL.linear_dgrad(dqkv, wqkv)
+        dln1 = BL.linear_dgrad(dqkv, wqkv, p=Pm[2])
         dattn_w, dattn_b = sink.linear(Pm[2], Pm[3], dqkv, ln1)
         dx, dln1w, dln1b = sink.layernorm(dln1, x, ln1w, m1, r1, dx1, Pm[0], Pm[1])
         sink.done()
@@ -289,6 +289,7 @@ class LMHeadLossFn(torch.autograd.Function):
         ctx.save_for_backward(x, xf, m, r, logits, targets, lse, acc, lnw, wte_k)
         ctx.eps = eps
         ctx.params = (lnw, lnb)
+        ctx.wte = wte
         return acc[0] / acc[1].clamp_min(1.0)
 
     @staticmethod
@@ -296,10 +297,11 @@ class LMHeadLossFn(torch.autograd.Function):
         x, xf, m, r, logits, targets, lse, acc, lnw, wte_k = ctx.saved_tensors
         gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
         dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
-        dxf = BL.linear_dgrad(dlogits, wte_k)
+        dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
         dwte = _wgrad(dlogits, xf, wte_k.shape)         # tied weight: summed by autograd (not direct)
         sink = _Sink()
         dx, dlnw, dlnb = sink.layernorm(dxf, x, lnw, m, r, None, *ctx.params)
         ctx.params = None
+        ctx.wte = None
         sink.done()
         return dx, None, None, None, dlnw, dlnb, dwte

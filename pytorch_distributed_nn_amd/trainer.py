@@ -99,9 +99,13 @@ class Trainer:
         n_per_epoch = steps_per_epoch or (len(loader) if hasattr(loader, "__len__") else 100)
         it = iter(loader)
         done = False
-        for ep in range(self.epoch, epochs):          # a resumed run continues from its checkpoint's epoch
+        # a resumed run continues at its checkpoint: `epoch` is the epoch in progress (epoch-end checkpoints
+        # store the NEXT epoch), and a mid-epoch checkpoint resumes after the steps that epoch already ran
+        first_i = max(0, self.step_no - self.epoch * n_per_epoch)
+        for ep in range(self.epoch, epochs):
             self.epoch = ep
-            for i in range(n_per_epoch):
+            start, first_i = (first_i if first_i < n_per_epoch else 0), 0
+            for i in range(start, n_per_epoch):
                 tf = time.perf_counter()
                 x, y = next(it)
                 if x.device != self.device:
@@ -133,10 +137,13 @@ class Trainer:
                 if max_steps and self.step_no >= max_steps:
                     done = True
                     break
-            if self.checkpoint_dir and self.rank == 0:
+            if self.checkpoint_dir and self.rank == 0 and not done:
+                self.epoch = ep + 1                   # the checkpoint resumes at the start of the next epoch
                 self.save(f"{self.checkpoint_dir}/checkpoint_ep{ep}.pt")
             if done:
                 break
+        else:
+            self.epoch = max(self.epoch, epochs)
         if self.tracer is not None:
             self.tracer.save()
         return self.history
@@ -168,12 +175,26 @@ class Trainer:
 
     def resume(self, path):
         """Restore model / optimizer / step / RNG from ``path`` (``"auto"``: the newest checkpoint in
-        ``checkpoint_dir``, no-op when there is none — the restart-after-hang path of parallel/watchdog.py)."""
-        if path == "auto":
-            from .parallel.watchdog import latest_checkpoint
-            path = latest_checkpoint(self.checkpoint_dir)
-            if path is None:
-                return None
-        ck = load_checkpoint(path, self.model, self.opt, map_location=self.device)
+        ``checkpoint_dir``, no-op when there is none — the restart-after-hang path of parallel/watchdog.py).
+
+        With more than one rank, only rank 0 resolves and reads the checkpoint (checkpoint directories are
+        written by rank 0 and need not be shared) and broadcasts it; every rank then loads the same model,
+        optimizer state and step, so no rank continues with stale weights or an empty optimizer state."""
+        import torch.distributed as dist
+        multi = self.world > 1 and dist.is_available() and dist.is_initialized()
+        ck = None
+        if not multi or dist.get_rank() == 0:
+            if path == "auto":
+                from .parallel.watchdog import latest_checkpoint
+                path = latest_checkpoint(self.checkpoint_dir)
+            if path is not None:
+                ck = torch.load(path, map_location="cpu", weights_only=True)
+        if multi:
+            box = [ck]
+            dist.broadcast_object_list(box, src=0)
+            ck = box[0]
+        if ck is None:
+            return None
+        load_checkpoint(ck, self.model, self.opt, map_location=self.device, restore_rng=not multi)
         self.epoch, self.step_no = ck.get("epoch", 0), ck.get("step", 0)
         return ck

@@ -123,7 +123,22 @@ class GraphedStep:
         self.opt.pre_replay()
         self.graph.replay()
         self.replays += 1
+        # the replayed optimizer updated the flat arenas without running host code: bump their update
+        # generation so host-side caches keyed on it (transposed / fp8 weight copies) rebuild when an
+        # eager call follows (inside the graph they are rebuilt by captured kernels on every replay)
+        for fp in self._flat_arenas():
+            fp.generation += 1
         return self.static_loss
+
+    def _flat_arenas(self):
+        if not hasattr(self, "_flats"):
+            seen = {}
+            for p in self.model.parameters():
+                fp = getattr(p, "_pdnn_flat", None)
+                if fp is not None:
+                    seen[id(fp)] = fp
+            self._flats = list(seen.values())
+        return self._flats
 
     def reset(self):
         """Drop the captured graph (e.g. after changing the model); the next call re-captures."""

@@ -67,9 +67,12 @@ def lib():
     global _LIB
     if _LIB is None:
         p = Path(__file__).resolve().parent.parent / "_lib" / "libpdnn_runtime.so"
+        from .. import _build
         if not p.exists():
-            from .. import _build
-            _build.build_runtime()
+            _build.build_runtime()          # under an inter-process lock; objects renamed into place
+        elif _build.stale_sources("runtime"):
+            import warnings
+            warnings.warn(f"{p} is older than its C++ sources; rebuild with `python -m pytorch_distributed_nn_amd._build`")
         l = ctypes.CDLL(str(p))
         for n, (res, args) in _SIGS.items():
             f = getattr(l, n)

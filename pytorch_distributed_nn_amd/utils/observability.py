@@ -116,7 +116,8 @@ def save_checkpoint(path, model, optimizer=None, epoch=0, step=0, arch="", best_
 
 
 def load_checkpoint(path, model, optimizer=None, map_location="cpu", restore_rng=True):
-    ck = torch.load(path, map_location=map_location, weights_only=True)
+    """``path``: a checkpoint file (loaded with weights_only=True) or an already loaded checkpoint dict."""
+    ck = path if isinstance(path, dict) else torch.load(path, map_location=map_location, weights_only=True)
     m = model.module if hasattr(model, "module") else model
     m.load_state_dict(ck["state_dict"])
     fp = getattr(m, "_pdnn_flat", None)

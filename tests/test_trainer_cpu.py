@@ -1,0 +1,58 @@
+"""Trainer resume semantics (epoch-end checkpoints must resume at the NEXT epoch, mid-epoch
+checkpoints after the steps already run) on CPU."""
+import torch
+
+from pytorch_distributed_nn_amd.trainer import Trainer
+
+
+class _Loader:
+    def __init__(self, n=3, bs=4):
+        self.n, self.bs = n, bs
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        g = torch.Generator().manual_seed(0)
+        while True:
+            yield torch.randn(self.bs, 8, generator=g), torch.randint(0, 4, (self.bs,), generator=g)
+
+
+def _trainer(ckdir, **kw):
+    torch.manual_seed(0)
+    m = torch.nn.Linear(8, 4)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    return Trainer(m, opt, loss_fn=torch.nn.functional.cross_entropy, checkpoint_dir=str(ckdir), log_interval=100,
+                   printer=lambda *a: None, **kw)
+
+
+def test_epoch_end_resume_runs_only_remaining_epochs(tmp_path):
+    t = _trainer(tmp_path)
+    t.train(_Loader(), epochs=2)
+    assert t.step_no == 6
+    t2 = _trainer(tmp_path)
+    ck = t2.resume(str(tmp_path / "checkpoint_ep1.pt"))
+    assert ck["epoch"] == 2 and t2.step_no == 6
+    t2.train(_Loader(), epochs=3)
+    assert t2.step_no == 9                      # exactly one more epoch, not a repeat of epoch 1
+    assert [r["epoch"] for r in t2.history] == [2, 2, 2]
+
+
+def test_mid_epoch_resume_continues_inside_the_epoch(tmp_path):
+    t = _trainer(tmp_path, checkpoint_interval=2)
+    t.train(_Loader(), epochs=5, max_steps=5)
+    t2 = _trainer(tmp_path)
+    ck = t2.resume("auto")
+    assert ck["step"] == 4 and ck["epoch"] == 1   # newest: checkpoint_step4 (epoch 1 in progress)
+    t2.train(_Loader(), epochs=2)
+    assert t2.step_no == 6                       # steps 5 and 6 complete epoch 1
+    assert [r["epoch"] for r in t2.history] == [1, 1]
+
+
+def test_resume_restores_weights(tmp_path):
+    t = _trainer(tmp_path)
+    t.train(_Loader(), epochs=1)
+    w = t.model.weight.detach().clone()
+    t2 = _trainer(tmp_path)
+    t2.resume("auto")
+    assert torch.equal(t2.model.weight, w)
