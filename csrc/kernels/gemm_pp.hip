@@ -264,42 +264,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
         s = 0;
         int m0, n0, z;
         item(cur++, m0, n0, z);
-        // Epilogue inputs are loaded ahead of the stores that precede their use: bias once per item, the
-        // streamed input (dGELU pre-activation or residual) one fragment row ahead.  A load consumed after a
-        // store makes hipcc wait for that store too (stores count in vmcnt), which serialised the rows on
-        // store latency while every CU writes its tile at once (C192 GELU / dGELU items: +55 us measured).
-        constexpr bool PF = EM == E_BF16 && C::FN <= 6;
-        constexpr int PFN = PF ? C::FN : 1;
-        float4 bv[PFN];
-        u16x4_t xnx[PFN];
-        const bf16_t* const ein = a.ep_dgelu ? a.ep_dgelu : a.ep_res;
-        const bool pf_in = PF && ein && !(a.ep_dgelu && a.ep_res);
-        if constexpr (PF) {
-#pragma unroll
-            for (int fn = 0; fn < PFN; ++fn) {
-                const int n = n0 + bcol + fn * 16 + 4 * lg;
-                bv[fn] = (a.bias && n + 4 <= a.N) ? *reinterpret_cast<const float4*>(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-                const int m = m0 + arow + lm;
-                xnx[fn] = u16x4_t{0, 0, 0, 0};
-                if (pf_in && m < a.M && n + 4 <= a.N) xnx[fn] = *reinterpret_cast<const u16x4_t*>(ein + (long)m * a.ldc + n);
-            }
-        }
         static_for<0, C::FM>([&](auto FMC) {
             constexpr int fm = decltype(FMC)::value;
             const int m = m0 + arow + fm * 16 + lm;
             const bool mv = m < a.M;
             if constexpr (EM == E_BF16) {
                 uint32_t pk[C::FN][2];
-                u16x4_t xin[PFN];
-                if constexpr (PF) {
-#pragma unroll
-                    for (int fn = 0; fn < PFN; ++fn) {
-                        xin[fn] = xnx[fn];
-                        const int n = n0 + bcol + fn * 16 + 4 * lg, m1 = m + 16;
-                        if (fm + 1 < C::FM && pf_in && m1 < a.M && n + 4 <= a.N)
-                            xnx[fn] = *reinterpret_cast<const u16x4_t*>(ein + (long)m1 * a.ldc + n);
-                    }
-                }
 #pragma unroll
                 for (int fn = 0; fn < C::FN; ++fn) {
                     const int n = n0 + bcol + fn * 16 + 4 * lg;
@@ -308,9 +278,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     float v[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
-                    if constexpr (PF) {
-                        v[0] += bv[fn].x; v[1] += bv[fn].y; v[2] += bv[fn].z; v[3] += bv[fn].w;
-                    } else if (a.bias && n + 4 <= a.N) {
+                    if (a.bias && n + 4 <= a.N) {
                         const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
                         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
                     }
@@ -325,26 +293,15 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
                     }
-                    if (pf_in) {
-                        const u16x4_t x = xin[PF ? fn : 0];
-                        if (a.ep_dgelu) {
+                    if (a.ep_dgelu && ok) {
+                        const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(x[j]));
-                        } else {
+                        for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
+                    }
+                    if (a.ep_res && ok) {
+                        const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] += bf2f(x[j]);
-                        }
-                    } else {
-                        if (a.ep_dgelu && ok) {
-                            const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
-                        }
-                        if (a.ep_res && ok) {
-                            const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
-                        }
+                        for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
                     }
                     pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
                     pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);

@@ -155,7 +155,11 @@ def main(argv=None):
 
     net = model
     if mode == "ddp" and world > 1:
-        net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, straggler_mode=args.straggler_mode)
+        # --straggler-mode: k-of-n kill (--num-aggregate k) or backup workers (--n-to-collect k) and/or a step
+        # deadline (--interval-ms) in collective form (parallel/ddp.py)
+        kofn = (args.n_to_collect or args.num_aggregate) if args.straggler_mode else 0
+        net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, straggler_mode=args.straggler_mode,
+                                      num_aggregate=kofn, deadline_ms=args.interval_ms if args.straggler_mode else 0.0)
     else:
         flatten_module(model)
     params = model.parameters()

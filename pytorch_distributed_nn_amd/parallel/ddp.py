@@ -22,10 +22,21 @@ What it does, and how it differs from the reference's design:
   spread one collective across many channels/links, small buckets are latency bound (~10-30 us per
   collective).  Defaults: 1 MiB first bucket, 32 MiB afterwards (ResNet-50's 102 MB of fp32 gradients =
   4-5 collectives) — sweep with ``tools/bench_allreduce.py``.
-* **Straggler tolerance** (PAR-DP-KILL / PAR-DP-BACKUP in all-reduce form): a rank
-  marked not-alive contributes zeros; the alive count is all-reduced alongside the buckets and the
-  optimizer divides by it (device scalar, no host sync) — the count-correct average of the C++ master
-  (sync_replicas_master_nn.h:125), fixing the reference's divide-by-(N-1) defect D3.
+* **k-of-n straggler kill / backup workers in collective form** (PAR-DP-KILL / PAR-DP-BACKUP, SURVEY.md
+  §5.3; reference: pytorch_code/sync_replicas_master_nn.py:172-186 kill on the k-th arrival,
+  pytorch_code/model_ops/lenet.py:168-178 worker poll, MPI_code/src/distributed/worker_nn.h:59-84
+  short-circuit).  ``num_aggregate=k``: every rank reports "backward done" to the control-plane store
+  (an atomic counter per step); the k-th reporter closes the step (``deadline_ms``: rank 0 also closes it
+  when the deadline passes — the backup-worker / interval form).  A watcher thread per rank blocks on
+  the close key and raises a host flag; the gradient hooks poll that flag (a Python attribute, no RPC)
+  and a rank that is still computing abandons the rest of its backward (``StepAborted`` stops autograd,
+  so no further kernels are enqueued; on GPU the host is kept at most two buckets ahead of the device so
+  the decision reflects real GPU progress).  Collectives must stay matched, so the aborted rank still
+  all-reduces every remaining bucket, zero-filled.  Each rank records per bucket whether it sent real
+  gradients; that contribution vector is all-reduced after the buckets and every bucket is divided by
+  ITS count — the count-correct average of the C++ master (sync_replicas_master_nn.h:125) per bucket,
+  like the reference's per-parameter counters (sync_replicas_master_nn.py:30-79), fixing defect D3.
+  ``straggler_mode`` alone keeps the manual form (``set_alive``).
 * Optional **bf16 gradient compression** on the wire (``comm_dtype=torch.bfloat16``).
 """
 from __future__ import annotations
@@ -41,6 +52,105 @@ import torch.nn as nn
 from ..optim.flat import flatten_module, register_grad_ready_hook
 
 
+class StepAborted(RuntimeError):
+    """Raised inside a rank's backward to abandon the rest of the step (k-of-n kill / short-circuit)."""
+
+
+class _KofN:
+    """Control plane of the k-of-n step close: two TCPStore clients on the rendezvous store (MASTER_ADDR /
+    MASTER_PORT) — one for the main thread's reports, one blocked in `wait` by the watcher thread."""
+
+    _instances = 0            # same construction order on every rank -> same key namespace
+
+    def __init__(self, ddp, k: int, deadline_ms: float):
+        import threading
+        from datetime import timedelta
+        self.ddp, self.k, self.deadline_ms = ddp, k, deadline_ms
+        host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500"))
+        _KofN._instances += 1
+        self.prefix = f"pdnn_kofn/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/{_KofN._instances}"
+        mk = lambda: dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=3600))  # noqa: E731
+        self.store, self.wstore = mk(), mk()
+        dist.barrier(group=ddp.pg)                # every rank's clients exist before the first step
+        self.abort_step = -1                      # written by the watcher, read by the gradient hooks
+        self.done_step = 0
+        self.watch_step = 1
+        self._stop = False
+        self._cv = threading.Condition()
+        self._begun = 0
+        self.thread = threading.Thread(target=self._watch, daemon=True)
+        self.thread.start()
+        if deadline_ms and ddp.rank == 0:         # rank 0 closes a step when its deadline passes
+            self.timer = threading.Thread(target=self._deadline, daemon=True)
+            self.timer.start()
+
+    def key(self, step, what):
+        return f"{self.prefix}/{step}/{what}"
+
+    def begin(self, step):
+        with self._cv:
+            self._begun = step
+            self._t_begin = time.monotonic()
+            self._cv.notify_all()
+
+    def report_done(self, step):
+        self.done_step = step
+        n = self.store.add(self.key(step, "done"), 1)
+        if n == self.k:
+            self.store.set(self.key(step, "closed"), "k")
+
+    def _watch(self):
+        # blocks server-side on each step's close key in turn (every step is closed: by the k-th finisher,
+        # by the deadline, or by stop()) -- no polling traffic
+        step = 1
+        while not self._stop:
+            try:
+                self.wstore.wait([self.key(step, "closed")])
+            except Exception:
+                if self._stop:
+                    return
+                continue
+            if self.done_step < step:             # still computing this step: abandon the rest of it
+                self.abort_step = step
+            step += 1
+            self.watch_step = step
+
+    def _deadline(self):
+        step = 1
+        while not self._stop:
+            with self._cv:
+                while self._begun < step and not self._stop:
+                    self._cv.wait(1.0)
+                t0 = self._t_begin
+            rest = self.deadline_ms / 1e3 - (time.monotonic() - t0)
+            if rest > 0:
+                time.sleep(rest)
+            try:
+                if not self.store.check([self.key(step, "closed")]):
+                    self.store.set(self.key(step, "closed"), "deadline")
+            except Exception:
+                return
+            step += 1
+
+    def cleanup(self, step):
+        if self.ddp.rank == 0 and step > 2:
+            for w in ("done", "closed"):
+                try:
+                    self.store.delete_key(self.key(step - 2, w))
+                except Exception:
+                    pass
+
+    def stop(self):
+        self._stop = True
+        try:                                      # wake the watcher blocked on the step it is waiting for
+            self.store.set(self.key(self.watch_step, "closed"), "stop")
+        except Exception:
+            pass
+        with self._cv:
+            self._cv.notify_all()
+
+
 def _is_nccl(pg):
     try:
         return dist.get_backend(pg) == "nccl"
@@ -51,7 +161,8 @@ def _is_nccl(pg):
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_cap_mb: float = 1.0, broadcast_buffers: bool = False, comm_dtype=None,
-                 average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None):
+                 average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
+                 num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -61,8 +172,10 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.comm_dtype = comm_dtype
         self.average = average
-        self.straggler_mode = straggler_mode
+        self.kofn = None
+        self.straggler_mode = straggler_mode or num_aggregate > 0 or deadline_ms > 0
         self.tracer = tracer
+        self.throttle = throttle
         self.nccl = _is_nccl(process_group)
         # communicate even at world size 1 (PDNN_DDP_FORCE_COMM=1 with a 1-rank process group): exercises the
         # bucket hooks and RCCL launches on a single GPU exactly as at world size 8
@@ -74,8 +187,14 @@ class DistributedDataParallel(nn.Module):
         self._broadcast_init()
         self._build_buckets(bucket_cap_mb, first_bucket_cap_mb)
         self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
+        self.step = 0
+        self.last_counts = None          # per-bucket contributor counts of the last step (k-of-n)
+        self.aborted_steps = 0
         self._reset()
         self.step_comm_log = []
+        if self._comm and (num_aggregate > 0 or deadline_ms > 0):
+            k = num_aggregate if num_aggregate > 0 else self.world
+            self.kofn = _KofN(self, min(k, self.world), deadline_ms)
 
     # ------------------------------------------------------------------ init broadcast (C-13)
     @torch.no_grad()
@@ -138,38 +257,53 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         self._works = []
         self._armed = False
+        self._aborted = False
+        self._contrib = [0.0] * len(self.buckets)
+        self._events = []
+
+    def _arm(self):
+        self._armed = True
+        self.step += 1
+        self._t0 = time.perf_counter()
+        torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+        if self.kofn is not None:
+            self.kofn.begin(self.step)
 
     def _on_grad(self, p):
-        if not self._sync or not self._comm:
+        if not self._sync or not self._comm or self._aborted:
             return
         if not self._armed:
-            self._armed = True
-            self._t0 = time.perf_counter()
-            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-            if self.straggler_mode:
-                self._launch_alive()
+            self._arm()
+        if self.kofn is not None and self.kofn.abort_step == self.step:
+            self._aborted = True                 # closed by the k-th finisher / deadline: short-circuit
+            raise StepAborted(f"rank {self.rank} step {self.step}")
         b = self._pbucket[id(p)]
         self._ready[b] += 1
         while self._next < len(self.buckets) and self._ready[self._next] == self.buckets[self._next][2]:
             self._launch(self._next)
             self._next += 1
+        if self.kofn is not None and self._next == len(self.buckets):
+            self.kofn.report_done(self.step)     # this rank's full gradient is in flight
 
     def _op(self):
         if self.straggler_mode or not self.average:
             return dist.ReduceOp.SUM
         return dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
 
-    def _launch_alive(self):
-        dev = self.flat.grad.device
-        self._alive_t = torch.full((1,), 1.0 if self.alive else 0.0, device=dev)
-        self._works.append((-1, dist.all_reduce(self._alive_t, op=dist.ReduceOp.SUM, group=self.pg,
-                                                async_op=True)))
-
-    def _launch(self, b):
+    def _launch(self, b, zero=False):
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
-        if self.straggler_mode and not self.alive:
+        if self.straggler_mode and (zero or not self.alive):
             view.zero_()                       # zero contribution: collective stays matched
+        else:
+            self._contrib[b] = 1.0
+        if self.kofn is not None and self.throttle and view.is_cuda:
+            # keep the host at most two buckets ahead of the GPU, so an abort stops real GPU work
+            if len(self._events) >= 2:
+                self._events[-2].synchronize()
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events.append(ev)
         t = view
         if self.comm_dtype is not None:
             t = self._wire[b]
@@ -187,26 +321,55 @@ class DistributedDataParallel(nn.Module):
         self._works.append((b, dist.all_reduce(t, op=op, group=self.pg, async_op=True)))
 
     def _finish(self):
-        while self._next < len(self.buckets):      # buckets holding unused parameters
-            self._launch(self._next)
+        if not self._armed:
+            return
+        while self._next < len(self.buckets):      # unused parameters, or everything after an abort
+            self._launch(self._next, zero=self._aborted)
             self._next += 1
+        fp = self.flat
+        if self.straggler_mode:
+            # per-bucket contributor counts: all-reduced after the buckets (same collective order everywhere)
+            cnt = torch.tensor(self._contrib, dtype=torch.float32, device=fp.grad.device)
+            self._works.append((-1, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
         for b, w in self._works:
             w.wait()
-        fp = self.flat
         if self.comm_dtype is not None:
             for b, (s, e, _) in enumerate(self.buckets):
                 fp.grad[s:e].copy_(self._wire[b])
         elif self.average and not self.straggler_mode and not self.nccl:
             fp.grad.mul_(1.0 / self.world)
         if self.straggler_mode:
-            # 1 / max(alive, 1) as a device scalar, consumed by the fused optimizer without a host sync
-            self.grad_scale_dev = torch.reciprocal(self._alive_t.clamp_min(1.0))
+            # every bucket divided by ITS count (device tensors: no host sync on GPU)
+            inv = torch.reciprocal(cnt.clamp_min(1.0))
+            for b, (s, e, _) in enumerate(self.buckets):
+                fp.grad[s:e].mul_(inv[b])
+            self.last_counts = cnt
+            self.grad_scale_dev = None
             for opt in getattr(self, "_optimizers", []):
-                opt.grad_scale_dev = self.grad_scale_dev
+                opt.grad_scale_dev = None
+        if self.kofn is not None:
+            self.kofn.cleanup(self.step)
+        self.last_contrib = list(self._contrib)
+        self.aborted_steps += int(self._aborted)
         self.step_comm_log.append(time.perf_counter() - self._t0)
         self._reset()
 
     # ------------------------------------------------------------------ public API
+    def backward(self, loss):
+        """``loss.backward()`` that tolerates a k-of-n abort: the rest of the backward is skipped, the
+        remaining buckets are all-reduced zero-filled and the step completes with count-correct buckets.
+        Returns True when this rank was short-circuited."""
+        try:
+            loss.backward()
+            return False
+        except StepAborted:
+            self._finish()
+            return True
+
+    def close(self):
+        if self.kofn is not None:
+            self.kofn.stop()
+
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self._comm and self.module.training:
             self._broadcast_buffers()

@@ -81,7 +81,10 @@ class Trainer:
         self._sync()
         t1 = time.perf_counter()
         with self._span("backward+allreduce"):
-            loss.backward()
+            if getattr(self.model, "kofn", None) is not None:
+                self.model.backward(loss)        # k-of-n DDP: a killed rank skips the rest of its backward
+            else:
+                loss.backward()
         self._sync()
         t2 = time.perf_counter()
         if self.grad_clip:

@@ -102,3 +102,41 @@ def test_ddp_rccl_single_rank_rehearsal():
     assert ncomm == 3 and nb >= 2
     assert max(rels) < 1e-5, rels           # AVG over one rank passes gradients through
     assert min(moved) > 0, moved
+
+
+def _rccl_kofn_job(rank, world):
+    """The k-of-n collective control plane on RCCL at world 1 (PDNN_FORCE_PG): store reports, watcher
+    thread, host throttle against CUDA events, zero-fill path and the per-bucket count all-reduce."""
+    import torch.distributed as dist
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim.flat import flatten_module
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    assert dist.get_backend() == "nccl"
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = build_model("resnet18", 10).to(dev)
+    ref = copy.deepcopy(m)
+    fref = flatten_module(ref)
+    net = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5, num_aggregate=1)
+    x, y = torch.randn(8, 3, 32, 32, device=dev), torch.randint(0, 10, (8,), device=dev)
+    out = []
+    for _ in range(2):
+        fref.data.copy_(net.flat.data)
+        fref.refresh_shadow()
+        fref.zero_grad()
+        OF.cross_entropy(ref(x), y).backward()
+        net.zero_grad()
+        aborted = net.backward(OF.cross_entropy(net(x), y))
+        torch.cuda.synchronize()
+        rel = ((net.flat.grad - fref.grad).norm() / fref.grad.norm()).item()
+        out.append((aborted, rel, net.last_counts.cpu().tolist()))
+    net.close()
+    return out
+
+
+def test_ddp_rccl_kofn_single_rank():
+    res = run_world(_rccl_kofn_job, 1, (), timeout=600, device=None, backend="nccl",
+                    env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
+    for aborted, rel, counts in res:
+        assert not aborted and rel < 1e-5 and all(c == 1.0 for c in counts), res
