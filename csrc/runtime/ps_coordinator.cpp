@@ -83,6 +83,8 @@ RT_API int pdnn_ps_offer(void* h, int worker, int layer, int64_t step, double t_
     return static_cast<PS*>(h)->offer(worker, layer, step, t_ms);
 }
 RT_API int pdnn_ps_done(void* h) { return static_cast<PS*>(h)->done() ? 1 : 0; }
+// close the step from outside the count rule (interval / deadline): later offers return 3 (closed)
+RT_API void pdnn_ps_close(void* h) { static_cast<PS*>(h)->closed = true; }
 RT_API int pdnn_ps_count(void* h, int layer) {
     auto* p = static_cast<PS*>(h);
     return (layer >= 0 && layer < p->n_layers) ? p->count[layer] : -1;

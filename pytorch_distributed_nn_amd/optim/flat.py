@@ -107,6 +107,32 @@ class FlatParams:
         return start, end
 
 
+def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float):
+    """Gradient buckets over the flat arena in REVERSE parameter order (the order backward produces
+    them), a small first bucket so communication starts early.  -> ([(start, end, n_params)], {id(p): b})."""
+    n = len(fp.params)
+    ends = fp.offsets[1:] + [fp.numel]
+    groups, cur, cur_bytes = [], [], 0
+    cap = first_mb * 2 ** 20
+    for i in reversed(range(n)):
+        nb = (ends[i] - fp.offsets[i]) * 4
+        if cur and cur_bytes + nb > cap:          # close the bucket before it would overflow
+            groups.append(cur)
+            cur, cur_bytes = [], 0
+            cap = cap_mb * 2 ** 20
+        cur.append(i)
+        cur_bytes += nb
+    if cur:
+        groups.append(cur)
+    buckets, pbucket = [], {}
+    for bi, idxs in enumerate(groups):
+        lo, hi = min(idxs), max(idxs)
+        buckets.append((fp.offsets[lo], ends[hi], len(idxs)))
+        for i in idxs:
+            pbucket[id(fp.params[i])] = bi
+    return buckets, pbucket
+
+
 def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatParams:
     """Move ``module``'s trainable parameters into a :class:`FlatParams` arena (idempotent)."""
     fp = getattr(module, "_pdnn_flat", None)

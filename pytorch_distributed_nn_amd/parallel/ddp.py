@@ -49,7 +49,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..optim.flat import flatten_module, register_grad_ready_hook
+from ..optim.flat import flatten_module, register_grad_ready_hook, reverse_buckets
 
 
 class StepAborted(RuntimeError):
@@ -223,30 +223,9 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self, cap_mb, first_mb):
-        fp = self.flat
-        n = len(fp.params)
-        ends = fp.offsets[1:] + [fp.numel]
-        buckets, cur, cur_bytes = [], [], 0
-        cap = first_mb * 2 ** 20
-        for i in reversed(range(n)):
-            nb = (ends[i] - fp.offsets[i]) * 4
-            if cur and cur_bytes + nb > cap:          # close the bucket before it would overflow
-                buckets.append(cur)
-                cur, cur_bytes = [], 0
-                cap = cap_mb * 2 ** 20
-            cur.append(i)
-            cur_bytes += nb
-        if cur:
-            buckets.append(cur)
-        self.buckets = []
-        self._pbucket = {}
-        for bi, idxs in enumerate(buckets):
-            lo, hi = min(idxs), max(idxs)
-            self.buckets.append((fp.offsets[lo], ends[hi], len(idxs)))
-            for i in idxs:
-                self._pbucket[id(fp.params[i])] = bi
+        self.buckets, self._pbucket = reverse_buckets(self.flat, cap_mb, first_mb)
         if self.comm_dtype is not None:
-            self._wire = [torch.empty(e - s, dtype=self.comm_dtype, device=fp.grad.device) for s, e, _ in self.buckets]
+            self._wire = [torch.empty(e - s, dtype=self.comm_dtype, device=self.flat.grad.device) for s, e, _ in self.buckets]
 
     def bucket_sizes_mb(self):
         return [(e - s) * 4 / 2 ** 20 for s, e, _ in self.buckets]

@@ -7,39 +7,54 @@ Reference behaviour reproduced (defec
 * weight push every step: ``comm_type="Bcast"`` — ONE broadcast of the flat fp32 weight arena from the
   master (reference: one MPI Bcast per parameter, sync_replicas_master_nn.py:259-272);
   ``comm_type="Async"`` — point-to-point sends of the flat arena to each worker (reference Isend per
-  parameter per worker, :243-257).  Over RCCL both are single collectives / grouped p2p per step.
-* gradient gather: every worker sends its flat gradient to the master point-to-point; the master
-  processes arrivals in completion order through the C++ :class:`PSCoordinator` (full sync, k-of-n
-  kill on the k-th arrival, or backup workers n_to_collect < n), accumulates only fresh gradients and
-  averages by the REAL count (fixes D3), then applies SGD with momentum honoured (fixes D9).
-* kill / short-circuit: the master publishes ``kill/<step>`` and the new ``step`` in the control-plane
-  store (replaces MPI tags 77 / 10 / 0); workers poll the store between layers of their backward (a
-  post-accumulate-grad hook) and abort the rest of the backward by raising :class:`StepAborted`
-  (reference busy-polls Iprobe(0, 77), lenet.py:168-178; short-circuit worker_nn.h:59-64,79-84).  An
-  aborted worker still sends its (stale-tagged) gradient message so every p2p op stays matched; the
-  master drops it as stale (CPP-03 stale-by-tag, sync_replicas_master_nn.h:85).
-* straggler injection: ``inject_straggler={rank: delay_ms}`` sleeps per layer on those ranks
+  parameter per worker, :243-257).
+* **gradient streaming per bucket**: the worker's gradient arena is cut into reverse-order buckets (the
+  order backward produces them, as the DDP wrapper does); a post-accumulate-grad hook sends each bucket
+  to the master the moment its last parameter is ready (reference: every parameter is Isent as soon as
+  the layer-wise backward produced it, pytorch_code/model_ops/lenet.py:106-152, resnet_split.py:235-326,
+  MPI_code/src/distributed/worker_nn.h:97-107).  Each send is announced as one entry
+  ``rank,step,bucket`` in a global arrival queue in the control-plane store; the master consumes the
+  queue in order with BLOCKING reads (no polling) — the store-side equivalent of the reference master's
+  ``Irecv(ANY_SOURCE)`` + ``Waitany`` loop (sync_replicas_master_nn.py:150-206), and it works unchanged on
+  gloo and on RCCL (whose p2p has no any-source receive).
+* the master feeds every arrival to the C++ :class:`PSCoordinator` (per-bucket counts; full sync, k-of-n
+  kill on the k-th arrival of the sentinel = the last bucket, i.e. parameter 0 as in the reference, or
+  backup workers n_to_collect < n), accumulates only fresh gradients of the current step, divides every
+  bucket by ITS count (fixes D3) and applies the update with the fused SGD kernel (optim.hip; momentum and
+  weight decay honoured, fixes D9).  Once the step is closed, the buckets still in flight are received
+  and DROPPED (CPP-03 drops gradients tagged with an old step, sync_replicas_master_nn.h:85): every
+  worker ends its step with an end marker in the queue and the master drains up to the markers before
+  the next weight push, so every p2p send is matched (a collective weight push must not wait on a send
+  the master has not received).
+* kill / short-circuit: when the master closes a step it publishes ``kill/<step>`` (the late workers,
+  possibly none) in the store; a watcher thread per worker blocks on that key and raises a host flag,
+  which the gradient hooks poll between buckets (an attribute read, no RPC).  A killed worker raises
+  :class:`StepAborted` from the hook: autograd stops, so no further kernels are enqueued, and on GPU the
+  host is kept at most two buckets ahead of the device so the flag reflects real GPU progress
+  (reference busy-polls Iprobe(0, 77), lenet.py:168-178; short-circuit worker_nn.h:59-64,79-84).
+* straggler injection: ``inject_straggler={rank: delay_ms}`` sleeps per parameter on those ranks
   (pure_py_code/distributed_worker.py:131-132's ``sleep(0.5)`` on ranks 1-3).
-* interval mode (TF TimeoutReplicasOptimizer, sync_replicas_optimizer_modified.py:208-215): the master
-  closes a step after ``interval_ms`` with whatever gradients arrived.
+* interval mode (TF TimeoutReplicasOptimizer, sync_replicas_optimizer_modified.py:208-215): the timer
+  runs from the moment the step is OPENED (the reference fires ``_update_op`` on a wall-clock timer
+  regardless of arrivals); when it expires the step closes with what arrived, provided every bucket has
+  at least one gradient (the reference's ``take_grad(1)`` blocks for one).  Arrivals after the close are
+  dropped (the coordinator is closed too).
 * evaluator: receives the weights (Bcast: joins the broadcast; Async: its own p2p copy) every
   ``eval_interval`` steps and appends ``step time_ms loss err`` to ``time_loss_out_<scheme>``.
-
-Message tags: step numbers are carried in a small header tensor sent before each gradient payload,
-so no tag arithmetic can collide (fixes D1: weight tag 11+p reaching the kill tag 77).
 """
 from __future__ import annotations
 
 import json
 import os
+import threading
 import time
 from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
 
-from ..optim.flat import flatten_module, register_grad_ready_hook
-from ..utils.native import PSCoordinator, Store, StoreServer
+from ..optim.flat import flatten_module, register_grad_ready_hook, reverse_buckets
+from ..utils.native import PSCoordinator, Store, StoreServer, StoreTimeout
 
 
 class StepAborted(RuntimeError):
@@ -52,16 +67,18 @@ class PSConfig:
     num_aggregate: int = 0            # k of k-of-n kill (0 = off)
     n_to_collect: int = 0             # backup-worker mode (0 = all workers)
     shortcircuit: bool = True
-    interval_ms: float = 0.0          # >0: timeout-driven step close (TF interval method)
+    interval_ms: float = 0.0          # >0: timer-driven step close (TF interval method)
     evaluator: bool = False           # rank 1 evaluates instead of training
     eval_interval: int = 10
-    inject_straggler: dict = field(default_factory=dict)   # {rank: delay_ms per layer}
+    inject_straggler: dict = field(default_factory=dict)   # {rank: delay_ms per parameter}
     lr: float = 0.01
     momentum: float = 0.0
     weight_decay: float = 0.0
     max_steps: int = 100
     out_dir: str = "outfiles"
     store_port: int = 0               # 0 = MASTER_PORT + 1
+    bucket_cap_mb: float = 4.0        # gradient streaming granularity
+    first_bucket_mb: float = 0.25
 
 
 def _store_port(cfg: PSConfig) -> int:
@@ -76,6 +93,8 @@ class _Base:
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         self.flat = flatten_module(model)
+        self.buckets, self.pbucket = reverse_buckets(self.flat, cfg.bucket_cap_mb, cfg.first_bucket_mb)
+        self.nb = len(self.buckets)
         self.first_worker = 2 if cfg.evaluator else 1
         self.workers = list(range(self.first_worker, self.world))
         self.n_workers = len(self.workers)
@@ -85,8 +104,8 @@ class _Base:
         if self.rank == 0:
             self._server = StoreServer(_store_port(cfg))
         dist.barrier()
-        self.store = Store(os.environ.get("MASTER_ADDR", "127.0.0.1"), _store_port(cfg))
-        self.header = torch.zeros(2, dtype=torch.int64, device=device)   # [step, status]
+        self.host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        self.store = Store(self.host, _store_port(cfg))
 
     def _push_weights(self, step: int):
         """Master -> everyone: the flat fp32 weight arena."""
@@ -110,101 +129,167 @@ class _Base:
 
 
 class PSMaster(_Base):
-    """Rank 0: pushes weights, gathers gradients (k-of-n / backup / full sync / interval), updates."""
+    """Rank 0: pushes weights, consumes the per-bucket arrival queue (k-of-n / backup / full sync /
+    interval), averages each bucket by its count, applies the fused SGD update."""
 
     def __init__(self, model, cfg, device):
         super().__init__(model, cfg, device)
-        self.coord = PSCoordinator(self.n_workers, 1, cfg.n_to_collect, cfg.num_aggregate)
-        self.momentum_buf = torch.zeros_like(self.flat.data) if cfg.momentum else None
-        self.recv_bufs = {w: torch.zeros_like(self.flat.grad) for w in self.workers}
-        self.recv_hdr = {w: torch.zeros(2, dtype=torch.int64, device=device) for w in self.workers}
+        from ..optim import SGD
+        # coordinator layers = buckets in reverse, so layer 0 is the LAST bucket (parameter 0: the sentinel)
+        self.coord = PSCoordinator(self.n_workers, self.nb, cfg.n_to_collect, cfg.num_aggregate)
+        self.opt = SGD(self.flat.params, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay)
+        big = max(e - s for s, e, _ in self.buckets)
+        self.stage = torch.zeros(big, dtype=torch.float32, device=self.flat.grad.device)
+        self.qpos = 0                          # next arrival-queue entry to read
         self.log = []
         self.store.set("scheme", self.scheme)
+
+    def _next_arrival(self, timeout_ms):
+        """(worker rank, step, bucket) of the next queued send, or None on timeout."""
+        try:
+            v = self.store.get(f"q/{self.qpos + 1}", timeout_ms=timeout_ms)
+        except StoreTimeout:
+            return None
+        self.qpos += 1
+        self.store.delete(f"q/{self.qpos}")
+        r, s, b = (int(t) for t in v.decode().split(","))
+        return r, s, b
+
+    def _receive(self, r, b):
+        s, e, _ = self.buckets[b]
+        buf = self.stage[: e - s]
+        dist.recv(buf, r)
+        return buf
 
     def train(self):
         cfg = self.cfg
         t0 = time.perf_counter()
-        timeline = []
         for step in range(1, cfg.max_steps + 1):
             self.store.set_int(f"go/{step}", step)              # step broadcast (C-01 / C-08)
             self._push_weights(step)                            # C-02 / C-03
             self.coord.begin_step(step)
-            acc = torch.zeros_like(self.flat.grad)
+            self.flat.grad.zero_()
             tstep = time.perf_counter()
-            closed = False
-            arrived, reported = [], set()
-            # arrival order comes from the control plane (workers announce done/<step>/<rank> before
-            # sending); this works identically on gloo and RCCL, whose p2p completion cannot be polled
-            while len(reported) < self.n_workers:
-                for k in self.store.keys(f"done/{step}/"):
-                    w = int(k.rsplit("/", 1)[1])
-                    if w in reported:
-                        continue
-                    reported.add(w)
-                    ok = self.store.get_int(k)
-                    tms = (time.perf_counter() - t0) * 1e3
-                    if ok and self.coord.offer(self.workers.index(w), 0, step, tms) == PSCoordinator.ACCEPTED:
-                        arrived.append(w)
-                        timeline.append((tms, step, w))
-                if not closed and (self.coord.done() or (cfg.interval_ms and arrived and
-                                                         (time.perf_counter() - tstep) * 1e3 >= cfg.interval_ms)):
+            closed, stale, ended = False, 0, set()
+
+            def take(timeout):
+                nonlocal closed, stale
+                a = self._next_arrival(timeout)
+                if a is None:
+                    return
+                r, s, b = a
+                if b < 0:                                       # end-of-step marker of worker r
+                    ended.add(r) if s == step else None
+                    return
+                g = self._receive(r, b)
+                tms = (time.perf_counter() - t0) * 1e3
+                res = self.coord.offer(self.workers.index(r), self.nb - 1 - b, s, tms)
+                if res == PSCoordinator.ACCEPTED:
+                    bs, be, _ = self.buckets[b]
+                    self.flat.grad[bs:be].add_(g)
+                elif res == PSCoordinator.STALE:
+                    stale += 1
+                if self.coord.done():
                     closed = True
-                    late = [w for w in self.workers if w not in arrived]
-                    if late:                                     # kill signal (C-06, tag 77)
-                        self.store.set(f"kill/{step}", json.dumps(late))
-                if len(reported) < self.n_workers:
-                    time.sleep(5e-5)
-            for w in self.workers:                               # every worker sent exactly one message
-                dist.recv(self.recv_hdr[w], w)
-                dist.recv(self.recv_bufs[w], w)
-                if w in arrived:
-                    acc += self.recv_bufs[w]
-            # count-correct average + SGD(momentum, wd) (fixes D3, D9)
-            cnt = max(1, len(arrived))
-            g = acc / cnt
-            if cfg.weight_decay:
-                g = g + cfg.weight_decay * self.flat.data
-            if self.momentum_buf is not None:
-                self.momentum_buf.mul_(cfg.momentum).add_(g)
-                g = self.momentum_buf
-            self.flat.data.add_(g, alpha=-cfg.lr)
-            self.log.append({"step": step, "arrived": arrived, "count": cnt,
-                             "gather_ms": (time.perf_counter() - tstep) * 1e3})
+
+            while not closed and len(ended) < self.n_workers:
+                timeout = -1
+                if cfg.interval_ms:
+                    rest = cfg.interval_ms - (time.perf_counter() - tstep) * 1e3
+                    timeout = max(1, int(rest)) if rest > 0 else 1
+                take(timeout)
+                if (not closed and cfg.interval_ms and (time.perf_counter() - tstep) * 1e3 >= cfg.interval_ms
+                        and all(self.coord.count(li) >= 1 for li in range(self.nb))):
+                    closed = True
+            self.coord.close()                                  # later arrivals of this step are dropped
+            # workers that did not deliver every bucket are killed (C-06, tag 77); published always so
+            # every worker's watcher wakes for this step
+            late = [w for i, w in enumerate(self.workers)
+                    if not all(self.coord.contributed(li, i) for li in range(self.nb))]
+            self.store.set(f"kill/{step}", json.dumps(late))
+            while len(ended) < self.n_workers:                  # receive (and drop) the late buckets, so
+                take(-1)                                        # every p2p send of the step is matched
+            # count-correct per-bucket average (fixes D3) + fused SGD (momentum, wd: fixes D9)
+            counts = [self.coord.count(self.nb - 1 - b) for b in range(self.nb)]
+            for b, (bs, be, _) in enumerate(self.buckets):
+                if counts[b] > 1:
+                    self.flat.grad[bs:be].mul_(1.0 / counts[b])
+            self.opt.step()
+            arrived = [w for i, w in enumerate(self.workers)
+                       if all(self.coord.contributed(li, i) for li in range(self.nb))]
+            self.log.append({"step": step, "arrived": arrived, "count": min(counts), "bucket_counts": counts,
+                             "stale_dropped": stale, "gather_ms": (time.perf_counter() - tstep) * 1e3})
         self.store.set_int(f"go/{cfg.max_steps + 1}", -1)
         self._push_weights(cfg.max_steps + 1)       # final weights, so evaluator/workers end consistent
         os.makedirs(cfg.out_dir, exist_ok=True)
         with open(os.path.join(cfg.out_dir, f"timeline_out_{self.scheme}"), "w") as f:
-            for t, s, w in timeline:
-                f.write(f"{t:.3f} {s} {w}\n")
+            for t, s, w, li in self.coord.timeline():      # time_ms step worker bucket (arrival timeline)
+                f.write(f"{t:.3f} {s} {self.workers[w]} {self.nb - 1 - li}\n")
         return self.log
 
 
 class PSWorker(_Base):
-    """Worker: receive weights, compute a gradient on its next batch, stream it to the master; abort the
-    backward when killed or when a newer step was published (short-circuit)."""
+    """Worker: receive weights, compute a gradient on its next batch, stream it to the master bucket by
+    bucket; abort the backward when killed (short-circuit)."""
 
     def __init__(self, model, cfg, device, loss_fn):
         super().__init__(model, cfg, device)
         self.loss_fn = loss_fn
         self.delay = cfg.inject_straggler.get(self.rank, 0) / 1e3
         self.cur = 0
-        self._hooks = [register_grad_ready_hook(p, self._layer_done) for p in self.flat.params]
+        self.abort_step = -1
+        self.done_step = 0
+        self._hooks = [register_grad_ready_hook(p, self._param_done) for p in self.flat.params]
         self.aborted_steps = 0
+        self.sent = []                      # (step, bucket) in send order (tests / timeline)
+        self._stop = False
+        self.wstore = Store(self.host, _store_port(cfg))    # the watcher's own connection
+        self._watcher = threading.Thread(target=self._watch, daemon=True)
+        self._watcher.start()
 
-    def _should_abort(self):
-        # the master publishes kill/<step> with the late workers when it closes a step early (k-of-n,
-        # backup workers, interval); those workers abandon the rest of their backward (short-circuit)
-        if not (self.cfg.shortcircuit or self.cfg.num_aggregate):
-            return False
-        if self.store.check(f"kill/{self.cur}"):
-            return self.rank in json.loads(self.store.get(f"kill/{self.cur}"))
-        return False
+    def _watch(self):
+        # blocks on each step's kill key in turn (always published when the master closes the step)
+        step = 1
+        while not self._stop:
+            try:
+                v = self.wstore.get(f"kill/{step}", timeout_ms=500)
+            except StoreTimeout:
+                continue
+            except Exception:
+                return
+            if (self.cfg.shortcircuit or self.cfg.num_aggregate) and self.rank in json.loads(v.decode()) \
+                    and self.done_step < step:
+                self.abort_step = step
+            step += 1
 
-    def _layer_done(self, p):
+    def _param_done(self, p):
         if self.delay:
-            time.sleep(self.delay)                      # straggler injection, per layer
-        if self._should_abort():
+            time.sleep(self.delay)                      # straggler injection, per parameter
+        if self._aborted:
+            return
+        if self.abort_step == self.cur:                 # killed: skip the rest of the backward
+            self._aborted = True
             raise StepAborted(f"rank {self.rank} step {self.cur}")
+        b = self.pbucket[id(p)]
+        self._ready[b] += 1
+        while self._next < self.nb and self._ready[self._next] == self.buckets[self._next][2]:
+            self._send(self._next)
+            self._next += 1
+
+    def _send(self, b):
+        s, e, _ = self.buckets[b]
+        view = self.flat.grad[s:e]
+        if view.is_cuda:
+            # keep the host at most two buckets ahead of the GPU so a kill stops real GPU work
+            if len(self._events) >= 2:
+                self._events[-2].synchronize()
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events.append(ev)
+        n = self.store.add("q_n", 1)
+        self.store.set(f"q/{n}", f"{self.rank},{self.cur},{b}")
+        self._works.append(dist.isend(view, 0))
+        self.sent.append((self.cur, b))
 
     def train(self, batches):
         it = iter(batches)
@@ -216,19 +301,28 @@ class PSWorker(_Base):
             self.cur = s
             x, y = next(it)
             self.flat.zero_grad()
-            ok = 1
+            self._ready, self._next, self._works, self._events, self._aborted = [0] * self.nb, 0, [], [], False
             try:
                 loss = self.loss_fn(self.model(x.to(self.device)), y.to(self.device))
                 loss.backward()
+                self.done_step = s
             except StepAborted:
-                ok = 0
                 self.aborted_steps += 1
-                self.flat.grad.zero_()
-            self.header[0], self.header[1] = s, ok
-            self.store.set_int(f"done/{s}/{self.rank}", ok)      # arrival notice (master's Waitany)
-            dist.send(self.header, 0)
-            dist.send(self.flat.grad, 0)
+            # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped)
+            n = self.store.add("q_n", 1)
+            self.store.set(f"q/{n}", f"{self.rank},{s},-1")
+            for w in self._works:
+                w.wait()
+        self._stop = True
         return self.aborted_steps
+
+    def close(self):
+        self._stop = True
+        super().close()
+        # the watcher may be inside a blocking get on its connection: let it leave before freeing it
+        self._watcher.join(timeout=5.0)
+        if not self._watcher.is_alive():
+            self.wstore.close()
 
 
 class PSEvaluator(_Base):

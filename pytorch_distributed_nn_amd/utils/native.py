@@ -41,6 +41,7 @@ _SIGS = {
     "pdnn_ps_begin_step": (None, [_P, _L]),
     "pdnn_ps_offer": (_I, [_P, _I, _I, _L, _D]),
     "pdnn_ps_done": (_I, [_P]),
+    "pdnn_ps_close": (None, [_P]),
     "pdnn_ps_count": (_I, [_P, _I]),
     "pdnn_ps_stragglers": (_I, [_P, _I, _P]),
     "pdnn_ps_contributed": (_I, [_P, _I, _I]),
@@ -198,6 +199,10 @@ class PSCoordinator:
 
     def done(self) -> bool:
         return bool(lib().pdnn_ps_done(self.h))
+
+    def close(self):
+        """Close the step regardless of counts (interval / deadline): later offers are rejected."""
+        lib().pdnn_ps_close(self.h)
 
     def count(self, layer: int) -> int:
         return lib().pdnn_ps_count(self.h, layer)

@@ -110,3 +110,53 @@ def test_ps_interval_mode_closes_steps_on_timer():
     master_log = res[0][0]
     assert all(1 <= r["count"] <= 2 for r in master_log)
     assert sum(r["count"] == 1 for r in master_log) >= 4            # the timer closed most steps early
+
+
+def _ps_stream_job(rank, world, cfg_kw, out_dir, steps):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    model = build_model("mlp_cpp", 10)
+    x, y = _data()
+    cfg = PSConfig(lr=0.05, max_steps=steps, out_dir=out_dir, bucket_cap_mb=0.5, first_bucket_mb=0.05, **cfg_kw)
+
+    def batches():
+        i = 0
+        while True:
+            sl = slice((i * 32) % 512, (i * 32) % 512 + 32)
+            yield x[sl], y[sl]
+            i += 1
+
+    res = run_ps(model, cfg, torch.device("cpu"), loss_fn=OF.cross_entropy, batches=batches())
+    return res
+
+
+def test_ps_streams_gradients_per_bucket():
+    """Gradients reach the master bucket by bucket as backward produces them (reverse parameter order),
+    visible as several arrivals per worker per step in the arrival timeline."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_stream_job, 3, ({"comm_type": "Async"}, out, 4))
+    log = res[0]
+    nb = len(log[0]["bucket_counts"])
+    assert nb >= 3 and all(r["bucket_counts"] == [2] * nb for r in log)
+    tl = [line.split() for line in open(os.path.join(out, [f for f in os.listdir(out)
+                                                           if f.startswith("timeline_out_")][0]))]
+    per = {}
+    for t, step, w, b in tl:
+        per.setdefault((int(step), int(w)), []).append((float(t), int(b)))
+    for key, arr in per.items():
+        assert [b for _, b in arr] == list(range(nb)), (key, arr)     # bucket 0 (last layers) first
+
+
+def test_ps_interval_without_shortcircuit_drops_late_worker():
+    """with shortcircuit off and k-of-n off, a worker slower than the interval keeps computing,
+    but its gradients arrive after the step closed and must NOT be averaged in."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_stream_job, 4, ({"interval_ms": 60.0, "shortcircuit": False,
+                                         "inject_straggler": {3: 15}}, out, 4))
+    log = res[0]
+    for r in log[1:]:
+        assert 3 not in r["arrived"], r                  # the straggler never delivers a full gradient
+        assert min(r["bucket_counts"]) < 3, r            # its late buckets (the first layers) were dropped
+    assert res[3] == 0                                   # and it was never aborted (short-circuit off)
