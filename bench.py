@@ -30,6 +30,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 STOCK_PYTORCH_1GPU = 6629.4   # profiles/stock_pytorch_resnet50.jsonl: torch autocast-bf16 channels_last, bs256
 
 
+def native_loaded():
+    """In-tree native libraries mapped into this process (proves the HIP kernels, not a fallback, ran)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({os.path.basename(ln.split()[-1]) for ln in f if "libpdnn" in ln})
+    except OSError:
+        return []
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,6 +149,7 @@ def main():
             "dtype": "fp8(e4m3) fwd GEMMs + bf16" if a.fp8 else "bf16",
             "data": "synthetic (device-resident random token ids), random-init weights",
             "final_loss": round(float(loss.detach()), 4),
+            "native_loaded": native_loaded(),
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
@@ -164,6 +174,7 @@ def main():
             "data": f"synthetic (device-resident random {in_chw[1]}x{in_chw[2]}x{in_chw[0]} images, random labels), "
                     "random-init weights",
             "final_loss": round(float(loss.detach()), 4),
+            "native_loaded": native_loaded(),
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",

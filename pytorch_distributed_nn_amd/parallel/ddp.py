@@ -160,16 +160,26 @@ def _is_nccl(pg):
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
-                 first_bucket_cap_mb: float = 1.0, broadcast_buffers: bool = False, comm_dtype=None,
+                 first_bucket_cap_mb: float = 1.0, broadcast_buffers: bool = True, comm_dtype=None,
                  average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
-                 num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True):
+                 num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True,
+                 buffer_sync_interval: int = 1, comm_timing: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.flat = flatten_module(module)
+        # rank 0's module buffers (BN running statistics) are broadcast every `buffer_sync_interval`
+        # training forwards (reference: every forward, data_parallel_dist.py:133-138), so the ranks' BN
+        # statistics never drift apart; one collective per dtype over a persistent flat buffer
         self.broadcast_buffers = broadcast_buffers
+        self.buffer_sync_interval = max(1, int(buffer_sync_interval))
+        self._fwd_count = 0
+        self._buf_flat = {}
+        # device-side per-bucket all-reduce latency (HIP events, read lazily: no host sync in the step)
+        self.comm_timing = comm_timing
+        self._ev_log = []
         self.comm_dtype = comm_dtype
         self.average = average
         self.kofn = None
@@ -213,13 +223,22 @@ class DistributedDataParallel(nn.Module):
         for b in self._buffers_list:
             by_dtype.setdefault(b.dtype, []).append(b)
         for dt, bufs in by_dtype.items():
-            flat = torch.cat([b.reshape(-1) for b in bufs])
-            dist.broadcast(flat, 0, group=self.pg)
+            n_all = sum(b.numel() for b in bufs)
+            flat = self._buf_flat.get(dt)
+            if flat is None or flat.numel() != n_all or flat.device != bufs[0].device:
+                flat = self._buf_flat[dt] = torch.empty(n_all, dtype=dt, device=bufs[0].device)
             o = 0
-            for b in bufs:
-                n = b.numel()
-                b.copy_(flat[o:o + n].view_as(b))
-                o += n
+            if self.rank == 0:
+                for b in bufs:
+                    flat[o:o + b.numel()].copy_(b.reshape(-1))
+                    o += b.numel()
+            dist.broadcast(flat, 0, group=self.pg)
+            if self.rank != 0:
+                o = 0
+                for b in bufs:
+                    n = b.numel()
+                    b.copy_(flat[o:o + n].view_as(b))
+                    o += n
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self, cap_mb, first_mb):
@@ -239,6 +258,8 @@ class DistributedDataParallel(nn.Module):
         self._aborted = False
         self._contrib = [0.0] * len(self.buckets)
         self._events = []
+        self.launch_order = []
+        self._ev_start, self._ev_done = {}, {}
 
     def _arm(self):
         self._armed = True
@@ -297,6 +318,11 @@ class DistributedDataParallel(nn.Module):
             op = self._op()
         if self.tracer is not None:
             self.tracer.instant(f"allreduce_bucket{b}", args={"mb": (e - s) * 4 / 2 ** 20})
+        self.launch_order.append(b)
+        if self.comm_timing and view.is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._ev_start[b] = ev
         self._works.append((b, dist.all_reduce(t, op=op, group=self.pg, async_op=True)))
 
     def _finish(self):
@@ -312,6 +338,13 @@ class DistributedDataParallel(nn.Module):
             self._works.append((-1, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
         for b, w in self._works:
             w.wait()
+            if self.comm_timing and b in self._ev_start:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()                          # the compute stream now waits on RCCL's stream
+                self._ev_done[b] = ev
+        if self.comm_timing and self._ev_start:
+            self._ev_log.append([(self._ev_start[b], self._ev_done[b]) for b in sorted(self._ev_start)
+                                 if b in self._ev_done])
         if self.comm_dtype is not None:
             for b, (s, e, _) in enumerate(self.buckets):
                 fp.grad[s:e].copy_(self._wire[b])
@@ -329,6 +362,7 @@ class DistributedDataParallel(nn.Module):
         if self.kofn is not None:
             self.kofn.cleanup(self.step)
         self.last_contrib = list(self._contrib)
+        self.last_launch_order = list(self.launch_order)
         self.aborted_steps += int(self._aborted)
         self.step_comm_log.append(time.perf_counter() - self._t0)
         self._reset()
@@ -351,8 +385,25 @@ class DistributedDataParallel(nn.Module):
 
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self._comm and self.module.training:
-            self._broadcast_buffers()
+            if self._fwd_count % self.buffer_sync_interval == 0:
+                self._broadcast_buffers()
+            self._fwd_count += 1
         return self.module(*args, **kwargs)
+
+    def sync_buffers(self):
+        """Broadcast rank 0's buffers now (e.g. before evaluation or a checkpoint: the last training forward
+        updated every rank's BN running statistics with its own batch)."""
+        self._broadcast_buffers()
+
+    def comm_times_ms(self):
+        """Per step, per bucket: device time from the bucket's launch to its all-reduce completing (HIP
+        events on the compute stream around RCCL's stream-ordered collective), for the steps logged since
+        the last call (``comm_timing=True``).  Synchronises on the recorded events."""
+        out = []
+        for evs in self._ev_log:
+            out.append([s.elapsed_time(e) for s, e in evs])
+        self._ev_log = []
+        return out
 
     @contextlib.contextmanager
     def no_sync(self):

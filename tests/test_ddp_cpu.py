@@ -233,3 +233,45 @@ def test_ddp_step_deadline_drops_late_rank():
         assert aborted and dt < 0.25, out[1]            # 16 x 20 ms = 0.32 s without the deadline
         assert min(counts) >= 1 and max(counts) <= 2
     assert not any(a for a, _, _ in out[0])
+
+
+def _world4_consistency(rank, world):
+    """Fused-backward DDP at world 4: after the all-reduce every rank holds BIT-identical gradients,
+    buckets launch in the same order everywhere, and BN running statistics stay identical (buffers are
+    broadcast from rank 0 every forward, data_parallel_dist.py:133-138)."""
+    import torch.distributed as dist
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(rank)
+    m = build_model("resnet18", 10)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_cap_mb=0.25)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9)
+    orders = []
+    for step in range(2):
+        g = torch.Generator().manual_seed(100 * step + rank)       # different data per rank
+        x, y = torch.randn(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)
+        opt.zero_grad()
+        OF.cross_entropy(ddp(x), y).backward()
+        grads = ddp.flat.grad.clone()
+        allg = [torch.empty_like(grads) for _ in range(world)]
+        dist.all_gather(allg, grads)
+        for r in range(world):
+            assert torch.equal(allg[r], allg[0]), (step, r)
+        orders.append(ddp.last_launch_order)
+        opt.step()
+    ddp.sync_buffers()
+    bufs = torch.cat([b.float().reshape(-1) for b in m.buffers()])
+    allb = [torch.empty_like(bufs) for _ in range(world)]
+    dist.all_gather(allb, bufs)
+    return orders, all(torch.equal(b, allb[0]) for b in allb), len(ddp.buckets)
+
+
+def test_world4_bit_identical_grads_and_launch_order():
+    out = run_world(_world4_consistency, 4, timeout=300)
+    orders0, same_bufs, nb = out[0]
+    assert nb >= 3 and same_bufs
+    for orders, _, _ in out:
+        assert orders == orders0
+        assert all(o == list(range(nb)) for o in orders)           # strictly in bucket order

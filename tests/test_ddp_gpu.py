@@ -140,3 +140,47 @@ def test_ddp_rccl_kofn_single_rank():
                     env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
     for aborted, rel, counts in res:
         assert not aborted and rel < 1e-5 and all(c == 1.0 for c in counts), res
+
+
+def _rccl_graph_job(rank, world):
+    """GraphedStep(allow_collectives=True) at world 1 over RCCL: the bucket all-reduces (and the buffer
+    broadcast) are captured into the step's hipGraph; replays match an eager DDP copy of the model."""
+    import torch.distributed as dist
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
+    assert dist.get_backend() == "nccl"
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    ma = build_model("resnet18", 10).to(dev)
+    mb = copy.deepcopy(ma)
+    na = DistributedDataParallel(ma, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
+    nb = DistributedDataParallel(mb, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
+    oa = SGD(ma.parameters(), lr=0.01, momentum=0.9)
+    ob = SGD(mb.parameters(), lr=0.01, momentum=0.9)
+    gstep = GraphedStep(nb, ob, loss_fn=OF.cross_entropy, warmup=2, allow_collectives=True)
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randn(16, 3, 32, 32, generator=g).to(dev), torch.randint(0, 10, (16,), generator=g).to(dev))
+            for _ in range(6)]
+    la, lb = [], []
+    for x, y in data:
+        oa.zero_grad()
+        loss = OF.cross_entropy(na(x), y)
+        loss.backward()
+        oa.step()
+        la.append(float(loss))
+        lb.append(float(gstep(x, y)))
+    torch.cuda.synchronize()
+    rel = ((na.flat.data - nb.flat.data).norm() / na.flat.data.norm()).item()
+    return la, lb, rel, gstep.replays
+
+
+def test_graphed_step_captures_rccl_collectives():
+    la, lb, rel, replays = run_world(_rccl_graph_job, 1, (), timeout=600, device=None, backend="nccl",
+                                     env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
+    assert replays >= 3
+    assert rel < 1e-3, rel
+    for a, b in zip(la, lb):
+        assert abs(a - b) / abs(a) < 2e-2, (la, lb)
