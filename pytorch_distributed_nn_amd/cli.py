@@ -43,6 +43,14 @@ def add_fit_args(p: argparse.ArgumentParser):
     p.add_argument("--max-steps", type=int, default=None)
     p.add_argument("--optimizer", type=str, default="sgd", choices=["sgd", "adam", "adamw"])
     p.add_argument("--weight-decay", type=float, default=0.0)
+    # exponential staircase decay (TF trainer, distributed_TF/src/distributed_train.py:143-147):
+    # lr = lr0 * factor ** floor(step / (steps_per_epoch * epochs_per_decay))
+    p.add_argument("--lr-decay-factor", type=float, default=1.0)
+    p.add_argument("--epochs-per-decay", type=float, default=0.0)
+    p.add_argument("--num-workers", type=int, default=0, help="data-loader worker processes (0: a thread)")
+    p.add_argument("--compute-times", action="store_true",
+                   help="every rank appends per-step compute-time records to OUT_DIR/compute_times_rank<r>.jsonl "
+                        "(TF timeout_manager.py:48-70 side channel; CDF/percentiles: tools/report.py cdf)")
     p.add_argument("--n-to-collect", type=int, default=0)
     p.add_argument("--interval-ms", type=float, default=0.0)
     p.add_argument("--no-shortcircuit", action="store_true")
@@ -126,7 +134,8 @@ def main(argv=None):
 
     if mode == "ps":
         from .parallel.ps import PSConfig, run_ps
-        cfg = PSConfig(comm_type=args.comm_type if args.comm_type != "AllReduce" else "Bcast",
+        cfg = PSConfig(compute_times=args.compute_times,
+                       comm_type=args.comm_type if args.comm_type != "AllReduce" else "Bcast",
                        num_aggregate=args.num_aggregate if args.n_to_collect == 0 else 0,
                        n_to_collect=args.n_to_collect, shortcircuit=not args.no_shortcircuit,
                        interval_ms=args.interval_ms, evaluator=args.evaluator, eval_interval=args.eval_interval,
@@ -177,7 +186,8 @@ def main(argv=None):
         for p in model.parameters():
             p.register_post_accumulate_grad_hook(lambda _p, d=strag[rank] / 1e3: _t.sleep(d))
 
-    loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world)
+    loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world, num_workers=args.num_workers,
+                        seed=args.seed)
 
     hang_at = None
     if args.inject_hang and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0":
@@ -205,9 +215,15 @@ def main(argv=None):
     if args.watchdog_timeout > 0:
         from .parallel.watchdog import CommWatchdog
         wd = CommWatchdog(args.watchdog_timeout, out_dir=args.out_dir, rank=rank).start()
+    lr_schedule = None
+    if args.lr_decay_factor != 1.0 and args.epochs_per_decay > 0:
+        decay_steps = max(1, int(len(loader) * args.epochs_per_decay))
+        lr_schedule = lambda step, lr0=args.lr, f=args.lr_decay_factor: lr0 * f ** (step // decay_steps)  # noqa: E731
     tr = Trainer(net, opt, OF.cross_entropy, dev, rank, world, args.log_interval, args.metrics,
                  args.trace, args.checkpoint_dir, arch=args.network, printer=print if rank == 0 else (lambda *a: None),
-                 graph=graph, checkpoint_interval=args.checkpoint_interval, watchdog=wd)
+                 graph=graph, checkpoint_interval=args.checkpoint_interval, watchdog=wd, lr_schedule=lr_schedule,
+                 compute_log=(os.path.join(args.out_dir, f"compute_times_rank{rank}.jsonl")
+                              if args.compute_times else None))
     if args.resume:
         ck = tr.resume(args.resume)
         if ck is not None and rank == 0:

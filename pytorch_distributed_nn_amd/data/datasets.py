@@ -165,15 +165,38 @@ class SyntheticTokens:
 
 
 # ------------------------------------------------------------------------------------------------ loader
+def _loader_worker(images, labels, transform, index_q, data_q, wid, seed):
+    """Worker process (PT-11 my_data_loader.py:37-53): (seq, indices) -> (seq, x, y), gathered and
+    transformed in this process; None ends it."""
+    np.random.seed(seed + wid)
+    while True:
+        job = index_q.get()
+        if job is None:
+            break
+        seq, idx = job
+        x, y = images[idx], labels[idx]
+        if transform is not None:
+            x = transform(x)
+        data_q.put((seq, np.ascontiguousarray(x), np.ascontiguousarray(y)))
+
+
 class DataLoader:
-    """Batches from a :class:`DataSet`, sharded by rank, prefetched by a background thread into pinned
-    memory and copied to the device asynchronously on a side stream.
+    """Batches from a :class:`DataSet`, sharded by rank, prefetched into pinned memory and copied to the
+    device asynchronously on a side stream.
 
     ``rank``/``world`` shard the sample stream (each rank draws every world-th batch), so DDP ranks see
-    disjoint data like torch's DistributedSampler."""
+    disjoint data like torch's DistributedSampler.
+
+    ``num_workers = 0``: one background thread draws batches (epoch-wrapping ``next_batch``).
+    ``num_workers > 0`` (PT-11, pytorch_code/data_loader_ops/my_data_loader.py:37-53, 137-251): the main
+    process keeps the sampler (a per-epoch permutation, seeded, sharded by rank) and feeds ``(seq, indices)``
+    jobs round-robin to worker PROCESSES through per-worker index queues; the workers gather and transform
+    the samples (the CPU-heavy part: augmentation) and return ``(seq, x, y)`` on one data queue; batches are
+    reassembled in sequence order (out-of-order arrivals wait in a reorder buffer, :185-211) before
+    pinning."""
 
     def __init__(self, dataset: DataSet, batch_size: int, device="cpu", prefetch: int = 4, rank: int = 0,
-                 world: int = 1, transform=None, drop_last: bool = True):
+                 world: int = 1, transform=None, drop_last: bool = True, num_workers: int = 0, seed: int = 0):
         self.ds, self.bs = dataset, batch_size
         self.device = torch.device(device)
         self.rank, self.world = rank, world
@@ -181,10 +204,64 @@ class DataLoader:
         self.q: queue.Queue = queue.Queue(maxsize=prefetch)
         self._stop = False
         self._pin = self.device.type == "cuda"
-        self._thread = threading.Thread(target=self._worker, daemon=True)
+        self.num_workers = num_workers
+        self._procs = []
+        if num_workers > 0:
+            import multiprocessing as mp
+            ctx = mp.get_context("spawn")          # workers never touch the GPU; spawn is fork-safe with HIP
+            self._index_qs = [ctx.Queue() for _ in range(num_workers)]
+            self._data_q = ctx.Queue(maxsize=max(2, prefetch) * num_workers)
+            for w in range(num_workers):
+                p = ctx.Process(target=_loader_worker, args=(dataset.images, dataset.labels, transform,
+                                                             self._index_qs[w], self._data_q, w, seed), daemon=True)
+                p.start()
+                self._procs.append(p)
+            self._sampler_rng = np.random.RandomState(seed)
+            self._perm, self._pos = self._sampler_rng.permutation(len(dataset)), 0
+            self._send_seq, self._recv_seq, self._reorder = 0, 0, {}
+            for _ in range(max(2, prefetch) * num_workers):      # keep every worker busy
+                self._dispatch()
+        self._thread = threading.Thread(target=self._worker if num_workers == 0 else self._collector, daemon=True)
         self._thread.start()
         self._stream = torch.cuda.Stream(self.device) if self._pin else None
 
+    # -------------------------------------------------------------- multiprocess path
+    def _next_indices(self):
+        """The next batch of this rank: batches are dealt round-robin over ranks from one permutation per
+        epoch (a partial batch at the epoch end wraps into the next permutation)."""
+        out = []
+        need = self.bs * self.world
+        while len(out) < need:
+            take = min(need - len(out), len(self._perm) - self._pos)
+            out.extend(self._perm[self._pos:self._pos + take].tolist())
+            self._pos += take
+            if self._pos == len(self._perm):
+                self._perm, self._pos = self._sampler_rng.permutation(len(self.ds)), 0
+        return np.asarray(out[self.rank * self.bs:(self.rank + 1) * self.bs])
+
+    def _dispatch(self):
+        self._index_qs[self._send_seq % self.num_workers].put((self._send_seq, self._next_indices()))
+        self._send_seq += 1
+
+    def _collector(self):
+        while not self._stop:
+            while self._recv_seq not in self._reorder:
+                try:
+                    seq, x, y = self._data_q.get(timeout=1.0)
+                except queue.Empty:
+                    if self._stop:
+                        return
+                    continue
+                self._reorder[seq] = (x, y)
+            x, y = self._reorder.pop(self._recv_seq)
+            self._recv_seq += 1
+            self._dispatch()
+            xt, yt = torch.from_numpy(x), torch.from_numpy(y)
+            if self._pin:
+                xt, yt = xt.pin_memory(), yt.pin_memory()
+            self.q.put((xt, yt))
+
+    # -------------------------------------------------------------- thread path
     def _worker(self):
         while not self._stop:
             for _ in range(self.rank):
@@ -219,6 +296,12 @@ class DataLoader:
 
     def close(self):
         self._stop = True
+        for q in getattr(self, "_index_qs", []):
+            q.put(None)
+        for p in self._procs:
+            p.join(timeout=5)
+            if p.is_alive():
+                p.kill()
 
 
 class MNISTDataset(torch.utils.data.Dataset):

@@ -79,6 +79,7 @@ class PSConfig:
     store_port: int = 0               # 0 = MASTER_PORT + 1
     bucket_cap_mb: float = 4.0        # gradient streaming granularity
     first_bucket_mb: float = 0.25
+    compute_times: bool = False       # workers write compute_times_rank<r>.jsonl (TF-04 side channel)
 
 
 def _store_port(cfg: PSConfig) -> int:
@@ -241,6 +242,7 @@ class PSWorker(_Base):
         self.done_step = 0
         self._hooks = [register_grad_ready_hook(p, self._param_done) for p in self.flat.params]
         self.aborted_steps = 0
+        self.compute_records = []
         self.sent = []                      # (step, bucket) in send order (tests / timeline)
         self._stop = False
         self.wstore = Store(self.host, _store_port(cfg))    # the watcher's own connection
@@ -299,6 +301,7 @@ class PSWorker(_Base):
             if s == -1:
                 break
             self.cur = s
+            t_deq = time.perf_counter()                       # step dequeued (TF-04 "worker_dequeued_token")
             x, y = next(it)
             self.flat.zero_grad()
             self._ready, self._next, self._works, self._events, self._aborted = [0] * self.nb, 0, [], [], False
@@ -308,12 +311,20 @@ class PSWorker(_Base):
                 self.done_step = s
             except StepAborted:
                 self.aborted_steps += 1
+            self.compute_records.append({"rank": self.rank, "step": s, "t_dequeue": t_deq,
+                                         "t_finish": time.perf_counter(), "aborted": self.done_step != s,
+                                         "compute_ms": 1e3 * (time.perf_counter() - t_deq)})
             # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped)
             n = self.store.add("q_n", 1)
             self.store.set(f"q/{n}", f"{self.rank},{s},-1")
             for w in self._works:
                 w.wait()
         self._stop = True
+        if self.cfg.compute_times:
+            os.makedirs(self.cfg.out_dir, exist_ok=True)
+            with open(os.path.join(self.cfg.out_dir, f"compute_times_rank{self.rank}.jsonl"), "w") as f:
+                for r in self.compute_records:
+                    f.write(json.dumps(r) + "\n")
         return self.aborted_steps
 
     def close(self):

@@ -24,7 +24,7 @@ class Trainer:
     def __init__(self, model, optimizer, loss_fn=None, device=None, rank=0, world=1, log_interval=10,
                  metrics_path=None, trace_path=None, checkpoint_dir=None, arch="", timing=True, printer=print,
                  lr_schedule=None, grad_clip=None, graph=False, graph_warmup=2, checkpoint_interval=0,
-                 watchdog=None):
+                 watchdog=None, compute_log=None):
         self.model = model
         self.opt = optimizer
         self.loss_fn = loss_fn or OF.cross_entropy
@@ -44,6 +44,9 @@ class Trainer:
         self.history = []
         self.checkpoint_interval = checkpoint_interval     # steps between rank-0 checkpoints (0: epoch ends)
         self.watchdog = watchdog                           # parallel.watchdog.CommWatchdog, fed every step
+        # per-step compute-time records (TF-04 timeout_manager.py:48-70: dequeue / finish times per worker
+        # and iteration), one JSONL per rank; tools/report.py cdf builds the CDF and p80/p90/p95/p99
+        self.compute_log = MetricsSink(compute_log) if compute_log else None
         # hipGraph-captured step (utils/graphs.py): one replay per iteration instead of ~1000 launches
         self.graph_step = None
         if graph and self.device.type == "cuda":
@@ -122,6 +125,8 @@ class Trainer:
                        "samples_per_s": bs * self.world / max(total, 1e-9)}
                 if self.step_no % self.log_interval == 0 or (max_steps and self.step_no >= max_steps):
                     lv = float(loss.detach())
+                    if lv != lv or lv in (float("inf"), float("-inf")):      # TF trainer's NaN assert
+                        raise FloatingPointError(f"Model diverged with loss = {lv} at step {self.step_no}")
                     p1 = float(accuracy(out.detach(), y, (1,))[0]) if out.dim() == 2 else float("nan")
                     rec["loss"], rec["prec1"] = lv, p1
                     seen = (i + 1) * bs
@@ -132,6 +137,9 @@ class Trainer:
                                f"Samples/s: {rec['samples_per_s']:.1f}, Prec@1: {p1:.2f}")
                 self.metrics.log(**rec)
                 self.history.append(rec)
+                if self.compute_log is not None:
+                    self.compute_log.log(rank=self.rank, step=self.step_no, t_dequeue=tf, t_finish=time.perf_counter(),
+                                         compute_ms=1e3 * (tfw + tbw + topt))
                 if self.watchdog is not None:
                     self.watchdog.beat(self.step_no)
                 if (self.checkpoint_dir and self.checkpoint_interval and self.rank == 0

@@ -70,6 +70,8 @@ class Tracer:
 class MetricsSink:
     def __init__(self, path: str | None):
         self.path = path
+        if path:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         self._f = open(path, "a") if path else None
 
     def log(self, **rec):

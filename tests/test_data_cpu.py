@@ -1,0 +1,82 @@
+"""Data pipeline on CPU: multiprocess loader workers with in-order reassembly (PT-11
+pytorch_code/data_loader_ops/my_data_loader.py:37-53, 185-211), rank sharding, augmentation helpers."""
+import numpy as np
+import pytest
+import torch
+
+from pytorch_distributed_nn_amd.data.datasets import DataLoader, DataSet
+
+
+def _slow_identity(x):
+    import random
+    import time
+    time.sleep(random.random() * 0.02)           # workers finish out of order
+    return x
+
+
+def _expected(n, bs, world, rank, seed, batches):
+    rng = np.random.RandomState(seed)
+    perm, pos, out = rng.permutation(n), 0, []
+    for _ in range(batches):
+        got = []
+        while len(got) < bs * world:
+            take = min(bs * world - len(got), n - pos)
+            got.extend(perm[pos:pos + take].tolist())
+            pos += take
+            if pos == n:
+                perm, pos = rng.permutation(n), 0
+        out.append(got[rank * bs:(rank + 1) * bs])
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_multiprocess_loader_in_order_and_sharded(world):
+    n, bs = 100, 8
+    imgs = np.arange(n, dtype=np.float32).reshape(n, 1)
+    ds = DataSet(imgs, np.arange(n, dtype=np.int64), shuffle=False)
+    seen = []
+    for rank in range(world):
+        dl = DataLoader(ds, bs, num_workers=3, rank=rank, world=world, transform=_slow_identity, seed=7)
+        got = [dl.next_batch()[1].tolist() for _ in range(20)]
+        dl.close()
+        assert got == _expected(n, bs, world, rank, 7, 20)          # sampler order despite out-of-order workers
+        seen.append(got)
+    if world == 2:                                                  # disjoint within an epoch
+        a = {i for b in seen[0][:6] for i in b}
+        b = {i for b in seen[1][:6] for i in b}
+        assert not a & b
+
+
+def _plus(x):
+    return x + 1000
+
+
+def test_multiprocess_loader_applies_transform_in_workers():
+    ds = DataSet(np.zeros((32, 3), np.float32), np.zeros(32, np.int64))
+    dl = DataLoader(ds, 4, num_workers=2, transform=_plus)
+    x, _ = dl.next_batch()
+    dl.close()
+    assert torch.all(x == 1000)
+
+
+def test_augmentation_helpers():
+    from pytorch_distributed_nn_amd.data import augment as A
+    rng = np.random.RandomState(0)
+    x = rng.rand(6, 3, 8, 8).astype(np.float32)
+    c = A.random_crop(x, (8, 8), padding=2, rng=rng)
+    assert c.shape == x.shape
+    cf = A.random_crop_and_flip(x, padding=0, rng=np.random.RandomState(1))      # no padding: flip only
+    assert all(np.array_equal(a, b) or np.array_equal(a, b[..., ::-1]) for a, b in zip(cf, x))
+    w = A.whiten(x)
+    assert np.allclose(w.reshape(6, -1).mean(1), 0, atol=1e-5) and np.allclose(w.reshape(6, -1).std(1), 1, atol=1e-3)
+    flat = rng.rand(5, 784).astype(np.float32)
+    assert A.random_crop(flat, (28, 28), padding=2, rng=rng).shape == (5, 784)
+    n = A.add_noise_wrt_distance(x, (8, 8), padding=2, rng=rng)
+    assert n.shape == x.shape
+    labels = np.array([0, 1, 2, 0, 1, 2])
+    lx, ly = A.line_among_labels(x, labels, num_per_label=2, fraction=0.1, rng=rng)
+    assert lx.shape == (6 * 2 * 2, 3, 8, 8) and set(ly.tolist()) == {0, 1, 2}
+    tx, ty, vx, vy = A.extract_binary(x, np.array([6, 8, 1, 6, 2, 8]), x, np.array([1, 1, 6, 8, 8, 3]))
+    assert len(tx) == 4 and set(ty.tolist()) == {6, 8} and len(vx) == 3
+    ax, ay = A.aug_data_set(x, labels, times_expand=3, aug_type="noise", rng=rng)
+    assert ax.shape[0] == 18 and len(ay) == 18

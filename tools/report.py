@@ -3,6 +3,7 @@
     python tools/report.py time-loss  outfiles/time_loss_out_*        # loss / error vs wall time and step
     python tools/report.py timeline   outfiles/timeline_out_*         # gradient arrivals per step
     python tools/report.py percentiles metrics.jsonl [--field backward_ms]   # p50/p80/p90/p95/p99
+    python tools/report.py cdf outfiles/compute_times_rank*.jsonl      # per-worker compute-time CDF
 
 File formats (written by parallel/ps.py and the native csrc/runtime/mlp_native.cpp roles):
   time_loss_out_<scheme>:  "step time_ms loss error_rate" per evaluation (MPI_code/src/python/plot_time_loss.py:10-34)
@@ -98,9 +99,38 @@ def percentiles(path, field):
                       **{f"p{q}": round(x, 4) for q, x in qs.items()}}))
 
 
+def compute_cdf(files, out):
+    """Per-worker compute-time CDF and pooled percentiles from compute_times_rank<r>.jsonl files (the TF
+    benchmark driver's "time-CDF" curves and p80/p90/p95/p99 prints, distributed_TF/tools/benchmark.py:60-111,
+    fed by the timeout manager's per-worker records, distributed_TF/src/timeout_manager.py:48-70)."""
+    per = collections.defaultdict(list)
+    for f in files:
+        for line in open(f):
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            if r.get("compute_ms") is not None:
+                per[int(r.get("rank", -1))].append(float(r["compute_ms"]))
+    if not per:
+        print("no compute_ms records")
+        return None
+    series = {}
+    for rank, v in sorted(per.items()):
+        v = np.sort(np.asarray(v))
+        series[f"rank {rank}"] = (v.tolist(), (np.arange(1, len(v) + 1) / len(v)).tolist())
+    pooled = np.concatenate([np.asarray(v) for v in per.values()])
+    summary = {"n": int(len(pooled)), "workers": len(per), "mean_ms": float(pooled.mean()),
+               **{f"p{q}": round(float(np.percentile(pooled, q)), 4) for q in (50, 80, 90, 95, 99)},
+               "slowest_worker": max(per, key=lambda r: float(np.mean(per[r])))}
+    print(json.dumps(summary))
+    _plot(series, "compute time (ms)", "CDF", f"{out}_compute_cdf.png")
+    return summary
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["time-loss", "timeline", "percentiles"])
+    ap.add_argument("kind", choices=["time-loss", "timeline", "percentiles", "cdf"])
     ap.add_argument("files", nargs="+")
     ap.add_argument("--field", default="backward_ms")
     ap.add_argument("--out", default="report")
@@ -109,6 +139,8 @@ def main(argv=None):
         time_loss(a.files, a.out)
     elif a.kind == "timeline":
         timeline(a.files)
+    elif a.kind == "cdf":
+        compute_cdf(a.files, a.out)
     else:
         for f in a.files:
             percentiles(f, a.field)
