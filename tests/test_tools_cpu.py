@@ -49,8 +49,9 @@ def test_report_percentiles(tmp_path):
 
 def test_cli_yaml_config_defaults(tmp_path):
     from pytorch_distributed_nn_amd.cli import parse_args
-    for f in os.listdir(os.path.join(ROOT, "configs")):
-        parse_args(["--config", os.path.join(ROOT, "configs", f)])      # every shipped config parses
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "configs", "**", "*.yaml"), recursive=True):
+        parse_args(["--config", f])                                     # every shipped config parses
     a = parse_args(["--config", os.path.join(ROOT, "configs", "ps_mlp_backup_workers.yaml"), "--lr", "0.5"])
     assert a.network == "mlp_cpp" and a.n_to_collect == 2 and a.evaluator and a.lr == 0.5
 
