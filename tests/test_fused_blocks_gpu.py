@@ -1,11 +1,13 @@
 """Each fused ResNet block (one autograd node = a hand-scheduled HIP kernel sequence) against the CPU
-fp32 reference forward/backward of the same nn.Module: output, input gradient, every parameter gradient
-and the BN running statistics.  Shapes keep >= 256 elements per BN channel so batch statistics are
-well conditioned and the comparison measures kernel numerics, not bf16 noise amplified by tiny batches."""
+fp32 reference forward/backward of the same nn.Module that rounds to bf16 at the same points as the
+kernels (tests/bf16_mirror.py): output, input gradient, every parameter gradient (<= 5% relative L2,
+cosine >= 0.998) and the BN running statistics.  Shapes keep >= 256 elements per BN channel."""
 import copy
 
 import pytest
 import torch
+
+from bf16_mirror import mirror, round_bf16
 
 pytestmark = pytest.mark.gpu
 
@@ -21,22 +23,22 @@ def cos(a, b):
     return torch.nn.functional.cosine_similarity(a.float().cpu().flatten(), b.float().cpu().flatten(), dim=0).item()
 
 
-def _check_block(block, x_nchw, tol_out=2e-2, tol_grad=1.5e-1):
-    ref = block
+def _check_block(block, x_nchw, tol_out=2e-2, tol_grad=5e-2):
+    ref = mirror(block)
     gpu = copy.deepcopy(block).cuda()
-    xr = x_nchw.clone().requires_grad_(True)
+    xr = round_bf16(x_nchw).detach().requires_grad_(True)
     yr = ref(xr)
-    g = torch.randn_like(yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
     yr.backward(g)
     xg = x_nchw.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16).requires_grad_(True)
     yg = gpu.forward_nhwc(xg)
     yg.backward(g.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16))
     assert rel(yg, yr.permute(0, 2, 3, 1)) < tol_out
     assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < tol_grad
-    assert cos(xg.grad, xr.grad.permute(0, 2, 3, 1)) > 0.99
+    assert cos(xg.grad, xr.grad.permute(0, 2, 3, 1)) > 0.998
     for (n, pr), (_, pg) in zip(ref.named_parameters(), gpu.named_parameters()):
         assert rel(pg.grad, pr.grad) < tol_grad, (n, rel(pg.grad, pr.grad))
-        assert cos(pg.grad, pr.grad) > 0.99, (n, cos(pg.grad, pr.grad))
+        assert cos(pg.grad, pr.grad) > 0.998, (n, cos(pg.grad, pr.grad))
     for (n, br), (_, bg) in zip(ref.named_buffers(), gpu.named_buffers()):
         if br.dtype.is_floating_point:
             assert rel(bg, br) < 2e-2, n
@@ -47,7 +49,7 @@ def test_bottleneck(inp, planes, stride):
     from pytorch_distributed_nn_amd.models.resnet import Bottleneck
     torch.manual_seed(0)
     blk = Bottleneck(inp, planes, stride, "downsample")
-    _check_block(blk, torch.randn(4, inp, 16, 16))
+    _check_block(blk, torch.randn(8, inp, 16, 16))
 
 
 @pytest.mark.parametrize("inp,planes,stride", [(64, 64, 1), (64, 128, 2)])
@@ -55,7 +57,7 @@ def test_basic_block(inp, planes, stride):
     from pytorch_distributed_nn_amd.models.resnet import BasicBlock
     torch.manual_seed(0)
     blk = BasicBlock(inp, planes, stride, "shortcut")
-    _check_block(blk, torch.randn(4, inp, 16, 16))
+    _check_block(blk, torch.randn(8, inp, 16, 16))
 
 
 @pytest.mark.parametrize("imagenet", [True, False])

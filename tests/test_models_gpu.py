@@ -5,6 +5,8 @@ import copy
 import pytest
 import torch
 
+from bf16_mirror import cos, mirror, round_bf16
+
 pytestmark = pytest.mark.gpu
 
 
@@ -117,3 +119,58 @@ def test_direct_grad_accumulation_matches_autograd_path(arch):
     g1 = fp.grad.clone()
     run(m).backward()                      # accumulates
     assert torch.allclose(fp.grad, 2 * g1, rtol=1e-3, atol=1e-6 * g1.abs().max().item())
+
+
+@pytest.mark.parametrize("name,shape,nc", [
+    ("ResNet18", (32, 3, 32, 32), 10),
+    ("ResNet50", (32, 3, 32, 32), 10),
+    ("resnet50", (32, 3, 64, 64), 1000),
+])
+def test_every_block_in_situ_against_mirrored_reference(name, shape, nc):
+    """End-to-end at batch 32: the whole network runs fused on the GPU; every residual block is then
+    replayed on the bf16-mirrored fp32 CPU reference with the block's OWN recorded input and output
+    gradient from that run, and its parameter gradients and input gradient must match (<= 5% relative L2,
+    cosine >= 0.998).  End-to-end gradient comparisons of a random-init deep ResNet are meaningless beyond
+    the head: the fp32 reference itself moves its gradients by 13-18% (ResNet-18) and >100% (ResNet-50)
+    under a 1e-3 relative input perturbation, so bf16 noise is amplified chaotically.  Replaying each block
+    in situ checks every BN-backward / residual / dgrad term at its real position and shape in the net."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    torch.manual_seed(0)
+    base = build_model(name, nc)
+    gpu = copy.deepcopy(base).cuda()
+    rec = []
+    for blk in gpu._blocks():
+        f = blk.forward_nhwc
+
+        def wrapped(x, f=f, blk=blk):
+            y = f(x)
+            e = {"x": x.detach().clone(), "blk": blk}
+            y.register_hook(lambda g, e=e: e.__setitem__("g", g.detach().clone()))
+            rec.append(e)
+            return y
+        blk.forward_nhwc = wrapped
+    x = torch.randn(*shape)
+    y = torch.randint(0, nc, (shape[0],))
+    loss = OF.cross_entropy(gpu(x.cuda()), y.cuda())
+    loss.backward()
+    ref_blocks = list(base._blocks())
+    assert len(rec) == len(ref_blocks)
+    worst = 0.0
+    for i, (e, rb) in enumerate(zip(rec, ref_blocks)):
+        ref = mirror(rb)
+        xr = e["x"].float().cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+        yr = ref(xr)
+        yr.backward(e["g"].float().cpu().permute(0, 3, 1, 2))
+        for (n, pr), (_, pg) in zip(ref.named_parameters(), e["blk"].named_parameters()):
+            r = rel(pg.grad, pr.grad)
+            worst = max(worst, r)
+            assert r < 5e-2 and cos(pg.grad, pr.grad) > 0.998, (name, i, n, r, cos(pg.grad, pr.grad))
+        if i > 0:                       # this block's input gradient is the previous block's output gradient
+            gin = rec[i - 1]["g"].float().cpu().permute(0, 3, 1, 2)
+            assert rel(gin, xr.grad) < 5e-2 and cos(gin, xr.grad) > 0.998, (name, i, rel(gin, xr.grad))
+    # the loss of the whole network against the mirrored reference (the logits of a 16-block random-init
+    # ResNet-50 move by ~20% under bf16 noise, the mean loss by < 1%)
+    from pytorch_distributed_nn_amd.ops import functional as OF2
+    lr_ = OF2.cross_entropy(mirror(base)(round_bf16(x)), y).item()
+    assert abs(loss.item() - lr_) / lr_ < 2e-2, (loss.item(), lr_)
