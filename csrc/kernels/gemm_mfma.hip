@@ -691,6 +691,26 @@ FastDiv make_fdiv(uint32_t d) {
     return f;
 }
 
+// smallest output width a 1x1 conv is sent to the ping-pong engine with (its tiles are 128 / 256 wide);
+// PDNN_PP_CONV_MINN for A/B runs
+// and the shortest reduction (PDNN_PP_CONV_FWD_K / PDNN_PP_CONV_DGRAD_K).  Measured per layer at bs256
+// (tools/bench_conv.py, tools/pp_one.py --kind fwd1x1|dgrad1x1bn): the plain / residual data gradient wins
+// on pp from K >= 256; the forward with BN statistics and the data gradient with the BN-backward epilogue
+// are slower there than on the 128-row kernel (the fused epilogue roughly doubles the pp epilogue time),
+// so by default those stay off pp (PDNN_PP_CONV_FWD_K, PDNN_PP_CONV_BNB=1 turn them on).
+int g_pp_conv_min_n = -1, g_pp_conv_fwd_k = -1, g_pp_conv_dgrad_k = -1, g_pp_conv_bnb = 0;
+int pp_conv_min_n() {
+    if (g_pp_conv_min_n < 0) {
+        g_pp_conv_min_n = env_int("PDNN_PP_CONV_MINN", 128);
+        g_pp_conv_fwd_k = env_int("PDNN_PP_CONV_FWD_K", 1 << 30);
+        g_pp_conv_dgrad_k = env_int("PDNN_PP_CONV_DGRAD_K", 256);
+        g_pp_conv_bnb = env_int("PDNN_PP_CONV_BNB", 0);
+    }
+    return g_pp_conv_min_n;
+}
+int pp_conv_fwd_k() { pp_conv_min_n(); return g_pp_conv_fwd_k; }
+int pp_conv_dgrad_k() { pp_conv_min_n(); return g_pp_conv_dgrad_k; }
+
 int g_stage_store = -1;
 int stage_store_mode() {
     if (g_stage_store < 0) { const char* e = getenv("PDNN_STAGED_STORE"); g_stage_store = e ? atoi(e) : 1; }
@@ -944,6 +964,13 @@ PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && Ko >= pp_conv_min_n() && C >= pp_conv_fwd_k()) {
+        // 1x1 stride-1 conv = plain GEMM  y[M][Ko] = x[M][C] . w[Ko][C]^T: the ping-pong engine (prologue and
+        // BN statistics fused there too)
+        GemmArgs p = a;
+        p.lda = C;
+        if (pp_supported(p, A_KMAJOR, B_KMAJOR, E_BF16, 1, 1)) return pp_launch(p, A_KMAJOR, B_KMAJOR, E_BF16, stream);
+    }
     if (pro_scale) return launch<A_CONV, B_KMAJOR, E_BF16, true, false>(a, 1, stream);
     return launch<A_CONV, B_KMAJOR, E_BF16, false, false>(a, 1, stream);
 }
@@ -992,6 +1019,16 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
                              const bf16_t* res, const bf16_t* bn_x, const float* bn_mean, const float* bn_invstd,
                              const float* bn_mscale, const float* bn_mshift, hipStream_t stream) {
     ensure_attrs();
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() && Ko >= pp_conv_dgrad_k() &&
+        (!bn_x || g_pp_conv_bnb)) {
+        // 1x1 stride-1: dx[M][C] = dy[M][Ko] . w[Ko][C] (w as a [k][n] matrix) on the ping-pong engine
+        GemmArgs a{};
+        a.M = Nimg * H * W; a.N = C; a.K = Ko;
+        a.A = dy; a.lda = Ko; a.B = w; a.ldb = C; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
+        a.ep_res = res;
+        a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+        if (pp_supported(a, A_KMAJOR, B_MNMAJOR, E_BF16, 1, 1)) return pp_launch(a, A_KMAJOR, B_MNMAJOR, E_BF16, stream);
+    }
     DgradClass cl[16];
     bool any_empty;
     const int ncl = dgrad_classes(H, W, R, S, st, pad, cl, &any_empty);

@@ -42,6 +42,13 @@ constexpr int PP_BM = 256;
 constexpr int PP_SK = 32;                 // K depth of one slice
 constexpr int PP_GROUP = 4;               // tile rows per L2 group
 
+// fusion flags (gemm_pp_kernel FX)
+constexpr int FX_PRO = 1;      // A := relu(A * pro_scale[k] + pro_shift[k])  (K-major A, no split-K, K <= PP_PRO_MAXK)
+// (FX_PRO keeps the scale/shift table in LDS behind the ring; FX_BNB keeps mscale/mshift there, N <= PP_PRO_MAXK)
+constexpr int FX_STATS = 2;    // per-column (sum, sum of squares) of the bf16 output, one slab row pair per 64 rows
+constexpr int FX_BNB = 4;      // output gm = v * [ep_x*mscale + mshift > 0]; slab gets sum gm, sum gm*xhat
+constexpr int PP_PRO_MAXK = 1024;
+
 template <int BN_, int WR_, int NB_>
 struct PPC {
     static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_;
@@ -129,17 +136,33 @@ __device__ __forceinline__ void pp_retire(int keep) {
 // current item finishes and stores its tile, so a tile boundary costs only the epilogue.
 // ABL (timing ablations, PDNN_PP_ABLATE with tools/pp_one.py; results are garbage): bit 0 = no MFMA,
 // bit 1 = no global->LDS copies in the loop, bit 2 = no LDS fragment reads (1..7)
-template <class C, int AM, int BMODE, int EM, int ABL = 0>
+// FX (fusions, FX_* bits): A-operand BN-affine+ReLU prologue, BN partial statistics of the output,
+// BN-backward masking + statistics (the conv/1x1 paths of the ResNet blocks).
+template <class C, int AM, int BMODE, int EM, int ABL = 0, int FX = 0>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
+    static_assert(!(FX & FX_PRO) || AK, "prologue: K-major A only");
     constexpr int NB = C::NB, D = NB - 1;
     using LA = PPLoader<PP_BM, AK>;
     using LB = PPLoader<C::BN, BKm>;
     constexpr int NIT = LA::NI + LB::NI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const sb = reinterpret_cast<bf16_t*>(smem);
+    float* const ptab = reinterpret_cast<float*>(smem + C::SMEM);     // FX_PRO: [scale | shift] per k
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if constexpr ((FX & FX_PRO) != 0) {
+        for (int i = tid; i < a.K; i += 512) {
+            ptab[i] = a.pro_scale[i];
+            ptab[PP_PRO_MAXK + i] = a.pro_shift[i];
+        }
+    }
+    if constexpr ((FX & FX_BNB) != 0) {     // the BN-output ReLU mask coefficients of every column
+        for (int i = tid; i < a.N; i += 512) {
+            ptab[i] = a.ep_mscale[i];
+            ptab[PP_PRO_MAXK + i] = a.ep_mshift[i];
+        }
+    }
     const int grp = wave >> 2, wr = (wave & 3) / C::WC, wc = (wave & 3) % C::WC;
     const int tiles_m = (a.M + PP_BM - 1) / PP_BM, tiles_n = (a.N + C::BN - 1) / C::BN;
     const int ntiles = tiles_m * tiles_n;
@@ -198,6 +221,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     for (int q = 0; q < D && q < Q; ++q) issue_next();
     pp_retire<NIT, D>(min(Q, D) - 1);
     if (dbg) dbg[1] = wall_clock64();
+    if constexpr ((FX & (FX_PRO | FX_BNB)) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // table written
     __builtin_amdgcn_s_barrier();
     if (grp == 1) __builtin_amdgcn_s_barrier();          // stagger: group 1 runs one barrier behind
 
@@ -208,167 +232,264 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     if (a.alpha_ptr) alpha *= *a.alpha_ptr;
 
     int s = 0, cur = 0, rd_off = 0;                      // slice within the current item, item index, read slot
-    for (int q = 0; q < Q; ++q) {
-        // ---------------- load segment ----------------
-        const bool more = q + D < Q;
-        if (more) pp_vmwait<(D - 2) * NIT>();            // stream slice q+1 landed (this wave's copies)
-        else pp_retire<NIT, D>(Q - q - 2);
-        const bf16_t* A_ = sb + rd_off;
-        const bf16_t* B_ = A_ + C::IMA;
-        rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
-        bf16x8_t af[C::FM], bfr[C::FN];
-        if constexpr ((ABL & 4) != 0) {
+    auto epilogue = [&]() {
+            // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
+            if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
+            s = 0;
+            int m0, n0, z;
+            item(cur++, m0, n0, z);
+            constexpr bool SUMS = (FX & (FX_STATS | FX_BNB)) != 0;
+            float s_[SUMS ? C::FN : 1][4], q_[SUMS ? C::FN : 1][4];   // per-column partial sums over 64 rows
+            if constexpr (SUMS) {
 #pragma unroll
-            for (int f = 0; f < C::FN; ++f) bfr[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)q, 1, 2, 3, 4, 5, 6, 7});
+                for (int fn = 0; fn < C::FN; ++fn)
 #pragma unroll
-            for (int f = 0; f < C::FM; ++f) af[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)f, 1, 2, 3, 4, 5, 6, 7});
-        } else {
+                    for (int j = 0; j < 4; ++j) s_[fn][j] = q_[fn][j] = 0.f;
+            }
+            static_for<0, C::FM>([&](auto FMC) {
+                constexpr int fm = decltype(FMC)::value;
+                // BN-backward epilogue: keep each fragment's loads inside its own iteration (hoisted loads of
+                // every fragment's t / coefficients pushed the 256-wide variant into scratch)
+                if constexpr ((FX & FX_BNB) != 0) __builtin_amdgcn_sched_barrier(0);
+                const int m = m0 + arow + fm * 16 + lm;
+                const bool mv = m < a.M;
+                if constexpr (EM == E_BF16) {
+                    uint32_t pk[C::FN][2];
 #pragma unroll
-        for (int f = 0; f < C::FN; ++f) {
-            if constexpr (BKm) bfr[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
-                                           B_ + (bcol + f * 16) * PP_SK + koffl));
-            else bfr[f] = frag_mnmajor<C::BN>(B_, bcol + f * 16, 0, lane);
-        }
+                    for (int fn = 0; fn < C::FN; ++fn) {
+                        const int n = n0 + bcol + fn * 16 + 4 * lg;
+                        const bool ok = mv && n + 4 <= a.N;
+                        const long off = (long)m * a.ldc + n;
+                        float v[4];
 #pragma unroll
-        for (int f = 0; f < C::FM; ++f) {
-            if constexpr (AK) af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
-                                          A_ + (arow + f * 16) * PP_SK + koffl));
-            else af[f] = frag_mnmajor<PP_BM>(A_, arow + f * 16, 0, lane);
-        }
-        }
-        if (!(ABL & 2) && more) issue_next();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        // ---------------- compute segment ----------------
-        __builtin_amdgcn_s_setprio(1);
-        if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-            for (int f = 0; f < C::FM; ++f) asm volatile("" ::"v"(af[f]));
-#pragma unroll
-            for (int f = 0; f < C::FN; ++f) asm volatile("" ::"v"(bfr[f]));
-        } else {
-#pragma unroll
-        for (int fm = 0; fm < C::FM; ++fm)
-#pragma unroll
-            for (int fn = 0; fn < C::FN; ++fn)
-                acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        if (++s < nsl) continue;
-
-        // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
-        if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
-        s = 0;
-        int m0, n0, z;
-        item(cur++, m0, n0, z);
-        static_for<0, C::FM>([&](auto FMC) {
-            constexpr int fm = decltype(FMC)::value;
-            const int m = m0 + arow + fm * 16 + lm;
-            const bool mv = m < a.M;
-            if constexpr (EM == E_BF16) {
-                uint32_t pk[C::FN][2];
-#pragma unroll
-                for (int fn = 0; fn < C::FN; ++fn) {
-                    const int n = n0 + bcol + fn * 16 + 4 * lg;
-                    const bool ok = mv && n + 4 <= a.N;
-                    const long off = (long)m * a.ldc + n;
-                    float v[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
-                    if (a.bias && n + 4 <= a.N) {
-                        const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
-                        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-                    }
-                    if (a.relu == 1) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-                    } else if (a.relu == 2) {
-                        u16x4_t pre;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
-                        if (a.ep_aux && ok) *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
-                    }
-                    if (a.ep_dgelu && ok) {
-                        const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
-                    }
-                    if (a.ep_res && ok) {
-                        const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
-                    }
-                    pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                    pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                }
-                bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc;
-#pragma unroll
-                for (int fp = 0; fp < C::FN / 2; ++fp) {   // 16-byte stores: permlane16 swap pairs fragments
-                    const auto s0_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
-                    const auto s1_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][1], pk[2 * fp + 1][1], false, false);
-                    const int n = n0 + bcol + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
-                    if (mv && n + 8 <= a.N) {
-                        *reinterpret_cast<uint4*>(Crow + n) = make_uint4(s0_[0], s1_[0], s0_[1], s1_[1]);
-                    } else if (mv && n < a.N) {
-                        const uint32_t w4[4] = {s0_[0], s1_[0], s0_[1], s1_[1]};
-                        for (int j = 0; j < 8 && n + j < a.N; ++j) Crow[n + j] = (bf16_t)(w4[j >> 1] >> (16 * (j & 1)));
-                    }
-                }
-                if constexpr (C::FN % 2) {                 // odd fragment count: 8-byte stores for the last one
-                    const int n = n0 + bcol + (C::FN - 1) * 16 + 4 * lg;
-                    if (mv && n + 4 <= a.N)
-                        *reinterpret_cast<uint2*>(Crow + n) = make_uint2(pk[C::FN - 1][0], pk[C::FN - 1][1]);
-                }
-            } else {
-                // fp32: K-split items write partial slabs at C + z * sC1 (pp_slab_reduce_kernel sums them),
-                // otherwise store / accumulate (acc_c) into C
-                const bool slab = splits > 1;
-                float* const Cb = reinterpret_cast<float*>(a.C) + (slab ? z * a.sC1 : 0);
-#pragma unroll
-                for (int fn = 0; fn < C::FN; ++fn) {
-                    const int n = n0 + bcol + fn * 16 + 4 * lg;
-                    if (!mv || n >= a.N) continue;
-                    float v[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
-                    float* Cp = Cb + (long)m * a.ldc + n;
-                    const bool n4 = n + 4 <= a.N;
-                    if (!slab && a.bias && n4) {
-                        const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
-                        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-                    }
-                    if (!slab && a.relu == 1) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-                    } else if (!slab && a.relu == 2) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-                    }
-                    if (n4 && (a.ldc & 3) == 0) {
-                        float4* C4 = reinterpret_cast<float4*>(Cp);
-                        if (a.acc_c && !slab) {
-                            const float4 o = *C4;
-                            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+                        for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
+                        if (a.bias && n + 4 <= a.N) {
+                            const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+                            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
                         }
-                        *C4 = make_float4(v[0], v[1], v[2], v[3]);
-                    } else {
-                        for (int j = 0; j < 4 && n + j < a.N; ++j) Cp[j] = v[j] + ((a.acc_c && !slab) ? Cp[j] : 0.f);
+                        if (a.relu == 1) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+                        } else if (a.relu == 2) {
+                            u16x4_t pre;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
+                            if (a.ep_aux && ok) *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
+                        }
+                        if (a.ep_dgelu && ok) {
+                            const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
+                        }
+                        if (a.ep_res && ok) {
+                            const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
+                        }
+                        if constexpr ((FX & FX_BNB) != 0) {
+                            // gm = v * [t*mscale + mshift > 0] (ReLU mask of the BN output recomputed from its
+                            // input t); sums of gm and gm * t here, sum gm * xhat = invstd (sum gm t - mean sum gm)
+                            // at the flush (per-fragment mean / invstd loads pushed this variant into scratch)
+                            u16x4_t tv = {0, 0, 0, 0};
+                            float4 ms = {0, 0, 0, 0}, mh = ms;
+                            if (ok) tv = *reinterpret_cast<const u16x4_t*>(a.ep_x + off);
+                            ms = *reinterpret_cast<const float4*>(ptab + n);
+                            mh = *reinterpret_cast<const float4*>(ptab + PP_PRO_MAXK + n);
+                            const float msa[4] = {ms.x, ms.y, ms.z, ms.w}, mha[4] = {mh.x, mh.y, mh.z, mh.w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const float tt = bf2f(tv[j]);
+                                const float gm = (ok && fmaf(tt, msa[j], mha[j]) > 0.f) ? bf2f(f2bf(v[j])) : 0.f;
+                                v[j] = gm;
+                                s_[fn][j] += gm;
+                                q_[fn][j] += gm * tt;
+                            }
+                        } else if constexpr ((FX & FX_STATS) != 0) {
+                            if (ok) {
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    const float rr = bf2f(f2bf(v[j]));
+                                    s_[fn][j] += rr;
+                                    q_[fn][j] += rr * rr;
+                                }
+                            }
+                        }
+                        pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                        pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
                     }
+                    bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc;
+#pragma unroll
+                    for (int fp = 0; fp < C::FN / 2; ++fp) {   // 16-byte stores: permlane16 swap pairs fragments
+                        const auto s0_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
+                        const auto s1_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][1], pk[2 * fp + 1][1], false, false);
+                        const int n = n0 + bcol + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
+                        if (mv && n + 8 <= a.N) {
+                            *reinterpret_cast<uint4*>(Crow + n) = make_uint4(s0_[0], s1_[0], s0_[1], s1_[1]);
+                        } else if (mv && n < a.N) {
+                            const uint32_t w4[4] = {s0_[0], s1_[0], s0_[1], s1_[1]};
+                            for (int j = 0; j < 8 && n + j < a.N; ++j) Crow[n + j] = (bf16_t)(w4[j >> 1] >> (16 * (j & 1)));
+                        }
+                    }
+                    if constexpr (C::FN % 2) {                 // odd fragment count: 8-byte stores for the last one
+                        const int n = n0 + bcol + (C::FN - 1) * 16 + 4 * lg;
+                        if (mv && n + 4 <= a.N)
+                            *reinterpret_cast<uint2*>(Crow + n) = make_uint2(pk[C::FN - 1][0], pk[C::FN - 1][1]);
+                    }
+                    if constexpr (SUMS) {
+                        // flush one slab row pair per 64 rows (4 fragments) of the wave; the slab has one row pair
+                        // per 64 rows of M rounded up to 128 (the layout of the 128-row kernel)
+                        if constexpr (fm % 4 == 3 || fm == C::FM - 1) {
+#pragma unroll
+                            for (int fn = 0; fn < C::FN; ++fn)
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    s_[fn][j] = row16_sum(s_[fn][j]);
+                                    q_[fn][j] = row16_sum(q_[fn][j]);
+                                }
+                            const int g64 = m0 + arow + (fm / 4) * 64;
+                            if (lm == 0 && g64 < ((a.M + 127) / 128) * 128) {
+#pragma unroll
+                                for (int fn = 0; fn < C::FN; ++fn) {
+                                    const int n = n0 + bcol + fn * 16 + 4 * lg;
+                                    if (n < a.N) {
+                                        if constexpr ((FX & FX_BNB) != 0) {
+                                            const float4 mu = *reinterpret_cast<const float4*>(a.ep_mean + n);
+                                            const float4 is = *reinterpret_cast<const float4*>(a.ep_invstd + n);
+                                            q_[fn][0] = is.x * (q_[fn][0] - mu.x * s_[fn][0]);
+                                            q_[fn][1] = is.y * (q_[fn][1] - mu.y * s_[fn][1]);
+                                            q_[fn][2] = is.z * (q_[fn][2] - mu.z * s_[fn][2]);
+                                            q_[fn][3] = is.w * (q_[fn][3] - mu.w * s_[fn][3]);
+                                        }
+                                        float* ps = a.stats + (long)(2 * (g64 / 64)) * a.N + n;
+                                        *reinterpret_cast<float4*>(ps) = make_float4(s_[fn][0], s_[fn][1], s_[fn][2], s_[fn][3]);
+                                        *reinterpret_cast<float4*>(ps + a.N) = make_float4(q_[fn][0], q_[fn][1], q_[fn][2], q_[fn][3]);
+                                    }
+                                }
+                            }
+#pragma unroll
+                            for (int fn = 0; fn < C::FN; ++fn)
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) s_[fn][j] = q_[fn][j] = 0.f;
+                        }
+                    }
+                } else {
+                    // fp32: K-split items write partial slabs at C + z * sC1 (pp_slab_reduce_kernel sums them),
+                    // otherwise store / accumulate (acc_c) into C
+                    const bool slab = splits > 1;
+                    float* const Cb = reinterpret_cast<float*>(a.C) + (slab ? z * a.sC1 : 0);
+#pragma unroll
+                    for (int fn = 0; fn < C::FN; ++fn) {
+                        const int n = n0 + bcol + fn * 16 + 4 * lg;
+                        if (!mv || n >= a.N) continue;
+                        float v[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
+                        float* Cp = Cb + (long)m * a.ldc + n;
+                        const bool n4 = n + 4 <= a.N;
+                        if (!slab && a.bias && n4) {
+                            const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+                            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                        }
+                        if (!slab && a.relu == 1) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+                        } else if (!slab && a.relu == 2) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
+                        }
+                        if (n4 && (a.ldc & 3) == 0) {
+                            float4* C4 = reinterpret_cast<float4*>(Cp);
+                            if (a.acc_c && !slab) {
+                                const float4 o = *C4;
+                                v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+                            }
+                            *C4 = make_float4(v[0], v[1], v[2], v[3]);
+                        } else {
+                            for (int j = 0; j < 4 && n + j < a.N; ++j) Cp[j] = v[j] + ((a.acc_c && !slab) ? Cp[j] : 0.f);
+                        }
+                    }
+                }
+            });
+            if (dbg && cur <= 31) dbg[1 + 2 * cur] = wall_clock64();
+#pragma unroll
+            for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+                for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    };
+    {
+        for (int q = 0; q < Q; ++q) {
+            // ---------------- load segment ----------------
+            const bool more = q + D < Q;
+            if (more) pp_vmwait<(D - 2) * NIT>();       // stream slice q+1 landed (this wave's copies)
+            else pp_retire<NIT, D>(Q - q - 2);
+            const bf16_t* A_ = sb + rd_off;
+            const bf16_t* B_ = A_ + C::IMA;
+            rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
+            bf16x8_t af[C::FM], bfr[C::FN];
+            if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+                for (int f = 0; f < C::FN; ++f) bfr[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)q, 1, 2, 3, 4, 5, 6, 7});
+#pragma unroll
+                for (int f = 0; f < C::FM; ++f) af[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)f, 1, 2, 3, 4, 5, 6, 7});
+            } else {
+#pragma unroll
+            for (int f = 0; f < C::FN; ++f) {
+                if constexpr (BKm) bfr[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
+                                               B_ + (bcol + f * 16) * PP_SK + koffl));
+                else bfr[f] = frag_mnmajor<C::BN>(B_, bcol + f * 16, 0, lane);
+            }
+#pragma unroll
+            for (int f = 0; f < C::FM; ++f) {
+                if constexpr (AK) af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(
+                                              A_ + (arow + f * 16) * PP_SK + koffl));
+                else af[f] = frag_mnmajor<PP_BM>(A_, arow + f * 16, 0, lane);
+            }
+            }
+            if (!(ABL & 2) && more) issue_next();
+            if constexpr ((FX & FX_PRO) != 0) {
+                // this lane's 8 reduction indices of the slice: k = 32 s + 8 lg .. +7 (no split-K with FX_PRO)
+                const float* ps = ptab + s * PP_SK + 8 * (lane >> 4);
+                const float4 c0 = *reinterpret_cast<const float4*>(ps), c1 = *reinterpret_cast<const float4*>(ps + 4);
+                const float4 h0 = *reinterpret_cast<const float4*>(ps + PP_PRO_MAXK);
+                const float4 h1 = *reinterpret_cast<const float4*>(ps + PP_PRO_MAXK + 4);
+                const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+                for (int f = 0; f < C::FM; ++f) {
+                    u16x8_t v = __builtin_bit_cast(u16x8_t, af[f]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = f2bf(fmaxf(fmaf(bf2f(v[j]), sc[j], sh[j]), 0.f));
+                    af[f] = __builtin_bit_cast(bf16x8_t, v);
                 }
             }
-        });
-        if (dbg && cur <= 31) dbg[1 + 2 * cur] = wall_clock64();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            // ---------------- compute segment ----------------
+            __builtin_amdgcn_s_setprio(1);
+            if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-        for (int i = 0; i < C::FM; ++i)
+                for (int f = 0; f < C::FM; ++f) asm volatile("" ::"v"(af[f]));
 #pragma unroll
-            for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                for (int f = 0; f < C::FN; ++f) asm volatile("" ::"v"(bfr[f]));
+            } else {
+#pragma unroll
+            for (int fm = 0; fm < C::FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < C::FN; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            if (++s < nsl) continue;
+            epilogue();
+        }
+        if (grp == 0) __builtin_amdgcn_s_barrier();      // balance the stagger
     }
-    if (grp == 0) __builtin_amdgcn_s_barrier();          // balance the stagger
 }
 
 // out[m][n] (+)= sum_z slab[z][m][n]  (fp32, ld = ldc, slab stride sz).  float4 per thread.
@@ -433,17 +554,21 @@ int device_cus() {
 
 int g_pp_ablate = -1;
 
-template <class C, int AM, int BMODE, int EM, int ABL>
+template <class C, int FX>
+constexpr int pp_smem() { return C::SMEM + ((FX & (FX_PRO | FX_BNB)) ? 2 * PP_PRO_MAXK * 4 : 0); }
+
+template <class C, int AM, int BMODE, int EM, int ABL, int FX = 0>
 void set_attr() {
     static bool attr = false;
     if (!attr) {
         attr = true;
-        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<C, AM, BMODE, EM, ABL>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+        static_assert(pp_smem<C, FX>() <= 160 * 1024, "LDS");
+        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<C, AM, BMODE, EM, ABL, FX>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, pp_smem<C, FX>());
     }
 }
 
-template <class C, int AM, int BMODE, int EM>
+template <class C, int AM, int BMODE, int EM, int FX = 0>
 int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     if (g_pp_ablate < 0) { const char* e = getenv("PDNN_PP_ABLATE"); g_pp_ablate = e ? atoi(e) : 0; }
     const long items = cdiv(a.M, PP_BM) * cdiv(a.N, C::BN) * splits;
@@ -452,19 +577,20 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     GemmArgs b = a;
     b.nb2 = splits;
     b.dbg = g_pp_trace;
-    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16) {
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16 && FX == 0) {
 #define PP_ABL_CASE(X) if (g_pp_ablate == X) { set_attr<C, AM, BMODE, EM, X>(); hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, X>), dim3(grid), dim3(512), C::SMEM, st, b); PDNN_LAUNCH_RET; }
         PP_ABL_CASE(1) PP_ABL_CASE(2) PP_ABL_CASE(3) PP_ABL_CASE(4) PP_ABL_CASE(5) PP_ABL_CASE(6) PP_ABL_CASE(7)
 #undef PP_ABL_CASE
     }
-    set_attr<C, AM, BMODE, EM, 0>();
-    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM>), dim3(grid), dim3(512), C::SMEM, st, b);
+    constexpr int SM = pp_smem<C, FX>();
+    set_attr<C, AM, BMODE, EM, 0, FX>();
+    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, 0, FX>), dim3(grid), dim3(512), SM, st, b);
     PDNN_LAUNCH_RET;
 }
 
-template <int AM, int BMODE, int EM>
+template <int AM, int BMODE, int EM, int FX = 0>
 int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
-    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR) {
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && FX == 0) {
         switch (bn) {
             case 96: return launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
             case 192: return launch_cfg<C192, AM, BMODE, EM>(a, splits, st);
@@ -473,8 +599,9 @@ int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
             default: break;
         }
     }
-    if (bn == 128) return launch_cfg<C128, AM, BMODE, EM>(a, splits, st);
-    return launch_cfg<C256, AM, BMODE, EM>(a, splits, st);
+    if (bn == 128) return launch_cfg<C128, AM, BMODE, EM, FX>(a, splits, st);
+    if constexpr ((FX & (FX_BNB | FX_PRO)) == 0) return launch_cfg<C256, AM, BMODE, EM, FX>(a, splits, st);
+    return (int)hipErrorInvalidValue;
 }
 
 // relative per-CU throughput of the tile widths (A/B measured, tools/pp_check.py)
@@ -487,6 +614,7 @@ double bn_eff(int bn) {
     }
 }
 
+// kk: both operands K-major (every tile width); otherwise / with fusions only 128 and 256
 int pick_bn(const GemmArgs& a, bool kk) {
     if (g_pp_force_bn < 0) { const char* e = getenv("PDNN_PP_BN"); g_pp_force_bn = e ? atoi(e) : 0; }
     const int cus = device_cus();
@@ -511,6 +639,10 @@ int pick_bn(const GemmArgs& a, bool kk) {
     return best;
 }
 
+int fx_of(const GemmArgs& a) {
+    return (a.pro_scale ? FX_PRO : 0) | (a.ep_x ? FX_BNB : (a.stats ? FX_STATS : 0));
+}
+
 }  // namespace
 
 int& pp_mode_ref() {
@@ -521,28 +653,54 @@ int& pp_mode_ref() {
 bool pp_supported(const GemmArgs& a, int amode, int bmode, int em, int batch, int splits) {
     const int mode = pp_mode_ref();
     if (!mode || batch != 1 || splits != 1 || em == E_ATOMIC) return false;
-    if (a.causal || a.scatter || a.stats || a.ep_x || a.transC || a.pro_scale) return false;
+    if (a.causal || a.scatter || a.transC || a.stats_row0) return false;
     if (a.K % PP_SK || a.M < 16 || a.N < 16 || a.N % 8 || a.lda % 8 || a.ldb % 8) return false;
     if (!((amode == A_KMAJOR && (bmode == B_KMAJOR || bmode == B_MNMAJOR)) ||
           (amode == A_MNMAJOR && bmode == B_MNMAJOR)))
         return false;
     if (amode == A_MNMAJOR && a.M % 8) return false;
+    const int fx = fx_of(a);
+    if (fx && em != E_BF16) return false;
+    if ((fx & FX_PRO) && (amode != A_KMAJOR || a.K > PP_PRO_MAXK)) return false;
+    if ((fx & FX_BNB) && (!a.stats || a.N > PP_PRO_MAXK)) return false;
     if (mode == 2) return true;
     return cdiv(a.M, PP_BM) * cdiv(a.N, 256) >= 48 || (long)a.M * a.N >= (1L << 22);
+}
+
+template <int FX>
+int pp_launch_fx(const GemmArgs& a, int amode, int bmode, int em, hipStream_t st) {
+    // the BN-backward epilogue and the operand prologue fit the 256-wide tile's registers only with scratch
+    // spills: 128 wide
+    const int bn = (FX & (FX_BNB | FX_PRO)) ? 128 : pick_bn(a, FX == 0 && amode == A_KMAJOR && bmode == B_KMAJOR);
+    const int key = amode * 100 + bmode * 10 + em;
+    if constexpr (FX != 0) {      // fusions: bf16 output, A K-major
+        switch (key) {
+            case 0: return launch_bn<A_KMAJOR, B_KMAJOR, E_BF16, FX>(a, bn, 1, st);
+            case 10: return launch_bn<A_KMAJOR, B_MNMAJOR, E_BF16, FX>(a, bn, 1, st);
+            default: return (int)hipErrorInvalidValue;
+        }
+    } else {
+        switch (key) {
+            case 0: return launch_bn<A_KMAJOR, B_KMAJOR, E_BF16>(a, bn, 1, st);
+            case 1: return launch_bn<A_KMAJOR, B_KMAJOR, E_F32>(a, bn, 1, st);
+            case 10: return launch_bn<A_KMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
+            case 11: return launch_bn<A_KMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+            case 110: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
+            case 111: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+            default: return (int)hipErrorInvalidValue;
+        }
+    }
 }
 
 int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) {
     GemmArgs a = a0;
     a.ktiles_per_split = a.K / PP_SK;
-    const int bn = pick_bn(a, amode == A_KMAJOR && bmode == B_KMAJOR);
-    const int key = amode * 100 + bmode * 10 + em;
-    switch (key) {
-        case 0: return launch_bn<A_KMAJOR, B_KMAJOR, E_BF16>(a, bn, 1, st);
-        case 1: return launch_bn<A_KMAJOR, B_KMAJOR, E_F32>(a, bn, 1, st);
-        case 10: return launch_bn<A_KMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
-        case 11: return launch_bn<A_KMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
-        case 110: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_BF16>(a, bn, 1, st);
-        case 111: return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
+    switch (fx_of(a)) {
+        case 0: return pp_launch_fx<0>(a, amode, bmode, em, st);
+        case FX_STATS: return pp_launch_fx<FX_STATS>(a, amode, bmode, em, st);
+        case FX_BNB: return pp_launch_fx<FX_BNB>(a, amode, bmode, em, st);
+        case FX_PRO: return pp_launch_fx<FX_PRO>(a, amode, bmode, em, st);
+        case FX_PRO | FX_STATS: return pp_launch_fx<FX_PRO | FX_STATS>(a, amode, bmode, em, st);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -563,6 +721,13 @@ PP_I2(C128, A_KMAJOR, B_KMAJOR) PP_I2(C256, A_KMAJOR, B_KMAJOR) PP_I2(C256b, A_K
 PP_I2(C128, A_KMAJOR, B_MNMAJOR) PP_I2(C256, A_KMAJOR, B_MNMAJOR)
 PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)
 #undef PP_I2
+#define PP_F(CFG, BM_, FX) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::BM_, pg::E_BF16, 0, FX>(pg::GemmArgs);
+#define PP_F2(BM_, FX) PP_F(C128, BM_, FX) PP_F(C256, BM_, FX)
+#define PP_F5(BM_) PP_F(C128, BM_, 1) PP_F2(BM_, 2) PP_F(C128, BM_, 3) PP_F(C128, BM_, 4)
+PP_F5(B_KMAJOR) PP_F5(B_MNMAJOR)
+#undef PP_F5
+#undef PP_F2
+#undef PP_F
 #undef PP_I
 
 // pp_wgrad: out[M][N] (fp32) += alpha * A[K][M]^T . B[K][N] with split-K partial slabs in `ws`

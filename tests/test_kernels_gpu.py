@@ -22,17 +22,20 @@ def K():
     return kernels
 
 
-@pytest.fixture(autouse=True, params=[(1, 1), (0, 1), (0, 0), (2, 1)],
-                ids=["auto", "reg128", "reg128-direct-store", "glds"])
+@pytest.fixture(autouse=True, params=[(1, 1, 1), (0, 1, 0), (0, 0, 0), (2, 1, 0), (1, 1, 2)],
+                ids=["auto", "reg128", "reg128-direct-store", "glds", "pp"])
 def engine(request, K):
     """Every GEMM/conv test runs with automatic engine choice, the register-staged 128-tile kernel only
-    (LDS-staged and direct epilogue stores), and the glds 256-row engine forced wherever it applies."""
-    glds, staged = request.param
+    (LDS-staged and direct epilogue stores), the glds 256-row engine forced wherever it applies, and the
+    ping-pong engine forced wherever it applies (plain GEMMs, 1x1 stride-1 convs with their fusions)."""
+    glds, staged, pp = request.param
     old = K.set_glds_mode(glds)
     old_s = K.set_staged_store(staged)
+    old_p = K.set_pp_mode(pp)
     yield request.param
     K.set_glds_mode(old)
     K.set_staged_store(old_s)
+    K.set_pp_mode(old_p)
 
 
 def rnd(*s, scale=1.0):
@@ -338,6 +341,45 @@ def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
     xh = (t.float() - mean) * inv
     assert torch.allclose(sums[0], gm_ref.reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
     assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(16, 28, 28, 128, 512, False), (16, 28, 28, 512, 128, True),
+                                   (4, 14, 14, 1024, 256, True), (3, 10, 10, 256, 128, True)])
+def test_conv1x1_fused_resnet_shapes(K, shape):
+    """1x1 stride-1 convs at bottleneck shapes (the ping-pong engine in auto mode): forward with the
+    BN-affine+ReLU prologue and BN statistics; data gradient with residual, and with the BN-backward
+    masking + reduction epilogue."""
+    N, H, W, C, Ko, pro = shape
+    x, w = rnd(N, H, W, C), rnd(Ko, 1, 1, C, scale=0.1)
+    prolog, xin = None, x
+    if pro:
+        sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
+        prolog, xin = (sc, sh), F.relu(x.float() * sc + sh).to(BF)
+    y, stats = K.conv_fwd(x, w, 1, 0, pro=prolog, want_stats=True)
+    ref = conv_ref(xin, w, 1, 0)
+    assert rel(y, ref) < 1.5e-2
+    yf = y.float().reshape(-1, Ko)
+    s = stats.view(-1, 2, Ko).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    # data gradient: dy [N,H,W,Ko] -> dx [N,H,W,C]
+    dy = rnd(N, H, W, Ko)
+    dx_ref = (dy.float().reshape(-1, Ko) @ w.float().reshape(Ko, C)).view(N, H, W, C)
+    res = rnd(N, H, W, C)
+    assert rel(K.conv_dgrad(dy, w, (N, H, W, C), 1, 0, res=res), dx_ref + res.float()) < 1.5e-2
+    t = rnd(N, H, W, C) + 0.3
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    bsc, bsh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), 1, 0, bn=(t, mean, inv, bsc, bsh))
+    z = t.float() * bsc + bsh
+    gm_ref = dx_ref.to(BF).float() * (z > 0)
+    sure = z.abs() > 1e-4          # the kernel evaluates the mask with one fma: skip sign ties
+    assert rel(gm.float() * sure, gm_ref * sure) < 1.5e-2
+    sums = slab.view(-1, 2, C).sum(0)
+    xh = (t.float() - mean) * inv
+    tol = 1e-2 * gm_ref.abs().sum(dim=(0, 1, 2)).max().item() / 10
+    assert torch.allclose(sums[0], gm_ref.reshape(-1, C).sum(0), atol=max(tol, 5e-2), rtol=1e-2)
+    assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=max(tol, 5e-2), rtol=1e-2)
 
 
 @pytest.mark.parametrize("R,C", [(100, 10), (8192, 768), (8192, 3072), (3000, 2304), (513, 40), (260, 1032), (100000, 64),

@@ -1,6 +1,10 @@
 """Run one ping-pong GEMM configuration repeatedly (rocprofv3 --pmc target).
 
-    python tools/pp_one.py M N K [--bn BN] [--kind nt|nn|wgrad] [--iters 20]
+    python tools/pp_one.py M N K [--bn BN] [--kind nt|nn|wgrad|fwd1x1|fwd1x1pro|dgrad1x1bn] [--iters 20]
+
+The conv kinds run a 1x1 stride-1 conv (M pixels, C = K in, Ko = N out) through the conv API with BN statistics
+(fwd1x1), plus the BN-affine+ReLU prologue (fwd1x1pro), or the data gradient with the BN-backward epilogue
+(dgrad1x1bn: M pixels, N = C out, K = Ko in); set PDNN_PP_CONV_FWD_K=0 / PDNN_PP_CONV_DGRAD_K=0 to force pp.
 """
 import argparse
 import os
@@ -29,6 +33,14 @@ def main():
         x, y = r(a.K, a.M), r(a.K, a.N)
         out = torch.zeros(a.M, a.N, device="cuda")
         fn = lambda: K.pp_wgrad(x, y, out)  # noqa: E731
+    elif a.kind in ("fwd1x1", "fwd1x1pro"):
+        x, w = r(1, a.M, 1, a.K), r(a.N, 1, 1, a.K)
+        pro = (torch.rand(a.K, device="cuda") + 0.5, torch.randn(a.K, device="cuda")) if a.kind == "fwd1x1pro" else None
+        fn = lambda: K.conv_fwd(x, w, 1, 0, pro=pro, want_stats=True)  # noqa: E731
+    elif a.kind == "dgrad1x1bn":
+        dy, w, t = r(1, a.M, 1, a.K), r(a.K, 1, 1, a.N), r(1, a.M, 1, a.N)
+        v = [torch.rand(a.N, device="cuda") + 0.5 for _ in range(4)]
+        fn = lambda: K.conv_dgrad(dy, w, (1, a.M, 1, a.N), 1, 0, bn=(t, *v))  # noqa: E731
     else:
         x, w = r(a.M, a.K), r(a.N, a.K)
         wt = w.t().contiguous()
