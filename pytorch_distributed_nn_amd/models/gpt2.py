@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from ..ops import functional as OF
 from ..ops import transformer as TX
+from ..optim.flat import direct_grad
 
 
 @dataclass
@@ -143,7 +144,9 @@ class GPT2(nn.Module):
         tr = self.transformer
         wte, wpe = tr.wte.weight, tr.wpe.weight
         wte_k, wpe_k = OF.weight_bf16(wte), OF.weight_bf16(wpe)
-        x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, wte, wpe)
+        # tied wte: with targets the fused LM head and the embedding both accumulate into its arena gradient
+        hd = targets is not None and direct_grad(wte) is not None
+        x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, wte, wpe, hd)
         for blk in tr.h:
             params, shadows = blk.fused_params()
             metas = blk.fp8_metas(x.device) if c.fp8 else None
@@ -152,7 +155,7 @@ class GPT2(nn.Module):
             xf = TX.layer_norm(x, tr.ln_f.weight, tr.ln_f.bias, c.eps)
             return OF.linear(xf, wte).view(B, T, -1)
         return TX.LMHeadLossFn.apply(x, targets.reshape(-1).long().contiguous(), c.eps, wte_k, tr.ln_f.weight,
-                                     tr.ln_f.bias, wte)
+                                     tr.ln_f.bias, wte, hd)
 
     def _forward_reference(self, idx, targets=None):
         B, T = idx.shape

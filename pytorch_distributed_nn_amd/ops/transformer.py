@@ -133,25 +133,33 @@ def layer_norm(x, weight, bias, eps=1e-5):
 # ------------------------------------------------------------------------------------------------
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe):
+    def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe, head_direct=False):
         ctx.save_for_backward(idx)
         ctx.conf = (T, wte.shape, wpe.shape)
-        ctx.wpe = wpe
+        ctx.wpe, ctx.wte = wpe, wte
+        ctx.head_direct = head_direct       # the tied LM head accumulates its wte gradient in the arena too
         return K.embedding_fwd(idx, wte_k, wpe_k, T)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         T, s_te, s_pe = ctx.conf
-        dwte = torch.zeros(s_te, device=g.device, dtype=F32)       # tied with the LM head: returned
+        # wte is tied with the LM head, whose backward ran first and (with a flat arena) already accumulated
+        # its part in place: the embedding adds its rows on top (atomics) and announces the parameter, so no
+        # zero-filled temporaries and no autograd sum of the two gradients
+        tte = direct_grad(ctx.wte) if ctx.head_direct else None
+        dwte = tte if tte is not None else torch.zeros(s_te, device=g.device, dtype=F32)
         tpe = direct_grad(ctx.wpe)
         dwpe = tpe if tpe is not None else torch.zeros(s_pe, device=g.device, dtype=F32)
         K.embedding_bwd(idx, g, dwte, dwpe, T)
         if tpe is not None:
             grad_ready(ctx.wpe)
             dwpe = None
-        ctx.wpe = None
-        return None, None, None, None, dwte, dwpe
+        if tte is not None:
+            grad_ready(ctx.wte)
+            dwte = None
+        ctx.wpe = ctx.wte = None
+        return None, None, None, None, dwte, dwpe, None
 
 
 # ------------------------------------------------------------------------------------------------
@@ -282,7 +290,8 @@ class LMHeadLossFn(torch.autograd.Function):
     """loss = mean CE(LN_f(x) . Wte^T, targets); logits bf16 [B*T][V] live only inside this op."""
 
     @staticmethod
-    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte):
+    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte, head_direct=False):
+        ctx.head_direct = head_direct
         xf, m, r = K.layernorm_fwd(x, lnw, lnb, eps)
         logits = BL.linear_fwd(xf, wte_k)
         _, lse, acc = K.xent_fwd(logits, targets)
@@ -298,10 +307,15 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
         dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
         dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
-        dwte = _wgrad(dlogits, xf, wte_k.shape)         # tied weight: summed by autograd (not direct)
+        tte = direct_grad(ctx.wte) if ctx.head_direct else None
+        if tte is not None:     # tied weight: the embedding backward adds its part and announces it
+            BL.wgrad_acc(dlogits, xf, tte)
+            dwte = None
+        else:
+            dwte = _wgrad(dlogits, xf, wte_k.shape)     # summed with the embedding's by autograd
         sink = _Sink()
         dx, dlnw, dlnb = sink.layernorm(dxf, x, lnw, m, r, None, *ctx.params)
         ctx.params = None
         ctx.wte = None
         sink.done()
-        return dx, None, None, None, dlnw, dlnb, dwte
+        return dx, None, None, None, dlnw, dlnb, dwte, None

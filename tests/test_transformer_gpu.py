@@ -196,6 +196,24 @@ def test_gpt2_tiny_loss_and_grads():
         assert cos(p.grad.cpu(), pr.grad) > 0.99, n
 
 
+def test_gpt2_flat_arena_grads_match_autograd_path():
+    """With a flat arena the fused ops accumulate gradients in place (the tied wte: LM head then embedding,
+    both into the arena); every gradient must equal the autograd-returned path's."""
+    from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
+    m = _tiny(seed=3).cuda()
+    mf = copy.deepcopy(m)
+    flatten_module(mf)
+    opt = AdamW(mf.parameters(), lr=1e-3)
+    opt.zero_grad()
+    B, T = 4, 128
+    idx = torch.randint(0, m.config.vocab_size, (B, T), device="cuda")
+    tgt = torch.randint(0, m.config.vocab_size, (B, T), device="cuda")
+    m(idx, tgt).backward()
+    mf(idx, tgt).backward()
+    for (n, p), (_, pf) in zip(m.named_parameters(), mf.named_parameters()):
+        assert rel2(pf.grad, p.grad) < 1e-3, n
+
+
 def test_gpt2_tiny_trains():
     from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
     m = _tiny(seed=1).cuda()
