@@ -791,17 +791,24 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
 
 PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
     using namespace pg;
-    // enough blocks to cover the CUs once, each with >= 16 slices; capped by the slab workspace volume
+    // K-splits (equal slice counts, >= 16 slices each) minimising  rounds x (slices per item + ~10 slices of
+    // per-item prologue/epilogue), with a 4% per-split surcharge for the fp32 slab traffic and reduction:
+    // a split count that spills a few items into a second round of the persistent grid costs as much as
+    // halving it (GPT-2 fc / fc2: 4 -> 2 splits, tools/pp_check.py wg_* rows)
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K;
     const int bn = pick_bn(a, false);
     const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
     const int cus = device_cus();
-    if (tiles >= cus / 2) return 1;
-    int s = (int)cdiv(cus, tiles);
     const int nsl = K / PP_SK;
-    while (s > 1 && (nsl / s < 16 || nsl % s)) --s;
-    return s < 1 ? 1 : s;
+    int best = 1;
+    double bt = 1e300;
+    for (int s = 1; s <= 32; ++s) {
+        if (nsl % s || (s > 1 && nsl / s < 16)) continue;
+        const double t = (double)cdiv(tiles * s, cus) * (nsl / s + 10) * (1.0 + 0.04 * (s - 1));
+        if (t < bt) { bt = t; best = s; }
+    }
+    return best;
 }
 
 // phase trace buffer for the next pp launches (null = off): 2 * grid * 64 int64 timestamps (100 MHz)
