@@ -35,27 +35,37 @@
 
 namespace {
 
-// C[M][N] (+)= A[M][K] * B[K][N], all row-major; optional transposes via strides.
+// C[M][N] (+)= A[M][K] * B[K][N], all row-major; optional transposes via strides.  Blocked over (k, n);
+// a transposed B block is packed k-major first so the inner loop is a contiguous axpy the compiler
+// vectorises (the strided B[j][k] walk was the slow path of the data-gradient GEMM).
 void gemm(int M, int N, int K, const float* A, int lda, bool ta, const float* B, int ldb, bool tb, float* C,
           int ldc, bool accumulate) {
     if (!accumulate)
         for (int i = 0; i < M; ++i) std::fill(C + (long)i * ldc, C + (long)i * ldc + N, 0.f);
     constexpr int BK = 64, BN = 256;
+    std::vector<float> pack(tb ? (size_t)BK * BN : 0);
     for (int k0 = 0; k0 < K; k0 += BK) {
         const int k1 = std::min(K, k0 + BK);
         for (int n0 = 0; n0 < N; n0 += BN) {
-            const int n1 = std::min(N, n0 + BN);
+            const int n1 = std::min(N, n0 + BN), nw = n1 - n0;
+            const float* bblk;
+            long bld;
+            if (tb) {
+                for (int j = n0; j < n1; ++j)
+                    for (int k = k0; k < k1; ++k) pack[(size_t)(k - k0) * nw + (j - n0)] = B[(long)j * ldb + k];
+                bblk = pack.data() - (long)k0 * nw - n0;
+                bld = nw;
+            } else {
+                bblk = B;
+                bld = ldb;
+            }
             for (int i = 0; i < M; ++i) {
                 float* c = C + (long)i * ldc;
                 for (int k = k0; k < k1; ++k) {
                     const float a = ta ? A[(long)k * lda + i] : A[(long)i * lda + k];
                     if (a == 0.f) continue;
-                    if (!tb) {
-                        const float* b = B + (long)k * ldb;
-                        for (int j = n0; j < n1; ++j) c[j] += a * b[j];
-                    } else {
-                        for (int j = n0; j < n1; ++j) c[j] += a * B[(long)j * ldb + k];
-                    }
+                    const float* b = bblk + (long)k * bld;
+                    for (int j = n0; j < n1; ++j) c[j] += a * b[j];
                 }
             }
         }
