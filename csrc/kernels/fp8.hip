@@ -7,6 +7,7 @@
 namespace {
 constexpr int NT = 256;
 constexpr float FP8_MAX = 448.f;     // e4m3fn
+constexpr int FP8_AMAX_PARTS = 1024;  // per-block amax partials of a delayed-scaling quantisation (quant grid cap)
 
 typedef __attribute__((ext_vector_type(8))) int v8i;
 
@@ -54,16 +55,28 @@ __global__ void fp8_scale_kernel(const float* amax, float* scale, float* inv, in
 // Delayed-scaling bookkeeping of one fp8 GEMM input, run right after its quantisation:
 // gemm_scale = inv (the inverse scale the tensor was just quantised with) * inv_w; then the next call's
 // scale is derived from the amax recorded by that quantisation, and the amax accumulator is reset.
-__global__ void fp8_scale_step_kernel(float* amax, float* scale, float* inv, const float* inv_w, float* gemm_scale,
-                                      int margin) {
-    gemm_scale[0] = inv[0] * (inv_w ? inv_w[0] : 1.f);
-    const float a = amax[0];
-    if (a > 0.f) {
-        const float s = ldexpf(FP8_MAX / a, -margin);
-        scale[0] = s;
-        inv[0] = 1.f / s;
+__global__ void __launch_bounds__(NT) fp8_scale_step_kernel(float* amax, float* scale, float* inv, const float* inv_w,
+                                                            float* gemm_scale, int margin) {
+    // amax holds FP8_AMAX_PARTS per-block partial maxima of the last quantisation (quant_fp8_kernel)
+    float m = 0.f;
+    for (int i = threadIdx.x; i < FP8_AMAX_PARTS; i += NT) {
+        m = fmaxf(m, amax[i]);
+        amax[i] = 0.f;
     }
-    amax[0] = 0.f;
+    m = wave_max(m);
+    __shared__ float sm[NT / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = sm[0];
+        for (int i = 1; i < NT / 64; ++i) a = fmaxf(a, sm[i]);
+        gemm_scale[0] = inv[0] * (inv_w ? inv_w[0] : 1.f);
+        if (a > 0.f) {
+            const float s = ldexpf(FP8_MAX / a, -margin);
+            scale[0] = s;
+            inv[0] = 1.f / s;
+        }
+    }
 }
 
 // out = e4m3(x * scale[0]), optionally also tracking amax of x (for the next step's delayed scale)
@@ -82,9 +95,16 @@ __global__ void __launch_bounds__(NT) quant_fp8_kernel(const bf16_t* __restrict_
         }
         *reinterpret_cast<uint2*>(out + 8 * i) = f32x8_to_fp8(v);
     }
-    if (amax) {
+    if (amax) {      // one partial per block (no same-address atomics: 8k of them serialised this kernel)
         m = wave_max(m);
-        if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+        __shared__ float sm[NT / 64];
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = sm[0];
+            for (int i = 1; i < NT / 64; ++i) t = fmaxf(t, sm[i]);
+            amax[blockIdx.x] = fmaxf(amax[blockIdx.x], t);
+        }
     }
 }
 
@@ -161,7 +181,9 @@ PDNN_API int pdnn_fp8_probe(const uint8_t* A, const uint8_t* Bt, float* D, int l
 
 PDNN_API int pdnn_amax_bf16(const bf16_t* x, long n, float* amax, hipStream_t st) {
     if (n % 8) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(amax_bf16_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, x, n / 8, amax);
+    unsigned g = stream_grid(n / 8, NT);
+    if (g > 256) g = 256;            // one same-address atomic per block: keep them few
+    hipLaunchKernelGGL(amax_bf16_kernel, dim3(g), dim3(NT), 0, st, x, n / 8, amax);
     PDNN_LAUNCH_RET;
 }
 
@@ -177,13 +199,17 @@ PDNN_API int pdnn_fp8_scale(const float* amax, float* scale, float* inv, int mar
 
 PDNN_API int pdnn_fp8_scale_step(float* amax, float* scale, float* inv, const float* inv_w, float* gemm_scale,
                                  int margin, hipStream_t st) {
-    hipLaunchKernelGGL(fp8_scale_step_kernel, dim3(1), dim3(1), 0, st, amax, scale, inv, inv_w, gemm_scale, margin);
+    hipLaunchKernelGGL(fp8_scale_step_kernel, dim3(1), dim3(NT), 0, st, amax, scale, inv, inv_w, gemm_scale, margin);
     PDNN_LAUNCH_RET;
 }
 
+// amax (optional): FP8_AMAX_PARTS floats of per-block partial maxima (max-accumulated; reduced and reset by
+// pdnn_fp8_scale_step)
 PDNN_API int pdnn_quant_fp8(const bf16_t* x, long n, const float* scale, uint8_t* out, float* amax, hipStream_t st) {
     if (n % 8) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(quant_fp8_kernel, dim3(stream_grid(n / 8, NT)), dim3(NT), 0, st, x, n / 8, scale, out, amax);
+    unsigned g = stream_grid(n / 8, NT);
+    if (g > FP8_AMAX_PARTS) g = FP8_AMAX_PARTS;
+    hipLaunchKernelGGL(quant_fp8_kernel, dim3(g), dim3(NT), 0, st, x, n / 8, scale, out, amax);
     PDNN_LAUNCH_RET;
 }
 

@@ -141,6 +141,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // pp_supported: operand/shape conditions of the engine; pp_launch returns a hipError_t.
 bool pp_supported(const GemmArgs& a, int amode, int bmode, int em, int batch, int splits);
 int pp_launch(const GemmArgs& a, int amode, int bmode, int em, hipStream_t st);
+int pp_fp8_launch(const GemmArgs& a, int em, hipStream_t st);   // e4m3 operands, K / ld in 2-byte units
 int& pp_mode_ref();
 
 }  // namespace pg

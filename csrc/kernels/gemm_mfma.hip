@@ -900,6 +900,9 @@ PDNN_API int pdnn_gemm_fp8(const uint8_t* X, long ldx, const uint8_t* W, long ld
     a.C = Y; a.ldc = ldy; a.alpha = 1.f; a.alpha_ptr = scale;
     a.bias = bias; a.relu = act; a.ep_aux = aux; a.ep_res = res; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
+    // ping-pong engine (fp8 slices of 128 bytes per row) unless PDNN_PP_FP8=0 / pp off: the glds engine
+    if (pp_mode_ref() && env_int("PDNN_PP_FP8", 1) && M >= 16 && N >= 16)
+        return pp_fp8_launch(a, out_f32 ? E_F32 : E_BF16, st);
     const int bn = glds_bn(N);
     if (out_f32) {
         if (bn == 256) return launch_glds_w<A_KMAJOR, B_KMAJOR, E_F32, 256, 1>(a, 1, st, 1);

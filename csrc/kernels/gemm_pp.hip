@@ -49,12 +49,16 @@ constexpr int FX_STATS = 2;    // per-column (sum, sum of squares) of the bf16 o
 constexpr int FX_BNB = 4;      // output gm = v * [ep_x*mscale + mshift > 0]; slab gets sum gm, sum gm*xhat
 constexpr int PP_PRO_MAXK = 1024;
 
-template <int BN_, int WR_, int NB_>
+// DT = 1: fp8 (OCP e4m3) operands, both K-major, every K / ld in units of 2 fp8 (the loaders move bytes);
+// a slice is then 64 units = 128 fp8 per row, consumed by one block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+// per fragment pair (unit block scales; the per-tensor scales come in through alpha_ptr).
+template <int BN_, int WR_, int NB_, int DT_ = 0>
 struct PPC {
-    static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_;
+    static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_, DT = DT_;
+    static constexpr int SK = DT ? 64 : PP_SK;            // slice depth in bf16 units
     static constexpr int WTM = 128 / WR, WTN = BN / WC;
     static constexpr int FM = WTM / 16, FN = WTN / 16;
-    static constexpr int IMA = PP_BM * PP_SK, IMB = BN * PP_SK, SLOT = IMA + IMB;
+    static constexpr int IMA = PP_BM * SK, IMB = BN * SK, SLOT = IMA + IMB;
     static constexpr int SMEM = NB * SLOT * 2;
     static_assert(WTN % 16 == 0 && WTM % 16 == 0, "wave tile");
     static_assert(SMEM <= 160 * 1024, "LDS");
@@ -63,13 +67,27 @@ struct PPC {
 __device__ __forceinline__ int pp_swz(int row) { return (0x78 >> (((row >> 2) & 3) << 1)) & 3; }
 __device__ __forceinline__ int pp_koff(int row, int chunk) { return row * PP_SK + ((chunk ^ pp_swz(row)) << 3); }
 
+typedef __attribute__((ext_vector_type(8))) int v8i_t;
+typedef __attribute__((ext_vector_type(4))) int v4i_t;
+// fp8 fragment of the 16x16x128 MFMA from a 128-byte-row image: lane l holds k-bytes [32 (l >> 4), +32)
+// of its row = 16-byte chunks 2g, 2g + 1 (g = l >> 4)
+__device__ __forceinline__ v8i_t frag8(const bf16_t* img, int row, int lane) {
+    const int g = lane >> 4;
+    const v4i_t lo = *reinterpret_cast<const v4i_t*>(img + kimg_off(row, 2 * g));
+    const v4i_t hi = *reinterpret_cast<const v4i_t*>(img + kimg_off(row, 2 * g + 1));
+    return v8i_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // One operand's copies: NR = ROWS/16 wave-instructions of 1 KiB per slice, spread over the 8 waves
 // (NI each; instructions past NR duplicate the last one: identical bytes to identical LDS addresses).
 //   K-major  [rows][K]: instruction j covers rows 16 j .. 16 j + 15 (lane: row 16 j + lane / 4, chunk lane & 3)
 //   MN-major [K][cols]: instruction j covers k-rows RPI j .. RPI j + RPI - 1, RPI = 512 / ROWS
-template <int ROWS, bool KMAJ>
+template <int ROWS, bool KMAJ, int SK = PP_SK>
 struct PPLoader {
-    static constexpr int NR = ROWS / 16;
+    static_assert(SK == PP_SK || KMAJ, "128-byte slices: K-major operands only");
+    // SK = 64 (fp8): 128-byte rows, instruction j covers rows 8 j .. 8 j + 7 (lane: row 8 j + lane / 8,
+    // 16-byte chunk (lane & 7) ^ ((row >> 1) & 7): the kimg_off image read by the fp8 fragments)
+    static constexpr int NR = SK == PP_SK ? ROWS / 16 : ROWS / 8;
     static constexpr int NI = (NR + 7) / 8;
     const bf16_t* src[NI];
     int dst[NI];
@@ -81,7 +99,11 @@ struct PPLoader {
             int j = wave * NI + i;
             j = j < NR ? j : NR - 1;
             dst[i] = j * 512;
-            if constexpr (KMAJ) {
+            if constexpr (KMAJ && SK != PP_SK) {
+                const int row = 8 * j + (lane >> 3);
+                const int g = min(base + row, extent - 1);
+                src[i] = p + (long)g * ld + (((lane & 7) ^ ((row >> 1) & 7)) << 3);
+            } else if constexpr (KMAJ) {
                 const int row = 16 * j + (lane >> 2);
                 const int g = min(base + row, extent - 1);
                 src[i] = p + (long)g * ld + (((lane & 3) ^ pp_swz(row)) << 3);
@@ -93,7 +115,7 @@ struct PPLoader {
                 src[i] = p + (long)kr * ld + col;
             }
         }
-        step = KMAJ ? PP_SK : PP_SK * ld;
+        step = KMAJ ? SK : SK * ld;
     }
     __device__ __forceinline__ void skip(int slices) {
 #pragma unroll
@@ -143,8 +165,9 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
     static_assert(!(FX & FX_PRO) || AK, "prologue: K-major A only");
     constexpr int NB = C::NB, D = NB - 1;
-    using LA = PPLoader<PP_BM, AK>;
-    using LB = PPLoader<C::BN, BKm>;
+    static_assert(!C::DT || (AK && BKm && !(FX & FX_PRO) && ABL == 0), "fp8: K-major operands, no prologue");
+    using LA = PPLoader<PP_BM, AK, C::SK>;
+    using LB = PPLoader<C::BN, BKm, C::SK>;
     constexpr int NIT = LA::NI + LB::NI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const sb = reinterpret_cast<bf16_t*>(smem);
@@ -428,8 +451,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             const bf16_t* A_ = sb + rd_off;
             const bf16_t* B_ = A_ + C::IMA;
             rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
-            bf16x8_t af[C::FM], bfr[C::FN];
-            if constexpr ((ABL & 4) != 0) {
+            bf16x8_t af[C::DT ? 1 : C::FM], bfr[C::DT ? 1 : C::FN];
+            v8i_t aq[C::DT ? C::FM : 1], bq[C::DT ? C::FN : 1];   // fp8: 32 k-bytes per lane and fragment
+            if constexpr (C::DT == 1) {
+#pragma unroll
+                for (int f = 0; f < C::FN; ++f) bq[f] = frag8(B_, bcol + f * 16 + (lane & 15), lane);
+#pragma unroll
+                for (int f = 0; f < C::FM; ++f) aq[f] = frag8(A_, arow + f * 16 + (lane & 15), lane);
+            } else if constexpr ((ABL & 4) != 0) {
 #pragma unroll
                 for (int f = 0; f < C::FN; ++f) bfr[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)q, 1, 2, 3, 4, 5, 6, 7});
 #pragma unroll
@@ -470,7 +499,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             __builtin_amdgcn_s_barrier();
             // ---------------- compute segment ----------------
             __builtin_amdgcn_s_setprio(1);
-            if constexpr ((ABL & 1) != 0) {
+            if constexpr (C::DT == 1) {
+#pragma unroll
+                for (int fm = 0; fm < C::FM; ++fm)
+#pragma unroll
+                    for (int fn = 0; fn < C::FN; ++fn)
+                        acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                            bq[fn], aq[fm], acc[fm][fn], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+            } else if constexpr ((ABL & 1) != 0) {
 #pragma unroll
                 for (int f = 0; f < C::FM; ++f) asm volatile("" ::"v"(af[f]));
 #pragma unroll
@@ -537,6 +573,8 @@ using C192 = PPC<192, 2, 5>;
 using C256 = PPC<256, 1, 4>;
 using C288 = PPC<288, 2, 4>;
 using C256b = PPC<256, 1, 5>;        // 160 KiB ring (A/B: PDNN_PP_BN=257)
+using C8_128 = PPC<128, 2, 3, 1>;    // fp8: 48 KiB slots (128-byte rows), 3 in the ring
+using C8_96 = PPC<96, 2, 3, 1>;
 
 int g_pp_mode = -1;
 int g_pp_force_bn = -1;
@@ -577,7 +615,7 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     GemmArgs b = a;
     b.nb2 = splits;
     b.dbg = g_pp_trace;
-    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16 && FX == 0) {
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16 && FX == 0 && C::DT == 0) {
 #define PP_ABL_CASE(X) if (g_pp_ablate == X) { set_attr<C, AM, BMODE, EM, X>(); hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, X>), dim3(grid), dim3(512), C::SMEM, st, b); PDNN_LAUNCH_RET; }
         PP_ABL_CASE(1) PP_ABL_CASE(2) PP_ABL_CASE(3) PP_ABL_CASE(4) PP_ABL_CASE(5) PP_ABL_CASE(6) PP_ABL_CASE(7)
 #undef PP_ABL_CASE
@@ -692,6 +730,24 @@ int pp_launch_fx(const GemmArgs& a, int amode, int bmode, int em, hipStream_t st
     }
 }
 
+// fp8 GEMM (both operands K-major e4m3, K / ld in units of 2 bytes, K % 64 units): tile width 128 or 96,
+// whichever fills the CUs in fewer rounds (same efficiency weights as the bf16 widths)
+int pp_fp8_launch(const GemmArgs& a0, int em, hipStream_t st) {
+    GemmArgs a = a0;
+    if (a.K % 64 || a.N % 8 || a.M < 16 || a.lda % 8 || a.ldb % 8) return (int)hipErrorInvalidValue;
+    a.ktiles_per_split = a.K / 64;
+    const int cus = device_cus();
+    const double t128 = (double)cdiv(cdiv(a.M, PP_BM) * cdiv(a.N, 128), cus) * 128 / bn_eff(128);
+    const double t96 = (double)cdiv(cdiv(a.M, PP_BM) * cdiv(a.N, 96), cus) * 96 / bn_eff(96);
+    const bool w96 = g_pp_force_bn == 96 || (g_pp_force_bn != 128 && t96 < t128 * 0.999);
+    if (em == E_F32) return w96 ? launch_cfg<C8_96, A_KMAJOR, B_KMAJOR, E_F32>(a, 1, st)
+                                : launch_cfg<C8_128, A_KMAJOR, B_KMAJOR, E_F32>(a, 1, st);
+    if (a.stats) return w96 ? launch_cfg<C8_96, A_KMAJOR, B_KMAJOR, E_BF16, FX_STATS>(a, 1, st)
+                            : launch_cfg<C8_128, A_KMAJOR, B_KMAJOR, E_BF16, FX_STATS>(a, 1, st);
+    return w96 ? launch_cfg<C8_96, A_KMAJOR, B_KMAJOR, E_BF16>(a, 1, st)
+               : launch_cfg<C8_128, A_KMAJOR, B_KMAJOR, E_BF16>(a, 1, st);
+}
+
 int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) {
     GemmArgs a = a0;
     a.ktiles_per_split = a.K / PP_SK;
@@ -724,6 +780,11 @@ PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)
 #define PP_F(CFG, BM_, FX) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::BM_, pg::E_BF16, 0, FX>(pg::GemmArgs);
 #define PP_F2(BM_, FX) PP_F(C128, BM_, FX) PP_F(C256, BM_, FX)
 #define PP_F5(BM_) PP_F(C128, BM_, 1) PP_F2(BM_, 2) PP_F(C128, BM_, 3) PP_F(C128, BM_, 4)
+#define PP_8(CFG) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 0, 0>(pg::GemmArgs); \
+    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_F32, 0, 0>(pg::GemmArgs); \
+    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 0, 2>(pg::GemmArgs);
+PP_8(C8_128) PP_8(C8_96)
+#undef PP_8
 PP_F5(B_KMAJOR) PP_F5(B_MNMAJOR)
 #undef PP_F5
 #undef PP_F2

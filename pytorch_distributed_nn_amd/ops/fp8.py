@@ -2,14 +2,15 @@
 per-tensor scaling"; BASELINE.json config 5 "ResNet-152 fp8 weights").
 
 Recipe (the usual fp8-training split): forward GEMMs read fp8 operands on the block-scaled
-``v_mfma_scale_f32_16x16x128_f8f6f4`` path (2x the bf16 MFMA rate, ``csrc/kernels/gemm_mfma.hip``
-``pdnn_gemm_fp8``); backward GEMMs stay bf16 on the saved bf16 activations and the bf16 weight shadow.
+``v_mfma_scale_f32_16x16x128_f8f6f4`` path (2x the bf16 MFMA rate; ``pdnn_gemm_fp8`` runs the ping-pong
+engine with 128-byte fp8 slices, ``csrc/kernels/gemm_pp.hip`` DT = 1); backward GEMMs stay bf16 on the saved bf16 activations and the bf16 weight shadow.
 
 * **Weights** are quantised with *current* scaling once per optimizer step (amax pass -> scale -> quant,
   three tiny launches), cached against the parameter's version counter like the bf16 shadow.
-* **Activations** use *delayed* scaling: the quantisation kernel records the tensor's amax while it
-  converts with the scale derived from the previous step's amax; one single-thread kernel then forms the
-  GEMM's dequantisation factor (1 / (s_x s_w)) and rolls the scale forward.  No host synchronisation.
+* **Activations** use *delayed* scaling: the quantisation kernel records the tensor's amax (one partial
+  per block, no same-address atomics) while it converts with the scale derived from the previous step's
+  amax; one small kernel then reduces the partials, forms the GEMM's dequantisation factor (1 / (s_x s_w))
+  and rolls the scale forward.  No host synchronisation.
   The very first call primes the scale with a real amax pass.
 """
 from __future__ import annotations
@@ -25,8 +26,10 @@ F32 = torch.float32
 class Fp8Meta:
     """Device-side scaling state of one fp8 GEMM input."""
 
+    AMAX_PARTS = 1024      # per-block partial maxima written by quant_fp8 (csrc/kernels/fp8.hip FP8_AMAX_PARTS)
+
     def __init__(self, device, margin: int = 0):
-        self.amax = torch.zeros(1, device=device, dtype=F32)
+        self.amax = torch.zeros(self.AMAX_PARTS, device=device, dtype=F32)
         self.scale = torch.ones(1, device=device, dtype=F32)
         self.inv = torch.ones(1, device=device, dtype=F32)
         self.gemm_scale = torch.ones(1, device=device, dtype=F32)

@@ -45,8 +45,20 @@ def test_quant_dequant_roundtrip(K):
     assert ((back - x.float()).abs() <= x.float().abs() * 0.07 + 1e-3).all()
 
 
-@pytest.mark.parametrize("M,N,Kd", [(512, 256, 256), (1000, 776, 512), (4096, 3072, 768), (300, 64, 128)])
-def test_gemm_fp8(K, M, N, Kd):
+@pytest.mark.parametrize("pp", [1, 0], ids=["pp", "glds"])
+@pytest.mark.parametrize("M,N,Kd", [(512, 256, 256), (1000, 776, 512), (4096, 3072, 768), (300, 64, 128),
+                                    (8192, 2304, 768), (2000, 768, 3072)])
+def test_gemm_fp8(K, M, N, Kd, pp):
+    """fp8 GEMM on the ping-pong engine (128-byte slices, 3-slot ring) and on the glds engine, against an
+    fp32 product of the dequantised operands; plus the fused BN statistics of the bf16 output."""
+    old = K.set_pp_mode(pp)
+    try:
+        _gemm_fp8_case(K, M, N, Kd)
+    finally:
+        K.set_pp_mode(old)
+
+
+def _gemm_fp8_case(K, M, N, Kd):
     x = torch.randn(M, Kd, device="cuda")
     w = torch.randn(N, Kd, device="cuda") * 0.05
     sx, sw = 448 / x.abs().max(), 448 / w.abs().max()
@@ -60,6 +72,12 @@ def test_gemm_fp8(K, M, N, Kd):
     assert ((y.float() - (ref + b)).norm() / (ref + b).norm()) < 1e-2
     y32 = K.gemm_fp8(xq, wq, scale, out_f32=True)
     assert ((y32 - ref).norm() / ref.norm()) < 1e-4
+    slab = torch.empty(2 * K.stats_rows(M), N, device="cuda")
+    ys = K.gemm_fp8(xq, wq, scale, stats=slab)
+    yf = ys.float()
+    sums = slab.view(-1, 2, N).sum(0)
+    assert torch.allclose(sums[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(sums[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
 
 
 def test_gpt2_tiny_fp8_close_to_bf16_and_trains():
