@@ -108,6 +108,50 @@ __global__ void __launch_bounds__(NT) quant_fp8_kernel(const bf16_t* __restrict_
     }
 }
 
+// Current scaling in two launches and no fill: amax_parts_kernel writes one partial max per block of a fixed
+// FP8_AMAX_PARTS-block grid (every entry overwritten); quant_fp8_cur_kernel reduces the partials in every
+// block, quantises with scale = FP8_MAX / amax * 2^-margin and block 0 stores inv = 1 / scale.
+__global__ void __launch_bounds__(NT) amax_parts_kernel(const bf16_t* __restrict__ x, long n8, float* __restrict__ parts) {
+    float m = 0.f;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+        float v[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(x + 8 * i), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    }
+    m = wave_max(m);
+    __shared__ float sm[NT / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = sm[0];
+        for (int i = 1; i < NT / 64; ++i) t = fmaxf(t, sm[i]);
+        parts[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(NT) quant_fp8_cur_kernel(const bf16_t* __restrict__ x, long n8,
+                                                           const float* __restrict__ parts, uint8_t* __restrict__ out,
+                                                           float* __restrict__ inv, int margin) {
+    float m = 0.f;
+    for (int i = threadIdx.x; i < FP8_AMAX_PARTS; i += NT) m = fmaxf(m, parts[i]);
+    m = wave_max(m);
+    __shared__ float sm[NT / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    float a = sm[0];
+    for (int i = 1; i < NT / 64; ++i) a = fmaxf(a, sm[i]);
+    const float s = a > 0.f ? ldexpf(FP8_MAX / a, -margin) : 1.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) inv[0] = 1.f / s;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+        float v[8];
+        unpack8(*reinterpret_cast<const u16x8_t*>(x + 8 * i), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= s;
+        *reinterpret_cast<uint2*>(out + 8 * i) = f32x8_to_fp8(v);
+    }
+}
+
 // fp32 master weights -> e4m3 with the given scale (the optimizer's fp8 weight shadow)
 __global__ void __launch_bounds__(NT) quant_fp8_f32_kernel(const float* __restrict__ x, long n8,
                                                            const float* __restrict__ scale, uint8_t* __restrict__ out) {
@@ -210,6 +254,17 @@ PDNN_API int pdnn_quant_fp8(const bf16_t* x, long n, const float* scale, uint8_t
     unsigned g = stream_grid(n / 8, NT);
     if (g > FP8_AMAX_PARTS) g = FP8_AMAX_PARTS;
     hipLaunchKernelGGL(quant_fp8_kernel, dim3(g), dim3(NT), 0, st, x, n / 8, scale, out, amax);
+    PDNN_LAUNCH_RET;
+}
+
+// out = e4m3(x * s), s from the tensor's own amax (current scaling), inv[0] = 1 / s; parts: FP8_AMAX_PARTS
+// floats of workspace
+PDNN_API int pdnn_quant_fp8_current(const bf16_t* x, long n, float* parts, uint8_t* out, float* inv, int margin,
+                                    hipStream_t st) {
+    if (n % 8) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(amax_parts_kernel, dim3(FP8_AMAX_PARTS), dim3(NT), 0, st, x, n / 8, parts);
+    hipLaunchKernelGGL(quant_fp8_cur_kernel, dim3(FP8_AMAX_PARTS), dim3(NT), 0, st, x, n / 8, (const float*)parts,
+                       out, inv, margin);
     PDNN_LAUNCH_RET;
 }
 

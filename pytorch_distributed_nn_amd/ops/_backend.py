@@ -95,6 +95,7 @@ _SIGS = {
     "pdnn_fp8_scale": [P, P, P, I, P],
     "pdnn_fp8_scale_step": [P, P, P, P, P, I, P],
     "pdnn_quant_fp8": [P, L, P, P, P, P],
+    "pdnn_quant_fp8_current": [P, L, P, P, P, I, P],
     "pdnn_quant_fp8_f32": [P, L, P, P, P],
     "pdnn_dequant_fp8": [P, L, P, P, P],
 }

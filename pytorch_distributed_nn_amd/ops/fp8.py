@@ -56,20 +56,17 @@ def _weight_version(p):
 
 
 def weight_fp8(p: torch.Tensor, krsc: bool = False):
-    """(e4m3 weight [N][K] (conv: [K][R*S*C]), device inverse scale) cached per parameter version."""
+    """(e4m3 weight [N][K] (conv: [K][R*S*C]), device inverse scale) cached per parameter version.
+    Current scaling (exact amax of this version) in two launches: per-block amax partials, then a quantiser
+    that reduces them itself (no fill, no single-thread scale kernel)."""
     st = getattr(p, "_pdnn_fp8", None)
     ver = _weight_version(p)
     if st is not None and st[0] == ver:
         return st[1], st[2]
     wb = weight_bf16(p, krsc=krsc)
-    w2 = wb.reshape(wb.shape[0], -1)
-    dev = p.device
-    amax = torch.zeros(1, device=dev, dtype=F32)
-    scale = torch.empty(1, device=dev, dtype=F32)
-    inv = torch.empty(1, device=dev, dtype=F32)
-    K.amax_(w2, amax)
-    K.fp8_scale(amax, scale, inv)
-    q = K.quant_fp8(w2.contiguous(), scale)
+    w2 = wb.reshape(wb.shape[0], -1).contiguous()
+    inv = st[2] if st is not None else torch.empty(1, device=p.device, dtype=F32)
+    q = K.quant_fp8_current(w2, inv, out=st[1] if st is not None and st[1].shape == w2.shape else None)
     p._pdnn_fp8 = (ver, q, inv)
     return q, inv
 

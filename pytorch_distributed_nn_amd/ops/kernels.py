@@ -585,6 +585,22 @@ def fp8_scale_step(amax, scale, inv, inv_w, gemm_scale, margin=0):
     call("pdnn_fp8_scale_step", ptr(amax), ptr(scale), ptr(inv), ptr(inv_w), ptr(gemm_scale), int(margin), stream())
 
 
+_FP8_PARTS = {}
+
+
+def quant_fp8_current(x, inv, margin=0, out=None):
+    """e4m3 copy of bf16 ``x`` with current scaling (scale from x's own amax, two launches, no fill);
+    ``inv`` (1 device float) receives 1 / scale."""
+    _chk(x.dtype == BF16 and x.is_contiguous() and x.numel() % 8 == 0, "quant_fp8_current: contiguous bf16")
+    parts = _FP8_PARTS.get(x.device)
+    if parts is None:
+        parts = _FP8_PARTS[x.device] = torch.empty(1024, device=x.device, dtype=F32)
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=U8)
+    call("pdnn_quant_fp8_current", ptr(x), x.numel(), ptr(parts), ptr(out), ptr(inv), int(margin), stream())
+    return out
+
+
 def quant_fp8(x, scale, out=None, amax=None):
     """e4m3(x * scale) as uint8; bf16 input may also record its amax (delayed scaling)."""
     _chk(x.is_contiguous() and x.numel() % 8 == 0, "quant_fp8: contiguous, numel % 8")

@@ -45,6 +45,18 @@ def test_quant_dequant_roundtrip(K):
     assert ((back - x.float()).abs() <= x.float().abs() * 0.07 + 1e-3).all()
 
 
+@pytest.mark.parametrize("n", [8, 4096 * 8 + 8, 768 * 3072])
+def test_quant_current_scaling(K, n):
+    """Two-launch current scaling (amax partials + self-reducing quantiser) = quantise with 448 / amax."""
+    x = (torch.randn(n, device="cuda") * 3).to(torch.bfloat16)
+    inv = torch.empty(1, device="cuda")
+    q = K.quant_fp8_current(x, inv)
+    s = 448.0 / x.float().abs().max()
+    assert abs(inv.item() - 1.0 / s.item()) <= 1e-6 * abs(1.0 / s.item())
+    ref = K.quant_fp8(x, s.reshape(1).float())
+    assert torch.equal(q, ref)
+
+
 @pytest.mark.parametrize("pp", [1, 0], ids=["pp", "glds"])
 @pytest.mark.parametrize("M,N,Kd", [(512, 256, 256), (1000, 776, 512), (4096, 3072, 768), (300, 64, 128),
                                     (8192, 2304, 768), (2000, 768, 3072)])
