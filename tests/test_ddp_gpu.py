@@ -142,9 +142,26 @@ def test_ddp_rccl_kofn_single_rank():
         assert not aborted and rel < 1e-5 and all(c == 1.0 for c in counts), res
 
 
+def _sync_state(dst_net, dst_opt, src_net, src_opt):
+    """dst := src (flat weights + bf16 shadow, BN buffers, momentum)."""
+    dst_net.flat.data.copy_(src_net.flat.data)
+    dst_net.flat.refresh_shadow()
+    for bd, bs in zip(dst_net.module.buffers(), src_net.module.buffers()):
+        bd.copy_(bs)
+    dst = dst_opt.state.setdefault("flat0", {})
+    for k, v in src_opt.state.get("flat0", {}).items():
+        if torch.is_tensor(v) and k in dst:
+            dst[k].copy_(v)
+        else:
+            dst[k] = v.clone() if torch.is_tensor(v) else v
+
+
 def _rccl_graph_job(rank, world):
     """GraphedStep(allow_collectives=True) at world 1 over RCCL: the bucket all-reduces (and the buffer
-    broadcast) are captured into the step's hipGraph; replays match an eager DDP copy of the model."""
+    broadcast) are captured into the step's hipGraph.  Lockstep check: before every replay two eager DDP
+    copies are re-synced to the graphed model; the replay's update must sit within the eager-vs-eager
+    (fp32 atomics) floor of one step — a multi-step trajectory comparison of a BN net at batch 16 is chaotic
+    even between two eager runs."""
     import torch.distributed as dist
     from pytorch_distributed_nn_amd.models import build_model
     from pytorch_distributed_nn_amd.ops import functional as OF
@@ -154,33 +171,42 @@ def _rccl_graph_job(rank, world):
     assert dist.get_backend() == "nccl"
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    ma = build_model("resnet18", 10).to(dev)
-    mb = copy.deepcopy(ma)
-    na = DistributedDataParallel(ma, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
-    nb = DistributedDataParallel(mb, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
-    oa = SGD(ma.parameters(), lr=0.01, momentum=0.9)
-    ob = SGD(mb.parameters(), lr=0.01, momentum=0.9)
+    m0 = build_model("resnet18", 10).to(dev)
+    nets = [DistributedDataParallel(copy.deepcopy(m0), bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
+            for _ in range(3)]
+    opts = [SGD(n.module.parameters(), lr=0.01, momentum=0.9) for n in nets]
+    (na, nc, nb), (oa, oc, ob) = nets, opts
     gstep = GraphedStep(nb, ob, loss_fn=OF.cross_entropy, warmup=2, allow_collectives=True)
     g = torch.Generator().manual_seed(3)
-    data = [(torch.randn(16, 3, 32, 32, generator=g).to(dev), torch.randint(0, 10, (16,), generator=g).to(dev))
-            for _ in range(6)]
-    la, lb = [], []
-    for x, y in data:
-        oa.zero_grad()
-        loss = OF.cross_entropy(na(x), y)
-        loss.backward()
-        oa.step()
-        la.append(float(loss))
-        lb.append(float(gstep(x, y)))
-    torch.cuda.synchronize()
-    rel = ((na.flat.data - nb.flat.data).norm() / na.flat.data.norm()).item()
-    return la, lb, rel, gstep.replays
+    res = []
+    for i in range(7):
+        x = torch.randn(16, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (16,), generator=g).to(dev)
+        if i >= 2:
+            _sync_state(na, oa, nb, ob)
+            _sync_state(nc, oc, nb, ob)
+        before = nb.flat.data.clone()
+        losses = []
+        for n, o in ((na, oa), (nc, oc)) if i >= 2 else ((na, oa),):
+            o.zero_grad()
+            loss = OF.cross_entropy(n(x), y)
+            loss.backward()
+            o.step()
+            losses.append(float(loss.detach()))
+        lg = float(gstep(x, y))
+        torch.cuda.synchronize()
+        if i >= 2:
+            de = (na.flat.data - before).norm()
+            err = ((nb.flat.data - na.flat.data).norm() / de).item()
+            noise = ((nc.flat.data - na.flat.data).norm() / de).item()
+            res.append((i, err, noise, losses[0], lg))
+    return res, gstep.replays
 
 
 def test_graphed_step_captures_rccl_collectives():
-    la, lb, rel, replays = run_world(_rccl_graph_job, 1, (), timeout=600, device=None, backend="nccl",
-                                     env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
-    assert replays >= 3
-    assert rel < 1e-3, rel
-    for a, b in zip(la, lb):
-        assert abs(a - b) / abs(a) < 2e-2, (la, lb)
+    res, replays = run_world(_rccl_graph_job, 1, (), timeout=600, device=None, backend="nccl",
+                             env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
+    assert replays >= 4
+    for i, err, noise, le, lg in res:
+        assert err < 3 * noise + 2e-3, res
+        assert abs(le - lg) < 1e-2 * max(1.0, abs(lg)), res
