@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
     ap.add_argument("--graph", default="auto", choices=["off", "on", "auto", "collectives"],
-                    help="replay each step as one captured hipGraph (auto: single-GPU runs only)")
+                    help="replay each step as one captured hipGraph (auto: single-GPU runs, not the side-stream ResNets)")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -97,7 +97,13 @@ def main():
         xs = [torch.randn(B, *in_chw, device=dev).to(torch.bfloat16) for _ in range(2)]
         ys = [torch.randint(0, nc, (B,), device=dev) for _ in range(2)]
 
-    use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1)
+    # auto: graphed on one GPU, except the ImageNet ResNets, whose weight gradients run on a side stream
+    # concurrently with the data-gradient chain (ops/fused_resnet.py): eager launches overlap the two
+    # streams (ResNet-50 8,635 vs 8,013 img/s serial), a replayed hipGraph ran the branches nearly serially
+    # (8,160-8,196 img/s; gpurun_out/r2_32)
+    side_overlap = not lm and not small and os.environ.get("PDNN_SIDE_WGRAD", "1") != "0"
+    use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1
+                                                                   and not side_overlap)
     if use_graph:
         # whole step (fwd + bwd + optimizer [+ RCCL buckets if 'collectives']) replayed as one hipGraph
         from pytorch_distributed_nn_amd.utils.graphs import GraphedStep

@@ -21,6 +21,8 @@ Fusion plan of a Bottleneck (x -> out):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..optim.flat import direct_grad, grad_ready
@@ -54,13 +56,37 @@ def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
     return t, mean, inv, sc, sh
 
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """The weight-gradient side stream of a device (PDNN_SIDE_WGRAD=0 disables it)."""
+    if os.environ.get("PDNN_SIDE_WGRAD", "1") == "0" or dev.type != "cuda":
+        return None
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 class _Sink:
     """Parameter-gradient routing of one fused backward: gradients go straight into the flat arena
     (optim.flat.direct_grad) when possible — the op then returns None for them and announces them with
-    grad_ready — otherwise they are returned to autograd."""
+    grad_ready — otherwise they are returned to autograd.
 
-    def __init__(self):
+    Weight gradients run on a side HIP stream: a conv's wgrad (dt, x -> dW) and the data-gradient chain
+    (dt -> dgrad -> BN backward -> next dt) are independent, so the split-K wgrad blocks fill the partial
+    last rounds of the dgrad grids (and vice versa) instead of each kernel draining the chip on its own.
+    Each wgrad is ordered after everything queued on the compute stream so far (its operands); `done()`
+    joins the side stream back before the gradients are announced.  The operands stay referenced by the
+    block's backward until that join, so the caching allocator cannot hand their memory out early; a
+    hipGraph capture records the fork/join as graph edges."""
+
+    def __init__(self, device=None):
         self.ready = []
+        self.side = _side_stream(device) if device is not None else None
+        self.forked = False
+        self.returned = False
 
     def acc(self, *ps):
         tg = [direct_grad(p) for p in ps]
@@ -76,6 +102,23 @@ class _Sink:
         return (dg, db), ((None, None) if acc is not None else (dg, db))
 
     def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
+        if self.side is None:
+            return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
+        main = torch.cuda.current_stream(x.device)
+        self.side.wait_stream(main)
+        self.forked = True
+        with torch.cuda.stream(self.side):
+            g = self._wgrad(w_p, x, dy, R, S, st, pad, pro)
+        # the side stream may still read the operands after this block's backward returned (deferred join):
+        # the caching allocator must not hand their memory to the compute stream before that work is done
+        for t in (x, dy) + (tuple(pro) if pro is not None else ()):
+            t.record_stream(self.side)
+        if g is not None:
+            g.record_stream(main)        # allocated on the side stream, consumed by autograd on the main one
+            self.returned = True
+        return g
+
+    def _wgrad(self, w_p, x, dy, R, S, st, pad, pro):
         acc = self.acc(w_p)
         if acc is not None:
             K.conv_wgrad(x, dy, R, S, st, pad, pro=pro, out=acc[0].permute(0, 2, 3, 1))
@@ -83,8 +126,24 @@ class _Sink:
         return _krsc_grad(K.conv_wgrad(x, dy, R, S, st, pad, pro=pro))
 
     def done(self):
+        if self.forked:
+            self.forked = False
+            if self.returned or any(getattr(p, "_pdnn_grad_hooks", None) for p in self.ready):
+                # gradients consumed now (autograd, DDP bucket hooks): join before announcing them
+                torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+            else:
+                # nothing reads them before the optimizer: join once at the end of the backward, so a block's
+                # last weight gradients also overlap the next block's data-gradient chain
+                _join_at_backward_end(self.side)
         for p in self.ready:
             grad_ready(p)
+
+
+def _join_at_backward_end(side):
+    # one callback per block (not a shared "already queued" flag, which an aborted backward would leave set)
+    def join():
+        torch.cuda.current_stream(side.device).wait_stream(side)
+    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 def _conv1x1_bn_fp8(x, w_param, meta, training, bn_params, bufs, mom, eps):
@@ -182,7 +241,7 @@ class BottleneckFn(torch.autograd.Function):
         # block output BN3 (+BNd) with the ReLU mask of `out`
         P = ctx.params
         ctx.params = None
-        sink = _Sink()
+        sink = _Sink(gout.device)
         slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
                                              x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
         (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
@@ -256,7 +315,7 @@ class BasicBlockFn(torch.autograd.Function):
         g2d, t2_2d = gout.view(-1, C2), t2.view(-1, C2)
         P = ctx.params
         ctx.params = None
-        sink = _Sink()
+        sink = _Sink(gout.device)
         slab2, slabd, rows = K.bn_bwd_reduce(g2d, t2_2d, m2, i2, mode=3, msrc=mb,
                                              x2=td.view(-1, C2) if down else None, mean2=md, invstd2=idd)
         (dg2, db2), (rg2, rb2) = sink.bn(slab2, rows, P[4], P[5])

@@ -88,3 +88,39 @@ def test_stem(imagenet):
     assert rel(bn_g.weight.grad, bn.weight.grad) < 1.5e-1
     assert rel(bn_g.bias.grad, bn.bias.grad) < 1.5e-1
     assert rel(bn_g.running_var, bn.running_var) < 2e-2
+
+
+@pytest.mark.parametrize("flat", [True, False])
+def test_side_stream_wgrad_matches_serial(monkeypatch, flat):
+    """Weight gradients on the side stream (deferred join for arena gradients, immediate join for returned
+    ones) == the serial schedule, for a whole ImageNet ResNet-50 at batch 4.  Two back-to-back backwards at
+    the same weights with a zero_grad between them: the second one's zero-fill would race with the first
+    one's side-stream atomics if the end-of-backward join did not hold."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD, flatten_module
+    torch.manual_seed(0)
+    m0 = build_model("resnet50", 1000)
+    ms = [copy.deepcopy(m0).cuda() for _ in range(3)]
+    opts = [None] * 3
+    if flat:
+        for m in ms:
+            flatten_module(m)
+        opts = [SGD(m.parameters(), lr=0.05, momentum=0.9) for m in ms]
+    g = torch.Generator().manual_seed(1)
+    data = [(torch.randn(4, 3, 96, 96, generator=g).cuda().to(torch.bfloat16), torch.randint(0, 1000, (4,), generator=g).cuda())
+            for _ in range(2)]
+    grads = []
+    for side, m, o in zip(("1", "0", "0"), ms, opts):
+        monkeypatch.setenv("PDNN_SIDE_WGRAD", side)
+        for x, y in data:
+            if o is not None:
+                o.zero_grad()
+            else:
+                m.zero_grad()
+            OF.cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads.append(torch.cat([p.grad.float().flatten() for p in m.parameters()]))
+    floor = rel(grads[2], grads[1])          # serial vs serial: fp32 atomics ordering
+    r = rel(grads[0], grads[1])
+    assert r < 10 * floor + 1e-3, (r, floor)
