@@ -59,13 +59,21 @@ def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
 _SIDE = {}
 
 
+def side_stream_if_active(t):
+    """The side stream that may still be writing weight gradients of `t`'s device, else None."""
+    if not t.is_cuda:
+        return None
+    return _SIDE.get(t.device.index)
+
+
 def _side_stream(dev):
     """The weight-gradient side stream of a device (PDNN_SIDE_WGRAD=0 disables it)."""
     if os.environ.get("PDNN_SIDE_WGRAD", "1") == "0" or dev.type != "cuda":
         return None
     s = _SIDE.get(dev.index)
     if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+        # PDNN_SIDE_PRIO: stream priority of the side stream (lower = more urgent; clamped to the device range)
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev, priority=int(os.environ.get("PDNN_SIDE_PRIO", "0")))
     return s
 
 
@@ -128,8 +136,12 @@ class _Sink:
     def done(self):
         if self.forked:
             self.forked = False
-            if self.returned or any(getattr(p, "_pdnn_grad_hooks", None) for p in self.ready):
-                # gradients consumed now (autograd, DDP bucket hooks): join before announcing them
+            if self.returned or not all(getattr(fn, "_pdnn_side_aware", False)
+                                        for p in self.ready for fn in getattr(p, "_pdnn_grad_hooks", ())):
+                # gradients consumed now (autograd, or grad-ready hooks that read them on the compute
+                # stream): join before announcing them.  Side-aware hooks (DDP bucket launches) order their
+                # collectives after the side stream themselves (side_stream_if_active), so the compute
+                # stream is not held up.
                 torch.cuda.current_stream(self.side.device).wait_stream(self.side)
             else:
                 # nothing reads them before the optimizer: join once at the end of the backward, so a block's
@@ -201,6 +213,18 @@ class BottleneckFn(torch.autograd.Function):
         down = len(params) == 12
         w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
         k1, k2, k3 = shadows[:3]
+        side_down = None
+        side = _side_stream(x.device) if (down and os.environ.get("PDNN_SIDE_DOWN", "1") == "1") else None
+        if side is not None:
+            # the shortcut conv only depends on x: run it (and its BN statistics) beside conv1 -> conv2 -> conv3
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                side_down = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]), bufs[6:8],
+                                     mom, eps)
+            x.record_stream(side)
+            for t in side_down:
+                t.record_stream(main)
         if fp8_meta is not None:
             t1, m1, i1, s1, h1 = _conv1x1_bn_fp8(x, w1, fp8_meta, training, (g1, b1), bufs[0:2], mom, eps)
         else:
@@ -213,8 +237,12 @@ class BottleneckFn(torch.autograd.Function):
         t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
         C3 = t3.shape[-1]
         if down:
-            wd, gd, bd = params[9:]
-            td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (gd, bd), bufs[6:8], mom, eps)
+            if side_down is not None:
+                main.wait_stream(side)
+                td, md, idd, sd, hd = side_down
+            else:
+                td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]),
+                                               bufs[6:8], mom, eps)
             out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=td.view(-1, C3), rscale=sd, rshift=hd, relu=True,
                                  want_mask=training)
         else:
