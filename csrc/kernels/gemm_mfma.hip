@@ -37,9 +37,6 @@
 //  * XCD-aware bijective block remap (T1) so neighbouring tiles share an XCD's L2.
 #include "gemm_common.h"
 
-#ifndef PDNN_PF2
-#define PDNN_PF2 0      // register prefetch distance 2 in gemm_kernel (A/B builds: -DPDNN_PF2=1)
-#endif
 
 namespace {
 using namespace pg;
@@ -360,66 +357,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     lb.store(sbase + BMt * BK, rb, tid);
 
     int cur = 0;
-#if PDNN_PF2
-    // Prefetch distance 2: two register sets alternate, so a K-tile's global loads are issued two MFMA phases
-    // before they are written to LDS (one phase of 2x32 MFMAs per wave is shorter than HBM latency under
-    // load).  Loader state always points at the last tile loaded.
-    u16x8_t ra2[LA::NCH], rb2[LB::NCH];
-    if (kt0 + 1 < kt1) {
-        la.advance(a);
-        lb.advance(a);
-        la.load(a, a.K, ra2);
-        lb.load(a, a.K, rb2);
-    }
-    __syncthreads();
-    auto mfma_phase = [&](int buf) {
-        const bf16_t* A_ = sbase + buf * BUF;
-        const bf16_t* B_ = A_ + BMt * BK;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8_t af[4], bfr[FN];
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                if constexpr (AK) af[f] = frag_kmajor(A_, wm * 64 + f * 16 + (lane & 15), ks, lane);
-                else af[f] = frag_mnmajor<128>(A_, wm * 64 + f * 16, ks, lane);
-            }
-#pragma unroll
-            for (int f = 0; f < FN; ++f) {
-                if constexpr (BKm) bfr[f] = frag_kmajor(B_, wn * WTN + f * 16 + (lane & 15), ks, lane);
-                else bfr[f] = frag_mnmajor<BNW>(B_, wn * WTN + f * 16, ks, lane);
-            }
-#pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-                for (int fn = 0; fn < FN; ++fn)
-                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
-        }
-    };
-    // one phase: issue tile kt+2 into (lA, lB), MFMAs of tile kt, write tile kt+1 from (sA, sB) to LDS
-#define PDNN_PF2_PHASE(kt, lA, lB, sA, sB)                                        \
-    {                                                                             \
-        if ((kt) + 2 < kt1) {                                                     \
-            la.advance(a);                                                        \
-            lb.advance(a);                                                        \
-            la.load(a, a.K, lA);                                                  \
-            lb.load(a, a.K, lB);                                                  \
-        }                                                                         \
-        mfma_phase(cur);                                                          \
-        if ((kt) + 1 < kt1) {                                                     \
-            bf16_t* nA = sbase + (cur ^ 1) * BUF;                                 \
-            la.store(nA, sA, tid);                                                \
-            lb.store(nA + BMt * BK, sB, tid);                                     \
-        }                                                                         \
-        __syncthreads();                                                          \
-        cur ^= 1;                                                                 \
-    }
-    for (int kt = kt0; kt < kt1; kt += 2) {
-        PDNN_PF2_PHASE(kt, ra, rb, ra2, rb2)
-        if (kt + 1 >= kt1) break;
-        PDNN_PF2_PHASE(kt + 1, ra2, rb2, ra, rb)
-    }
-#undef PDNN_PF2_PHASE
-#else
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
@@ -458,7 +395,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         __syncthreads();
         cur ^= 1;
     }
-#endif
 
     // ---------------- epilogue ----------------
     // lane holds C[m = mb + (lane&15)][n = nb + 4*(lane>>4) + j] in acc[fm][fn][j]
