@@ -103,8 +103,14 @@ def main():
     # streams (ResNet-50 8,635 vs 8,013 img/s serial), a replayed hipGraph ran the branches nearly serially
     # (8,160-8,196 img/s; gpurun_out/r2_32)
     side_overlap = not lm and not small and os.environ.get("PDNN_SIDE_WGRAD", "1") != "0"
+    # GPT-2 on one GPU: AdamW chunks run on a side stream during the backward (optim/overlap.py)
+    opt_overlap = lm and world == 1 and not use_ddp and os.environ.get("PDNN_OPT_OVERLAP", "0") == "1"
     use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1
-                                                                   and not side_overlap)
+                                                                   and not side_overlap and not opt_overlap)
+    ov = None
+    if opt_overlap:
+        from pytorch_distributed_nn_amd.optim.overlap import BackwardOverlappedStep
+        ov = BackwardOverlappedStep(opt)
     if use_graph:
         # whole step (fwd + bwd + optimizer [+ RCCL buckets if 'collectives']) replayed as one hipGraph
         from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
@@ -116,12 +122,15 @@ def main():
         if use_graph:
             return gstep(xs[i % 2], ys[i % 2])
         opt.zero_grad()
+        if ov is not None:
+            ov.arm()
         if lm:
             loss = net(xs[i % 2], ys[i % 2])
         else:
             loss = OF.cross_entropy(net(xs[i % 2]), ys[i % 2])
         loss.backward()
-        opt.step()
+        if ov is None:
+            opt.step()
         return loss
 
     # The side-stream ResNets run their compute stream at high priority (the side stream stays at the default,
