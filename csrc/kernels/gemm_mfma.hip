@@ -739,20 +739,20 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     PDNN_LAUNCH_RET;
 }
 
+// PDNN_LOWK_BN64=k: GEMMs of at most k K-steps use the 128x64 tile (fewer registers: more blocks per CU
+// to hide the load -> MFMA -> store latency of short reductions); 0 = off.  Default 24 (ResNet-50 bs256,
+// gpurun_out/r2_42-44: off 8,818, k = 1-4 8,930-8,975, 8 8,990, 16 8,963-9,010, 24 8,988 vs 16 8,963 and
+// 36 8,932 on one box, every GEMM 8,930 img/s)
 int g_lowk_bn64 = -1;
 int lowk_bn64_mode() {
-    if (g_lowk_bn64 < 0) { const char* e = getenv("PDNN_LOWK_BN64"); g_lowk_bn64 = e ? atoi(e) : 0; }
+    if (g_lowk_bn64 < 0) { const char* e = getenv("PDNN_LOWK_BN64"); g_lowk_bn64 = e ? atoi(e) : 24; }
     return g_lowk_bn64;
 }
 
-// the register-staged 128-row kernel: N <= 64 -> 128x64 tile, otherwise 128x128
+// the register-staged 128-row kernel only (the weight gradients' split-K atomics): N <= 64 -> 128x64 tile
 template <int AM, int BMODE, int EM, bool PA, bool PB>
-int launch_old(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
+int launch_reg(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
-    // one K-step: the block's life is load -> 32 MFMAs -> store; the 64-wide tile needs 128 VGPRs
-    // (4 blocks/CU instead of 2), which hides the memory latency better
-    if (lowk_bn64_mode() && EM != E_ATOMIC && a.ktiles_per_split <= 1)
-        return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
     return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
 }
 
@@ -768,6 +768,8 @@ int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
         }
     }
     if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
+    if (lowk_bn64_mode() && EM != E_ATOMIC && a.ktiles_per_split <= lowk_bn64_mode())
+        return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
     return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
 }
 
@@ -1102,11 +1104,11 @@ PDNN_API int pdnn_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int N
     a.ktiles_per_split = (int)cdiv(ktiles, splits);
     const int nz = (int)cdiv(ktiles, a.ktiles_per_split);
     if (swap) {
-        if (pro_scale) return launch_old<A_IM2COL, B_MNMAJOR, E_ATOMIC, true, false>(a, nz, stream);
-        return launch_old<A_IM2COL, B_MNMAJOR, E_ATOMIC, false, false>(a, nz, stream);
+        if (pro_scale) return launch_reg<A_IM2COL, B_MNMAJOR, E_ATOMIC, true, false>(a, nz, stream);
+        return launch_reg<A_IM2COL, B_MNMAJOR, E_ATOMIC, false, false>(a, nz, stream);
     }
-    if (pro_scale) return launch_old<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
-    return launch_old<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
+    if (pro_scale) return launch_reg<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, true>(a, nz, stream);
+    return launch_reg<A_MNMAJOR, B_IM2COL, E_ATOMIC, false, false>(a, nz, stream);
 }
 
 // Number of stats rows the fused epilogue writes for M output rows (2 wave-rows per 128-row tile).
