@@ -776,9 +776,11 @@ int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
 template <int BNW>
 int tiles_of(const GemmArgs& a) { return (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW)); }
 
+int g_split_blocks = -1;
 int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
-    // enough workgroups to cover 256 CUs twice, but keep >= 4 K-steps per split
-    int want = (512 + tiles - 1) / tiles;
+    // enough workgroups to cover 256 CUs twice (PDNN_SPLIT_BLOCKS, A/B knob), but keep >= 4 K-steps per split
+    if (g_split_blocks < 0) g_split_blocks = env_int("PDNN_SPLIT_BLOCKS", 512);
+    int want = (g_split_blocks + tiles - 1) / tiles;
     int s = want < max_splits ? want : max_splits;
     int cap = ktiles / 4;
     if (s > cap) s = cap;
