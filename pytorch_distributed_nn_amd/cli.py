@@ -67,6 +67,12 @@ def add_fit_args(p: argparse.ArgumentParser):
     p.add_argument("--inject-hang", type=str, default="",
                    help="RANK:STEP - that rank stops making progress before step STEP on the FIRST attempt only "
                         "(fault injection for the watchdog + restart path; TORCHELASTIC_RESTART_COUNT == 0)")
+    p.add_argument("--save-model-secs", type=float, default=0.0,
+                   help="PS mode: the master checkpoints every N seconds of wall time into --checkpoint-dir, plus a "
+                        "final save (TF Supervisor(save_model_secs) + chief save, distributed_train.py:215-223,346-350)")
+    p.add_argument("--ps-workers", type=int, default=0,
+                   help="PS mode: the number of gradient workers this launch must have (fails loudly otherwise; the "
+                        "r-of-N sweeps need exactly N)")
     p.add_argument("--trace", type=str, default=None)
     p.add_argument("--graph", type=str, default="off", choices=["off", "on", "collectives"],
                    help="replay each training step as one captured hipGraph (utils/graphs.py); 'on' applies to "
@@ -98,6 +104,35 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+# flags each mode does not use: given explicitly (or by a YAML config) with a non-default value they are an
+# error, never silently dropped (a PS sweep config that says "optimizer: adam" must run Adam or fail)
+_PS_IGNORED = ("graph", "straggler_mode", "resume", "watchdog_timeout", "inject_hang", "trace", "metrics",
+               "num_workers", "checkpoint_interval")
+_COLLECTIVE_IGNORED = ("evaluator", "eval_interval", "no_shortcircuit", "save_model_secs", "ps_workers")
+_STRAGGLER_ONLY = ("n_to_collect", "interval_ms", "num_aggregate")
+
+
+def check_mode_flags(args, mode: str, world: int):
+    """Raise SystemExit naming every flag the chosen mode would ignore."""
+    base = vars(add_fit_args(argparse.ArgumentParser()).parse_args([]))
+    given = {k for k, v in vars(args).items() if k in base and v != base[k] and k != "config"}
+    bad = []
+    if mode == "ps":
+        bad += [k for k in _PS_IGNORED if k in given]
+    else:
+        bad += [k for k in _COLLECTIVE_IGNORED if k in given]
+        if args.comm_type in ("Async",) and "comm_type" in given:
+            bad.append("comm_type")
+        if not (mode == "ddp" and args.straggler_mode and world > 1):
+            bad += [k for k in _STRAGGLER_ONLY if k in given]
+        if mode == "single" and "straggler_mode" in given:
+            bad.append("straggler_mode")
+    if bad:
+        flags = ", ".join("--" + k.replace("_", "-") for k in sorted(set(bad)))
+        raise SystemExit(f"--mode {mode} (world size {world}) does not use {flags}: remove them or pick the mode "
+                         f"that implements them")
+
+
 def parse_stragglers(s: str) -> dict:
     out = {}
     for part in filter(None, s.split(",")):
@@ -121,6 +156,7 @@ def main(argv=None):
     world, rank = runtime.world_size(), runtime.rank()
     dev = torch.device("cpu") if args.no_cuda or not torch.cuda.is_available() else runtime.device()
     mode = args.mode or ("single" if world == 1 else ("ddp" if args.comm_type == "AllReduce" else "ps"))
+    check_mode_flags(args, mode, world)
 
     train_ds, test_ds = dataset_from_args(args.dataset, args.data_dir, args.synthetic, dev, args.batch_size,
                                           args.network)
@@ -134,14 +170,25 @@ def main(argv=None):
 
     if mode == "ps":
         from .parallel.ps import PSConfig, run_ps
-        cfg = PSConfig(compute_times=args.compute_times,
+        n_workers = world - (2 if args.evaluator else 1)
+        if args.ps_workers and args.ps_workers != n_workers:
+            raise SystemExit(f"--ps-workers {args.ps_workers}: this launch has {n_workers} workers (world {world} = "
+                             f"master{' + evaluator' if args.evaluator else ''} + workers); launch "
+                             f"{args.ps_workers + world - n_workers} processes")
+        # TF staircase decay counts master updates: decay_steps = batches per epoch * epochs_per_decay / replicas
+        # aggregated per update (distributed_train.py:138)
+        agg = max(1, args.n_to_collect or n_workers)
+        decay_steps = (max(1, int(len(train_ds) // args.batch_size * args.epochs_per_decay / agg))
+                       if args.lr_decay_factor != 1.0 and args.epochs_per_decay > 0 else 0)
+        cfg = PSConfig(compute_times=args.compute_times, log_compute_times=args.compute_times,
                        comm_type=args.comm_type if args.comm_type != "AllReduce" else "Bcast",
                        num_aggregate=args.num_aggregate if args.n_to_collect == 0 else 0,
                        n_to_collect=args.n_to_collect, shortcircuit=not args.no_shortcircuit,
                        interval_ms=args.interval_ms, evaluator=args.evaluator, eval_interval=args.eval_interval,
                        inject_straggler=parse_stragglers(args.inject_straggler), lr=args.lr, momentum=args.momentum,
-                       weight_decay=args.weight_decay, max_steps=args.max_steps or 1000, out_dir=args.out_dir)
-        n_workers = world - (2 if args.evaluator else 1)
+                       weight_decay=args.weight_decay, optimizer=args.optimizer, lr_decay_factor=args.lr_decay_factor,
+                       decay_steps=decay_steps, checkpoint_dir=args.checkpoint_dir or "",
+                       save_model_secs=args.save_model_secs, max_steps=args.max_steps or 1000, out_dir=args.out_dir)
         wrank = max(0, rank - (2 if args.evaluator else 1))
         loader = DataLoader(train_ds, args.batch_size, "cpu", rank=wrank, world=max(1, n_workers))
 

@@ -165,10 +165,14 @@ class SyntheticTokens:
 
 
 # ------------------------------------------------------------------------------------------------ loader
-def _loader_worker(images, labels, transform, index_q, data_q, wid, seed):
+def _loader_worker(images, labels, transform, index_q, data_q, wid, seed, rank=0):
     """Worker process (PT-11 my_data_loader.py:37-53): (seq, indices) -> (seq, x, y), gathered and
-    transformed in this process; None ends it."""
-    np.random.seed(seed + wid)
+    transformed in this process; None ends it.  ``images``/``labels`` arrive as shared-memory tensors (one
+    copy per node, not one pickled copy per worker per rank); the augmentation stream is seeded per rank
+    AND worker, so ranks do not draw identical random crops/flips."""
+    if isinstance(images, torch.Tensor):
+        images, labels = images.numpy(), labels.numpy()
+    np.random.seed((seed + 1000 * rank + wid) % (2 ** 32))
     while True:
         job = index_q.get()
         if job is None:
@@ -207,13 +211,16 @@ class DataLoader:
         self.num_workers = num_workers
         self._procs = []
         if num_workers > 0:
-            import multiprocessing as mp
+            import torch.multiprocessing as mp
             ctx = mp.get_context("spawn")          # workers never touch the GPU; spawn is fork-safe with HIP
             self._index_qs = [ctx.Queue() for _ in range(num_workers)]
             self._data_q = ctx.Queue(maxsize=max(2, prefetch) * num_workers)
+            # shared-memory tensors pickle as handles: every worker maps the same pages
+            shm_x = torch.from_numpy(np.ascontiguousarray(dataset.images)).share_memory_()
+            shm_y = torch.from_numpy(np.ascontiguousarray(dataset.labels)).share_memory_()
             for w in range(num_workers):
-                p = ctx.Process(target=_loader_worker, args=(dataset.images, dataset.labels, transform,
-                                                             self._index_qs[w], self._data_q, w, seed), daemon=True)
+                p = ctx.Process(target=_loader_worker, args=(shm_x, shm_y, transform, self._index_qs[w],
+                                                             self._data_q, w, seed, rank), daemon=True)
                 p.start()
                 self._procs.append(p)
             self._sampler_rng = np.random.RandomState(seed)

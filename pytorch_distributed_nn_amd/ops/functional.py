@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from ..optim.flat import direct_grad, grad_ready
+from ..optim.flat import await_param, direct_grad, grad_ready
 from . import kernels as K
 
 BF16 = torch.bfloat16
@@ -26,6 +26,7 @@ BF16 = torch.bfloat16
 # ------------------------------------------------------------------------------------------------
 def weight_bf16(p: torch.Tensor, krsc: bool = False) -> torch.Tensor:
     """bf16 copy of parameter ``p`` for the kernels ([K][R][S][C] for 4-D conv weights if krsc)."""
+    await_param(p)
     sh = getattr(p, "_pdnn_shadow", None)
     if sh is not None and getattr(p, "_pdnn_shadow_ver", None) == p._version:
         return sh

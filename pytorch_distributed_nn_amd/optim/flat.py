@@ -78,6 +78,21 @@ class FlatParams:
             self.shadow.copy_(self.data)
         self.mark_shadow_fresh()
 
+    def refresh_shadow_range(self, start, end):
+        """Re-cast one slice [start, end) of the arena (a weight bucket that just arrived) and mark the
+        parameters inside it fresh."""
+        if self.shadow is None:
+            return
+        if self.data.is_cuda:
+            from ..ops import kernels as K
+            K.cast_f32_bf16(self.data[start:end], self.shadow[start:end])
+        else:
+            self.shadow[start:end].copy_(self.data[start:end])
+        self.generation += 1
+        for p, o in zip(self.params, self.offsets):
+            if start <= o < end:
+                p._pdnn_shadow_ver = p._version
+
     def mark_shadow_fresh(self):
         self.generation += 1
         for p in self.params:
@@ -158,6 +173,14 @@ def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatPar
 # Only for parameters used ONCE per forward (a tied weight's contributions are summed by autograd).
 # ------------------------------------------------------------------------------------------------
 DIRECT_GRAD = os.environ.get("PDNN_DIRECT_GRAD", "1") == "1"
+
+
+def await_param(p):
+    """Block until ``p``'s weights are current: a PS worker receiving weights bucket by bucket installs
+    ``p._pdnn_await`` (parallel/ps.py); everywhere else this is one dict lookup."""
+    w = p.__dict__.get("_pdnn_await")
+    if w is not None:
+        w(p)
 
 
 def direct_grad(p):

@@ -227,9 +227,9 @@ class Adam(_FusedBase):
                     p.mul_(1 - lr * wd)
                 elif wd:
                     g = g.add(p, alpha=wd)
-                st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+                st["exp_avg"].lerp_(g, 1 - b1)
                 st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
-                denom = (st["exp_avg_sq"] / (1 - b2 ** t)).sqrt_().add_(eps)
+                denom = (st["exp_avg_sq"].sqrt() / math.sqrt(1 - b2 ** t)).add_(eps)    # torch.optim.Adam's order
                 p.addcdiv_(st["exp_avg"], denom, value=-lr / (1 - b1 ** t))
         return loss
 

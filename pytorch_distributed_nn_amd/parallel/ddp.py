@@ -73,6 +73,7 @@ class _KofN:
         self.prefix = f"pdnn_kofn/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/{_KofN._instances}"
         mk = lambda: dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=3600))  # noqa: E731
         self.store, self.wstore = mk(), mk()
+        warm_abort_path()
         dist.barrier(group=ddp.pg)                # every rank's clients exist before the first step
         self.abort_step = -1                      # written by the watcher, read by the gradient hooks
         self.done_step = 0
@@ -80,6 +81,7 @@ class _KofN:
         self._stop = False
         self._cv = threading.Condition()
         self._begun = 0
+        self._t_begin = {}                        # step -> monotonic begin time (deadline thread)
         self.thread = threading.Thread(target=self._watch, daemon=True)
         self.thread.start()
         if deadline_ms and ddp.rank == 0:         # rank 0 closes a step when its deadline passes
@@ -92,7 +94,8 @@ class _KofN:
     def begin(self, step):
         with self._cv:
             self._begun = step
-            self._t_begin = time.monotonic()
+            self._t_begin[step] = time.monotonic()
+            self._t_begin.pop(step - 8, None)
             self._cv.notify_all()
 
     def report_done(self, step):
@@ -106,6 +109,9 @@ class _KofN:
         # by the deadline, or by stop()) -- no polling traffic
         step = 1
         while not self._stop:
+            # a step this rank has already left is over everywhere (its collectives completed): never wait on
+            # its key, which cleanup() may already have deleted
+            step = max(step, self._begun)
             try:
                 self.wstore.wait([self.key(step, "closed")])
             except Exception:
@@ -118,17 +124,30 @@ class _KofN:
             self.watch_step = step
 
     def _deadline(self):
+        # Handles the NEWEST begun step only: steps that began while this thread slept are over (closed by
+        # their k-th finisher) or superseded, so it jumps straight to the latest one instead of walking a
+        # backlog one deadline at a time, which made a later straggler step's deadline fire late and re-set
+        # keys cleanup() had already deleted.
         step = 1
         while not self._stop:
             with self._cv:
                 while self._begun < step and not self._stop:
                     self._cv.wait(1.0)
-                t0 = self._t_begin
+                if self._stop:
+                    return
+                step = max(step, self._begun)
+                t0 = self._t_begin.get(step, time.monotonic())
+            try:
+                if self.store.check([self.key(step, "closed")]):
+                    step += 1                     # already closed by the k-th finisher: no deadline needed
+                    continue
+            except Exception:
+                return
             rest = self.deadline_ms / 1e3 - (time.monotonic() - t0)
             if rest > 0:
                 time.sleep(rest)
             try:
-                if not self.store.check([self.key(step, "closed")]):
+                if self._begun == step and not self.store.check([self.key(step, "closed")]):
                     self.store.set(self.key(step, "closed"), "deadline")
             except Exception:
                 return
@@ -150,6 +169,24 @@ class _KofN:
             pass
         with self._cv:
             self._cv.notify_all()
+
+
+def warm_abort_path(exc_type=None):
+    """Raise and catch one exception from inside an autograd hook.  The FIRST exception that crosses the
+    autograd engine costs ~0.3 s of one-time setup on this torch build (0.001 s afterwards): paid here, at
+    construction, instead of delaying the first real straggler abort by that much."""
+    exc_type = exc_type or StepAborted
+    w = torch.ones(1, requires_grad=True)
+
+    def boom(_p):
+        raise exc_type("warm-up")
+    h = w.register_post_accumulate_grad_hook(boom)
+    try:
+        (w * 2).sum().backward()
+    except exc_type:
+        pass
+    finally:
+        h.remove()
 
 
 def _is_nccl(pg):
@@ -379,6 +416,10 @@ class DistributedDataParallel(nn.Module):
         while self._next < len(self.buckets):      # unused parameters, or everything after an abort
             self._launch(self._next, zero=self._aborted)
             self._next += 1
+        if self.kofn is not None and not self._aborted and self.kofn.done_step < self.step:
+            # buckets of parameters without a gradient launch only here: this rank's gradient is now complete
+            # (otherwise no rank reports and the k-th-finisher close never fires)
+            self.kofn.report_done(self.step)
         fp = self.flat
         if self.straggler_mode:
             # per-bucket contributor counts: all-reduced after the buckets (same collective order everywhere)

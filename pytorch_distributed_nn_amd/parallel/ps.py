@@ -4,10 +4,25 @@ Reference behaviour reproduced (defec
 
 * roles: rank 0 = master (PT-02 SyncReplicasMaster_NN / CPP-03), optional rank 1 = evaluator (CPP-05,
   TF-06), the rest = workers (PT-03 DistributedWorker / CPP-04 WorkerNN).
-* weight push every step: ``comm_type="Bcast"`` — ONE broadcast of the flat fp32 weight arena from the
+* **layer-pipelined weight push** every step, in FORWARD bucket order (the reverse of the gradient
+  buckets): ``comm_type="Bcast"`` — one broadcast per bucket of the flat fp32 weight arena from the
   master (reference: one MPI Bcast per parameter, sync_replicas_master_nn.py:259-272);
-  ``comm_type="Async"`` — point-to-point sends of the flat arena to each worker (reference Isend per
-  parameter per worker, :243-257).
+  ``comm_type="Async"`` — point-to-point sends of each bucket to each worker (reference Isend per
+  parameter per worker, :243-257; the C++ master's per-layer Isend tagged with the step,
+  MPI_code/src/distributed/sync_replicas_master_nn.h:193-211).  A worker posts every bucket's receive at
+  once and a forward pre-hook on each module waits only for the bucket(s) holding that module's weights,
+  so layer i computes while the weights of layers > i are still in flight (the C++ worker's
+  ``MPI_Wait`` on layer i's request just before computing layer i, worker_nn.h:66-70).
+* **optimizer parity**: the master applies the averaged gradient with the configured fused optimizer —
+  SGD (momentum / weight decay), Adam or AdamW — and the TF trainer's exponential staircase LR decay
+  (``lr * factor ** (step // decay_steps)``; distributed_TF/src/distributed_train.py:143-147,160-173; the
+  wrapped optimizer applies the aggregated gradient, sync_replicas_optimizer_modified.py:363-410).
+* **checkpointing on the master** (TF ``Supervisor(save_model_secs=...)`` plus the chief's final save,
+  distributed_train.py:215-223,346-350): every ``save_model_secs`` of wall time and once at the end.
+* **live compute-time side channel** (TF-04 TimeoutServer, timeout_manager.py:48-70,132-162): each
+  worker's end-of-step marker carries its dequeue->finish compute time; the master logs the sorted
+  per-step ELAPSED times of all workers while the run is in progress (``log_compute_times``) and keeps
+  them in its per-step log.
 * **gradient streaming per bucket**: the worker's gradient arena is cut into reverse-order buckets (the
   order backward produces them, as the DDP wrapper does); a post-accumulate-grad hook sends each bucket
   to the master the moment its last parameter is ready (reference: every parameter is Isent as soon as
@@ -61,6 +76,31 @@ class StepAborted(RuntimeError):
     """Raised inside a worker's backward to abandon a step (kill signal or a newer step)."""
 
 
+class _WeightUseMode(torch.overrides.TorchFunctionMode):
+    """Active during a PS worker's forward while weight buckets are still in flight: a torch op that takes
+    a parameter whose bucket has not landed yet waits for that bucket first (``p._pdnn_await``)."""
+
+    def __init__(self, pending):
+        super().__init__()
+        self.pending = pending
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if self.pending:
+            for a in list(args) + list(kwargs.values()):
+                for t in (a if isinstance(a, (list, tuple)) else (a,)):
+                    if isinstance(t, torch.nn.Parameter):
+                        w = t.__dict__.get("_pdnn_await")
+                        if w is not None:
+                            w(t)
+        return func(*args, **kwargs)
+
+
+def _nullcontext():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 @dataclass
 class PSConfig:
     comm_type: str = "Bcast"          # "Bcast" | "Async"
@@ -74,12 +114,42 @@ class PSConfig:
     lr: float = 0.01
     momentum: float = 0.0
     weight_decay: float = 0.0
+    optimizer: str = "sgd"            # "sgd" | "adam" | "adamw" (applied by the master)
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    lr_decay_factor: float = 1.0      # staircase decay: lr * factor ** (step // decay_steps)
+    decay_steps: int = 0              # 0 = constant lr
     max_steps: int = 100
     out_dir: str = "outfiles"
     store_port: int = 0               # 0 = MASTER_PORT + 1
     bucket_cap_mb: float = 4.0        # gradient streaming granularity
     first_bucket_mb: float = 0.25
     compute_times: bool = False       # workers write compute_times_rank<r>.jsonl (TF-04 side channel)
+    log_compute_times: bool = False   # master prints the sorted per-step worker compute times (live)
+    pipelined_push: bool = True       # per-bucket weight push + per-module waits (False: one transfer)
+    push_delay_ms: float = 0.0        # fault injection: master pauses between weight buckets (slow link)
+    checkpoint_dir: str = ""          # master checkpoints here every save_model_secs and at the end
+    save_model_secs: float = 0.0
+
+
+def make_optimizer(params, cfg: PSConfig):
+    """The master's optimizer over the flat arena (fused kernel on GPU, torch reference on CPU)."""
+    from ..optim import SGD, Adam, AdamW
+    if cfg.optimizer == "sgd":
+        return SGD(params, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay)
+    if cfg.optimizer == "adam":
+        return Adam(params, lr=cfg.lr, betas=tuple(cfg.betas), eps=cfg.eps, weight_decay=cfg.weight_decay)
+    if cfg.optimizer == "adamw":
+        return AdamW(params, lr=cfg.lr, betas=tuple(cfg.betas), eps=cfg.eps, weight_decay=cfg.weight_decay)
+    raise ValueError(f"PSConfig.optimizer: unknown optimizer {cfg.optimizer!r}")
+
+
+def staircase_lr(cfg: PSConfig, step: int) -> float:
+    """Learning rate of 1-based master step ``step`` (TF exponential_decay(staircase=True) of global_step =
+    step - 1, distributed_train.py:143-147)."""
+    if cfg.decay_steps <= 0 or cfg.lr_decay_factor == 1.0:
+        return cfg.lr
+    return cfg.lr * cfg.lr_decay_factor ** ((step - 1) // cfg.decay_steps)
 
 
 def _store_port(cfg: PSConfig) -> int:
@@ -107,20 +177,52 @@ class _Base:
         dist.barrier()
         self.host = os.environ.get("MASTER_ADDR", "127.0.0.1")
         self.store = Store(self.host, _store_port(cfg))
+        self._pending, self._land = {}, {}
+
+    def _weight_buckets(self):
+        """Weight-push units in forward order: the gradient buckets reversed (one unit when not pipelined)."""
+        if not self.cfg.pipelined_push:
+            return [(-1, 0, self.flat.numel)]
+        return [(b, s, e) for b, (s, e, _) in reversed(list(enumerate(self.buckets)))]
 
     def _push_weights(self, step: int):
-        """Master -> everyone: the flat fp32 weight arena."""
-        if self.cfg.comm_type == "Bcast":
-            dist.broadcast(self.flat.data, 0)
-        else:
-            if self.rank == 0:
-                reqs = [dist.isend(self.flat.data, r) for r in range(1, self.world)]
-                for q in reqs:
-                    q.wait()
+        """Master: send the flat fp32 weight arena bucket by bucket in forward order, then wait."""
+        works = []
+        for i, (b, s, e) in enumerate(self._weight_buckets()):
+            if self.cfg.push_delay_ms and i:
+                time.sleep(self.cfg.push_delay_ms / 1e3)
+            view = self.flat.data[s:e]
+            if self.cfg.comm_type == "Bcast":
+                works.append(dist.broadcast(view, 0, async_op=True))
             else:
-                dist.recv(self.flat.data, 0)
-        if self.rank != 0:
-            self.flat.refresh_shadow()
+                works += [dist.isend(view, r) for r in range(1, self.world)]
+        for w in works:
+            w.wait()
+
+    def _post_weight_recvs(self):
+        """Receivers: post every bucket's receive at once -> {bucket: work}.  :meth:`_wait_bucket` completes
+        one (and refreshes that slice of the bf16 shadow); nothing else blocks."""
+        self._pending = {}
+        self._land = {}
+        for b, s, e in self._weight_buckets():
+            view = self.flat.data[s:e]
+            if self.cfg.comm_type == "Bcast":
+                self._pending[b] = dist.broadcast(view, 0, async_op=True)
+            else:
+                self._pending[b] = dist.irecv(view, 0)
+
+    def _wait_bucket(self, b):
+        w = self._pending.pop(b, None)
+        if w is None:
+            return
+        w.wait()
+        s, e = (0, self.flat.numel) if b < 0 else self.buckets[b][:2]
+        self.flat.refresh_shadow_range(s, e)
+        self._land[b] = time.perf_counter()
+
+    def _wait_all_weights(self):
+        for b in list(self._pending):
+            self._wait_bucket(b)
 
     def close(self):
         dist.barrier()
@@ -135,10 +237,9 @@ class PSMaster(_Base):
 
     def __init__(self, model, cfg, device):
         super().__init__(model, cfg, device)
-        from ..optim import SGD
         # coordinator layers = buckets in reverse, so layer 0 is the LAST bucket (parameter 0: the sentinel)
         self.coord = PSCoordinator(self.n_workers, self.nb, cfg.n_to_collect, cfg.num_aggregate)
-        self.opt = SGD(self.flat.params, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay)
+        self.opt = make_optimizer(self.flat.params, cfg)
         big = max(e - s for s, e, _ in self.buckets)
         self.stage = torch.zeros(big, dtype=torch.float32, device=self.flat.grad.device)
         self.qpos = 0                          # next arrival-queue entry to read
@@ -146,15 +247,16 @@ class PSMaster(_Base):
         self.store.set("scheme", self.scheme)
 
     def _next_arrival(self, timeout_ms):
-        """(worker rank, step, bucket) of the next queued send, or None on timeout."""
+        """(worker rank, step, bucket, compute_ms) of the next queued send, or None on timeout."""
         try:
             v = self.store.get(f"q/{self.qpos + 1}", timeout_ms=timeout_ms)
         except StoreTimeout:
             return None
         self.qpos += 1
         self.store.delete(f"q/{self.qpos}")
-        r, s, b = (int(t) for t in v.decode().split(","))
-        return r, s, b
+        f = v.decode().split(",")
+        # end-of-step markers carry the worker's compute time (live TF-04 side channel) as a 4th field
+        return int(f[0]), int(f[1]), int(f[2]), (float(f[3]) if len(f) > 3 else None)
 
     def _receive(self, r, b):
         s, e, _ = self.buckets[b]
@@ -162,25 +264,38 @@ class PSMaster(_Base):
         dist.recv(buf, r)
         return buf
 
+    def _save(self, step, final=False):
+        from ..utils.observability import save_checkpoint
+        name = "checkpoint_final.pt" if final else f"checkpoint_step{step}.pt"
+        path = save_checkpoint(os.path.join(self.cfg.checkpoint_dir, name), self.model, self.opt, step=step,
+                               extra={"scheme": self.scheme})
+        self.saved.append((step, path))
+        return path
+
     def train(self):
         cfg = self.cfg
         t0 = time.perf_counter()
+        self.saved = []
+        last_save = t0
         for step in range(1, cfg.max_steps + 1):
             self.store.set_int(f"go/{step}", step)              # step broadcast (C-01 / C-08)
-            self._push_weights(step)                            # C-02 / C-03
+            self._push_weights(step)                            # C-02 / C-03, layer-pipelined
             self.coord.begin_step(step)
             self.flat.grad.zero_()
             tstep = time.perf_counter()
             closed, stale, ended = False, 0, set()
+            ctimes = {}
 
             def take(timeout):
                 nonlocal closed, stale
                 a = self._next_arrival(timeout)
                 if a is None:
                     return
-                r, s, b = a
+                r, s, b, cms = a
                 if b < 0:                                       # end-of-step marker of worker r
-                    ended.add(r) if s == step else None
+                    if s == step:
+                        ended.add(r)
+                        ctimes[r] = cms
                     return
                 g = self._receive(r, b)
                 tms = (time.perf_counter() - t0) * 1e3
@@ -215,13 +330,26 @@ class PSMaster(_Base):
             for b, (bs, be, _) in enumerate(self.buckets):
                 if counts[b] > 1:
                     self.flat.grad[bs:be].mul_(1.0 / counts[b])
+            lr = staircase_lr(cfg, step)
+            for g in self.opt.param_groups:
+                g["lr"] = lr
             self.opt.step()
             arrived = [w for i, w in enumerate(self.workers)
                        if all(self.coord.contributed(li, i) for li in range(self.nb))]
+            elapsed = sorted(v for v in ctimes.values() if v is not None)
             self.log.append({"step": step, "arrived": arrived, "count": min(counts), "bucket_counts": counts,
-                             "stale_dropped": stale, "gather_ms": (time.perf_counter() - tstep) * 1e3})
+                             "stale_dropped": stale, "gather_ms": (time.perf_counter() - tstep) * 1e3, "lr": lr,
+                             "compute_ms": elapsed})
+            if cfg.log_compute_times:      # timeout_manager.py:48-70 "ELAPSED TIMES" line, live
+                print(f"Master: step {step} ELAPSED TIMES (ms, sorted over workers) "
+                      f"{[round(v, 2) for v in elapsed]}", flush=True)
+            if cfg.checkpoint_dir and cfg.save_model_secs > 0 and time.perf_counter() - last_save >= cfg.save_model_secs:
+                self._save(step)
+                last_save = time.perf_counter()
         self.store.set_int(f"go/{cfg.max_steps + 1}", -1)
         self._push_weights(cfg.max_steps + 1)       # final weights, so evaluator/workers end consistent
+        if cfg.checkpoint_dir:                      # the chief's final save (distributed_train.py:346-350)
+            self._save(cfg.max_steps, final=True)
         os.makedirs(cfg.out_dir, exist_ok=True)
         with open(os.path.join(cfg.out_dir, f"timeline_out_{self.scheme}"), "w") as f:
             for t, s, w, li in self.coord.timeline():      # time_ms step worker bucket (arrival timeline)
@@ -241,13 +369,38 @@ class PSWorker(_Base):
         self.abort_step = -1
         self.done_step = 0
         self._hooks = [register_grad_ready_hook(p, self._param_done) for p in self.flat.params]
+        self._fwd_hooks = self._install_weight_waits()
+        self.fwd_start = {}                 # step -> time the first module's forward began (timeline)
+        self.landed = {}                    # step -> {weight bucket: time its receive completed}
         self.aborted_steps = 0
         self.compute_records = []
         self.sent = []                      # (step, bucket) in send order (tests / timeline)
         self._stop = False
         self.wstore = Store(self.host, _store_port(cfg))    # the watcher's own connection
+        from .ddp import warm_abort_path
+        warm_abort_path(StepAborted)        # the first exception through autograd costs ~0.3 s once
         self._watcher = threading.Thread(target=self._watch, daemon=True)
         self._watcher.start()
+
+    def _install_weight_waits(self):
+        """Per-parameter waits: the first use of a parameter in the forward blocks on the weight bucket that
+        holds it and nothing else (the C++ worker's per-layer MPI_Wait just before computing the layer,
+        worker_nn.h:66-70).  A use is (a) the bf16 shadow fetch of every fused GPU op (``weight_bf16`` calls
+        :func:`~..optim.flat.await_param`), and (b) any torch op taking the parameter as an argument, caught
+        by :class:`_WeightUseMode` around the worker's forward."""
+        if not self.cfg.pipelined_push:
+            return []
+        for p in self.flat.params:
+            p._pdnn_await = self._before_param
+        return list(self.flat.params)
+
+    def _before_param(self, p):
+        b = self.pbucket.get(id(p))
+        if b is None or b not in self._pending:
+            return
+        if self.cur not in self.fwd_start:
+            self.fwd_start[self.cur] = time.perf_counter()
+        self._wait_bucket(b)
 
     def _watch(self):
         # blocks on each step's kill key in turn (always published when the master closes the step)
@@ -297,7 +450,9 @@ class PSWorker(_Base):
         it = iter(batches)
         while True:
             s = self.store.get_int(f"go/{self.cur + 1}")      # blocks until the master opens the step
-            self._push_weights(s)
+            self._post_weight_recvs()                         # every bucket in flight; layers wait per bucket
+            if not self.cfg.pipelined_push or s == -1:
+                self._wait_all_weights()
             if s == -1:
                 break
             self.cur = s
@@ -306,7 +461,11 @@ class PSWorker(_Base):
             self.flat.zero_grad()
             self._ready, self._next, self._works, self._events, self._aborted = [0] * self.nb, 0, [], [], False
             try:
-                loss = self.loss_fn(self.model(x.to(self.device)), y.to(self.device))
+                with _WeightUseMode(self._pending) if self.cfg.pipelined_push else _nullcontext():
+                    out = self.model(x.to(self.device))
+                self._wait_all_weights()                      # buckets no module claimed (and the backward's)
+                self.landed[s] = dict(self._land)
+                loss = self.loss_fn(out, y.to(self.device))
                 loss.backward()
                 self.done_step = s
             except StepAborted:
@@ -314,9 +473,10 @@ class PSWorker(_Base):
             self.compute_records.append({"rank": self.rank, "step": s, "t_dequeue": t_deq,
                                          "t_finish": time.perf_counter(), "aborted": self.done_step != s,
                                          "compute_ms": 1e3 * (time.perf_counter() - t_deq)})
-            # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped)
+            # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped); it
+            # carries the dequeue -> finish compute time, the master's live per-step ELAPSED TIMES
             n = self.store.add("q_n", 1)
-            self.store.set(f"q/{n}", f"{self.rank},{s},-1")
+            self.store.set(f"q/{n}", f"{self.rank},{s},-1,{self.compute_records[-1]['compute_ms']:.4f}")
             for w in self._works:
                 w.wait()
         self._stop = True
@@ -354,7 +514,8 @@ class PSEvaluator(_Base):
             while True:
                 s = self.store.get_int(f"go/{cur + 1}")
                 cur += 1
-                self._push_weights(s)
+                self._post_weight_recvs()
+                self._wait_all_weights()
                 final = s == -1
                 if final or s % self.cfg.eval_interval == 0:
                     loss, err = self.eval_fn(self.model)

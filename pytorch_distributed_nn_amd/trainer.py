@@ -111,6 +111,10 @@ class Trainer:
         for ep in range(self.epoch, epochs):
             self.epoch = ep
             start, first_i = (first_i if first_i < n_per_epoch else 0), 0
+            for _ in range(start):
+                # mid-epoch resume: the loader restarts its stream, so consume the batches the checkpointed
+                # run already trained on; the step count, LR schedule and data then agree again
+                next(it)
             for i in range(start, n_per_epoch):
                 tf = time.perf_counter()
                 x, y = next(it)

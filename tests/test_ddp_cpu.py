@@ -235,6 +235,40 @@ def test_ddp_step_deadline_drops_late_rank():
     assert not any(a for a, _, _ in out[0])
 
 
+def _deadline_after_fast_steps(rank, world):
+    import time
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    m = build_model("mlp2", 10)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.5, first_bucket_cap_mb=0.05, deadline_ms=120.0)
+    slow = {"on": False}
+    if rank == 1:
+        for p in m.parameters():
+            p.register_post_accumulate_grad_hook(lambda _p: time.sleep(0.4) if slow["on"] else None)
+    res = []
+    for step in range(26):
+        slow["on"] = step == 25
+        x, y = torch.randn(8, 784), torch.randint(0, 10, (8,))
+        ddp.zero_grad()
+        t0 = time.perf_counter()
+        aborted = ddp.backward(OF.cross_entropy(ddp(x), y))
+        res.append((aborted, time.perf_counter() - t0))
+    ddp.close()
+    return res
+
+
+def test_ddp_deadline_fires_on_time_after_many_fast_steps():
+    """25 steps that finish well inside the 120 ms deadline, then one slow step on rank 1.  The
+    deadline thread must close the slow step ~120 ms after it began (it used to walk the backlog of fast
+    steps one deadline each and fire seconds late)."""
+    out = run_world(_deadline_after_fast_steps, 2)
+    aborted, dt = out[1][-1]
+    assert aborted and dt < 0.5, out[1][-3:]          # 4 params x 0.4 s = 1.6 s without the deadline
+    assert not any(a for a, _ in out[1][:-1])
+
+
 def _world4_consistency(rank, world):
     """Fused-backward DDP at world 4: after the all-reduce every rank holds BIT-identical gradients,
     buckets launch in the same order everywhere, and BN running statistics stay identical (buffers are

@@ -160,3 +160,147 @@ def test_ps_interval_without_shortcircuit_drops_late_worker():
         assert 3 not in r["arrived"], r                  # the straggler never delivers a full gradient
         assert min(r["bucket_counts"]) < 3, r            # its late buckets (the first layers) were dropped
     assert res[3] == 0                                   # and it was never aborted (short-circuit off)
+
+
+# ---------------------------------------------------------------------------------------------- round 3
+def _ps_opt_job(rank, world, cfg_kw, out_dir, steps):
+    """Workers take different batches (rank-dependent), so the master's averaged gradient is a real mean."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    model = build_model("mlp2", 10)
+    x, y = _data()
+    cfg = PSConfig(max_steps=steps, out_dir=out_dir, **cfg_kw)
+
+    def batches():
+        i = 0
+        while True:
+            j = 2 * i + (rank - 1)
+            yield x[j * 32:(j + 1) * 32], y[j * 32:(j + 1) * 32]
+            i += 1
+
+    res = run_ps(model, cfg, torch.device("cpu"), loss_fn=OF.cross_entropy, batches=batches())
+    w = torch.cat([p.detach().flatten() for p in model.parameters()])
+    return res, w
+
+
+def _reference_run(opt_name, steps, lr, decay=(1.0, 0)):
+    """Single process: the same model, the mean of the two workers' gradients, torch's optimizer."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    torch.manual_seed(0)
+    model = build_model("mlp2", 10)
+    x, y = _data()
+    opt = {"adam": lambda ps: torch.optim.Adam(ps, lr=lr), "adamw": lambda ps: torch.optim.AdamW(ps, lr=lr, weight_decay=0.0),
+           "sgd": lambda ps: torch.optim.SGD(ps, lr=lr)}[opt_name](list(model.parameters()))
+    factor, dsteps = decay
+    for i in range(steps):
+        grads = []
+        for r in (1, 2):
+            j = 2 * i + (r - 1)
+            model.zero_grad()
+            OF.cross_entropy(model(x[j * 32:(j + 1) * 32]), y[j * 32:(j + 1) * 32]).backward()
+            grads.append([p.grad.clone() for p in model.parameters()])
+        for p, g1, g2 in zip(model.parameters(), *grads):
+            p.grad = (g1 + g2) * 0.5
+        for g in opt.param_groups:
+            g["lr"] = lr * factor ** (i // dsteps) if dsteps else lr
+        opt.step()
+    return torch.cat([p.detach().flatten() for p in model.parameters()])
+
+
+@pytest.mark.parametrize("opt_name", ["adam", "adamw"])
+def test_ps_master_adam_equals_single_process(opt_name):
+    """PS mode applies the configured optimizer (TF SyncReplicas wraps Adam,
+    distributed_train.py:160-173); 3 steps of 2-worker full sync == single-process torch Adam on the mean
+    gradient."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_opt_job, 3, ({"optimizer": opt_name, "lr": 1e-3}, out, 3))
+    ref = _reference_run(opt_name, 3, 1e-3)
+    for r in res:
+        # a handful of near-zero-gradient elements differ by < 3% of one lr step (Adam's m / (sqrt(v) + eps)
+        # amplifies last-bit differences of the summation order there); everything else matches to 1e-6
+        torch.testing.assert_close(r[1], ref, rtol=1e-5, atol=3e-5)
+        assert (r[1] - ref).abs().gt(1e-6).sum() < 20
+
+
+def test_ps_master_staircase_lr():
+    """TF exponential_decay(staircase=True): lr * factor ** (step // decay_steps), applied by the master."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_opt_job, 3, ({"optimizer": "sgd", "lr": 0.1, "lr_decay_factor": 0.5, "decay_steps": 2},
+                                     out, 5))
+    assert [round(r["lr"], 6) for r in res[0][0]] == [0.1, 0.1, 0.05, 0.05, 0.025]
+    ref = _reference_run("sgd", 5, 0.1, decay=(0.5, 2))
+    torch.testing.assert_close(res[0][1], ref, rtol=1e-5, atol=1e-6)
+
+
+def _ps_pipe_job(rank, world, cfg_kw, out_dir, steps):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, PSMaster, PSWorker
+    torch.manual_seed(0)
+    model = build_model("mlp_cpp", 10)
+    x, y = _data()
+    cfg = PSConfig(lr=0.05, max_steps=steps, out_dir=out_dir, bucket_cap_mb=0.5, first_bucket_mb=0.05, **cfg_kw)
+
+    def batches():
+        i = 0
+        while True:
+            j = 2 * i + (rank - 1)
+            yield x[(j * 32) % 512:(j * 32) % 512 + 32], y[(j * 32) % 512:(j * 32) % 512 + 32]
+            i += 1
+
+    if rank == 0:
+        role = PSMaster(model, cfg, torch.device("cpu"))
+        role.train()
+        info = {"nb": role.nb}
+    else:
+        role = PSWorker(model, cfg, torch.device("cpu"), OF.cross_entropy)
+        role.train(batches())
+        info = {"fwd": role.fwd_start, "land": role.landed}
+    role.close()
+    return info, torch.cat([p.detach().flatten() for p in model.parameters()])
+
+
+def test_ps_layer_pipelined_weight_push():
+    """the master pushes weights bucket by bucket in forward order and each worker module
+    waits only for its own bucket (MPI_code worker_nn.h:66-70): with a slow link (40 ms between buckets) the
+    first layer's forward starts before the last weight bucket lands; numerics equal the one-transfer push."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_pipe_job, 3, ({"comm_type": "Bcast", "push_delay_ms": 40.0}, out, 3))
+    assert res[0][0]["nb"] >= 3
+    for info, _ in res[1:]:
+        for step, t_fwd in info["fwd"].items():
+            land = info["land"][step]
+            assert len(land) == res[0][0]["nb"]
+            assert t_fwd < max(land.values()) - 0.02, (step, t_fwd, land)
+    mono = run_world(_ps_pipe_job, 3, ({"comm_type": "Bcast", "pipelined_push": False}, out, 3))
+    for a, b in zip(res, mono):
+        assert torch.equal(a[1], b[1])
+    asyn = run_world(_ps_pipe_job, 3, ({"comm_type": "Async", "push_delay_ms": 5.0}, out, 3))
+    for a, b in zip(res, asyn):
+        assert torch.equal(a[1], b[1])
+
+
+def test_ps_master_checkpoints_by_time_and_final():
+    """TF Supervisor(save_model_secs) + the chief's final save (distributed_train.py:215-223,346-350)."""
+    out = tempfile.mkdtemp()
+    ck = os.path.join(out, "ck")
+    res = run_world(_ps_opt_job, 3, ({"optimizer": "adam", "lr": 1e-3, "checkpoint_dir": ck,
+                                      "save_model_secs": 1e-6}, out, 3))
+    files = sorted(os.listdir(ck))
+    assert "checkpoint_final.pt" in files and "checkpoint_step1.pt" in files, files
+    final = torch.load(os.path.join(ck, "checkpoint_final.pt"), weights_only=True)
+    assert final["step"] == 3 and "optimizer" in final
+    w = torch.cat([v.flatten() for k, v in final["state_dict"].items()])
+    torch.testing.assert_close(w, res[0][1])
+
+
+def test_ps_live_compute_times_in_master_log():
+    """TF-04 live side channel: every worker's compute time reaches the master with its end-of-step marker."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_opt_job, 3, ({"log_compute_times": True}, out, 3))
+    for r in res[0][0]:
+        assert len(r["compute_ms"]) == 2 and all(v > 0 for v in r["compute_ms"])
+        assert r["compute_ms"] == sorted(r["compute_ms"])

@@ -2,7 +2,7 @@
 run it to ``--max-steps``, collect its output directory, and report per config the final evaluator loss,
 the wall time, steps/s and the compute-time percentiles (p50/p80/p90/p95/p99), plus the time-loss curves.
 
-    python tools/sweep.py configs/sweeps/r*_of_50.yaml --nproc 50 --max-steps 2000 --out sweeps/
+    python tools/sweep.py configs/sweeps/r*_of_50.yaml --max-steps 2000 --out sweeps/   # 52 procs each
     python tools/sweep.py cfg1.yaml cfg2.yaml --nproc 3 --max-steps 20 --extra "--no-cuda --synthetic"
 
 Runs are local torchrun launches by default; ``--launcher`` takes a command template with {nproc}, {port}
@@ -25,15 +25,26 @@ DEFAULT_LAUNCHER = (f"{sys.executable} -m torch.distributed.run --nnodes 1 --npr
                     "--master-addr 127.0.0.1 --master-port {port} -m pytorch_distributed_nn_amd.cli {args}")
 
 
+def nproc_for(cfg, default):
+    """Processes a PS config needs: its ps-workers + the master (+ the evaluator); else ``default``."""
+    import yaml
+    with open(cfg) as f:
+        c = yaml.safe_load(f) or {}
+    if c.get("ps-workers"):
+        return int(c["ps-workers"]) + 1 + (1 if c.get("evaluator") else 0)
+    return default
+
+
 def run_one(cfg, out, nproc, max_steps, extra, launcher, port, timeout):
     os.makedirs(out, exist_ok=True)
+    nproc = nproc_for(cfg, nproc)
     args = f"--config {shlex.quote(cfg)} --max-steps {max_steps} --out-dir {shlex.quote(out)} --compute-times {extra}"
     cmd = launcher.format(nproc=nproc, port=port, args=args)
     t0 = time.time()
     r = subprocess.run(cmd, shell=True, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     wall = time.time() - t0
     open(os.path.join(out, "run.log"), "w").write(r.stdout + "\n" + r.stderr)
-    rec = {"config": os.path.basename(cfg), "returncode": r.returncode, "wall_s": round(wall, 2),
+    rec = {"config": os.path.basename(cfg), "nproc": nproc, "returncode": r.returncode, "wall_s": round(wall, 2),
            "steps_per_s": round(max_steps / wall, 3) if r.returncode == 0 else None}
     tl = glob.glob(os.path.join(out, "time_loss_out_*"))
     if tl:
