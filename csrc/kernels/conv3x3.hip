@@ -1,0 +1,388 @@
+// Direct 3x3 / stride-1 / pad-1 convolution on MFMA with an LDS-resident input halo (gfx950).
+//
+// The generic implicit-GEMM engine (gemm_mfma.hip) gathers the A operand of a 3x3 conv from global
+// memory once per tap: every input element is fetched 9 times through L1/L2, and the 128-row tiles
+// spend their K-steps waiting on those gathers (r3 PMC: the stage-1 3x3 data gradient ran at 9% of the
+// bf16 peak, 2-3x its HBM floor; profiles/resnet50_bs256_pmc_r3_before.txt).
+//
+// Here a block owns BM = 256 consecutive output pixels (row-major over the whole batch, so tiles may
+// straddle image boundaries) and NB = 64 / 128 output channels.  Per 64-channel input chunk it stages
+// the HALO of its pixels -- the full-width input rows from one above its first row to one below its
+// last, a CONTIGUOUS range of NHWC memory -- into LDS once (each input byte is read ~1.1-1.9x instead
+// of 9x), then runs the 9 taps as shifted LDS reads: the A fragment of tap (r, s) for output pixel
+// (y, x) is halo pixel (y + r - 1, x + s - 1).  Taps that fall outside the image (padding, or the
+// neighbouring image of a straddling tile) are redirected to an all-zero pixel at the end of the halo,
+// so there is no per-element predication in the MFMA loop.  The weights of one tap ([NB][64] bf16)
+// are double-buffered through LDS, the next tap's fetched into registers under the current tap's MFMAs.
+//
+// One kernel serves the forward (B = W[K][3][3][C]) and the data gradient (B = the tap-flipped,
+// transposed weight W'[C][3][3][K], built by conv3x3_flip_kernel): dx = conv3x3(dy, W').
+// Epilogues (same semantics and slab layout as the GEMM engine's, gemm_mfma.hip):
+//   C3_PLAIN  y = acc                       C3_RES  y = acc + res
+//   C3_STATS  y = acc, per-column partial (sum, sum of squares) of the bf16-rounded outputs
+//   C3_BNB    gm = acc * [t*mscale + mshift > 0]  (ReLU mask of the BN that produced t, recomputed),
+//             store gm, partial sums of gm and gm * (t - mean) * invstd  (BatchNorm backward)
+// one slab row pair per (tile, wave): pdnn_conv3x3_stats_rows().
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 with swapped operands (weight fragment first), so each lane ends
+// with 4 consecutive output channels of one pixel; 4 waves each own 64 pixels x NB channels.
+// Reference layers: pytorch_code/model_ops/resnet.py:19-21,44-48 (every 3x3 conv of the ResNets).
+#include "gemm_common.h"
+
+namespace {
+using namespace pg;
+
+constexpr int C3_BM = 256;
+enum { C3_PLAIN = 0, C3_STATS = 1, C3_BNB = 2, C3_RES = 3 };
+
+struct C3Args {
+    const bf16_t* x;     // [P][C]  NHWC input
+    const bf16_t* w;     // [N][3][3][C]
+    bf16_t* y;           // [P][N]
+    int Nimg, H, W, C, N, P;
+    FastDiv dW, dH;
+    int tiles, ntiles;
+    int halo_max;        // pixels of the largest halo (LDS layout)
+    float* stats;
+    const bf16_t* res;
+    const bf16_t* ep_x;
+    const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
+};
+
+__device__ __forceinline__ u16x8_t c3_zero8() {
+    u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    return z;
+}
+
+// halo image: pixel hp = 128 bytes (64 channels), 16-byte chunk q stored at q ^ ((hp >> 1) & 7)
+__device__ __forceinline__ int halo_off(int hp, int q) {   // bf16 elements
+    return hp * 64 + ((q ^ ((hp >> 1) & 7)) << 3);
+}
+
+template <int NB, int EPI>
+__global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
+    constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
+    constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const halo = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* const bbuf = halo + (a.halo_max + 1) * 64;          // [2][NB][64] K-major, kimg_off swizzle
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = xcd_remap(blockIdx.x, a.tiles * a.ntiles);
+    const int tile = t / a.ntiles, nt = t - tile * a.ntiles;
+    const int p0 = tile * C3_BM, n0 = nt * NB;
+    const int plast = min(a.P, p0 + C3_BM) - 1;
+    const int gr0 = (int)fdiv((uint32_t)p0, a.dW), gr1 = (int)fdiv((uint32_t)plast, a.dW);
+    const int nrows = gr1 - gr0 + 3;
+    const int hpx = nrows * a.W;                 // halo pixels of this tile; the zero pixel follows
+    const long gp0 = (long)(gr0 - 1) * a.W;      // global pixel of halo pixel 0 (may be negative)
+
+    // this lane's 4 output pixels (one per 16-row fragment): halo base, image coordinates
+    int hb[4], py[4], px[4];
+    bool pv[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int p = p0 + wave * 64 + f * 16 + (lane & 15);
+        pv[f] = p < a.P;
+        const int pp = pv[f] ? p : plast;
+        const int gr = (int)fdiv((uint32_t)pp, a.dW);
+        px[f] = pp - gr * a.W;
+        py[f] = gr - (int)fdiv((uint32_t)gr, a.dH) * a.H;
+        hb[f] = (gr - gr0 + 1) * a.W + px[f];
+    }
+
+    // the zero pixel (never overwritten: halos of this tile end before it)
+    if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + hpx * 64 + tid * 8) = c3_zero8();
+
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int nchunks = a.C >> 6;
+    const long wrow = 9L * a.C;                   // elements per weight row n
+    u16x8_t rb[BCH];
+    auto load_b = [&](int c0, int tap) {
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tap * a.C + c0 + q * 8);
+        }
+    };
+    auto store_b = [&](int buf) {
+        bf16_t* B = bbuf + buf * NB * 64;
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
+        }
+    };
+
+    for (int ck = 0; ck < nchunks; ++ck) {
+        const int c0 = ck << 6;
+        if (ck) __syncthreads();                 // the previous chunk's halo / weights are no longer read
+        // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
+        const int nch = hpx * 8;
+        for (int i0 = 0; i0 < nch; i0 += 256 * 8) {
+            u16x8_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // load unconditionally from a clamped (valid) address, then select: a conditional load
+                // makes hipcc branch around every element and drain vmcnt each time
+                const int i = i0 + j * 256 + tid;
+                const long gp = gp0 + (i >> 3);
+                const bool ok = i < nch && gp >= 0 && gp < a.P;
+                const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+                const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+                const unsigned short m = ok ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
+                v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // past the halo: the (zero) value goes to the zero pixel, so the store needs no branch either
+                const int i = i0 + j * 256 + tid;
+                const int off = i < nch ? halo_off(i >> 3, i & 7) : hpx * 64 + (i & 7) * 8;
+                *reinterpret_cast<u16x8_t*>(halo + off) = v[j];
+            }
+        }
+        load_b(c0, 0);
+        store_b(0);
+        __syncthreads();
+#pragma unroll 1
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dr = tap / 3 - 1, ds = tap - (tap / 3) * 3 - 1;
+            if (tap < 8) load_b(c0, tap + 1);                    // next tap's weights under this tap's MFMAs
+            int hp[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const bool v = pv[f] && (unsigned)(py[f] + dr) < (unsigned)a.H && (unsigned)(px[f] + ds) < (unsigned)a.W;
+                hp[f] = v ? hb[f] + dr * a.W + ds : hpx;
+            }
+            const bf16_t* B = bbuf + (tap & 1) * NB * 64;
+            // one 32-deep k-step at a time: both in flight would hold 2x the fragments (spills at NB = 128)
+#pragma unroll 1
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8_t af[4], bfr[FN];
+                const int q = ks * 4 + (lane >> 4);
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+                    af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(halo + halo_off(hp[f], q)));
+#pragma unroll
+                for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                    for (int fn = 0; fn < FN; ++fn)
+                        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+            }
+            if (tap < 8) {
+                store_b((tap + 1) & 1);
+                __syncthreads();
+            }
+        }
+    }
+
+    // ---------------- epilogue: lane holds y[pixel m = wave*64 + fm*16 + (lane&15)][n = fn*16 + 4*(lane>>4) + j]
+    const int lg = lane >> 4;
+    long orow[4];
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
+    // processed one fragment pair (fn, fn+1) at a time: only that pair's loads / packed results are live
+#pragma unroll
+    for (int fp = 0; fp < FN / 2; ++fp) {
+        uint32_t pk[4][2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int fn = 2 * fp + h;
+            const int n = n0 + fn * 16 + 4 * lg;
+            u16x4_t tv[4];
+            if constexpr (EPI == C3_BNB || EPI == C3_RES) {
+                const bf16_t* src = EPI == C3_BNB ? a.ep_x : a.res;
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    tv[fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(src + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
+            }
+            float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+            float bmu[4], bis[4], bms[4], bmh[4];
+            if constexpr (EPI == C3_BNB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bmu[j] = a.ep_mean[n + j]; bis[j] = a.ep_invstd[n + j];
+                    bms[j] = a.ep_mscale[n + j]; bmh[j] = a.ep_mshift[n + j];
+                }
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) {
+                const bool ok = pv[fm];
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j];
+                if constexpr (EPI == C3_RES) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] += bf2f(tv[fm][j]);
+                }
+                if constexpr (EPI == C3_BNB) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float tt = bf2f(tv[fm][j]);
+                        const float gm = (ok && fmaf(tt, bms[j], bmh[j]) > 0.f) ? bf2f(f2bf(v[j])) : 0.f;
+                        v[j] = gm;
+                        s[j] += gm;
+                        q[j] += ok ? gm * (tt - bmu[j]) * bis[j] : 0.f;
+                    }
+                } else if constexpr (EPI == C3_STATS) {
+                    if (ok) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float r = bf2f(f2bf(v[j]));
+                            s[j] += r;
+                            q[j] += r * r;
+                        }
+                    }
+                }
+                pk[fm][h][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                pk[fm][h][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            }
+            if constexpr (EPI == C3_STATS || EPI == C3_BNB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    s[j] = row16_sum(s[j]);
+                    q[j] = row16_sum(q[j]);
+                }
+                if ((lane & 15) == 0) {
+                    float* ps = a.stats + (long)(tile * 4 + wave) * 2 * a.N + n;
+                    float* pq = ps + a.N;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { ps[j] = s[j]; pq[j] = q[j]; }
+                }
+            }
+        }
+        // permlane16_swap pairs the two fragments: every lane then holds 8 consecutive channels (16 bytes)
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[fm][0][0], pk[fm][1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[fm][0][1], pk[fm][1][1], false, false);
+            const int n = n0 + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
+            if (pv[fm]) *reinterpret_cast<uint4*>(a.y + orow[fm] + n) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+    }
+}
+
+// W'[c][r][s][k] = W[k][2-r][2-s][c]: the data gradient of a 3x3 / stride-1 / pad-1 conv is that conv
+// of dy with the tap-flipped, transposed weight.
+__global__ void __launch_bounds__(256) conv3x3_flip_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                                           int K, int C) {
+    const long n = 9L * K * C;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const long r1 = i / C;
+        const int tap = (int)(r1 % 9);
+        const int k = (int)(r1 / 9);
+        wt[((long)c * 9 + (8 - tap)) * K + k] = w[i];
+    }
+}
+
+int c3_halo_max(int W) {
+    const int rows = (C3_BM - 1 + W - 1) / W + 1 + 2;
+    return rows * W;
+}
+
+template <int NB>
+int c3_smem(int W) { return (c3_halo_max(W) + 1) * 128 + 2 * NB * 128; }
+
+template <int NB, int EPI>
+int c3_launch(const C3Args& a, hipStream_t st) {
+    static int attr_done = 0;
+    const int sm = c3_smem<NB>(a.W);
+    if (sm > attr_done) {
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        attr_done = sm;
+    }
+    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    PDNN_LAUNCH_RET;
+}
+
+}  // namespace
+
+static int g_c3_force = -1;
+static int c3_force() {
+    if (g_c3_force < 0) { const char* e = getenv("PDNN_CONV3X3"); g_c3_force = (e && atoi(e) == 2) ? 1 : 0; }
+    return g_c3_force;
+}
+
+static FastDiv make_fdiv_c3(uint32_t d) {
+    FastDiv f;
+    f.d = d ? d : 1;
+    uint32_t l = 0;
+    while ((1ull << l) < f.d) ++l;
+    f.s = l;
+    f.m = (uint32_t)((((1ull << l) - f.d) << 32) / f.d + 1);
+    return f;
+}
+
+// Whether the halo kernel takes a 3x3 / stride-1 / pad-1 conv of this shape (channel multiples of 64,
+// the halo + weight buffers within 80 KB so two blocks share a CU).
+PDNN_API int pdnn_conv3x3_supported(int Nimg, int H, int W, int C, int N) {
+    if (C % 64 || N % 64 || C < 64 || N < 64 || W < 1 || H < 1) return 0;
+    // narrow images: a 256-pixel tile spans so many rows that the implicit-GEMM engine's 128-row tiles win
+    // (ResNet-50 7x7x512, tools/bench_conv3x3.py: 93 / 134 us vs 130 / 152 fwd / dgrad); PDNN_CONV3X3=2 forces
+    if (W < 12 && !c3_force()) return 0;
+    if ((long)Nimg * H * W >= (1L << 31) / 2) return 0;
+    const int nb = N % 128 == 0 ? 128 : 64;
+    const int sm = nb == 128 ? c3_smem<128>(W) : c3_smem<64>(W);
+    return sm <= 80 * 1024 ? 1 : 0;
+}
+
+// 1: take every supported channel shape regardless of the image width (tests); returns the previous
+PDNN_API int pdnn_conv3x3_force(int f) {
+    const int old = c3_force();
+    g_c3_force = f ? 1 : 0;
+    return old;
+}
+
+// Slab rows (pairs of sum / sum-of-squares rows) the C3_STATS / C3_BNB epilogues write.
+PDNN_API int pdnn_conv3x3_stats_rows(int Nimg, int H, int W) {
+    return (int)cdiv((long)Nimg * H * W, C3_BM) * 4;
+}
+
+PDNN_API int pdnn_conv3x3_flip(const bf16_t* w, bf16_t* wt, int K, int C, hipStream_t st) {
+    hipLaunchKernelGGL(conv3x3_flip_kernel, dim3(stream_grid(9L * K * C, 256)), dim3(256), 0, st, w, wt, K, C);
+    PDNN_LAUNCH_RET;
+}
+
+// y[P][N] = conv3x3(x, w) with pad 1, stride 1 (w: [N][3][3][C]); epilogue: stats (fwd BN statistics),
+// bn_x (BN-backward mask + sums), res (residual add), else plain.  nb: 0 = automatic, 64 / 128 forced.
+PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int C, int N,
+                          float* stats, const bf16_t* res, const bf16_t* bn_x, const float* bn_mean,
+                          const float* bn_invstd, const float* bn_mscale, const float* bn_mshift, int nb,
+                          hipStream_t st) {
+    if (!pdnn_conv3x3_supported(Nimg, H, W, C, N)) return (int)hipErrorInvalidValue;
+    C3Args a{};
+    a.x = x; a.w = w; a.y = y;
+    a.Nimg = Nimg; a.H = H; a.W = W; a.C = C; a.N = N; a.P = Nimg * H * W;
+    a.dW = make_fdiv_c3(W); a.dH = make_fdiv_c3(H);
+    a.tiles = (int)cdiv(a.P, C3_BM);
+    a.halo_max = c3_halo_max(W);
+    a.stats = stats; a.res = res;
+    a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+    if (nb == 0) nb = N % 128 == 0 ? 128 : 64;
+    if (nb == 128 && (N % 128 || c3_smem<128>(W) > 80 * 1024)) nb = 64;
+    a.ntiles = N / nb;
+    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    if (bn_x && !stats) return (int)hipErrorInvalidValue;
+    if (nb == 128) {
+        switch (epi) {
+            case C3_BNB: return c3_launch<128, C3_BNB>(a, st);
+            case C3_STATS: return c3_launch<128, C3_STATS>(a, st);
+            case C3_RES: return c3_launch<128, C3_RES>(a, st);
+            default: return c3_launch<128, C3_PLAIN>(a, st);
+        }
+    }
+    switch (epi) {
+        case C3_BNB: return c3_launch<64, C3_BNB>(a, st);
+        case C3_STATS: return c3_launch<64, C3_STATS>(a, st);
+        case C3_RES: return c3_launch<64, C3_RES>(a, st);
+        default: return c3_launch<64, C3_PLAIN>(a, st);
+    }
+}

@@ -1,0 +1,15 @@
+#!/bin/bash
+# halo 3x3 conv kernel: numerics, per-layer A/B vs the implicit-GEMM engine, end-to-end bench
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r3_02
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_conv3x3_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_c3.log 2>&1
+rc=$?; tail -n 5 $O/pytest_c3.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "conv" --timeout 120 --timeout-method thread > $O/pytest_k.log 2>&1
+rc=$?; tail -n 3 $O/pytest_k.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u tools/bench_conv3x3.py > $O/bench_c3.log 2>&1 && cat $O/bench_c3.log || exit 1
+timeout -k 10 200 python -u bench.py > $O/bench.log 2>&1 && tail -n 1 $O/bench.log | cut -c1-150 || exit 1
+PDNN_CONV3X3=0 timeout -k 10 200 python -u bench.py > $O/bench_off.log 2>&1 && tail -n 1 $O/bench_off.log | cut -c1-150 || exit 1
+echo done

@@ -145,6 +145,49 @@ def stats_rows(M: int) -> int:
     return lib().pdnn_gemm_stats_rows(M)
 
 
+# 3x3 / stride-1 / pad-1 convs run on the LDS-halo kernel (csrc/kernels/conv3x3.hip): 1 = whenever the
+# shape is supported (default), 0 = the implicit-GEMM engine (A/B runs; PDNN_CONV3X3 or set_conv3x3_mode)
+import os as _os
+_C3 = {"mode": int(_os.environ.get("PDNN_CONV3X3", "1")), "nb": 0}
+
+
+def set_conv3x3_mode(mode: int, nb: int = 0):
+    """Returns the previous (mode, nb).  nb: 0 automatic, 64 / 128 forced output-channel tile."""
+    old = (_C3["mode"], _C3["nb"])
+    _C3["mode"], _C3["nb"] = int(mode), int(nb)
+    return old
+
+
+def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
+    return (_C3["mode"] and R == 3 and S == 3 and st == 1 and pad == 1
+            and lib().pdnn_conv3x3_supported(N, H, W, Cin, Cout) == 1)
+
+
+def conv3x3_flip(w):
+    """W'[C][3][3][K] = W[K][2-r][2-s][C] (bf16): the data gradient's weight for the halo kernel."""
+    K, R, S, C = w.shape
+    wt = torch.empty(C, 3, 3, K, device=w.device, dtype=BF16)
+    call("pdnn_conv3x3_flip", ptr(w), ptr(wt), K, C, stream())
+    return wt
+
+
+def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None):
+    """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
+    conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
+    Nimg, H, W, C = x.shape
+    Ko = w.shape[0]
+    y = out if out is not None else torch.empty(Nimg, H, W, Ko, device=x.device, dtype=BF16)
+    slab = None
+    t = mean = inv = msc = msh = None
+    if want_stats or bn is not None:
+        slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
+    if bn is not None:
+        t, mean, inv, msc, msh = bn
+    call("pdnn_conv3x3", ptr(x), ptr(w), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(res), ptr(t), ptr(mean),
+         ptr(inv), ptr(msc), ptr(msh), _C3["nb"], stream())
+    return y, slab
+
+
 def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     """x: NHWC bf16 (N,H,W,C); w: bf16 [K][R][S][C] memory (shape K,C,R,S channels_last or K,R,S,C).
     pro: optional (scale, shift) fp32 [C] -> input transformed relu(x*scale+shift) on load.
@@ -156,6 +199,8 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     _chk(C2 == C, f"conv_fwd: weight {tuple(w.shape)} must be [K][R][S][C] with C={C}")
     _chk(C % 8 == 0 and K % 8 == 0, f"conv_fwd: channels must be multiples of 8 (C={C}, K={K})")
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
+    if pro is None and _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
+        return conv3x3(x, w, want_stats=want_stats)
     y = torch.empty(N, Ho, Wo, K, device=x.device, dtype=BF16)
     stats = None
     if want_stats:
@@ -183,13 +228,21 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None):
     if out is not None:
         _chk(tuple(out.shape) == (N, H, W, C) and out.dtype == BF16 and out.is_contiguous(), "conv_dgrad: out")
         _chk(bn is None, "conv_dgrad: out with a fused BN backward")
+    if bn is not None:
+        _bf16_c(bn[0], "conv_dgrad.bn_x")
+        _chk(tuple(bn[0].shape) == (N, H, W, C), "conv_dgrad: bn_x shape")
+    if res is not None:
+        _bf16_c(res, "conv_dgrad.res")
+        _chk(tuple(res.shape) == (N, H, W, C), "conv_dgrad: res shape")
+    if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
+        # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
+        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out)
+        return (y, slab) if bn is not None else y
     dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
     slab = None
     t = mean = inv = msc = msh = None
     if bn is not None:
         t, mean, inv, msc, msh = bn
-        _bf16_c(t, "conv_dgrad.bn_x")
-        _chk(tuple(t.shape) == (N, H, W, C), "conv_dgrad: bn_x shape")
         rows = lib().pdnn_conv_dgrad_stats_rows(N, H, W, R, S, st, pad)
         slab = torch.empty(2 * rows, C, device=dy.device, dtype=F32)
     if res is not None:

@@ -1,0 +1,97 @@
+"""LDS-halo 3x3 / stride-1 conv kernel (csrc/kernels/conv3x3.hip) against fp32 torch: forward with BN
+statistics, data gradient (tap-flipped weight) with the fused BN-backward epilogue and with a residual,
+at the ResNet shapes, odd image sizes (tiles straddling image boundaries, partial last tile) and both
+output-channel tiles."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.fixture(scope="module")
+def K():
+    from pytorch_distributed_nn_amd.ops import kernels, _backend
+    assert _backend.available()
+    return kernels
+
+
+SHAPES = [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (5, 7, 7, 512, 512),
+          (3, 9, 11, 64, 192), (2, 5, 6, 128, 64), (1, 16, 16, 192, 128), (7, 3, 3, 64, 128)]
+
+
+@pytest.fixture(params=[0, 64, 128], ids=["nb-auto", "nb64", "nb128"])
+def nb(request, K):
+    old = K.set_conv3x3_mode(1, request.param)
+    oldf = K.lib().pdnn_conv3x3_force(1)        # narrow images too (the router sends W < 12 to the GEMM engine)
+    yield request.param
+    K.lib().pdnn_conv3x3_force(oldf)
+    K.set_conv3x3_mode(*old)
+
+
+def conv_ref(x, w):
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, 1).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3x3_fwd_stats(K, nb, shape):
+    N, H, W, C, Ko = shape
+    assert K.lib().pdnn_conv3x3_supported(N, H, W, C, Ko) == 1
+    x = torch.randn(N, H, W, C, device="cuda").to(BF)
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(BF)
+    y, slab = K.conv3x3(x, w, want_stats=True)
+    ref = conv_ref(x, w)
+    assert rel(y, ref) < 1.5e-2
+    yf = y.float().reshape(-1, Ko)
+    s = slab.view(-1, 2, Ko).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    # routed through conv_fwd as well
+    y2, _ = K.conv_fwd(x, w, 1, 1, want_stats=True)
+    assert torch.equal(y2, y)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3x3_dgrad_bn_and_res(K, nb, shape):
+    N, H, W, C, Ko = shape
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(BF)
+    y = F.conv2d(x, w.float().permute(0, 3, 1, 2), None, 1, 1)
+    dy = torch.randn(*y.permute(0, 2, 3, 1).shape, device="cuda").to(BF)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dx_ref = x.grad.permute(0, 2, 3, 1)
+    assert rel(K.conv_dgrad(dy, w, (N, H, W, C), 1, 1), dx_ref) < 1.5e-2
+    res = torch.randn(N, H, W, C, device="cuda").to(BF)
+    assert rel(K.conv_dgrad(dy, w, (N, H, W, C), 1, 1, res=res), dx_ref + res.float()) < 1.5e-2
+    # fused BN backward: gm = dx * [t*msc + msh > 0], sums of gm and gm*(t-mean)*inv
+    t = torch.randn(N, H, W, C, device="cuda").to(BF)
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    msc, msh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), 1, 1, bn=(t, mean, inv, msc, msh))
+    mask = (t.float() * msc + msh) > 0
+    gm_ref = dx_ref * mask
+    assert rel(gm, gm_ref) < 1.5e-2
+    s = slab.view(-1, 2, C).sum(0)
+    gmf = gm.float().reshape(-1, C)
+    xhat = ((t.float() - mean) * inv).reshape(-1, C)
+    assert torch.allclose(s[0], gmf.sum(0), rtol=1e-3, atol=1e-3 * gmf.abs().sum(0).max().item())
+    assert torch.allclose(s[1], (gmf * xhat).sum(0), rtol=1e-3, atol=1e-3 * (gmf * xhat).abs().sum(0).max().item())
+
+
+def test_conv3x3_matches_gemm_engine_bitwise_stats_layout(K):
+    """The halo kernel and the implicit-GEMM engine agree on a ResNet-50 stage-1 layer (bs 8)."""
+    x = torch.randn(8, 56, 56, 64, device="cuda").to(BF)
+    w = (torch.randn(64, 3, 3, 64, device="cuda") * 0.05).to(BF)
+    old = K.set_conv3x3_mode(0)
+    y0, s0 = K.conv_fwd(x, w, 1, 1, want_stats=True)
+    K.set_conv3x3_mode(1)
+    y1, s1 = K.conv_fwd(x, w, 1, 1, want_stats=True)
+    K.set_conv3x3_mode(*old)
+    assert rel(y1, y0) < 1e-2
+    torch.testing.assert_close(s1.view(-1, 2, 64).sum(0), s0.view(-1, 2, 64).sum(0), rtol=2e-3, atol=1.0)
