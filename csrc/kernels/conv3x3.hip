@@ -59,131 +59,11 @@ __device__ __forceinline__ int halo_off(int hp, int q) {   // bf16 elements
     return hp * 64 + ((q ^ ((hp >> 1) & 7)) << 3);
 }
 
+// ---------------- epilogue: lane holds y[pixel m = wave*64 + fm*16 + (lane&15)][n = fn*16 + 4*(lane>>4) + j]
 template <int NB, int EPI>
-__global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
-    constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
-    constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* const halo = reinterpret_cast<bf16_t*>(smem);
-    bf16_t* const bbuf = halo + (a.halo_max + 1) * 64;          // [2][NB][64] K-major, kimg_off swizzle
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = xcd_remap(blockIdx.x, a.tiles * a.ntiles);
-    const int tile = t / a.ntiles, nt = t - tile * a.ntiles;
-    const int p0 = tile * C3_BM, n0 = nt * NB;
-    const int plast = min(a.P, p0 + C3_BM) - 1;
-    const int gr0 = (int)fdiv((uint32_t)p0, a.dW), gr1 = (int)fdiv((uint32_t)plast, a.dW);
-    const int nrows = gr1 - gr0 + 3;
-    const int hpx = nrows * a.W;                 // halo pixels of this tile; the zero pixel follows
-    const long gp0 = (long)(gr0 - 1) * a.W;      // global pixel of halo pixel 0 (may be negative)
-
-    // this lane's 4 output pixels (one per 16-row fragment): halo base, image coordinates
-    int hb[4], py[4], px[4];
-    bool pv[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        const int p = p0 + wave * 64 + f * 16 + (lane & 15);
-        pv[f] = p < a.P;
-        const int pp = pv[f] ? p : plast;
-        const int gr = (int)fdiv((uint32_t)pp, a.dW);
-        px[f] = pp - gr * a.W;
-        py[f] = gr - (int)fdiv((uint32_t)gr, a.dH) * a.H;
-        hb[f] = (gr - gr0 + 1) * a.W + px[f];
-    }
-
-    // the zero pixel (never overwritten: halos of this tile end before it)
-    if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + hpx * 64 + tid * 8) = c3_zero8();
-
-    f32x4_t acc[4][FN];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    const int nchunks = a.C >> 6;
-    const long wrow = 9L * a.C;                   // elements per weight row n
-    u16x8_t rb[BCH];
-    auto load_b = [&](int c0, int tap) {
-#pragma unroll
-        for (int i = 0; i < BCH; ++i) {
-            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
-            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tap * a.C + c0 + q * 8);
-        }
-    };
-    auto store_b = [&](int buf) {
-        bf16_t* B = bbuf + buf * NB * 64;
-#pragma unroll
-        for (int i = 0; i < BCH; ++i) {
-            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
-            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
-        }
-    };
-
-    for (int ck = 0; ck < nchunks; ++ck) {
-        const int c0 = ck << 6;
-        if (ck) __syncthreads();                 // the previous chunk's halo / weights are no longer read
-        // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
-        const int nch = hpx * 8;
-        for (int i0 = 0; i0 < nch; i0 += 256 * 8) {
-            u16x8_t v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                // load unconditionally from a clamped (valid) address, then select: a conditional load
-                // makes hipcc branch around every element and drain vmcnt each time
-                const int i = i0 + j * 256 + tid;
-                const long gp = gp0 + (i >> 3);
-                const bool ok = i < nch && gp >= 0 && gp < a.P;
-                const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
-                const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
-                const unsigned short m = ok ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
-                v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                // past the halo: the (zero) value goes to the zero pixel, so the store needs no branch either
-                const int i = i0 + j * 256 + tid;
-                const int off = i < nch ? halo_off(i >> 3, i & 7) : hpx * 64 + (i & 7) * 8;
-                *reinterpret_cast<u16x8_t*>(halo + off) = v[j];
-            }
-        }
-        load_b(c0, 0);
-        store_b(0);
-        __syncthreads();
-#pragma unroll 1
-        for (int tap = 0; tap < 9; ++tap) {
-            const int dr = tap / 3 - 1, ds = tap - (tap / 3) * 3 - 1;
-            if (tap < 8) load_b(c0, tap + 1);                    // next tap's weights under this tap's MFMAs
-            int hp[4];
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                const bool v = pv[f] && (unsigned)(py[f] + dr) < (unsigned)a.H && (unsigned)(px[f] + ds) < (unsigned)a.W;
-                hp[f] = v ? hb[f] + dr * a.W + ds : hpx;
-            }
-            const bf16_t* B = bbuf + (tap & 1) * NB * 64;
-            // one 32-deep k-step at a time: both in flight would hold 2x the fragments (spills at NB = 128)
-#pragma unroll 1
-            for (int ks = 0; ks < 2; ++ks) {
-                bf16x8_t af[4], bfr[FN];
-                const int q = ks * 4 + (lane >> 4);
-#pragma unroll
-                for (int f = 0; f < 4; ++f)
-                    af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(halo + halo_off(hp[f], q)));
-#pragma unroll
-                for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-                    for (int fn = 0; fn < FN; ++fn)
-                        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
-            }
-            if (tap < 8) {
-                store_b((tap + 1) & 1);
-                __syncthreads();
-            }
-        }
-    }
-
-    // ---------------- epilogue: lane holds y[pixel m = wave*64 + fm*16 + (lane&15)][n = fn*16 + 4*(lane>>4) + j]
+__device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile, int p0, int n0,
+                                            int wave, int lane, const bool (&pv)[4]) {
+    constexpr int FN = NB / 16;
     const int lg = lane >> 4;
     long orow[4];
 #pragma unroll
@@ -269,6 +149,256 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
     }
 }
 
+template <int NB, int EPI>
+__global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
+    constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
+    constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const halo = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* const bbuf = halo + (a.halo_max + 1) * 64;          // [2][NB][64] K-major, kimg_off swizzle
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = xcd_remap(blockIdx.x, a.tiles * a.ntiles);
+    const int tile = t / a.ntiles, nt = t - tile * a.ntiles;
+    const int p0 = tile * C3_BM, n0 = nt * NB;
+    const int plast = min(a.P, p0 + C3_BM) - 1;
+    const int gr0 = (int)fdiv((uint32_t)p0, a.dW), gr1 = (int)fdiv((uint32_t)plast, a.dW);
+    const int nrows = gr1 - gr0 + 3;
+    const int hpx = nrows * a.W;                 // halo pixels of this tile; the zero pixel follows
+    const long gp0 = (long)(gr0 - 1) * a.W;      // global pixel of halo pixel 0 (may be negative)
+
+    // this lane's 4 output pixels (one per 16-row fragment): halo base, image coordinates
+    int hb[4], py[4], px[4];
+    bool pv[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int p = p0 + wave * 64 + f * 16 + (lane & 15);
+        pv[f] = p < a.P;
+        const int pp = pv[f] ? p : plast;
+        const int gr = (int)fdiv((uint32_t)pp, a.dW);
+        px[f] = pp - gr * a.W;
+        py[f] = gr - (int)fdiv((uint32_t)gr, a.dH) * a.H;
+        hb[f] = (gr - gr0 + 1) * a.W + px[f];
+    }
+
+    // the zero pixel sits after the largest halo (halo_max): taps outside the image read it
+    const int zpx = a.halo_max;
+    if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + zpx * 64 + tid * 8) = c3_zero8();
+
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int nchunks = a.C >> 6;
+    const long wrow = 9L * a.C;                   // elements per weight row n
+    u16x8_t rb[BCH];
+    auto load_b = [&](int c0, int tap) {
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tap * a.C + c0 + q * 8);
+        }
+    };
+    auto store_b = [&](int buf) {
+        bf16_t* B = bbuf + buf * NB * 64;
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
+        }
+    };
+
+    for (int ck = 0; ck < nchunks; ++ck) {
+        const int c0 = ck << 6;
+        if (ck) __syncthreads();                 // the previous chunk's halo / weights are no longer read
+        // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
+        const int nch = hpx * 8;
+        for (int i0 = 0; i0 < nch; i0 += 256 * 8) {
+            u16x8_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // load unconditionally from a clamped (valid) address, then select: a conditional load
+                // makes hipcc branch around every element and drain vmcnt each time
+                const int i = i0 + j * 256 + tid;
+                const long gp = gp0 + (i >> 3);
+                const bool ok = i < nch && gp >= 0 && gp < a.P;
+                const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+                const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+                const unsigned short m = ok ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
+                v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // past the halo: the (zero) value goes to the zero pixel, so the store needs no branch either
+                const int i = i0 + j * 256 + tid;
+                const int off = i < nch ? halo_off(i >> 3, i & 7) : zpx * 64 + (i & 7) * 8;
+                *reinterpret_cast<u16x8_t*>(halo + off) = v[j];
+            }
+        }
+        load_b(c0, 0);
+        store_b(0);
+        __syncthreads();
+#pragma unroll 1
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dr = tap / 3 - 1, ds = tap - (tap / 3) * 3 - 1;
+            if (tap < 8) load_b(c0, tap + 1);                    // next tap's weights under this tap's MFMAs
+            int hp[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const bool v = pv[f] && (unsigned)(py[f] + dr) < (unsigned)a.H && (unsigned)(px[f] + ds) < (unsigned)a.W;
+                hp[f] = v ? hb[f] + dr * a.W + ds : zpx;
+            }
+            const bf16_t* B = bbuf + (tap & 1) * NB * 64;
+            // one 32-deep k-step at a time: both in flight would hold 2x the fragments (spills at NB = 128)
+#pragma unroll 1
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8_t af[4], bfr[FN];
+                const int q = ks * 4 + (lane >> 4);
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+                    af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(halo + halo_off(hp[f], q)));
+#pragma unroll
+                for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                    for (int fn = 0; fn < FN; ++fn)
+                        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+            }
+            if (tap < 8) {
+                store_b((tap + 1) & 1);
+                __syncthreads();
+            }
+        }
+    }
+
+    c3_epilogue<NB, EPI>(a, acc, tile, p0, n0, wave, lane, pv);
+}
+
+// C = N = 64 (ResNet stage 1): all 9 taps of the weight stay resident in LDS (72 KB), one persistent
+// block per CU loops over pixel tiles, and the NEXT tile's halo is fetched into registers while the
+// current tile computes (cdna_hip_programming.md T14: issue early, write to LDS after the barrier).  No
+// barrier inside the 9-tap MFMA sequence; two per tile.
+constexpr int C3R_HREG = 16;                     // halo chunks per thread in flight (halo <= 512 pixels)
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
+    constexpr int NB = 64, FN = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const halo = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* const wres = halo + (a.halo_max + 1) * 64;       // [9][64 n][64 k], kimg_off per tap image
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int zpx = a.halo_max;
+
+    // resident weights: 9 * 64 rows * 8 chunks
+    for (int i = tid; i < 9 * 64 * 8; i += 256) {
+        const int tap = i / 512, row = (i >> 3) & 63, q = i & 7;
+        *reinterpret_cast<u16x8_t*>(wres + tap * 4096 + kimg_off(row, q)) =
+            *reinterpret_cast<const u16x8_t*>(a.w + (long)row * 576 + tap * 64 + q * 8);
+    }
+    if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + zpx * 64 + tid * 8) = c3_zero8();
+
+    u16x8_t hreg[C3R_HREG];
+    auto tile_geom = [&](int tile, int& gr0, int& nch, long& gp0) {
+        const int p0 = tile * C3_BM;
+        const int plast = min(a.P, p0 + C3_BM) - 1;
+        gr0 = (int)fdiv((uint32_t)p0, a.dW);
+        const int gr1 = (int)fdiv((uint32_t)plast, a.dW);
+        nch = (gr1 - gr0 + 3) * a.W * 8;
+        gp0 = (long)(gr0 - 1) * a.W;
+    };
+    auto fetch = [&](int tile) {                 // halo chunks -> registers (masked, unconditional loads)
+        int gr0, nch;
+        long gp0;
+        tile_geom(tile, gr0, nch, gp0);
+#pragma unroll
+        for (int j = 0; j < C3R_HREG; ++j) {
+            const int i = j * 256 + tid;
+            const long gp = gp0 + (i >> 3);
+            const bool ok = i < nch && gp >= 0 && gp < a.P;
+            const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+            const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * 64 + (i & 7) * 8);
+            const unsigned short m = ok ? 0xFFFF : 0;
+            hreg[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+        }
+    };
+    auto put = [&](int tile) {                   // registers -> LDS halo (past the halo: the zero pixel)
+        int gr0, nch;
+        long gp0;
+        tile_geom(tile, gr0, nch, gp0);
+#pragma unroll
+        for (int j = 0; j < C3R_HREG; ++j) {
+            const int i = j * 256 + tid;
+            const int off = i < nch ? halo_off(i >> 3, i & 7) : zpx * 64 + (i & 7) * 8;
+            *reinterpret_cast<u16x8_t*>(halo + off) = hreg[j];
+        }
+    };
+
+    int tile = blockIdx.x;
+    if (tile < a.tiles) fetch(tile);
+    for (; tile < a.tiles; tile += gridDim.x) {
+        __syncthreads();                          // the previous tile's halo is no longer read
+        put(tile);
+        __syncthreads();
+        const int next = tile + gridDim.x;
+        if (next < a.tiles) fetch(next);          // lands under this tile's MFMAs
+
+        int gr0, nch;
+        long gp0;
+        tile_geom(tile, gr0, nch, gp0);
+        const int p0 = tile * C3_BM;
+        const int plast = min(a.P, p0 + C3_BM) - 1;
+        int hb[4], py[4], px[4];
+        bool pv[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int p = p0 + wave * 64 + f * 16 + (lane & 15);
+            pv[f] = p < a.P;
+            const int pp = pv[f] ? p : plast;
+            const int gr = (int)fdiv((uint32_t)pp, a.dW);
+            px[f] = pp - gr * a.W;
+            py[f] = gr - (int)fdiv((uint32_t)gr, a.dH) * a.H;
+            hb[f] = (gr - gr0 + 1) * a.W + px[f];
+        }
+        f32x4_t acc[4][FN];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+            int hp[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const bool v = pv[f] && (unsigned)(py[f] + dr) < (unsigned)a.H && (unsigned)(px[f] + ds) < (unsigned)a.W;
+                hp[f] = v ? hb[f] + dr * a.W + ds : zpx;
+            }
+            const bf16_t* B = wres + tap * 4096;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8_t af[4], bfr[FN];
+                const int q = ks * 4 + (lane >> 4);
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+                    af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(halo + halo_off(hp[f], q)));
+#pragma unroll
+                for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                    for (int fn = 0; fn < FN; ++fn)
+                        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+            }
+        }
+        c3_epilogue<NB, EPI>(a, acc, tile, p0, 0, wave, lane, pv);
+    }
+}
+
+int c3r_smem(int W);
+
 // W'[c][r][s][k] = W[k][2-r][2-s][c]: the data gradient of a 3x3 / stride-1 / pad-1 conv is that conv
 // of dy with the tap-flipped, transposed weight.
 __global__ void __launch_bounds__(256) conv3x3_flip_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
@@ -290,6 +420,21 @@ int c3_halo_max(int W) {
 
 template <int NB>
 int c3_smem(int W) { return (c3_halo_max(W) + 1) * 128 + 2 * NB * 128; }
+
+int c3r_smem(int W) { return (c3_halo_max(W) + 1) * 128 + 9 * 64 * 128; }
+
+template <int EPI>
+int c3r_launch(const C3Args& a, hipStream_t st) {
+    static int attr_done = 0;
+    const int sm = c3r_smem(a.W);
+    if (sm > attr_done) {
+        (void)hipFuncSetAttribute((const void*)conv3x3_w64_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        attr_done = sm;
+    }
+    const int grid = a.tiles < 256 ? a.tiles : 256;        // one persistent block per CU
+    hipLaunchKernelGGL((conv3x3_w64_kernel<EPI>), dim3(grid), dim3(256), sm, st, a);
+    PDNN_LAUNCH_RET;
+}
 
 template <int NB, int EPI>
 int c3_launch(const C3Args& a, hipStream_t st) {
@@ -366,7 +511,22 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     a.halo_max = c3_halo_max(W);
     a.stats = stats; a.res = res;
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
-    if (nb == 0) nb = N % 128 == 0 ? 128 : 64;
+    const int epi0 = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    // 64 -> 64 channels: the weight-resident persistent kernel (nb = 1; measured slower than the streaming
+    // kernel at ResNet-50 stage 1, 125 / 173 vs 104 / 142 us fwd / dgrad, gpurun_out/r3_04: one wave per SIMD
+    // exposes the LDS latency of the unrolled tap sequence)
+    if (nb == 1 && C == 64 && N == 64 && c3_halo_max(W) * 8 <= C3R_HREG * 256 &&
+        c3r_smem(W) <= 160 * 1024) {
+        a.ntiles = 1;
+        if (bn_x && !stats) return (int)hipErrorInvalidValue;
+        switch (epi0) {
+            case C3_BNB: return c3r_launch<C3_BNB>(a, st);
+            case C3_STATS: return c3r_launch<C3_STATS>(a, st);
+            case C3_RES: return c3r_launch<C3_RES>(a, st);
+            default: return c3r_launch<C3_PLAIN>(a, st);
+        }
+    }
+    if (nb == 0 || nb == 1) nb = N % 128 == 0 ? 128 : 64;
     if (nb == 128 && (N % 128 || c3_smem<128>(W) > 80 * 1024)) nb = 64;
     a.ntiles = N / nb;
     const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));

@@ -57,6 +57,9 @@ def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
 
 
 _SIDE = {}
+# Bottleneck forward: materialise a2 = relu(bn2(t2)) for conv3 (1) or apply BN2+ReLU in conv3's operand
+# prologue (0).  PDNN_MATERIALIZE_A2 for A/B runs.
+MATERIALIZE_A2 = os.environ.get("PDNN_MATERIALIZE_A2", "1") == "1"
 
 
 def side_stream_if_active(t):
@@ -234,7 +237,17 @@ class BottleneckFn(torch.autograd.Function):
         C1 = t1.shape[-1]
         a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)
         t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
-        t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
+        if MATERIALIZE_A2:
+            # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
+            # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
+            # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs
+            # 0.29 + 1.87 materialised)
+            C2 = t2.shape[-1]
+            a2 = K.bn_apply(t2.view(-1, C2), s2, h2, relu=True).view(t2.shape)
+            t3, m3, i3, s3, h3 = _conv_bn(a2, k3, 1, 0, None, training, (g3, b3), bufs[4:6], mom, eps)
+        else:
+            a2 = None
+            t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
         C3 = t3.shape[-1]
         if down:
             if side_down is not None:
@@ -251,7 +264,7 @@ class BottleneckFn(torch.autograd.Function):
         out = out.view(t3.shape)
         # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
         ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
-                              g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None)
+                              g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2)
         ctx.conf = (stride, training, down)
         ctx.params = params
         return out
@@ -259,7 +272,7 @@ class BottleneckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
-         g1, g2, g3, gd, k1, k2, k3, kd) = ctx.saved_tensors
+         g1, g2, g3, gd, k1, k2, k3, kd, a2) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused Bottleneck backward requires training-mode BatchNorm")
@@ -283,7 +296,10 @@ class BottleneckFn(torch.autograd.Function):
             dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
-        dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        if a2 is not None:
+            dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
+        else:
+            dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
         dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5])
         dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
         dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])

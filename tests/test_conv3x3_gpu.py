@@ -23,10 +23,11 @@ def K():
 
 
 SHAPES = [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (5, 7, 7, 512, 512),
-          (3, 9, 11, 64, 192), (2, 5, 6, 128, 64), (1, 16, 16, 192, 128), (7, 3, 3, 64, 128)]
+          (3, 9, 11, 64, 192), (2, 5, 6, 128, 64), (1, 16, 16, 192, 128), (7, 3, 3, 64, 128),
+          (3, 7, 9, 64, 64), (5, 14, 14, 64, 64), (1, 1, 1, 64, 64)]
 
 
-@pytest.fixture(params=[0, 64, 128], ids=["nb-auto", "nb64", "nb128"])
+@pytest.fixture(params=[0, 1, 64, 128], ids=["nb-auto", "w64-resident", "nb64", "nb128"])
 def nb(request, K):
     old = K.set_conv3x3_mode(1, request.param)
     oldf = K.lib().pdnn_conv3x3_force(1)        # narrow images too (the router sends W < 12 to the GEMM engine)

@@ -1,0 +1,66 @@
+"""Per-layer timing of the 1x1 convs of the ResNet-50 bottleneck (bs256) as the fused block runs them:
+conv3 forward with the BN2+ReLU operand prologue vs materialised a2 = relu(bn2(t2)) (bn_apply) + plain
+conv, conv1 forward with BN statistics, conv3 data gradient with the BN-backward epilogue and conv1 data
+gradient with the residual.  Engine choice comes from the environment (PDNN_PP_CONV_FWD_K, PDNN_PP_CONV_BNB,
+PDNN_PP_CONV_DGRAD_K, PDNN_GLDS ...), so one call per configuration.
+
+    PDNN_PP_CONV_FWD_K=0 python tools/bench_conv1x1.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_nn_amd.ops import kernels as K   # noqa: E402
+
+# (H, C_mid, count): input/output channels 4*C_mid
+STAGES = [(56, 64, 3), (28, 128, 4), (14, 256, 6), (7, 512, 3)]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return round(e0.elapsed_time(e1) / iters * 1e3, 1)
+
+
+def main():
+    N = int(os.environ.get("BATCH", "256"))
+    tot = {}
+    tag = {k: v for k, v in os.environ.items() if k.startswith("PDNN_")}
+    for H, C, cnt in STAGES:
+        C4 = 4 * C
+        d = "cuda"
+        t2 = torch.randn(N, H, H, C, device=d).to(torch.bfloat16)
+        x4 = torch.randn(N, H, H, C4, device=d).to(torch.bfloat16)
+        k3 = (torch.randn(C4, 1, 1, C, device=d) * 0.05).to(torch.bfloat16)
+        k1 = (torch.randn(C, 1, 1, C4, device=d) * 0.05).to(torch.bfloat16)
+        sc, sh = torch.rand(C, device=d) + 0.5, torch.randn(C, device=d) * 0.1
+        mean, inv = torch.zeros(C, device=d), torch.ones(C, device=d)
+        dt3 = torch.randn(N, H, H, C4, device=d).to(torch.bfloat16)
+        dt1 = torch.randn(N, H, H, C, device=d).to(torch.bfloat16)
+        row = {"H": H, "C": C}
+        row["conv3_fwd_pro"] = timeit(lambda: K.conv_fwd(t2, k3, 1, 0, pro=(sc, sh), want_stats=True))
+        row["bn_apply_a2"] = timeit(lambda: K.bn_apply(t2.view(-1, C), sc, sh, relu=True))
+        a2 = K.bn_apply(t2.view(-1, C), sc, sh, relu=True).view(t2.shape)
+        row["conv3_fwd_plain"] = timeit(lambda: K.conv_fwd(a2, k3, 1, 0, want_stats=True))
+        row["conv1_fwd"] = timeit(lambda: K.conv_fwd(x4, k1, 1, 0, want_stats=True))
+        row["conv3_dgrad_bn"] = timeit(lambda: K.conv_dgrad(dt3, k3, t2.shape, 1, 0, bn=(t2, mean, inv, sc, sh)))
+        row["conv1_dgrad_res"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4))
+        print(json.dumps(row), flush=True)
+        for k, v in row.items():
+            if k not in ("H", "C"):
+                tot[k] = round(tot.get(k, 0.0) + cnt * v, 1)
+    print(json.dumps({"env": tag, "per_step_us": tot}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

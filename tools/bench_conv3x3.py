@@ -45,8 +45,9 @@ def main():
         sc, sh = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
         flops = 2.0 * N * H * W * C * C * 9
         row = {"shape": [H, W, C], "count": cnt}
-        for name, mode, nb in (("gemm", 0, 0), ("halo64", 1, 64), ("halo128", 1, 128), ("halo", 1, 0)):
-            if nb == 128 and C % 128:
+        for name, mode, nb in (("gemm", 0, 0), ("halo64", 1, 64), ("halo128", 1, 128), ("w64_resident", 1, 1),
+                               ("halo", 1, 0)):
+            if (nb == 128 and C % 128) or (nb == 1 and C != 64):
                 continue
             old = K.set_conv3x3_mode(mode, nb)
             tf = timeit(lambda: K.conv_fwd(x, w, 1, 1, want_stats=True), a.iters)
