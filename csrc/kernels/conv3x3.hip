@@ -45,6 +45,7 @@ struct C3Args {
     int halo_max;        // pixels of the largest halo (LDS layout)
     float* stats;
     const bf16_t* res;
+    const uint8_t* rmask;  // C3_RES: residual masked by these ReLU bits ([P][N/8] bytes), or null
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
 };
@@ -99,8 +100,9 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j];
                 if constexpr (EPI == C3_RES) {
+                    const uint32_t mb = (a.rmask && ok) ? (uint32_t)(a.rmask[(orow[fm] + n) >> 3] >> (n & 4)) : 0xFu;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] += bf2f(tv[fm][j]);
+                    for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(tv[fm][j]) : 0.f;
                 }
                 if constexpr (EPI == C3_BNB) {
 #pragma unroll
@@ -397,6 +399,129 @@ __global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// 1x1 / stride-1 convs with a short reduction (K = C_in <= 128) and a wide output: y[P][N] = x[P][K] . W^T.
+// The implicit-GEMM engine gives every 64-column output tile its own block, which re-fetches the A rows
+// and pays a full load -> MFMA -> epilogue latency chain for ONE k-step (ResNet-50 stage-1 conv3, K = 64
+// -> N = 256: 258 us against a ~100 us write floor, r3 trace).  Here a block owns 256 pixels: their A
+// panel ([256][K] bf16, <= 64 KB) is staged into LDS once, then the block walks its share of the output
+// columns in 64-wide chunks -- the weight tile of the next (chunk, k-chunk) step fetched into registers
+// under the current step's MFMAs, the epilogue of a chunk (BN statistics, stores) issued as soon as its
+// reduction ends.  Grid = pixel tiles x column groups (groups only when the pixel tiles alone cannot fill
+// the chip).  Same epilogues as the 3x3 kernel (stats / BN-backward / masked residual).
+// ---------------------------------------------------------------------------------------------------
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
+    constexpr int NB = 64, FN = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const panel = reinterpret_cast<bf16_t*>(smem);               // [K/64][257 px][64]
+    const int KC = a.C >> 6;
+    bf16_t* const bbuf = panel + KC * (C3_BM + 1) * 64;                  // [2][64][64]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int groups = a.ntiles;                                          // column groups
+    const int t = xcd_remap(blockIdx.x, a.tiles * groups);
+    const int tile = t / groups, grp = t - tile * groups;
+    const int chunks = (a.N >> 6) / groups;                               // 64-column chunks of this block
+    const int c00 = grp * chunks;
+    const int p0 = tile * C3_BM;
+    const int zpx = C3_BM;                                                // zero pixel of each k-chunk image
+
+    // ---- A panel: pixels p0 .. p0+255, all K channels (masked unconditional loads; rows >= P are zero)
+    for (int i0 = 0; i0 < KC * C3_BM * 8; i0 += 256 * 8) {
+        u16x8_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = i0 + j * 256 + tid;                 // = (kc * 256 + px) * 8 + q
+            const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
+            const long gp = (long)p0 + px;
+            const bool ok = i < KC * C3_BM * 8 && gp < a.P;
+            const long gc = gp < a.P ? gp : a.P - 1;
+            const int kk = kc < KC ? kc : KC - 1;
+            const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + kk * 64 + q * 8);
+            const unsigned short m = ok ? 0xFFFF : 0;
+            v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = i0 + j * 256 + tid;
+            const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
+            if (kc < KC) *reinterpret_cast<u16x8_t*>(panel + kc * (C3_BM + 1) * 64 + halo_off(px, q)) = v[j];
+        }
+    }
+    if (tid < 8 * KC) *reinterpret_cast<u16x8_t*>(panel + (tid >> 3) * (C3_BM + 1) * 64 + zpx * 64 + (tid & 7) * 8) =
+        c3_zero8();
+
+    bool pv[4];
+    int hp[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int m = wave * 64 + f * 16 + (lane & 15);
+        pv[f] = p0 + m < a.P;
+        hp[f] = pv[f] ? m : zpx;
+    }
+
+    // weight tile of step s = (chunk s / KC, k-chunk s % KC): rows n, 64 k, K-major kimg_off image
+    u16x8_t rb[2];
+    auto load_b = [&](int s) {
+        const int n0 = (c00 + s / KC) * NB, k0 = (s % KC) * 64;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * a.C + k0 + q * 8);
+        }
+    };
+    auto store_b = [&](int buf) {
+        bf16_t* B = bbuf + buf * NB * 64;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
+        }
+    };
+    load_b(0);
+    store_b(0);
+    __syncthreads();
+    const int steps = chunks * KC;
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < steps; ++s) {
+        const bool more = s + 1 < steps;
+        if (more) load_b(s + 1);
+        const int kc = s % KC;
+        const bf16_t* A = panel + kc * (C3_BM + 1) * 64;
+        const bf16_t* B = bbuf + (s & 1) * NB * 64;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8_t af[4], bfr[FN];
+            const int q = ks * 4 + (lane >> 4);
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(A + halo_off(hp[f], q)));
+#pragma unroll
+            for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+        }
+        if (kc == KC - 1) {                       // this chunk's reduction is complete: epilogue, then restart
+            c3_epilogue<NB, EPI>(a, acc, tile, p0, (c00 + s / KC) * NB, wave, lane, pv);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+        if (more) {
+            store_b((s + 1) & 1);
+            __syncthreads();
+        }
+    }
+}
+
 int c3r_smem(int W);
 
 // W'[c][r][s][k] = W[k][2-r][2-s][c]: the data gradient of a 3x3 / stride-1 / pad-1 conv is that conv
@@ -451,6 +576,17 @@ int c3_launch(const C3Args& a, hipStream_t st) {
 }  // namespace
 
 static int g_c3_force = -1;
+
+template <int EPI>
+int p1_launch(const C3Args& a, int sm, hipStream_t st) {
+    static int attr_done = 0;
+    if (sm > attr_done) {
+        (void)hipFuncSetAttribute((const void*)conv1x1_panel_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        attr_done = sm;
+    }
+    hipLaunchKernelGGL((conv1x1_panel_kernel<EPI>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    PDNN_LAUNCH_RET;
+}
 static int c3_force() {
     if (g_c3_force < 0) { const char* e = getenv("PDNN_CONV3X3"); g_c3_force = (e && atoi(e) == 2) ? 1 : 0; }
     return g_c3_force;
@@ -499,7 +635,8 @@ PDNN_API int pdnn_conv3x3_flip(const bf16_t* w, bf16_t* wt, int K, int C, hipStr
 // y[P][N] = conv3x3(x, w) with pad 1, stride 1 (w: [N][3][3][C]); epilogue: stats (fwd BN statistics),
 // bn_x (BN-backward mask + sums), res (residual add), else plain.  nb: 0 = automatic, 64 / 128 forced.
 PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int C, int N,
-                          float* stats, const bf16_t* res, const bf16_t* bn_x, const float* bn_mean,
+                          float* stats, const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x,
+                          const float* bn_mean,
                           const float* bn_invstd, const float* bn_mscale, const float* bn_mshift, int nb,
                           hipStream_t st) {
     if (!pdnn_conv3x3_supported(Nimg, H, W, C, N)) return (int)hipErrorInvalidValue;
@@ -509,7 +646,8 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     a.dW = make_fdiv_c3(W); a.dH = make_fdiv_c3(H);
     a.tiles = (int)cdiv(a.P, C3_BM);
     a.halo_max = c3_halo_max(W);
-    a.stats = stats; a.res = res;
+    a.stats = stats; a.res = res; a.rmask = res_mask;
+    if (res_mask && !res) return (int)hipErrorInvalidValue;
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
     const int epi0 = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
     // 64 -> 64 channels: the weight-resident persistent kernel (nb = 1; measured slower than the streaming
@@ -546,3 +684,37 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
         default: return c3_launch<64, C3_PLAIN>(a, st);
     }
 }
+
+// 1x1 / stride-1 conv on the pixel-panel kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128}, N % 64 == 0.
+// Epilogues as pdnn_conv3x3.  Returns hipErrorInvalidValue for shapes it does not take.
+PDNN_API int pdnn_conv1x1_panel_supported(long P, int K, int N) {
+    return (K == 64 || K == 128) && N % 64 == 0 && N >= 64 && P > 0 && P < (1L << 30) ? 1 : 0;
+}
+
+PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, long P, int K, int N, float* stats,
+                                const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x, const float* bn_mean,
+                                const float* bn_invstd, const float* bn_mscale, const float* bn_mshift,
+                                hipStream_t st) {
+    if (!pdnn_conv1x1_panel_supported(P, K, N) || (bn_x && !stats) || (res_mask && !res))
+        return (int)hipErrorInvalidValue;
+    C3Args a{};
+    a.x = x; a.w = w; a.y = y; a.C = K; a.N = N; a.P = (int)P;
+    a.tiles = (int)cdiv(P, C3_BM);
+    a.stats = stats; a.res = res; a.rmask = res_mask;
+    a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+    // column groups: split the output columns over blocks only until the grid covers ~2 blocks per CU
+    const int chunks = N / 64;
+    int g = 1;
+    while (g < chunks && (long)a.tiles * g < 512 && chunks % (2 * g) == 0) g *= 2;
+    a.ntiles = g;
+    const int sm = (K / 64) * (C3_BM + 1) * 128 + 2 * 64 * 128;
+    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    switch (epi) {
+        case C3_BNB: return p1_launch<C3_BNB>(a, sm, st);
+        case C3_STATS: return p1_launch<C3_STATS>(a, sm, st);
+        case C3_RES: return p1_launch<C3_RES>(a, sm, st);
+        default: return p1_launch<C3_PLAIN>(a, sm, st);
+    }
+}
+
+PDNN_API int pdnn_conv1x1_panel_stats_rows(long P) { return (int)cdiv(P, C3_BM) * 4; }

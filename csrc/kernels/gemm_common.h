@@ -58,6 +58,7 @@ struct GemmArgs {
     int stage_store;          // 128-row kernel: bf16 epilogue stores staged through LDS (full-row writes)
     // epilogue fusions (E_BF16): residual add, and BN-backward masking + statistics (see epilogue)
     const bf16_t* ep_res;
+    const uint8_t* ep_rmask;  // optional: residual masked by bit (n & 7) of ep_rmask[(row*ldc + n) >> 3] (ReLU bits)
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
     const float* alpha_ptr;   // optional device scalar multiplying alpha (fp8 per-tensor dequantisation)

@@ -450,8 +450,9 @@ gemm_glds_kernel(GemmArgs a) {
                     }
                     if (a.ep_res && ok) {
                         const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
+                        const uint32_t mb = a.ep_rmask ? (uint32_t)(a.ep_rmask[off >> 3] >> (off & 4)) : 0xFu;
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] += bf2f(r[j]);
+                        for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(r[j]) : 0.f;
                     }
                     if (bnb) {
                         // BN coefficients re-read per fragment (L1-resident): keeping them live across the

@@ -520,8 +520,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                         for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(tv[fm][fn][j]));
                     }
                     if (a.ep_res) {
+                        uint32_t mbits = 0xF;
+                        if (a.ep_rmask && ok) {
+                            const long off = orow[fm] * a.ldc + n;
+                            mbits = a.ep_rmask[off >> 3] >> (off & 4);
+                        }
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) v[j] += bf2f(rv[fm][fn][j]);
+                        for (int j = 0; j < 4; ++j) v[j] += ((mbits >> j) & 1) ? bf2f(rv[fm][fn][j]) : 0.f;
                     }
                     if (bnb) {
 #pragma unroll
@@ -1024,8 +1029,10 @@ PDNN_API int pdnn_conv_dgrad_stats_rows(int Nimg, int H, int W, int R, int S, in
 // gm * (bn_x - mean) * invstd (the BatchNorm backward reduction, see batchnorm.hip).
 PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nimg, int H, int W, int C,
                              int Ko, int R, int S, int st, int pad, int Ho, int Wo, float* stats,
-                             const bf16_t* res, const bf16_t* bn_x, const float* bn_mean, const float* bn_invstd,
-                             const float* bn_mscale, const float* bn_mshift, hipStream_t stream) {
+                             const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x, const float* bn_mean,
+                             const float* bn_invstd, const float* bn_mscale, const float* bn_mshift,
+                             hipStream_t stream) {
+    if (res_mask && (st != 1 || C % 8 || !res || res == dx)) return (int)hipErrorInvalidValue;
     ensure_attrs();
     if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() && Ko >= pp_conv_dgrad_k() &&
         (!bn_x || g_pp_conv_bnb)) {
@@ -1033,7 +1040,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
         GemmArgs a{};
         a.M = Nimg * H * W; a.N = C; a.K = Ko;
         a.A = dy; a.lda = Ko; a.B = w; a.ldb = C; a.C = dx; a.ldc = C; a.alpha = 1.f; a.stats = stats;
-        a.ep_res = res;
+        a.ep_res = res; a.ep_rmask = res_mask;
         a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
         if (pp_supported(a, A_KMAJOR, B_MNMAJOR, E_BF16, 1, 1)) return pp_launch(a, A_KMAJOR, B_MNMAJOR, E_BF16, stream);
     }
@@ -1058,7 +1065,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
         a.g.dHW = make_fdiv(c.Hc * c.Wc); a.g.dW = make_fdiv(c.Wc);
         a.scatter = st > 1;
         a.stats_row0 = row0;
-        a.ep_res = res;
+        a.ep_res = res; a.ep_rmask = res_mask;
         a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
         a.ktiles_per_split = (int)cdiv(a.K, BK);
         const int rc = launch<A_CONVT, B_WT, E_BF16, false, false>(a, 1, stream);

@@ -6,16 +6,22 @@
 // column appended to every activation (nn_layer.h:46-50); sigmoid hidden units whose derivative is
 // produced in the same pass (nn_layer.h:130-134); softmax output with the fused (p - onehot)/B
 // gradient (nn_layer.h:150-152); plain SGD W -= lr*G (nn_layer.h:78-83).  GEMMs are a cache-blocked
-// fp32 kernel (the reference calls cblas_dgemm in fp64, util.h:35-81).
+// kernel templated on the precision: fp32 by default, fp64 with --fp64 / the *_ex(fp64=1) entry points, which
+// is the reference's own arithmetic (cblas_dgemm over doubles, util.h:35-81).
 //
 // Distributed roles over the control-plane store (the reference uses MPI p2p with per-layer
 // communicators; here every message is a store key):
 //   step                      int64, current global step (-1 = shut down)          [C-08 / C-11]
 //   w/<step>/<layer>          weights of a layer for that step                     [C-09]
 //   g/<step>/<layer>/<worker> a worker's gradient of a layer for that step         [C-10]
+//   gq_n, gq/<n>              arrival queue: "<step> <layer> <worker>" per pushed gradient
+//   go/<step>                 opened steps (blocking waits of workers / evaluator)  [C-08]
 //   scheme                    run name for the evaluator's output file             [C-12]
-// Master: publishes step + weights, collects gradients with the PS coordinator (backup workers:
-// n_to_collect; stale-by-step drop), applies ApplyGrad(lr / count) (sync_replicas_master_nn.h:124-128).
+// Master: publishes step + weights, then BLOCKS on the arrival queue (the store-side MPI_Waitany of
+// sync_replicas_master_nn.h:66-74; no polling) and feeds every announced gradient to the PS coordinator
+// (backup workers: n_to_collect); a gradient of an older step -- a late worker of a closed step -- is
+// dropped by its step tag (:85) and its key deleted, so nothing leaks; applies ApplyGrad(lr / count)
+// (:124-128).
 // Worker: layer-pipelined forward (fetch layer i's weights just before computing it, worker_nn.h:66-70),
 // pushes each layer's gradient as soon as it exists, and SHORT-CIRCUITS (abandons the iteration)
 // whenever a newer step is published (worker_nn.h:59-64, 79-84).
@@ -38,17 +44,18 @@ namespace {
 // C[M][N] (+)= A[M][K] * B[K][N], all row-major; optional transposes via strides.  Blocked over (k, n);
 // a transposed B block is packed k-major first so the inner loop is a contiguous axpy the compiler
 // vectorises (the strided B[j][k] walk was the slow path of the data-gradient GEMM).
-void gemm(int M, int N, int K, const float* A, int lda, bool ta, const float* B, int ldb, bool tb, float* C,
+template <typename T>
+void gemm(int M, int N, int K, const T* A, int lda, bool ta, const T* B, int ldb, bool tb, T* C,
           int ldc, bool accumulate) {
     if (!accumulate)
-        for (int i = 0; i < M; ++i) std::fill(C + (long)i * ldc, C + (long)i * ldc + N, 0.f);
+        for (int i = 0; i < M; ++i) std::fill(C + (long)i * ldc, C + (long)i * ldc + N, T(0));
     constexpr int BK = 64, BN = 256;
-    std::vector<float> pack(tb ? (size_t)BK * BN : 0);
+    std::vector<T> pack(tb ? (size_t)BK * BN : 0);
     for (int k0 = 0; k0 < K; k0 += BK) {
         const int k1 = std::min(K, k0 + BK);
         for (int n0 = 0; n0 < N; n0 += BN) {
             const int n1 = std::min(N, n0 + BN), nw = n1 - n0;
-            const float* bblk;
+            const T* bblk;
             long bld;
             if (tb) {
                 for (int j = n0; j < n1; ++j)
@@ -60,11 +67,11 @@ void gemm(int M, int N, int K, const float* A, int lda, bool ta, const float* B,
                 bld = ldb;
             }
             for (int i = 0; i < M; ++i) {
-                float* c = C + (long)i * ldc;
+                T* c = C + (long)i * ldc;
                 for (int k = k0; k < k1; ++k) {
-                    const float a = ta ? A[(long)k * lda + i] : A[(long)i * lda + k];
-                    if (a == 0.f) continue;
-                    const float* b = bblk + (long)k * bld;
+                    const T a = ta ? A[(long)k * lda + i] : A[(long)i * lda + k];
+                    if (a == T(0)) continue;
+                    const T* b = bblk + (long)k * bld;
                     for (int j = n0; j < n1; ++j) c[j] += a * b[j];
                 }
             }
@@ -72,31 +79,33 @@ void gemm(int M, int N, int K, const float* A, int lda, bool ta, const float* B,
     }
 }
 
-struct Layer {
+template <typename T>
+struct LayerT {
     int nin, nout;
-    std::vector<float> W, G;   // (nin+1) x nout
+    std::vector<T> W, G;   // (nin+1) x nout
 };
 
-struct MLP {
+template <typename T>
+struct MLPT {
     std::vector<int> sizes;
     int batch;
     float lr;
-    std::vector<Layer> layers;
-    std::vector<std::vector<float>> Z, F, D;   // activations (with ones column), derivatives, deltas
+    std::vector<LayerT<T>> layers;
+    std::vector<std::vector<T>> Z, F, D;   // activations (with ones column), derivatives, deltas
 
-    MLP(const int* s, int n, int b, float lr_, uint64_t seed) : sizes(s, s + n), batch(b), lr(lr_) {
+    MLPT(const int* s, int n, int b, float lr_, uint64_t seed) : sizes(s, s + n), batch(b), lr(lr_) {
         std::mt19937_64 rng(seed);
         std::normal_distribution<float> nd(0.f, 1.f);
         for (int i = 0; i + 1 < n; ++i) {
-            Layer L;
+            LayerT<T> L;
             L.nin = s[i];
             L.nout = s[i + 1];
             L.W.resize((size_t)(L.nin + 1) * L.nout);
-            L.G.assign(L.W.size(), 0.f);
+            L.G.assign(L.W.size(), T(0));
             const float std_ = 1.f / std::sqrt((float)L.nin);      // Gaussian init (nn_layer.h:235-239)
             for (int r = 0; r < L.nin; ++r)
-                for (int c = 0; c < L.nout; ++c) L.W[(size_t)r * L.nout + c] = nd(rng) * std_;
-            for (int c = 0; c < L.nout; ++c) L.W[(size_t)L.nin * L.nout + c] = 0.f;
+                for (int c = 0; c < L.nout; ++c) L.W[(size_t)r * L.nout + c] = T(nd(rng) * std_);
+            for (int c = 0; c < L.nout; ++c) L.W[(size_t)L.nin * L.nout + c] = T(0);
             layers.push_back(std::move(L));
         }
         Z.resize(layers.size() + 1);
@@ -115,37 +124,37 @@ struct MLP {
 
     // forward one layer l: Z[l] -> Z[l+1] (hidden: sigmoid, last: softmax into Z[L] without ones col use)
     void forward_layer(size_t l, int B) {
-        const Layer& L = layers[l];
+        const LayerT<T>& L = layers[l];
         const int wi = L.nin + 1, wo = L.nout + 1;
-        std::vector<float> S((size_t)B * L.nout);
+        std::vector<T> S((size_t)B * L.nout);
         gemm(B, L.nout, wi, Z[l].data(), wi, false, L.W.data(), L.nout, false, S.data(), L.nout, false);
         const bool last = l + 1 == layers.size();
         for (int b = 0; b < B; ++b) {
-            float* z = Z[l + 1].data() + (size_t)b * wo;
-            const float* s = S.data() + (size_t)b * L.nout;
+            T* z = Z[l + 1].data() + (size_t)b * wo;
+            const T* s = S.data() + (size_t)b * L.nout;
             if (!last) {
-                float* f = F[l + 1].data() + (size_t)b * L.nout;
+                T* f = F[l + 1].data() + (size_t)b * L.nout;
                 for (int j = 0; j < L.nout; ++j) {
-                    const float y = 1.f / (1.f + std::exp(-s[j]));
+                    const T y = T(1) / (T(1) + std::exp(-s[j]));
                     z[j] = y;
-                    f[j] = y * (1.f - y);
+                    f[j] = y * (T(1) - y);
                 }
             } else {
-                float m = s[0];
+                T m = s[0];
                 for (int j = 1; j < L.nout; ++j) m = std::max(m, s[j]);
-                float sum = 0.f;
+                T sum = 0;
                 for (int j = 0; j < L.nout; ++j) { z[j] = std::exp(s[j] - m); sum += z[j]; }
                 for (int j = 0; j < L.nout; ++j) z[j] /= sum;
             }
-            z[L.nout] = 1.f;
+            z[L.nout] = T(1);
         }
     }
 
     void load_input(const float* x, int B) {
         const int w = sizes[0] + 1;
         for (int b = 0; b < B; ++b) {
-            memcpy(Z[0].data() + (size_t)b * w, x + (size_t)b * sizes[0], sizeof(float) * sizes[0]);
-            Z[0][(size_t)b * w + sizes[0]] = 1.f;
+            for (int j = 0; j < sizes[0]; ++j) Z[0][(size_t)b * w + j] = T(x[(size_t)b * sizes[0] + j]);
+            Z[0][(size_t)b * w + sizes[0]] = T(1);
         }
     }
 
@@ -154,8 +163,8 @@ struct MLP {
         double loss = 0;
         int bad = 0;
         for (int b = 0; b < B; ++b) {
-            const float* p = Z.back().data() + (size_t)b * w;
-            loss -= std::log(std::max(p[y[b]], 1e-10f));     // LogDot with the 1e-10 bump (util.h:138-144)
+            const T* p = Z.back().data() + (size_t)b * w;
+            loss -= std::log(std::max((double)p[y[b]], 1e-10));     // LogDot with the 1e-10 bump (util.h:138-144)
             int am = 0;
             for (int j = 1; j < nc; ++j)
                 if (p[j] > p[am]) am = j;
@@ -170,12 +179,12 @@ struct MLP {
     void backward(const int* y, int B, CB&& on_grad) {
         const size_t nl = layers.size();
         const int nc = sizes.back();
-        float* d = D[nl].data();
+        T* d = D[nl].data();
         for (int b = 0; b < B; ++b)
             for (int j = 0; j < nc; ++j)
-                d[(size_t)b * nc + j] = (Z[nl][(size_t)b * (nc + 1) + j] - (j == y[b] ? 1.f : 0.f)) / B;
+                d[(size_t)b * nc + j] = (Z[nl][(size_t)b * (nc + 1) + j] - (j == y[b] ? T(1) : T(0))) / T(B);
         for (size_t l = nl; l-- > 0;) {
-            Layer& L = layers[l];
+            LayerT<T>& L = layers[l];
             const int wi = L.nin + 1;
             // G = Z[l]^T . D[l+1]
             gemm(wi, L.nout, B, Z[l].data(), wi, true, D[l + 1].data(), L.nout, false, L.G.data(), L.nout, false);
@@ -200,7 +209,7 @@ struct MLP {
 
     void apply(float lr_scale) {
         for (auto& L : layers)
-            for (size_t i = 0; i < L.W.size(); ++i) L.W[i] -= lr * lr_scale * L.G[i];
+            for (size_t i = 0; i < L.W.size(); ++i) L.W[i] -= T(lr) * T(lr_scale) * L.G[i];
     }
 
     float evaluate(const float* x, const int* y, int n, float* err) {
@@ -220,6 +229,8 @@ struct MLP {
         return (float)(loss / n);
     }
 };
+
+using MLP = MLPT<float>;
 
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -260,10 +271,14 @@ RT_API float pdnn_mlp_loss(void* h, const float* x, const int* labels, int n, fl
     return static_cast<MLP*>(h)->evaluate(x, labels, n, err);
 }
 
-// Single-machine training (CPP-11 test_nn / nn.h:53-65): epoch-wrapping batches, returns iterations run.
-RT_API int pdnn_mlp_train_single(void* h, const float* x, const int* labels, int n, int iters, float* losses) {
-    auto* m = static_cast<MLP*>(h);
-    const int B = m->batch, d = m->sizes[0];
+
+}  // extern "C"
+
+namespace {
+
+template <typename M>
+int train_single_impl(M& m, const float* x, const int* labels, int n, int iters, float* losses) {
+    const int B = m.batch, d = m.sizes[0];
     int off = 0;
     std::vector<float> xb((size_t)B * d);
     std::vector<int> yb(B);
@@ -274,27 +289,33 @@ RT_API int pdnn_mlp_train_single(void* h, const float* x, const int* labels, int
             yb[b] = labels[r];
         }
         off = (off + B) % n;
-        const float l = m->step(xb.data(), yb.data(), B);
-        m->apply(1.f);
+        const float l = m.step(xb.data(), yb.data(), B);
+        m.apply(1.f);
         if (losses) losses[it] = l;
     }
     return iters;
 }
 
-// role: "master" | "worker" | "evaluator".  rank 0 = master, 1 = evaluator, >= 2 workers (CPP-01).
-// Returns 0 on success.  Master writes <out_prefix>timeline_out_<scheme>; evaluator writes
-// <out_prefix>time_loss_out_<scheme>.
-RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int rank, int n_procs, int n_to_collect,
-                             int iters, const float* x, const int* labels, int n, const int* sizes, int n_sizes,
-                             int batch, float lr, int shortcircuit, const char* out_prefix) {
+int64_t get_i64(void* st, const std::string& k, int64_t timeout_ms, bool* ok) {
+    int64_t v = 0;
+    *ok = pdnn_store_get(st, k.c_str(), timeout_ms) == 0 && pdnn_store_last_len(st) == 8;
+    if (*ok) pdnn_store_copy_last(st, &v);
+    return v;
+}
+
+template <typename T>
+int run_role_impl(const char* role, const char* host, int port, int rank, int n_procs, int n_to_collect, int iters,
+                  const float* x, const int* labels, int n, const int* sizes, int n_sizes, int batch, float lr,
+                  int shortcircuit, const char* out_prefix) {
     void* st = pdnn_store_connect(host, port, 30000);
     if (!st) return -1;
-    MLP m(sizes, n_sizes, batch, lr, 1234);
+    MLPT<T> m(sizes, n_sizes, batch, lr, 1234);
     const int L = (int)m.layers.size();
     const int n_workers = n_procs - 2;
     std::string r(role);
     const std::string scheme = "SyncReplicasWithBackup" + std::to_string(n_to_collect) + "_" +
-                               std::to_string(n_workers) + (shortcircuit ? "_shortcircuit" : "");
+                               std::to_string(n_workers) + (shortcircuit ? "_shortcircuit" : "") +
+                               (sizeof(T) == 8 ? "_fp64" : "");
     int rc = 0;
     if (r == "master") {
         pdnn_store_set(st, "scheme", scheme.data(), scheme.size());
@@ -302,52 +323,82 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
         std::string tl = std::string(out_prefix) + "timeline_out_" + scheme;
         FILE* tf = fopen(tl.c_str(), "w");
         const double t0 = now_ms();
-        std::vector<std::vector<float>> acc(L);
+        std::vector<std::vector<T>> acc(L);
+        std::vector<T> g;
+        int64_t qpos = 0;
         for (int64_t s = 1; s <= iters; ++s) {
             pdnn_ps_begin_step(ps, s);
             for (int l = 0; l < L; ++l) {
                 auto& W = m.layers[l].W;
-                pdnn_store_set(st, key("w", s, l).c_str(), W.data(), W.size() * sizeof(float));
-                acc[l].assign(W.size(), 0.f);
+                pdnn_store_set(st, key("w", s, l).c_str(), W.data(), W.size() * sizeof(T));
+                acc[l].assign(W.size(), T(0));
             }
             pdnn_store_set(st, "step", &s, 8);
+            pdnn_store_set(st, key("go", s).c_str(), &s, 8);
             if (tf) fprintf(tf, "%.3f %lld 1\n", now_ms() - t0, (long long)s);
             while (!pdnn_ps_done(ps)) {
-                bool any = false;
-                for (int l = 0; l < L; ++l)
-                    for (int w = 0; w < n_workers; ++w) {
-                        if (pdnn_ps_contributed(ps, l, w)) continue;
-                        const std::string k = key("g", s, l, w + 2);
-                        if (pdnn_store_check(st, k.c_str()) != 1) continue;
-                        if (pdnn_store_get(st, k.c_str(), 1000) != 0) continue;
-                        const size_t nb = pdnn_store_last_len(st);
-                        if (nb != acc[l].size() * sizeof(float)) continue;
-                        std::vector<float> g(acc[l].size());
-                        pdnn_store_copy_last(st, g.data());
-                        if (pdnn_ps_offer(ps, w, l, s, now_ms() - t0) == 0) {
-                            for (size_t i = 0; i < g.size(); ++i) acc[l][i] += g[i];
-                            if (tf) fprintf(tf, "%.3f %lld 0 %d %d\n", now_ms() - t0, (long long)s, w + 2, l);
-                        }
-                        pdnn_store_del(st, k.c_str());
-                        any = true;
+                // block on the next announced gradient (MPI_Waitany over the pre-posted receives)
+                const std::string qk = key("gq", qpos + 1);
+                if (pdnn_store_get(st, qk.c_str(), 60000) != 0) { rc = -4; break; }
+                std::string ent(pdnn_store_last_len(st), '\0');
+                pdnn_store_copy_last(st, &ent[0]);
+                ++qpos;
+                pdnn_store_del(st, qk.c_str());
+                long long gs = 0;
+                int gl = 0, gw = 0;
+                if (sscanf(ent.c_str(), "%lld %d %d", &gs, &gl, &gw) != 3) continue;
+                const std::string gk = key("g", gs, gl, gw);
+                if (gs == s && pdnn_store_get(st, gk.c_str(), 1000) == 0 &&
+                    pdnn_store_last_len(st) == acc[gl].size() * sizeof(T)) {
+                    g.resize(acc[gl].size());
+                    pdnn_store_copy_last(st, g.data());
+                    if (pdnn_ps_offer(ps, gw - 2, gl, gs, now_ms() - t0) == 0) {
+                        for (size_t i = 0; i < g.size(); ++i) acc[gl][i] += g[i];
+                        if (tf) fprintf(tf, "%.3f %lld 0 %d %d\n", now_ms() - t0, (long long)s, gw, gl);
                     }
-                if (!any) std::this_thread::sleep_for(std::chrono::microseconds(200));
+                } else {
+                    pdnn_ps_offer(ps, gw - 2, gl, gs, now_ms() - t0);   // an older step: counted stale, dropped
+                }
+                pdnn_store_del(st, gk.c_str());
             }
+            if (rc) break;
             for (int l = 0; l < L; ++l) {      // ApplyGrad(lr / count): count-correct average fused in
                 const int cnt = std::max(1, pdnn_ps_count(ps, l));
                 auto& W = m.layers[l].W;
-                for (size_t i = 0; i < W.size(); ++i) W[i] -= lr / cnt * acc[l][i];
+                for (size_t i = 0; i < W.size(); ++i) W[i] -= T(lr) / T(cnt) * acc[l][i];
                 if (s > 2) pdnn_store_del(st, key("w", s - 2, l).c_str());
             }
+            if (s > 2) pdnn_store_del(st, key("go", s - 2).c_str());
         }
         int64_t stop = -1;
         // publish the final weights as step iters+1 so the evaluator can score the final model
         const int64_t fin = iters + 1;
         for (int l = 0; l < L; ++l)
-            pdnn_store_set(st, key("w", fin, l).c_str(), m.layers[l].W.data(), m.layers[l].W.size() * sizeof(float));
+            pdnn_store_set(st, key("w", fin, l).c_str(), m.layers[l].W.data(), m.layers[l].W.size() * sizeof(T));
         pdnn_store_set(st, "final_step", &fin, 8);
         pdnn_store_set(st, "step", &stop, 8);
-        if (tf) fclose(tf);
+        pdnn_store_set(st, key("go", fin).c_str(), &stop, 8);
+        // late gradients of the last step(s): drain what is already announced (workers stop at go/<fin>)
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        for (;;) {
+            const std::string qk = key("gq", qpos + 1);
+            if (pdnn_store_get(st, qk.c_str(), 200) != 0) break;
+            std::string ent(pdnn_store_last_len(st), '\0');
+            pdnn_store_copy_last(st, &ent[0]);
+            ++qpos;
+            pdnn_store_del(st, qk.c_str());
+            long long gs = 0;
+            int gl = 0, gw = 0;
+            if (sscanf(ent.c_str(), "%lld %d %d", &gs, &gl, &gw) == 3) {
+                pdnn_ps_offer(ps, gw - 2, gl, gs, now_ms() - t0);
+                pdnn_store_del(st, key("g", gs, gl, gw).c_str());
+            }
+        }
+        if (tf) {
+            fprintf(tf, "# stale_dropped %lld leaked_keys %d\n", (long long)pdnn_ps_stale_dropped(ps),
+                    pdnn_store_keys(st, "g/"));
+            fclose(tf);
+        }
         pdnn_ps_destroy(ps);
     } else if (r == "worker") {
         const int B = batch, d = sizes[0];
@@ -356,16 +407,18 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
         int off = ((rank - 2) * B) % n;
         int64_t cur = 0;
         for (;;) {
-            // wait for a new step
-            int64_t s;
-            for (;;) {
-                s = read_step(st);
-                if (s == -1 || s == -2) break;
-                if (s > cur) break;
-                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            // a worker that fell behind jumps straight to the newest step (its go/ key may be deleted already);
+            // otherwise it blocks until the next step opens (C-08)
+            int64_t latest = read_step(st);
+            if (latest == -1 || latest == -2) break;
+            if (latest <= cur) {
+                bool ok = false;
+                const int64_t s = get_i64(st, key("go", cur + 1), 120000, &ok);
+                if (!ok || s < 0) break;
+                latest = std::max(s, read_step(st));
+                if (latest < 0) break;
             }
-            if (s < 0) break;
-            cur = s;
+            cur = latest;
             for (int b = 0; b < B; ++b) {
                 const int rr = (off + b) % n;
                 memcpy(xb.data() + (size_t)b * d, x + (size_t)rr * d, sizeof(float) * d);
@@ -390,7 +443,11 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
             m.backward(yb.data(), B, [&](size_t l) {
                 if (newer()) return false;
                 const auto& G = m.layers[l].G;
-                pdnn_store_set(st, key("g", cur, (int)l, rank).c_str(), G.data(), G.size() * sizeof(float));
+                pdnn_store_set(st, key("g", cur, (int)l, rank).c_str(), G.data(), G.size() * sizeof(T));
+                // announce it on the master's arrival queue (tagged with the step: stale-drop key)
+                const int64_t q = pdnn_store_add(st, "gq_n", 1);
+                const std::string ent = std::to_string(cur) + " " + std::to_string(l) + " " + std::to_string(rank);
+                pdnn_store_set(st, key("gq", q).c_str(), ent.data(), ent.size());
                 return true;
             });
         }
@@ -401,7 +458,6 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
         std::string fn = std::string(out_prefix) + "time_loss_out_" + sch;
         FILE* f = fopen(fn.c_str(), "w");
         const double t0 = now_ms();
-        int64_t last = 0;
         auto eval_step = [&](int64_t s) {
             for (int l = 0; l < L; ++l) {
                 if (pdnn_store_get(st, key("w", s, l).c_str(), 2000) != 0) return;
@@ -411,9 +467,14 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
             const float loss = m.evaluate(x, labels, n, &err);
             if (f) { fprintf(f, "%lld %.3f %.6f %.6f\n", (long long)s, now_ms() - t0, loss, err); fflush(f); }
         };
+        int64_t next = 1;
         for (;;) {
-            const int64_t s = read_step(st);
-            if (s == -2) break;
+            int64_t s = pdnn_store_check(st, "step") == 1 ? read_step(st) : 0;
+            if (s != -1 && s < next) {
+                bool ok = false;
+                s = get_i64(st, key("go", next), 120000, &ok);               // blocking: no polling
+                if (!ok) break;
+            }
             if (s == -1) {
                 if (pdnn_store_get(st, "final_step", 2000) == 0) {
                     int64_t fs;
@@ -422,8 +483,11 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
                 }
                 break;
             }
-            if (s > last) { last = s; eval_step(s); }
-            else std::this_thread::sleep_for(std::chrono::microseconds(500));
+            // skip to the newest step if training ran ahead of the evaluation
+            const int64_t latest = read_step(st);
+            const int64_t use = latest > s ? latest : s;
+            eval_step(use);
+            next = use + 1;
         }
         if (f) fclose(f);
     } else {
@@ -432,4 +496,50 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
     pdnn_store_close(st);
     return rc;
 }
+
+}  // namespace
+
+extern "C" {
+// Single-machine training (CPP-11 test_nn / nn.h:53-65): epoch-wrapping batches, returns iterations run.
+RT_API int pdnn_mlp_train_single(void* h, const float* x, const int* labels, int n, int iters, float* losses) {
+    return train_single_impl(*static_cast<MLP*>(h), x, labels, n, iters, losses);
 }
+
+// Same in the reference's fp64 (cblas_dgemm) arithmetic when fp64 != 0; the final full-set loss and error rate
+// go to *final_loss / *final_err.
+RT_API int pdnn_mlp_train_single_ex(const int* sizes, int n_sizes, int batch, float lr, uint64_t seed,
+                                    const float* x, const int* labels, int n, int iters, float* losses, int fp64,
+                                    float* final_loss, float* final_err) {
+    if (fp64) {
+        MLPT<double> m(sizes, n_sizes, batch, lr, seed);
+        train_single_impl(m, x, labels, n, iters, losses);
+        if (final_loss) *final_loss = m.evaluate(x, labels, n, final_err);
+    } else {
+        MLPT<float> m(sizes, n_sizes, batch, lr, seed);
+        train_single_impl(m, x, labels, n, iters, losses);
+        if (final_loss) *final_loss = m.evaluate(x, labels, n, final_err);
+    }
+    return iters;
+}
+
+// role: "master" | "worker" | "evaluator".  rank 0 = master, 1 = evaluator, >= 2 workers (CPP-01).
+// Returns 0 on success.  Master writes <out_prefix>timeline_out_<scheme> (ending with a "# stale_dropped N
+// leaked_keys K" summary line); evaluator writes <out_prefix>time_loss_out_<scheme>.
+RT_API int pdnn_mlp_run_role_ex(const char* role, const char* host, int port, int rank, int n_procs,
+                                int n_to_collect, int iters, const float* x, const int* labels, int n,
+                                const int* sizes, int n_sizes, int batch, float lr, int shortcircuit,
+                                const char* out_prefix, int fp64) {
+    if (fp64)
+        return run_role_impl<double>(role, host, port, rank, n_procs, n_to_collect, iters, x, labels, n, sizes,
+                                     n_sizes, batch, lr, shortcircuit, out_prefix);
+    return run_role_impl<float>(role, host, port, rank, n_procs, n_to_collect, iters, x, labels, n, sizes, n_sizes,
+                                batch, lr, shortcircuit, out_prefix);
+}
+
+RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int rank, int n_procs, int n_to_collect,
+                             int iters, const float* x, const int* labels, int n, const int* sizes, int n_sizes,
+                             int batch, float lr, int shortcircuit, const char* out_prefix) {
+    return pdnn_mlp_run_role_ex(role, host, port, rank, n_procs, n_to_collect, iters, x, labels, n, sizes, n_sizes,
+                                batch, lr, shortcircuit, out_prefix, 0);
+}
+}  // extern "C"

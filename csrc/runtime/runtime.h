@@ -63,4 +63,12 @@ RT_API int pdnn_mlp_run_role(const char* role, const char* host, int port, int r
                              int n_to_collect, int iters, const float* x, const int* labels, int n,
                              const int* sizes, int n_sizes, int batch, float lr, int shortcircuit,
                              const char* out_prefix);
+// fp64 != 0: the reference's double-precision arithmetic (MPI_code/src/util/util.h:35-81 cblas_dgemm)
+RT_API int pdnn_mlp_run_role_ex(const char* role, const char* host, int port, int rank, int n_procs,
+                                int n_to_collect, int iters, const float* x, const int* labels, int n,
+                                const int* sizes, int n_sizes, int batch, float lr, int shortcircuit,
+                                const char* out_prefix, int fp64);
+RT_API int pdnn_mlp_train_single_ex(const int* sizes, int n_sizes, int batch, float lr, uint64_t seed,
+                                    const float* x, const int* labels, int n, int iters, float* losses, int fp64,
+                                    float* final_loss, float* final_err);
 }

@@ -5,8 +5,8 @@
 // The reference runs one MPI rank per process (`mpirun -n 8 ./distributed_nn`).  Here the control
 // plane is the framework's TCP store (csrc/runtime/tcp_store.cpp) and the ranks are plain processes:
 //
-//   pdnn_mlp single      [--data DIR] [--iters N] [--batch B] [--lr LR]
-//   pdnn_mlp distributed [--nprocs 8] [--collect K] [--iters N] [--data DIR] [--shortcircuit] [--out PREFIX]
+//   pdnn_mlp single      [--data DIR] [--iters N] [--batch B] [--lr LR] [--fp64]
+//   pdnn_mlp distributed [--nprocs 8] [--collect K] [--iters N] [--data DIR] [--shortcircuit] [--fp64] [--out PREFIX]
 //                        (forks master + evaluator + nprocs-2 workers around a local store: `make distributed_run`)
 //   pdnn_mlp store       --port P                       (stand-alone store server for multi-host runs)
 //   pdnn_mlp role        --role master|evaluator|worker --rank R --nprocs N --host H --port P [...]
@@ -29,7 +29,7 @@ namespace {
 
 struct Args {
     std::string cmd, data, role = "worker", host = "127.0.0.1", out = "";
-    int iters = 100, batch = 128, nprocs = 8, collect = 0, rank = 0, port = 0, shortcircuit = 0;
+    int iters = 100, batch = 128, nprocs = 8, collect = 0, rank = 0, port = 0, shortcircuit = 0, fp64 = 0;
     float lr = 1e-3f;
 };
 
@@ -79,22 +79,20 @@ int run_single(const Args& a) {     // CPP-11: test_load_data(); test_nn();
     std::vector<float> x;
     std::vector<int> y;
     get_data(a, x, y);
-    void* m = pdnn_mlp_create(kSizes.data(), (int)kSizes.size(), a.batch, a.lr, 1234);
     std::vector<float> losses(a.iters);
-    pdnn_mlp_train_single(m, x.data(), y.data(), (int)y.size(), a.iters, losses.data());
+    float l = 0.f, err = 0.f;
+    pdnn_mlp_train_single_ex(kSizes.data(), (int)kSizes.size(), a.batch, a.lr, 1234, x.data(), y.data(),
+                             (int)y.size(), a.iters, losses.data(), a.fp64, &l, &err);
     for (int i = 0; i < a.iters; ++i)
         if (i % 10 == 0 || i == a.iters - 1) printf("iter %d loss %.5f\n", i, losses[i]);
-    float err = 0.f;
-    const float l = pdnn_mlp_loss(m, x.data(), y.data(), (int)y.size(), &err);
-    printf("final loss %.5f error rate %.4f\n", l, err);
-    pdnn_mlp_destroy(m);
+    printf("final loss %.5f error rate %.4f (%s)\n", l, err, a.fp64 ? "fp64" : "fp32");
     return std::isfinite(l) ? 0 : 1;
 }
 
 int run_role(const Args& a, const std::vector<float>& x, const std::vector<int>& y) {
-    return pdnn_mlp_run_role(a.role.c_str(), a.host.c_str(), a.port, a.rank, a.nprocs, a.collect, a.iters, x.data(),
-                             y.data(), (int)y.size(), kSizes.data(), (int)kSizes.size(), a.batch, a.lr,
-                             a.shortcircuit, a.out.c_str());
+    return pdnn_mlp_run_role_ex(a.role.c_str(), a.host.c_str(), a.port, a.rank, a.nprocs, a.collect, a.iters,
+                                x.data(), y.data(), (int)y.size(), kSizes.data(), (int)kSizes.size(), a.batch, a.lr,
+                                a.shortcircuit, a.out.c_str(), a.fp64);
 }
 
 int run_distributed(Args a) {       // CPP-12 distributed_run: master (0) + evaluator (1) + workers (2..)
@@ -134,7 +132,7 @@ int run_distributed(Args a) {       // CPP-12 distributed_run: master (0) + eval
 void usage() {
     fprintf(stderr,
             "usage: pdnn_mlp single|distributed|store|role [--data DIR] [--iters N] [--batch B] [--lr LR]\n"
-            "       [--nprocs N] [--collect K] [--shortcircuit] [--out PREFIX] [--role R] [--rank R]\n"
+            "       [--nprocs N] [--collect K] [--shortcircuit] [--fp64] [--out PREFIX] [--role R] [--rank R]\n"
             "       [--host H] [--port P]\n");
 }
 }  // namespace
@@ -159,6 +157,7 @@ int main(int argc, char** argv) {
         else if (k == "--nprocs") a.nprocs = atoi(val());
         else if (k == "--collect") a.collect = atoi(val());
         else if (k == "--shortcircuit") a.shortcircuit = 1;
+        else if (k == "--fp64") a.fp64 = 1;
         else if (k == "--out") a.out = val();
         else if (k == "--role") a.role = val();
         else if (k == "--rank") a.rank = atoi(val());

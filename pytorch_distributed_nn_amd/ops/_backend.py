@@ -34,15 +34,18 @@ _SIGS = {
     "pdnn_gemm_nn": [P, L, P, L, P, L, I, I, I, F, I, P],
     "pdnn_gemm_tn_acc": [P, L, P, L, P, L, I, I, I, F, P],
     "pdnn_conv_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
-    "pdnn_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P],
+    "pdnn_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P],
     "pdnn_conv_dgrad_stats_rows": [I, I, I, I, I, I, I],
     "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "pdnn_gemm_stats_rows": [I],
-    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, I, P],
+    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
     "pdnn_conv3x3_force": [I],
+    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P],
+    "pdnn_conv1x1_panel_supported": [L, I, I],
+    "pdnn_conv1x1_panel_stats_rows": [L],
     "pdnn_set_glds_mode": [I],
     "pdnn_set_pp_mode": [I],
     "pdnn_set_pp_bn": [I],

@@ -60,6 +60,8 @@ _SIDE = {}
 # Bottleneck forward: materialise a2 = relu(bn2(t2)) for conv3 (1) or apply BN2+ReLU in conv3's operand
 # prologue (0).  PDNN_MATERIALIZE_A2 for A/B runs.
 MATERIALIZE_A2 = os.environ.get("PDNN_MATERIALIZE_A2", "1") == "1"
+# identity-block backward: gout * mask added by conv1's dgrad epilogue (1) or materialised by the BN backward (0)
+MASKED_RES = os.environ.get("PDNN_MASKED_RES", "1") == "1"
 
 
 def side_stream_if_active(t):
@@ -292,6 +294,11 @@ class BottleneckFn(torch.autograd.Function):
                                          x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                          dbeta2=dbd)
             gres = None
+        elif MASKED_RES:
+            # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
+            # materialised here: one activation-sized write less per block
+            dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb)
+            gres = gout
         else:
             dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
@@ -313,7 +320,7 @@ class BottleneckFn(torch.autograd.Function):
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
             grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3, dwd, rgd, rbd)
         else:
-            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape))
+            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=mb if MASKED_RES else None)
             grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3)
         sink.done()
         return (dx, None, None, None) + grads
@@ -369,7 +376,8 @@ class BasicBlockFn(torch.autograd.Function):
                                          mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd, dbeta2=dbd)
             gres = None
         else:
-            dt2, _, gres = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=3, msrc=mb, want_gm=True)
+            dt2, _, _ = K.bn_bwd_apply(g2d, t2_2d, m2, i2, g2, dg2, db2, mode=3, msrc=mb)
+            gres = gout                                     # masked by conv1's data-gradient epilogue
         dt2 = dt2.view(t2.shape)
         dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, 1, 1)
         dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
@@ -381,7 +389,7 @@ class BasicBlockFn(torch.autograd.Function):
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)      # shortcut, in place
             grads = (dw1, rg1, rb1, dw2, rg2, rb2, dwd, rgd, rbd)
         else:
-            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape))
+            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape), res_mask=mb)
             grads = (dw1, rg1, rb1, dw2, rg2, rb2)
         sink.done()
         return (dx, None, None, None) + grads

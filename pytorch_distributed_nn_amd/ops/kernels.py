@@ -163,6 +163,38 @@ def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
             and lib().pdnn_conv3x3_supported(N, H, W, Cin, Cout) == 1)
 
 
+# 1x1 / stride-1 convs with K in {64, 128} run on the pixel-panel kernel (csrc/kernels/conv3x3.hip):
+# PDNN_PANEL1X1=0 / set_panel_mode(0) sends them back to the implicit-GEMM engines (A/B runs)
+_P1 = {"mode": int(_os.environ.get("PDNN_PANEL1X1", "1"))}
+
+
+def set_panel_mode(mode: int) -> int:
+    old = _P1["mode"]
+    _P1["mode"] = int(mode)
+    return old
+
+
+def _panel_ok(P, K, N, R, S, st, pad):
+    return (_P1["mode"] and R == 1 and S == 1 and st == 1 and pad == 0
+            and lib().pdnn_conv1x1_panel_supported(P, K, N) == 1)
+
+
+def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None):
+    """y[P][N] = x[P][K] . w[N][K]^T on the panel kernel; epilogues as conv3x3 / conv_dgrad."""
+    P, Kc = x2d.shape
+    N = w2d.shape[0]
+    y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
+    slab = None
+    t = mean = inv = msc = msh = None
+    if want_stats or bn is not None:
+        slab = torch.empty(2 * lib().pdnn_conv1x1_panel_stats_rows(P), N, device=x2d.device, dtype=F32)
+    if bn is not None:
+        t, mean, inv, msc, msh = bn
+    call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), stream())
+    return y, slab
+
+
 def conv3x3_flip(w):
     """W'[C][3][3][K] = W[K][2-r][2-s][C] (bf16): the data gradient's weight for the halo kernel."""
     K, R, S, C = w.shape
@@ -171,7 +203,7 @@ def conv3x3_flip(w):
     return wt
 
 
-def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None):
+def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None):
     """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
     conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
     Nimg, H, W, C = x.shape
@@ -183,8 +215,8 @@ def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None):
         slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
     if bn is not None:
         t, mean, inv, msc, msh = bn
-    call("pdnn_conv3x3", ptr(x), ptr(w), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(res), ptr(t), ptr(mean),
-         ptr(inv), ptr(msc), ptr(msh), _C3["nb"], stream())
+    call("pdnn_conv3x3", ptr(x), ptr(w), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), _C3["nb"], stream())
     return y, slab
 
 
@@ -201,6 +233,9 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
     if pro is None and _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
         return conv3x3(x, w, want_stats=want_stats)
+    if pro is None and _panel_ok(N * H * W, C, K, R, S, st, pad):
+        y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats)
+        return y.view(N, H, W, K), slab
     y = torch.empty(N, Ho, Wo, K, device=x.device, dtype=BF16)
     stats = None
     if want_stats:
@@ -211,13 +246,17 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     return y, stats
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None):
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None):
     """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
     conv only the pixels its taps reach are touched, the others keep ``res``).
 
     bn = (t, mean, invstd, mscale, mshift): fuse the BatchNorm backward of the layer that produced t:
     returns (gm, slab) where gm = dx * [t*mscale + mshift > 0] and slab holds the partial sums of gm and
-    gm*(t-mean)*invstd (finalize with bn_bwd_finalize)."""
+    gm*(t-mean)*invstd (finalize with bn_bwd_finalize).
+
+    res_mask: uint8 [N*H*W][C/8] ReLU bits (bn_apply's mask): the residual is added only where its bit is set,
+    i.e. res * mask -- the identity branch's gradient computed here instead of materialised by the BN
+    backward (stride 1 only)."""
     _bf16_c(dy, "conv_dgrad.dy")
     N, H, W, C = x_shape
     _bf16_c(w, "conv_dgrad.w")
@@ -234,9 +273,21 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None):
     if res is not None:
         _bf16_c(res, "conv_dgrad.res")
         _chk(tuple(res.shape) == (N, H, W, C), "conv_dgrad: res shape")
+    if res_mask is not None:
+        _chk(res is not None and st == 1 and res_mask.dtype == torch.uint8 and res_mask.is_contiguous()
+             and res_mask.numel() * 8 == N * H * W * C and (out is None or out.data_ptr() != res.data_ptr()),
+             "conv_dgrad: res_mask needs res, stride 1, uint8 [N*H*W][C/8], out not aliasing res")
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
-        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out)
+        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask)
+        return (y, slab) if bn is not None else y
+    if _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
+        # dx[P][C] = dy[P][K] . W[K][C]: the panel kernel with the transposed weight W^T [C][K]
+        y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)),
+                                res=None if res is None else res.view(-1, C), res_mask=res_mask,
+                                bn=None if bn is None else (bn[0].view(-1, C),) + tuple(bn[1:]),
+                                out=None if out is None else out.view(-1, C))
+        y = y.view(N, H, W, C)
         return (y, slab) if bn is not None else y
     dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
     slab = None
@@ -249,7 +300,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None):
         _bf16_c(res, "conv_dgrad.res")
         _chk(tuple(res.shape) == (N, H, W, C), "conv_dgrad: res shape")
     call("pdnn_conv_dgrad", ptr(dy), ptr(w), ptr(dx), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(slab), ptr(res),
-         ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), stream())
+         ptr(res_mask), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), stream())
     return (dx, slab) if bn is not None else dx
 
 

@@ -96,3 +96,52 @@ def test_conv3x3_matches_gemm_engine_bitwise_stats_layout(K):
     K.set_conv3x3_mode(*old)
     assert rel(y1, y0) < 1e-2
     torch.testing.assert_close(s1.view(-1, 2, 64).sum(0), s0.view(-1, 2, 64).sum(0), rtol=2e-3, atol=1.0)
+
+
+# ------------------------------------------------------------------- 1x1 pixel-panel kernel (K in {64, 128})
+PANEL = [(2, 56, 56, 64, 256), (3, 28, 28, 128, 512), (1, 7, 7, 128, 2048), (2, 9, 11, 64, 64), (5, 14, 14, 64, 1024),
+         (1, 1, 3, 128, 128)]
+
+
+@pytest.mark.parametrize("shape", PANEL)
+def test_conv1x1_panel_fwd_stats(K, shape):
+    N, H, W, C, Ko = shape
+    x = torch.randn(N, H, W, C, device="cuda").to(BF)
+    w = (torch.randn(Ko, 1, 1, C, device="cuda") * 0.1).to(BF)
+    y, slab = K.conv_fwd(x, w, 1, 0, want_stats=True)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert rel(y, ref) < 1.5e-2
+    assert slab.shape[0] == 2 * K.lib().pdnn_conv1x1_panel_stats_rows(N * H * W)
+    yf = y.float().reshape(-1, Ko)
+    s = slab.view(-1, 2, Ko).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", PANEL)
+def test_conv1x1_panel_dgrad(K, shape):
+    """dx = dy . W (K = dy channels in {64, 128}) plain / masked residual / fused BN backward."""
+    N, H, W, Kc, C = shape            # dy has Kc channels, dx has C
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = (torch.randn(Kc, 1, 1, C, device="cuda") * 0.1).to(BF)
+    y = F.conv2d(x, w.float().permute(0, 3, 1, 2))
+    dy = torch.randn(*y.permute(0, 2, 3, 1).shape, device="cuda").to(BF)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dx_ref = x.grad.permute(0, 2, 3, 1)
+    assert rel(K.conv_dgrad(dy, w, (N, H, W, C), 1, 0), dx_ref) < 1.5e-2
+    res = torch.randn(N, H, W, C, device="cuda").to(BF)
+    keep = torch.rand(N * H * W, C, device="cuda") > 0.5
+    bits = (keep.view(-1, C // 8, 8).to(torch.int32) << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1)
+    dxm = K.conv_dgrad(dy, w, (N, H, W, C), 1, 0, res=res, res_mask=bits.to(torch.uint8).contiguous())
+    assert rel(dxm, dx_ref + res.float() * keep.view(N, H, W, C)) < 1.5e-2
+    t = torch.randn(N, H, W, C, device="cuda").to(BF)
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    msc, msh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), 1, 0, bn=(t, mean, inv, msc, msh))
+    mask = (t.float() * msc + msh) > 0
+    assert rel(gm, dx_ref * mask) < 1.5e-2
+    s = slab.view(-1, 2, C).sum(0)
+    gmf = gm.float().reshape(-1, C)
+    xhat = ((t.float() - mean) * inv).reshape(-1, C)
+    assert torch.allclose(s[0], gmf.sum(0), rtol=1e-3, atol=1e-3 * gmf.abs().sum(0).max().item())
+    assert torch.allclose(s[1], (gmf * xhat).sum(0), rtol=1e-3, atol=1e-3 * (gmf * xhat).abs().sum(0).max().item())

@@ -416,3 +416,24 @@ def test_nchw_to_nhwc_pad(K, C, dt):
     ref = torch.zeros(3, 13, 11, cp, device="cuda", dtype=BF)
     ref[..., :C] = x.permute(0, 2, 3, 1).to(BF)
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 8, 64, 256, 1), (2, 56, 56, 64, 256, 1), (3, 7, 7, 512, 2048, 1),
+                                   (2, 14, 14, 256, 1024, 1), (2, 9, 9, 64, 64, 3), (2, 28, 28, 128, 128, 3)])
+def test_conv_dgrad_masked_residual(K, shape):
+    """dx = dgrad(dy) + res * mask (the identity branch of a residual block through the block output's ReLU
+    bits), on every engine: the BN backward no longer materialises res * mask."""
+    N, H, W, Co, C, R = shape
+    pad = R // 2
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = rnd(Co, R, R, C, scale=0.1)
+    y = F.conv2d(x, w.float().permute(0, 3, 1, 2), None, 1, pad)
+    dy = rnd(*y.permute(0, 2, 3, 1).shape)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    res = rnd(N, H, W, C)
+    keep = torch.rand(N * H * W, C, device="cuda") > 0.4
+    bits = (keep.view(-1, C // 8, 8).to(torch.int32) << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1)
+    mask_u8 = bits.to(torch.uint8).contiguous()
+    dx = K.conv_dgrad(dy, w, (N, H, W, C), 1, pad, res=res, res_mask=mask_u8)
+    ref = x.grad.permute(0, 2, 3, 1) + res.float() * keep.view(N, H, W, C)
+    assert rel(dx, ref) < 1.5e-2

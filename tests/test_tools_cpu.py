@@ -36,6 +36,33 @@ def test_pdnn_mlp_distributed_backup_workers(binary, tmp_path):
     assert 2.0 <= avg <= 3.0          # >= n_to_collect per step; late (stale) arrivals are logged too
 
 
+def test_pdnn_mlp_native_master_blocks_on_arrival_queue_and_drops_stale(binary, tmp_path):
+    """the native master consumes a blocking arrival queue (no per-key polling); with 6
+    workers and n_to_collect 2 the late gradients of closed steps are dropped by their step tag (the
+    coordinator's stale path, sync_replicas_master_nn.h:85) and every gradient key is deleted."""
+    out = str(tmp_path) + "/"
+    r = subprocess.run([binary, "distributed", "--nprocs", "8", "--collect", "2", "--iters", "12", "--out", out],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    tl = [f for f in os.listdir(tmp_path) if f.startswith("timeline_out_")][0]
+    summary = [ln for ln in open(os.path.join(tmp_path, tl)) if ln.startswith("# stale_dropped")][0].split()
+    stale, leaked = int(summary[2]), int(summary[4])
+    assert stale > 0 and leaked == 0, summary
+
+
+def test_pdnn_mlp_fp64_matches_fp32(binary):
+    """--fp64 runs the reference's double-precision arithmetic (cblas_dgemm, util.h:35-81); after 20 steps
+    its loss agrees with the fp32 build to float rounding."""
+    res = {}
+    for flag in ([], ["--fp64"]):
+        r = subprocess.run([binary, "single", "--iters", "20", *flag], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("final loss")][0]
+        assert ("fp64" in line) == bool(flag)
+        res[bool(flag)] = float(line.split()[2])
+    assert abs(res[True] - res[False]) < 1e-3 * abs(res[False]), res
+
+
 def test_report_percentiles(tmp_path):
     p = tmp_path / "m.jsonl"
     with open(p, "w") as f:

@@ -60,7 +60,7 @@ def timeline(files):
     for f in files:
         per_step = collections.Counter()
         starts = {}
-        lines = [ln.split() for ln in open(f)]
+        lines = [ln.split() for ln in open(f) if not ln.startswith("#")]     # "# stale_dropped ..." summary
         native = any(len(p) >= 5 for p in lines)
         for p in lines:
             if len(p) < 3:
