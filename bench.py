@@ -40,6 +40,30 @@ def native_loaded():
         return []
 
 
+def _ddp_rehearsal(a):
+    """Re-run this benchmark in a child process through the DDP path at world size 1 (PDNN_FORCE_PG +
+    PDNN_DDP_FORCE_COMM: RCCL process group of one rank); returns {value, ms_per_step} or an error note."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PDNN_FORCE_PG="1", PDNN_DDP_FORCE_COMM="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    argv = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.steps), "--warmup",
+            str(a.warmup), "--model", a.model, "--bucket-mb", str(a.bucket_mb), "--graph", a.graph,
+            "--ddp-rehearsal"] + (["--batch", str(a.batch)] if a.batch else []) + (["--fp8"] if a.fp8 else [])
+    try:
+        r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=900)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        rec = json.loads(line)
+        return {"value": rec["value"], "ms_per_step": rec["ms_per_step"],
+                "note": "same step through DDP: bucket hooks + RCCL all-reduce over a 1-rank process group"}
+    except Exception as e:       # never lose the headline line over the rehearsal
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,6 +78,13 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
     ap.add_argument("--graph", default="auto", choices=["off", "on", "auto", "collectives"],
                     help="replay each step as one captured hipGraph (auto: single-GPU runs, not the side-stream ResNets)")
+    ap.add_argument("--comm-bf16", action="store_true", help="DDP: all-reduce gradients in bf16 on the wire")
+    ap.add_argument("--num-aggregate", type=int, default=0,
+                    help="DDP k-of-n straggler mode with this k (control plane + host throttle on every step)")
+    ap.add_argument("--ddp-rehearsal", action="store_true",
+                    help="(internal) the 1-GPU DDP-path run: RCCL process group of one rank, every bucket all-reduced")
+    ap.add_argument("--no-ddp-rehearsal", action="store_true",
+                    help="at --gpus 1, skip the second measurement of the DDP code path")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -81,7 +112,8 @@ def main():
             model.enable_fp8()
     use_ddp = world > 1 or os.environ.get("PDNN_DDP_FORCE_COMM") == "1"     # 1-GPU rehearsal of the DDP path
     if use_ddp:
-        net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
+        net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb, num_aggregate=a.num_aggregate,
+                                      comm_dtype=torch.bfloat16 if a.comm_bf16 else None)
     else:
         flatten_module(model)
         net = model
@@ -102,9 +134,10 @@ def main():
     # concurrently with the data-gradient chain (ops/fused_resnet.py): eager launches overlap the two
     # streams (ResNet-50 8,635 vs 8,013 img/s serial), a replayed hipGraph ran the branches nearly serially
     # (8,160-8,196 img/s; gpurun_out/r2_32)
-    side_overlap = not lm and not small and os.environ.get("PDNN_SIDE_WGRAD", "1") != "0"
+    from pytorch_distributed_nn_amd import tuning
+    side_overlap = not lm and not small and tuning.get("side_wgrad") == 1
     # GPT-2 on one GPU: AdamW chunks run on a side stream during the backward (optim/overlap.py)
-    opt_overlap = lm and world == 1 and not use_ddp and os.environ.get("PDNN_OPT_OVERLAP", "0") == "1"
+    opt_overlap = lm and world == 1 and not use_ddp and tuning.get("opt_overlap") == 1
     use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1
                                                                    and not side_overlap and not opt_overlap)
     ov = None
@@ -128,18 +161,20 @@ def main():
             loss = net(xs[i % 2], ys[i % 2])
         else:
             loss = OF.cross_entropy(net(xs[i % 2]), ys[i % 2])
-        loss.backward()
+        if getattr(net, "kofn", None) is not None:
+            net.backward(loss)
+        else:
+            loss.backward()
         if ov is None:
             opt.step()
         return loss
 
     # The side-stream ResNets run their compute stream at high priority (the side stream stays at the default,
     # lowest one): the wavefront dispatcher then fills the CUs with the critical-path data-gradient chain first
-    # and the weight gradients take the gaps (+0.5% on ResNet-50, gpurun_out/r2_35).  PDNN_MAIN_PRIO overrides.
-    prio = os.environ.get("PDNN_MAIN_PRIO", "-1" if side_overlap else None)
+    # and the weight gradients take the gaps (+0.5% on ResNet-50, gpurun_out/r2_35).
     ctx = contextlib.nullcontext()
-    if prio is not None and dev.type == "cuda":
-        main_stream = torch.cuda.Stream(device=dev, priority=int(prio))
+    if side_overlap and dev.type == "cuda":
+        main_stream = torch.cuda.Stream(device=dev, priority=-1)
         main_stream.wait_stream(torch.cuda.current_stream(dev))     # the data tensors were made on the default one
         ctx = torch.cuda.stream(main_stream)
     with ctx:
@@ -159,6 +194,15 @@ def main():
     dt = t.item()
     ms = 1e3 * dt / a.steps
     value = B * world * a.steps / dt
+    if getattr(net, "kofn", None) is not None:
+        net.close()
+    # At one GPU the plain step above is the N = 1 point of the scaling curve (the fastest 1-GPU
+    # configuration); the same step through the DDP code path (bucket hooks, RCCL all-reduce of every bucket
+    # over a one-rank process group) is measured in a child process and reported alongside, so a scaling
+    # efficiency can be read against either.
+    ddp_rehearsal = None
+    if world == 1 and not use_ddp and not a.no_ddp_rehearsal and not a.ddp_rehearsal and env.rank == 0:
+        ddp_rehearsal = _ddp_rehearsal(a)
     if lm and env.rank == 0:
         tok = value * S
         print(json.dumps({
@@ -176,6 +220,8 @@ def main():
             "data": "synthetic (device-resident random token ids), random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "native_loaded": native_loaded(),
+            "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
+            "ddp_path_1gpu": ddp_rehearsal,
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
@@ -201,6 +247,8 @@ def main():
                     "random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "native_loaded": native_loaded(),
+            "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
+            "ddp_path_1gpu": ddp_rehearsal,
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",

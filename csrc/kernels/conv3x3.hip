@@ -28,6 +28,7 @@
 // with 4 consecutive output channels of one pixel; 4 waves each own 64 pixels x NB channels.
 // Reference layers: pytorch_code/model_ops/resnet.py:19-21,44-48 (every 3x3 conv of the ResNets).
 #include "gemm_common.h"
+#include "tuning.h"
 
 namespace {
 using namespace pg;
@@ -575,7 +576,7 @@ int c3_launch(const C3Args& a, hipStream_t st) {
 
 }  // namespace
 
-static int g_c3_force = -1;
+
 
 template <int EPI>
 int p1_launch(const C3Args& a, int sm, hipStream_t st) {
@@ -587,10 +588,7 @@ int p1_launch(const C3Args& a, int sm, hipStream_t st) {
     hipLaunchKernelGGL((conv1x1_panel_kernel<EPI>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }
-static int c3_force() {
-    if (g_c3_force < 0) { const char* e = getenv("PDNN_CONV3X3"); g_c3_force = (e && atoi(e) == 2) ? 1 : 0; }
-    return g_c3_force;
-}
+static int c3_force() { return pg::tune().conv3x3_force; }
 
 static FastDiv make_fdiv_c3(uint32_t d) {
     FastDiv f;
@@ -607,7 +605,7 @@ static FastDiv make_fdiv_c3(uint32_t d) {
 PDNN_API int pdnn_conv3x3_supported(int Nimg, int H, int W, int C, int N) {
     if (C % 64 || N % 64 || C < 64 || N < 64 || W < 1 || H < 1) return 0;
     // narrow images: a 256-pixel tile spans so many rows that the implicit-GEMM engine's 128-row tiles win
-    // (ResNet-50 7x7x512, tools/bench_conv3x3.py: 93 / 134 us vs 130 / 152 fwd / dgrad); PDNN_CONV3X3=2 forces
+    // (ResNet-50 7x7x512, tools/bench_conv3x3.py: 93 / 134 us vs 130 / 152 fwd / dgrad); tuning conv3x3_force
     if (W < 12 && !c3_force()) return 0;
     if ((long)Nimg * H * W >= (1L << 31) / 2) return 0;
     const int nb = N % 128 == 0 ? 128 : 64;
@@ -618,7 +616,7 @@ PDNN_API int pdnn_conv3x3_supported(int Nimg, int H, int W, int C, int N) {
 // 1: take every supported channel shape regardless of the image width (tests); returns the previous
 PDNN_API int pdnn_conv3x3_force(int f) {
     const int old = c3_force();
-    g_c3_force = f ? 1 : 0;
+    pg::tune().conv3x3_force = f ? 1 : 0;
     return old;
 }
 

@@ -557,11 +557,7 @@ inline int device_cus() {
     }
     return n;
 }
-int g_glds_persistent = -1;
-inline int glds_persistent() {
-    if (g_glds_persistent < 0) { const char* e = getenv("PDNN_GLDS_PERSISTENT"); g_glds_persistent = e ? atoi(e) : 0; }
-    return g_glds_persistent;
-}
+inline int glds_persistent() { return tune().glds_persistent; }
 
 template <int AM, int BMODE, int EM, int BN, int DT = 0>
 int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {

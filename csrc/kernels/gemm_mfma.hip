@@ -36,6 +36,7 @@
 //    accumulation for split-K weight gradients.
 //  * XCD-aware bijective block remap (T1) so neighbouring tiles share an XCD's L2.
 #include "gemm_common.h"
+#include "tuning.h"
 
 
 namespace {
@@ -641,49 +642,23 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
 #include "gemm_glds.h"
 
-// glds engine selection: 1 = automatic (default), 0 = off, 2 = whenever the operands allow (tests).
-// Environment PDNN_GLDS or pdnn_set_glds_mode().
-int g_glds_mode = -1;
-int glds_mode() {
-    if (g_glds_mode < 0) { const char* e = getenv("PDNN_GLDS"); g_glds_mode = e ? atoi(e) : 1; }
-    return g_glds_mode;
-}
+// Engine selection reads the dispatch table (tuning.h: entries glds, glds_min_tiles, glds_fwd_k,
+// glds_dgrad_n / _k, with the measurements behind each default).
+// The 256-row tiles win once the grid fills most of the 256 CUs; with fewer tiles the 128-tile kernel's finer
+// grid (2 blocks/CU) has better wave quantisation.  Per layer (profiles/conv_layers_glds_vs_reg_r1.json) glds
+// wins the implicit-GEMM forward once the reduction is long and the data gradient unless both C and K are
+// small, but the glds data gradient's BN-backward epilogue tiles ran 2.3% slower in the whole step, so the
+// data gradient stays on the register-staged kernel (7,790 -> 7,970 img/s).
+int glds_mode() { return tune().glds; }
 bool glds_enabled() { return glds_mode() != 0; }
-// measured (tools/bench_gemm.py, tools/bench_conv.py): the 256-row tiles win once the grid fills most of the
-// 256 CUs; with fewer tiles the 128-tile kernel's finer grid (2 blocks/CU) has better wave quantisation.
-// Per-layer conv measurements (profiles/conv_layers_glds_vs_reg_r1.json): the glds engine wins on the
-// implicit-GEMM forward once the reduction is long (K >= 512: 3x3 convs, wide 1x1s) and on the data
-// gradient unless both C and K are small; the low-K 1x1 convs are memory bound and prefer the 128-row
-// kernel's finer grid, and the weight gradient's split-K atomics are faster there too.
-// PDNN_GLDS_MIN_TILES: the grid-size threshold (A/B experiments; default 192)
-int g_glds_min_tiles = -1;
-int glds_min_tiles() {
-    if (g_glds_min_tiles < 0) { const char* e = getenv("PDNN_GLDS_MIN_TILES"); g_glds_min_tiles = e ? atoi(e) : 192; }
-    return g_glds_min_tiles;
-}
-// Per-operand-mode shape thresholds (A/B knobs): PDNN_GLDS_FWD_K (forward reduction length) and
-// PDNN_GLDS_DGRAD_N / PDNN_GLDS_DGRAD_K (data gradient: input channels / reduction length).
-// Whole-step A/B on ResNet-50 bs256 (tools/gpu_runs/gpu_run62.sh, gpu_run63.sh): the per-layer wins of the
-// glds data gradient do not survive inside the step (its BN-backward epilogue tiles at 256 rows run
-// 2.3% slower in aggregate than the 128-tile kernel), so dgrad stays on the register-staged kernel by
-// default (7,790 -> 7,970 img/s); forward K >= 1024 is within noise of 512 and of "never".
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-int g_glds_fwd_k = -1, g_glds_dgrad_n = -1, g_glds_dgrad_k = -1;
+int glds_min_tiles() { return tune().glds_min_tiles; }
 template <int AM>
 bool glds_worth(const GemmArgs& a, int batch, int splits) {
     if (glds_mode() == 2) return true;
     const long tiles = cdiv(a.M, GBM) * cdiv(a.N, glds_bn(a.N)) * (long)batch * splits;
     if (tiles < glds_min_tiles()) return false;
-    if (g_glds_fwd_k < 0) {
-        g_glds_fwd_k = env_int("PDNN_GLDS_FWD_K", 1024);
-        g_glds_dgrad_n = env_int("PDNN_GLDS_DGRAD_N", 1 << 30);
-        g_glds_dgrad_k = env_int("PDNN_GLDS_DGRAD_K", 1 << 30);
-    }
-    if constexpr (AM == A_CONV) return a.K >= g_glds_fwd_k;
-    if constexpr (AM == A_CONVT) return a.N >= g_glds_dgrad_n || a.K >= g_glds_dgrad_k;
+    if constexpr (AM == A_CONV) return a.K >= tune().glds_fwd_k;
+    if constexpr (AM == A_CONVT) return a.N >= tune().glds_dgrad_n || a.K >= tune().glds_dgrad_k;
     return true;
 }
 
@@ -697,31 +672,13 @@ FastDiv make_fdiv(uint32_t d) {
     return f;
 }
 
-// smallest output width a 1x1 conv is sent to the ping-pong engine with (its tiles are 128 / 256 wide);
-// PDNN_PP_CONV_MINN for A/B runs
-// and the shortest reduction (PDNN_PP_CONV_FWD_K / PDNN_PP_CONV_DGRAD_K).  Measured per layer at bs256
-// (tools/bench_conv.py, tools/pp_one.py --kind fwd1x1|dgrad1x1bn): the plain / residual data gradient wins
-// on pp from K >= 256; the forward with BN statistics and the data gradient with the BN-backward epilogue
-// are slower there than on the 128-row kernel (the fused epilogue roughly doubles the pp epilogue time),
-// so by default those stay off pp (PDNN_PP_CONV_FWD_K, PDNN_PP_CONV_BNB=1 turn them on).
-int g_pp_conv_min_n = -1, g_pp_conv_fwd_k = -1, g_pp_conv_dgrad_k = -1, g_pp_conv_bnb = 0;
-int pp_conv_min_n() {
-    if (g_pp_conv_min_n < 0) {
-        g_pp_conv_min_n = env_int("PDNN_PP_CONV_MINN", 128);
-        g_pp_conv_fwd_k = env_int("PDNN_PP_CONV_FWD_K", 1 << 30);
-        g_pp_conv_dgrad_k = env_int("PDNN_PP_CONV_DGRAD_K", 512);   // 256 before the 128x64 tiles (r2_46: +0.5%)
-        g_pp_conv_bnb = env_int("PDNN_PP_CONV_BNB", 0);
-    }
-    return g_pp_conv_min_n;
-}
-int pp_conv_fwd_k() { pp_conv_min_n(); return g_pp_conv_fwd_k; }
-int pp_conv_dgrad_k() { pp_conv_min_n(); return g_pp_conv_dgrad_k; }
-
-int g_stage_store = -1;
-int stage_store_mode() {
-    if (g_stage_store < 0) { const char* e = getenv("PDNN_STAGED_STORE"); g_stage_store = e ? atoi(e) : 1; }
-    return g_stage_store;
-}
+// 1x1 stride-1 convs on the ping-pong engine (tuning.h pp_conv_*): the plain / residual data gradient wins
+// there from K >= 512; the forward with BN statistics and the data gradient with the BN-backward epilogue
+// are slower there than on the 128-row kernel (the fused epilogue roughly doubles the pp epilogue time).
+int pp_conv_min_n() { return tune().pp_conv_min_n; }
+int pp_conv_fwd_k() { return tune().pp_conv_fwd_k; }
+int pp_conv_dgrad_k() { return tune().pp_conv_dgrad_k; }
+int stage_store_mode() { return tune().staged_store; }
 
 template <int AM, int BMODE, int EM, bool PA, bool PB, int BNW>
 int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
@@ -744,15 +701,9 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     PDNN_LAUNCH_RET;
 }
 
-// PDNN_LOWK_BN64=k: GEMMs of at most k K-steps use the 128x64 tile (fewer registers: more blocks per CU
-// to hide the load -> MFMA -> store latency of short reductions); 0 = off.  Default 24 (ResNet-50 bs256,
-// gpurun_out/r2_42-44: off 8,818, k = 1-4 8,930-8,975, 8 8,990, 16 8,963-9,010, 24 8,988 vs 16 8,963 and
-// 36 8,932 on one box, every GEMM 8,930 img/s)
-int g_lowk_bn64 = -1;
-int lowk_bn64_mode() {
-    if (g_lowk_bn64 < 0) { const char* e = getenv("PDNN_LOWK_BN64"); g_lowk_bn64 = e ? atoi(e) : 24; }
-    return g_lowk_bn64;
-}
+// lowk_bn64 = k: GEMMs of at most k K-steps use the 128x64 tile (fewer registers: more blocks per CU to hide
+// the load -> MFMA -> store latency of short reductions); 0 = off (r2_42-44 sweep in tuning.h)
+int lowk_bn64_mode() { return tune().lowk_bn64; }
 
 // the register-staged 128-row kernel only (the weight gradients' split-K atomics): N <= 64 -> 128x64 tile
 template <int AM, int BMODE, int EM, bool PA, bool PB>
@@ -781,11 +732,10 @@ int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
 template <int BNW>
 int tiles_of(const GemmArgs& a) { return (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW)); }
 
-int g_split_blocks = -1;
 int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
-    // enough workgroups to cover 256 CUs twice (PDNN_SPLIT_BLOCKS, A/B knob), but keep >= 4 K-steps per split
-    if (g_split_blocks < 0) g_split_blocks = env_int("PDNN_SPLIT_BLOCKS", 512);
-    int want = (g_split_blocks + tiles - 1) / tiles;
+    // enough workgroups to cover 256 CUs twice (tuning.h split_blocks), but keep >= 4 K-steps per split
+    const int blocks = tune().split_blocks;
+    int want = (blocks + tiles - 1) / tiles;
     int s = want < max_splits ? want : max_splits;
     int cap = ktiles / 4;
     if (s > cap) s = cap;
@@ -825,7 +775,7 @@ static void ensure_attrs() {}
 
 PDNN_API int pdnn_set_staged_store(int mode) {
     const int old = stage_store_mode();
-    g_stage_store = mode;
+    tune().staged_store = mode;
     return old;
 }
 
@@ -838,7 +788,7 @@ PDNN_API int pdnn_set_pp_mode(int mode) {
 
 PDNN_API int pdnn_set_glds_mode(int mode) {
     const int old = glds_mode();
-    g_glds_mode = mode;
+    tune().glds = mode;
     return old;
 }
 
@@ -910,8 +860,8 @@ PDNN_API int pdnn_gemm_fp8(const uint8_t* X, long ldx, const uint8_t* W, long ld
     a.C = Y; a.ldc = ldy; a.alpha = 1.f; a.alpha_ptr = scale;
     a.bias = bias; a.relu = act; a.ep_aux = aux; a.ep_res = res; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
-    // ping-pong engine (fp8 slices of 128 bytes per row) unless PDNN_PP_FP8=0 / pp off: the glds engine
-    if (pp_mode_ref() && env_int("PDNN_PP_FP8", 1) && M >= 16 && N >= 16)
+    // ping-pong engine (fp8 slices of 128 bytes per row) unless tuning pp_fp8 = 0 / pp off: the glds engine
+    if (pp_mode_ref() && tune().pp_fp8 && M >= 16 && N >= 16)
         return pp_fp8_launch(a, out_f32 ? E_F32 : E_BF16, st);
     const int bn = glds_bn(N);
     if (out_f32) {
@@ -1035,7 +985,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
     if (res_mask && (st != 1 || C % 8 || !res || res == dx)) return (int)hipErrorInvalidValue;
     ensure_attrs();
     if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() && Ko >= pp_conv_dgrad_k() &&
-        (!bn_x || g_pp_conv_bnb)) {
+        (!bn_x || tune().pp_conv_bnb)) {
         // 1x1 stride-1: dx[M][C] = dy[M][Ko] . w[Ko][C] (w as a [k][n] matrix) on the ping-pong engine
         GemmArgs a{};
         a.M = Nimg * H * W; a.N = C; a.K = Ko;

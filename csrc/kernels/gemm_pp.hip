@@ -34,6 +34,7 @@
 //  * Epilogues: alpha, bias, ReLU / GELU (+ pre-activation to ep_aux), dGELU, residual add (bf16);
 //    fp32 store / in-place accumulate (acc_c) / split-K partial slabs (slab reduction kernel below).
 #include "gemm_common.h"
+#include "tuning.h"
 
 namespace pg {
 namespace {
@@ -577,8 +578,6 @@ using C256b = PPC<256, 1, 5>;        // 160 KiB ring (A/B: PDNN_PP_BN=257)
 using C8_128 = PPC<128, 2, 3, 1>;    // fp8: 48 KiB slots (128-byte rows), 3 in the ring
 using C8_96 = PPC<96, 2, 3, 1>;
 
-int g_pp_mode = -1;
-int g_pp_force_bn = -1;
 long long* g_pp_trace = nullptr;
 
 int device_cus() {
@@ -591,7 +590,6 @@ int device_cus() {
     return n;
 }
 
-int g_pp_ablate = -1;
 
 template <class C, int FX>
 constexpr int pp_smem() { return C::SMEM + ((FX & (FX_PRO | FX_BNB)) ? 2 * PP_PRO_MAXK * 4 : 0); }
@@ -609,7 +607,7 @@ void set_attr() {
 
 template <class C, int AM, int BMODE, int EM, int FX = 0>
 int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
-    if (g_pp_ablate < 0) { const char* e = getenv("PDNN_PP_ABLATE"); g_pp_ablate = e ? atoi(e) : 0; }
+    const int g_pp_ablate = tune().pp_ablate;
     const long items = cdiv(a.M, PP_BM) * cdiv(a.N, C::BN) * splits;
     const int cus = device_cus();
     const int grid = items <= cus ? (int)items : (cus / 8) * 8;     // persistent: one block per CU
@@ -655,7 +653,7 @@ double bn_eff(int bn) {
 
 // kk: both operands K-major (every tile width); otherwise / with fusions only 128 and 256
 int pick_bn(const GemmArgs& a, bool kk) {
-    if (g_pp_force_bn < 0) { const char* e = getenv("PDNN_PP_BN"); g_pp_force_bn = e ? atoi(e) : 0; }
+    const int g_pp_force_bn = tune().pp_bn;
     const int cus = device_cus();
     static const int kk_opts[] = {256, 288, 192, 128, 96};
     static const int mn_opts[] = {256, 128};
@@ -684,10 +682,7 @@ int fx_of(const GemmArgs& a) {
 
 }  // namespace
 
-int& pp_mode_ref() {
-    if (g_pp_mode < 0) { const char* e = getenv("PDNN_PP"); g_pp_mode = e ? atoi(e) : 1; }
-    return g_pp_mode;
-}
+int& pp_mode_ref() { return tune().pp; }
 
 bool pp_supported(const GemmArgs& a, int amode, int bmode, int em, int batch, int splits) {
     const int mode = pp_mode_ref();
@@ -740,7 +735,7 @@ int pp_fp8_launch(const GemmArgs& a0, int em, hipStream_t st) {
     const int cus = device_cus();
     const double t128 = (double)cdiv(cdiv(a.M, PP_BM) * cdiv(a.N, 128), cus) * 128 / bn_eff(128);
     const double t96 = (double)cdiv(cdiv(a.M, PP_BM) * cdiv(a.N, 96), cus) * 96 / bn_eff(96);
-    const bool w96 = g_pp_force_bn == 96 || (g_pp_force_bn != 128 && t96 < t128 * 0.999);
+    const bool w96 = tune().pp_bn == 96 || (tune().pp_bn != 128 && t96 < t128 * 0.999);
     if (em == E_F32) return w96 ? launch_cfg<C8_96, A_KMAJOR, B_KMAJOR, E_F32>(a, 1, st)
                                 : launch_cfg<C8_128, A_KMAJOR, B_KMAJOR, E_F32>(a, 1, st);
     if (a.stats) return w96 ? launch_cfg<C8_96, A_KMAJOR, B_KMAJOR, E_BF16, FX_STATS>(a, 1, st)
@@ -878,7 +873,7 @@ PDNN_API void pdnn_set_pp_trace(long long* buf) { pg::g_pp_trace = buf; }
 
 // force a tile width (0 = automatic); returns the previous setting.  A/B experiments and tests.
 PDNN_API int pdnn_set_pp_bn(int bn) {
-    const int old = pg::g_pp_force_bn < 0 ? 0 : pg::g_pp_force_bn;
-    pg::g_pp_force_bn = bn;
+    const int old = pg::tune().pp_bn;
+    pg::tune().pp_bn = bn;
     return old;
 }

@@ -1,0 +1,91 @@
+// The dispatch table of tuning.h: defaults, the PDNN_TUNE override string and the C API.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "common.h"
+#include "tuning.h"
+
+namespace pg {
+namespace {
+std::string g_tune_error;
+
+int* field(Tune& t, const char* name) {
+#define PDNN_TUNE_LOOKUP(n, d, doc) if (!strcmp(name, #n)) return &t.n;
+    PDNN_TUNE_TABLE(PDNN_TUNE_LOOKUP)
+#undef PDNN_TUNE_LOOKUP
+    return nullptr;
+}
+
+// Python-side entries of the same variable (pytorch_distributed_nn_amd/tuning.py) are accepted here
+bool python_key(const std::string& k) {
+    static const char* keys[] = {"side_wgrad", "materialize_a2", "conv3x3", "panel1x1", "direct_grad", "opt_overlap"};
+    for (const char* p : keys)
+        if (k == p) return true;
+    return false;
+}
+
+Tune make() {
+    Tune t;
+    const char* e = getenv("PDNN_TUNE");
+    if (!e) return t;
+    std::string s(e);
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        size_t c = s.find(',', pos);
+        if (c == std::string::npos) c = s.size();
+        const std::string item = s.substr(pos, c - pos);
+        pos = c + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        const std::string k = item.substr(0, eq);
+        if (eq == std::string::npos) { g_tune_error += "PDNN_TUNE: '" + item + "' is not key=value; "; continue; }
+        int* f = field(t, k.c_str());
+        if (f) *f = atoi(item.c_str() + eq + 1);
+        else if (!python_key(k)) g_tune_error += "PDNN_TUNE: unknown key '" + k + "'; ";
+    }
+    return t;
+}
+}  // namespace
+
+Tune& tune() {
+    static Tune t = make();
+    return t;
+}
+
+}  // namespace pg
+
+// old value, or INT32_MIN for an unknown name
+PDNN_API int pdnn_tune_set(const char* name, int value) {
+    int* f = pg::field(pg::tune(), name);
+    if (!f) return (int)0x80000000;
+    const int old = *f;
+    *f = value;
+    return old;
+}
+
+PDNN_API int pdnn_tune_get(const char* name) {
+    int* f = pg::field(pg::tune(), name);
+    return f ? *f : (int)0x80000000;
+}
+
+// "name=value|default|doc\n" per entry into buf (truncated to n bytes); returns the full length
+PDNN_API int pdnn_tune_list(char* buf, int n) {
+    std::string out;
+    const pg::Tune& t = pg::tune();
+#define PDNN_TUNE_LIST(nm, d, doc) out += std::string(#nm) + "=" + std::to_string(t.nm) + "|" + std::to_string(d) + "|" + doc + "\n";
+    PDNN_TUNE_TABLE(PDNN_TUNE_LIST)
+#undef PDNN_TUNE_LIST
+    if (buf && n > 0) {
+        strncpy(buf, out.c_str(), n - 1);
+        buf[n - 1] = 0;
+    }
+    return (int)out.size();
+}
+
+// empty when PDNN_TUNE parsed cleanly
+PDNN_API const char* pdnn_tune_error() {
+    pg::tune();
+    return pg::g_tune_error.c_str();
+}

@@ -43,6 +43,10 @@ _SIGS = {
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
     "pdnn_conv3x3_force": [I],
+    "pdnn_tune_set": [ctypes.c_char_p, I],
+    "pdnn_tune_get": [ctypes.c_char_p],
+    "pdnn_tune_list": [ctypes.c_char_p, I],
+    "pdnn_tune_error": [],
     "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
@@ -143,6 +147,12 @@ def _load():
             continue
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
+    if getattr(lib, "pdnn_tune_error", None) is not None:
+        lib.pdnn_tune_error.restype = ctypes.c_char_p
+        err = lib.pdnn_tune_error().decode()
+        if err:                  # PDNN_TUNE names an entry that exists in neither table: fail loudly
+            _ERR = err
+            return None
     _LIB = lib
     return _LIB
 

@@ -25,6 +25,7 @@ import os
 
 import torch
 
+from .. import tuning
 from ..optim.flat import direct_grad, grad_ready
 from . import kernels as K
 from .functional import weight_bf16
@@ -57,11 +58,10 @@ def _conv_bn(x, wk, st, pad, pro, training, bn_params, bufs, mom, eps):
 
 
 _SIDE = {}
-# Bottleneck forward: materialise a2 = relu(bn2(t2)) for conv3 (1) or apply BN2+ReLU in conv3's operand
-# prologue (0).  PDNN_MATERIALIZE_A2 for A/B runs.
-MATERIALIZE_A2 = os.environ.get("PDNN_MATERIALIZE_A2", "1") == "1"
-# identity-block backward: gout * mask added by conv1's dgrad epilogue (1) or materialised by the BN backward (0)
-MASKED_RES = os.environ.get("PDNN_MASKED_RES", "1") == "1"
+# Bottleneck forward: materialise a2 = relu(bn2(t2)) for conv3 (tuning materialize_a2) or apply BN2+ReLU in
+# conv3's operand prologue.  Identity-block backward: gout * mask is added by conv1's dgrad epilogue rather
+# than materialised by the BN backward (one activation write less per block; +0.2%, gpurun_out/r3_07).
+MASKED_RES = True
 
 
 def side_stream_if_active(t):
@@ -72,13 +72,13 @@ def side_stream_if_active(t):
 
 
 def _side_stream(dev):
-    """The weight-gradient side stream of a device (PDNN_SIDE_WGRAD=0 disables it)."""
-    if os.environ.get("PDNN_SIDE_WGRAD", "1") == "0" or dev.type != "cuda":
+    """The weight-gradient side stream of a device (tuning side_wgrad = 0 disables it).  It runs at the
+    default (lowest) priority; the compute stream gets the high one (bench.py)."""
+    if not tuning.get("side_wgrad") or dev.type != "cuda":
         return None
     s = _SIDE.get(dev.index)
     if s is None:
-        # PDNN_SIDE_PRIO: stream priority of the side stream (lower = more urgent; clamped to the device range)
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev, priority=int(os.environ.get("PDNN_SIDE_PRIO", "0")))
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev, priority=0)
     return s
 
 
@@ -219,7 +219,7 @@ class BottleneckFn(torch.autograd.Function):
         w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
         k1, k2, k3 = shadows[:3]
         side_down = None
-        side = _side_stream(x.device) if (down and os.environ.get("PDNN_SIDE_DOWN", "1") == "1") else None
+        side = _side_stream(x.device) if down else None
         if side is not None:
             # the shortcut conv only depends on x: run it (and its BN statistics) beside conv1 -> conv2 -> conv3
             main = torch.cuda.current_stream(x.device)
@@ -239,7 +239,7 @@ class BottleneckFn(torch.autograd.Function):
         C1 = t1.shape[-1]
         a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)
         t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
-        if MATERIALIZE_A2:
+        if tuning.get("materialize_a2"):
             # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
             # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
             # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs

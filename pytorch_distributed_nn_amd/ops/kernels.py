@@ -146,9 +146,36 @@ def stats_rows(M: int) -> int:
 
 
 # 3x3 / stride-1 / pad-1 convs run on the LDS-halo kernel (csrc/kernels/conv3x3.hip): 1 = whenever the
-# shape is supported (default), 0 = the implicit-GEMM engine (A/B runs; PDNN_CONV3X3 or set_conv3x3_mode)
-import os as _os
-_C3 = {"mode": int(_os.environ.get("PDNN_CONV3X3", "1")), "nb": 0}
+# shape is supported (default), 0 = the implicit-GEMM engine (tuning conv3x3 / set_conv3x3_mode)
+from .. import tuning as _tuning
+_C3 = {"mode": _tuning.get("conv3x3"), "nb": 0}
+
+
+def tune_set(key: str, value: int) -> int:
+    """Set a kernel-side dispatch-table entry (csrc/kernels/tuning.h); returns the previous value."""
+    old = lib().pdnn_tune_set(key.encode(), int(value))
+    _chk(old != -2 ** 31, f"unknown kernel tuning key {key!r}")
+    return old
+
+
+def tune_get(key: str) -> int:
+    v = lib().pdnn_tune_get(key.encode())
+    _chk(v != -2 ** 31, f"unknown kernel tuning key {key!r}")
+    return v
+
+
+def tune_table():
+    """[(key, value, default, doc)] of the kernel-side dispatch table."""
+    import ctypes
+    n = lib().pdnn_tune_list(None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().pdnn_tune_list(buf, n + 1)
+    out = []
+    for line in buf.value.decode().splitlines():
+        kv, dflt, doc = line.split("|", 2)
+        k, v = kv.split("=")
+        out.append((k, int(v), int(dflt), doc))
+    return out
 
 
 def set_conv3x3_mode(mode: int, nb: int = 0):
@@ -164,8 +191,8 @@ def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
 
 
 # 1x1 / stride-1 convs with K in {64, 128} run on the pixel-panel kernel (csrc/kernels/conv3x3.hip):
-# PDNN_PANEL1X1=0 / set_panel_mode(0) sends them back to the implicit-GEMM engines (A/B runs)
-_P1 = {"mode": int(_os.environ.get("PDNN_PANEL1X1", "1"))}
+# tuning panel1x1 = 0 / set_panel_mode(0) sends them back to the implicit-GEMM engines (A/B runs)
+_P1 = {"mode": _tuning.get("panel1x1")}
 
 
 def set_panel_mode(mode: int) -> int:
@@ -281,7 +308,9 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
         y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask)
         return (y, slab) if bn is not None else y
-    if _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
+    # panel data gradient only for K = 64 (ResNet stage 1): at K = 128 -> 512 the implicit-GEMM engine was faster
+    # (154 vs 176 us, gpurun_out/r3_08)
+    if K == 64 and _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
         # dx[P][C] = dy[P][K] . W[K][C]: the panel kernel with the transposed weight W^T [C][K]
         y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)),
                                 res=None if res is None else res.view(-1, C), res_mask=res_mask,

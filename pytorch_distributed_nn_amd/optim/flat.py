@@ -20,6 +20,8 @@ import os
 
 import torch
 
+from .. import tuning as _tuning
+
 ALIGN = 64
 
 
@@ -172,7 +174,7 @@ def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatPar
 # torch build skip those hooks for None gradients (probed once), :func:`grad_ready` runs them instead.
 # Only for parameters used ONCE per forward (a tied weight's contributions are summed by autograd).
 # ------------------------------------------------------------------------------------------------
-DIRECT_GRAD = os.environ.get("PDNN_DIRECT_GRAD", "1") == "1"
+DIRECT_GRAD = bool(_tuning.get("direct_grad"))
 
 
 def await_param(p):

@@ -96,6 +96,28 @@ class _WeightUseMode(torch.overrides.TorchFunctionMode):
         return func(*args, **kwargs)
 
 
+class _StagedRecv:
+    """irecv of a CUDA tensor over gloo through a host buffer (gloo's p2p moves host memory only)."""
+
+    def __init__(self, dst, src):
+        self.dst = dst
+        self.buf = torch.empty(dst.shape, dtype=dst.dtype, pin_memory=True)
+        self.work = dist.irecv(self.buf, src)
+
+    def wait(self):
+        self.work.wait()
+        self.dst.copy_(self.buf, non_blocking=True)
+
+
+class _StagedSend:
+    def __init__(self, src, dst):
+        self.buf = src.detach().to("cpu")          # waits for the producing kernels
+        self.work = dist.isend(self.buf, dst)
+
+    def wait(self):
+        self.work.wait()
+
+
 def _nullcontext():
     import contextlib
     return contextlib.nullcontext()
@@ -179,6 +201,20 @@ class _Base:
         self.store = Store(self.host, _store_port(cfg))
         self._pending, self._land = {}, {}
 
+    # point-to-point transfers: direct on RCCL (and for host tensors); staged through host memory when CUDA
+    # tensors travel over gloo (the one-GPU test boxes run several ranks on one device)
+    def _staged(self, t):
+        return t.is_cuda and dist.get_backend() == "gloo"
+
+    def _isend(self, t, dst):
+        return _StagedSend(t, dst) if self._staged(t) else dist.isend(t, dst)
+
+    def _irecv(self, t, src):
+        return _StagedRecv(t, src) if self._staged(t) else dist.irecv(t, src)
+
+    def _recv(self, t, src):
+        self._irecv(t, src).wait()
+
     def _weight_buckets(self):
         """Weight-push units in forward order: the gradient buckets reversed (one unit when not pipelined)."""
         if not self.cfg.pipelined_push:
@@ -195,7 +231,7 @@ class _Base:
             if self.cfg.comm_type == "Bcast":
                 works.append(dist.broadcast(view, 0, async_op=True))
             else:
-                works += [dist.isend(view, r) for r in range(1, self.world)]
+                works += [self._isend(view, r) for r in range(1, self.world)]
         for w in works:
             w.wait()
 
@@ -209,7 +245,7 @@ class _Base:
             if self.cfg.comm_type == "Bcast":
                 self._pending[b] = dist.broadcast(view, 0, async_op=True)
             else:
-                self._pending[b] = dist.irecv(view, 0)
+                self._pending[b] = self._irecv(view, 0)
 
     def _wait_bucket(self, b):
         w = self._pending.pop(b, None)
@@ -261,7 +297,7 @@ class PSMaster(_Base):
     def _receive(self, r, b):
         s, e, _ = self.buckets[b]
         buf = self.stage[: e - s]
-        dist.recv(buf, r)
+        self._recv(buf, r)
         return buf
 
     def _save(self, step, final=False):
@@ -443,7 +479,7 @@ class PSWorker(_Base):
             self._events.append(ev)
         n = self.store.add("q_n", 1)
         self.store.set(f"q/{n}", f"{self.rank},{self.cur},{b}")
-        self._works.append(dist.isend(view, 0))
+        self._works.append(self._isend(view, 0))
         self.sent.append((self.cur, b))
 
     def train(self, batches):

@@ -1,0 +1,53 @@
+"""Python-side entries of the dispatch table (the kernel-side table is csrc/kernels/tuning.h).
+
+One environment variable overrides either side for A/B runs: ``PDNN_TUNE="key=value,key=value"`` (keys of
+both tables; the kernel library reports unknown ones when it loads).  Each default is the measured optimum:
+
+=================  =======  ===========================================================================
+key                default  meaning (measurement)
+=================  =======  ===========================================================================
+side_wgrad         1        conv weight gradients on a second HIP stream beside the data-gradient chain
+                            (ResNet-50 +8.3%, profiles/resnet50_bs256_side_stream_r2.txt)
+materialize_a2     1        Bottleneck: write a2 = relu(bn2(t2)) once instead of conv3's operand prologue
+                            (9,240 -> 9,596 img/s, gpurun_out/r3_05)
+conv3x3            1        3x3 / stride-1 convs on the LDS-halo kernel (+2.5%, gpurun_out/r3_07)
+panel1x1           1        1x1 / stride-1 convs with K <= 128 on the pixel-panel kernel (+1.1%, r3_08)
+direct_grad        1        fused ops accumulate weight gradients straight into the flat arena
+opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream during the backward
+=================  =======  ===========================================================================
+"""
+from __future__ import annotations
+
+import os
+
+DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "direct_grad": 1, "opt_overlap": 0}
+
+_VALUES = dict(DEFAULTS)
+
+
+def _parse(s: str) -> dict:
+    out = {}
+    for item in filter(None, (p.strip() for p in s.split(","))):
+        if "=" not in item:
+            raise ValueError(f"PDNN_TUNE: {item!r} is not key=value")
+        k, v = item.split("=", 1)
+        out[k.strip()] = int(v)
+    return out
+
+
+for _k, _v in _parse(os.environ.get("PDNN_TUNE", "")).items():
+    if _k in _VALUES:
+        _VALUES[_k] = _v
+
+
+def get(key: str) -> int:
+    return _VALUES[key]
+
+
+def set(key: str, value: int) -> int:        # noqa: A001 - mirrors pdnn_tune_set
+    """Set a Python-side entry; returns the previous value."""
+    if key not in _VALUES:
+        raise KeyError(f"unknown tuning key {key!r} (kernel-side keys: ops.kernels.tune_set)")
+    old = _VALUES[key]
+    _VALUES[key] = int(value)
+    return old

@@ -1,0 +1,114 @@
+"""The reference's namesake capability on the GPU: a straggler killed mid-backward.
+
+* DDP k-of-n (k = 1 of 2) around the FUSED ResNet-50 (two HIP streams: weight gradients on the side
+  stream): rank 1 sleeps in its gradient hooks, rank 0 finishes first and closes the step, rank 1 raises
+  StepAborted inside its backward while side-stream weight-gradient kernels are still in flight, zero-fills
+  its remaining buckets and every bucket is averaged by ITS contributor count.  The next step (no
+  straggler) must be exact again: nothing the aborted step left on the side stream may leak into it.
+  Run with the side stream on and off.
+* Parameter server with CUDA tensors: master + 2 workers on the GPU, k-of-n kill, fused SGD on the master,
+  layer-pipelined weight push (per-bucket bf16 shadow refresh on the device).
+References: pytorch_code/sync_replicas_master_nn.py:172-186 (kill on the k-th arrival),
+pytorch_code/model_ops/lenet.py:168-178 (worker kill poll), MPI_code/src/distributed/worker_nn.h:59-84."""
+import copy
+
+import pytest
+import torch
+
+from dist_utils import run_world
+
+pytestmark = pytest.mark.gpu
+
+
+def _ddp_kill_job(rank, world):
+    import time
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim.flat import flatten_module
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = build_model("resnet50").to(dev)
+    ref = copy.deepcopy(m)
+    fref = flatten_module(ref)
+    net = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5, num_aggregate=1)
+    slow = {"on": False}
+    if rank == 1:
+        for p in m.parameters():
+            p.register_post_accumulate_grad_hook(lambda _p: time.sleep(0.04) if slow["on"] else None)
+    out = []
+    for step in range(2):
+        g = [torch.Generator().manual_seed(10 * step + r) for r in range(world)]
+        data = [(torch.randn(4, 3, 64, 64, generator=g[r]).to(dev), torch.randint(0, 1000, (4,), generator=g[r]).to(dev))
+                for r in range(world)]
+        # local gradients of both ranks' batches on an un-wrapped copy with the same weights
+        fref.data.copy_(net.flat.data)
+        fref.refresh_shadow()
+        locs = []
+        for r in range(world):
+            fref.zero_grad()
+            OF.cross_entropy(ref(data[r][0]), data[r][1]).backward()
+            locs.append(fref.grad.clone())
+        torch.cuda.synchronize()
+        slow["on"] = step == 0
+        net.zero_grad()
+        aborted = net.backward(OF.cross_entropy(net(data[rank][0]), data[rank][1]))
+        torch.cuda.synchronize()
+        counts = [int(c) for c in net.last_counts.cpu().tolist()]
+        errs = []
+        for b, (s, e, _) in enumerate(net.buckets):
+            exp = (locs[0][s:e] + (locs[1][s:e] if counts[b] == 2 else 0)) / counts[b]
+            errs.append(((net.flat.grad[s:e] - exp).norm() / exp.norm().clamp_min(1e-12)).item())
+        out.append((aborted, counts, max(errs), bool(torch.isfinite(net.flat.grad).all())))
+    net.close()
+    return out
+
+
+@pytest.mark.parametrize("side", ["1", "0"], ids=["side-stream-wgrad", "serial-wgrad"])
+def test_ddp_kofn_kill_fused_resnet50_on_gpu(side):
+    res = run_world(_ddp_kill_job, 2, (), timeout=600, device=None, env={"PDNN_SIDE_WGRAD": side})
+    (a0, c0, e0, f0), (a0n, c0n, e0n, f0n) = res[0]
+    (a1, c1, e1, f1), (a1n, c1n, e1n, f1n) = res[1]
+    assert not a0 and a1, res                          # the straggler was killed mid-backward
+    assert c0 == c1 and min(c0) == 1 and max(c0) <= 2  # matched collectives, per-bucket counts
+    assert 1 in c0                                     # ... with buckets rank 1 never delivered
+    assert e0 < 2e-3 and e1 < 2e-3 and f0 and f1, res  # count-correct average, finite
+    # next step: nobody straggles -> exact two-rank average again (no leak from the aborted step)
+    assert not a0n and not a1n and c0n == [2] * len(c0n), res
+    assert e0n < 2e-3 and e1n < 2e-3 and f0n and f1n, res
+
+
+def _ps_gpu_job(rank, world, out_dir):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = build_model("mlp_cpp", 10).to(dev)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(512, 784, generator=g)
+    y = torch.randint(0, 10, (512,), generator=g)
+    cfg = PSConfig(comm_type="Bcast", num_aggregate=1, lr=0.05, momentum=0.9, max_steps=6, out_dir=out_dir,
+                   inject_straggler={2: 40.0}, bucket_cap_mb=0.5, first_bucket_mb=0.05)
+
+    def batches():
+        i = 0
+        while True:
+            sl = slice((i * 32) % 512, (i * 32) % 512 + 32)
+            yield x[sl].to(dev, torch.bfloat16), y[sl].to(dev)
+            i += 1
+
+    res = run_ps(model, cfg, dev, loss_fn=OF.cross_entropy, batches=batches())
+    w = torch.cat([p.detach().float().flatten() for p in model.parameters()])
+    return res, w.cpu(), next(model.parameters()).is_cuda
+
+
+def test_ps_kofn_kill_with_cuda_tensors(tmp_path):
+    res = run_world(_ps_gpu_job, 3, (str(tmp_path),), timeout=600, device=None)
+    log, w0, cuda0 = res[0]
+    assert cuda0 and all(r["count"] == 1 for r in log), log          # k = 1: one gradient per step
+    assert sum(1 in r["arrived"] for r in log) >= 4, log              # the fast worker wins
+    assert res[2][0] >= 3, res[2][0]                                  # the straggler was short-circuited
+    assert torch.isfinite(w0).all()
+    for r in res[1:]:
+        assert torch.equal(r[1], w0)                                  # final push: consistent weights
