@@ -984,8 +984,8 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
                              hipStream_t stream) {
     if (res_mask && (st != 1 || C % 8 || !res || res == dx)) return (int)hipErrorInvalidValue;
     ensure_attrs();
-    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() && Ko >= pp_conv_dgrad_k() &&
-        (!bn_x || tune().pp_conv_bnb)) {
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() &&
+        (bn_x ? Ko >= tune().pp_conv_bnb_k : Ko >= pp_conv_dgrad_k())) {
         // 1x1 stride-1: dx[M][C] = dy[M][Ko] . w[Ko][C] (w as a [k][n] matrix) on the ping-pong engine
         GemmArgs a{};
         a.M = Nimg * H * W; a.N = C; a.K = Ko;

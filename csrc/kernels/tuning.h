@@ -25,7 +25,7 @@ namespace pg {
     X(pp_conv_min_n, 128, "1x1 stride-1 convs on the ping-pong engine from this output width")               \
     X(pp_conv_fwd_k, 1 << 30, "... forward from this reduction length (off: BN-stats epilogue slower there)")  \
     X(pp_conv_dgrad_k, 512, "... data gradient from this reduction length (r2_46: 512 vs 256 +0.5%)")        \
-    X(pp_conv_bnb, 0, "... data gradient with the fused BN-backward epilogue (off: slower there)")           \
+    X(pp_conv_bnb_k, 1 << 30, "... data gradient with the fused BN-backward epilogue from this reduction length")  \
     X(staged_store, 1, "128-row kernel: bf16 epilogue stores staged through LDS (full rows)")                \
     X(lowk_bn64, 24, "GEMMs of <= this many K-steps take the 128x64 tile (r2_42-44 sweep: 24)")             \
     X(split_blocks, 512, "split-K weight gradients: target blocks (r2 sweep: 256/384 -2%/-1%, 768 equal)")   \

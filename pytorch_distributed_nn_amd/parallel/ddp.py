@@ -368,6 +368,16 @@ class DistributedDataParallel(nn.Module):
         # them (ops/fused_resnet.py): the bucket's collective (and any zero-fill / cast of the bucket) is issued
         # from the side stream after it has caught up with the compute stream, so it is ordered after both
         # while the compute stream runs on into the next block's backward.
+        if self.kofn is not None and self.throttle and self.flat.grad.is_cuda:
+            # keep the host at most two buckets ahead of the GPU, so an abort stops real GPU work.  The event is
+            # recorded on the COMPUTE stream (the data-gradient chain): recorded on the weight-gradient side
+            # stream, which runs at low priority and lags, it held the host back until the side stream caught up
+            # and starved the compute stream (k-of-n at world 1: 8,371 vs 9,409 img/s, gpurun_out/r3_09)
+            if len(self._events) >= 2:
+                self._events[-2].synchronize()
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.flat.grad.device))
+            self._events.append(ev)
         side = side_stream_if_active(self.flat.grad)
         if side is None:
             return self._launch_on(b, zero)
@@ -382,13 +392,6 @@ class DistributedDataParallel(nn.Module):
             view.zero_()                       # zero contribution: collective stays matched
         else:
             self._contrib[b] = 1.0
-        if self.kofn is not None and self.throttle and view.is_cuda:
-            # keep the host at most two buckets ahead of the GPU, so an abort stops real GPU work
-            if len(self._events) >= 2:
-                self._events[-2].synchronize()
-            ev = torch.cuda.Event()
-            ev.record()
-            self._events.append(ev)
         t = view
         if self.comm_dtype is not None:
             t = self._wire[b]

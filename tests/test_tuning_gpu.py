@@ -12,7 +12,7 @@ BF = torch.bfloat16
 ALT = {
     "glds": [0, 2], "glds_min_tiles": [1, 1 << 20], "glds_fwd_k": [64], "glds_dgrad_n": [64], "glds_dgrad_k": [64],
     "glds_persistent": [1], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "pp_fp8": [0], "pp_conv_min_n": [64],
-    "pp_conv_fwd_k": [64], "pp_conv_dgrad_k": [64], "pp_conv_bnb": [1], "staged_store": [0], "lowk_bn64": [0, 4],
+    "pp_conv_fwd_k": [64], "pp_conv_dgrad_k": [64], "pp_conv_bnb_k": [64], "staged_store": [0], "lowk_bn64": [0, 4],
     "split_blocks": [64, 2048], "conv3x3_force": [1],
 }
 

@@ -1,10 +1,10 @@
 """Per-layer timing of the 1x1 convs of the ResNet-50 bottleneck (bs256) as the fused block runs them:
 conv3 forward with the BN2+ReLU operand prologue vs materialised a2 = relu(bn2(t2)) (bn_apply) + plain
 conv, conv1 forward with BN statistics, conv3 data gradient with the BN-backward epilogue and conv1 data
-gradient with the residual.  Engine choice comes from the environment (PDNN_PP_CONV_FWD_K, PDNN_PP_CONV_BNB,
-PDNN_PP_CONV_DGRAD_K, PDNN_GLDS ...), so one call per configuration.
+gradient with the residual.  Engine choice comes from the dispatch table (PDNN_TUNE="pp_conv_fwd_k=0,pp_conv_bnb_k=0",
+csrc/kernels/tuning.h), so one call per configuration.
 
-    PDNN_PP_CONV_FWD_K=0 python tools/bench_conv1x1.py
+    PDNN_TUNE=pp_conv_fwd_k=0 python tools/bench_conv1x1.py
 """
 import json
 import os
