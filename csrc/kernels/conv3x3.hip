@@ -49,7 +49,37 @@ struct C3Args {
     const uint8_t* rmask;  // C3_RES: residual masked by these ReLU bits ([P][N/8] bytes), or null
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
+    // PRE operand prologue (BatchNorm backward apply of the layer whose gradient is the input): the staged
+    // operand is dt = k*gm + A*t + B per channel (pdnn_bn_bwd_apply's formula, same rounding) with gm = x;
+    // the own pixels' dt is also written to pre_out (the weight gradient's operand)
+    const bf16_t* pre_t;
+    const float *pre_mean, *pre_invstd, *pre_gamma, *pre_dgamma, *pre_dbeta;
+    bf16_t* pre_out;
 };
+
+// per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)
+struct PreCoef {
+    float k[8], A[8], B[8];
+};
+__device__ __forceinline__ void pre_coef(const C3Args& a, int c, PreCoef& pc) {
+    const float invL = (float)(1.0 / (double)a.P);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float is = a.pre_invstd[c + j], k = (a.pre_gamma ? a.pre_gamma[c + j] : 1.f) * is;
+        const float dg = a.pre_dgamma[c + j] * invL, db = a.pre_dbeta[c + j] * invL;
+        pc.k[j] = k;
+        pc.A[j] = -k * is * dg;
+        pc.B[j] = k * (a.pre_mean[c + j] * is * dg - db);
+    }
+}
+__device__ __forceinline__ u16x8_t pre_apply(const PreCoef& pc, const u16x8_t& gv, const u16x8_t& tv) {
+    float gm[8], t[8], o[8];
+    unpack8(gv, gm);
+    unpack8(tv, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(pc.k[j], gm[j], fmaf(t[j], pc.A[j], pc.B[j]));
+    return pack8(o);
+}
 
 __device__ __forceinline__ u16x8_t c3_zero8() {
     u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -152,7 +182,7 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
     }
 }
 
-template <int NB, int EPI>
+template <int NB, int EPI, bool PRE>
 __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
     constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
     constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
@@ -218,22 +248,38 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         if (ck) __syncthreads();                 // the previous chunk's halo / weights are no longer read
         // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
         const int nch = hpx * 8;
-        for (int i0 = 0; i0 < nch; i0 += 256 * 8) {
-            u16x8_t v[8];
+        constexpr int J = PRE ? (NB == 128 ? 2 : 4) : 8;   // PRE: two operands (and their coefficients) live
+        PreCoef pc;
+        if constexpr (PRE) pre_coef(a, c0 + (tid & 7) * 8, pc);   // this thread's 8 channels (i & 7 == tid & 7)
+        for (int i0 = 0; i0 < nch; i0 += 256 * J) {
+            u16x8_t v[J], tv[PRE ? J : 1];
+            bool okj[J];
+            int gpj[J];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < J; ++j) {
                 // load unconditionally from a clamped (valid) address, then select: a conditional load
                 // makes hipcc branch around every element and drain vmcnt each time
                 const int i = i0 + j * 256 + tid;
                 const long gp = gp0 + (i >> 3);
-                const bool ok = i < nch && gp >= 0 && gp < a.P;
+                okj[j] = i < nch && gp >= 0 && gp < a.P;
                 const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
-                const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
-                const unsigned short m = ok ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
-                v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+                gpj[j] = (int)gc;
+                v[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+                if constexpr (PRE) tv[j] = *reinterpret_cast<const u16x8_t*>(a.pre_t + gc * a.C + c0 + (i & 7) * 8);
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < J; ++j) {
+                if constexpr (PRE) {
+                    v[j] = pre_apply(pc, v[j], tv[j]);
+                    // own pixels (each written by exactly one block: column tile 0 of its pixel tile)
+                    if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
+                        *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 8) = v[j];
+                }
+                const unsigned short m = okj[j] ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
+                v[j] = v[j] & (u16x8_t){m, m, m, m, m, m, m, m};
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
                 // past the halo: the (zero) value goes to the zero pixel, so the store needs no branch either
                 const int i = i0 + j * 256 + tid;
                 const int off = i < nch ? halo_off(i >> 3, i & 7) : zpx * 64 + (i & 7) * 8;
@@ -411,7 +457,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
 // reduction ends.  Grid = pixel tiles x column groups (groups only when the pixel tiles alone cannot fill
 // the chip).  Same epilogues as the 3x3 kernel (stats / BN-backward / masked residual).
 // ---------------------------------------------------------------------------------------------------
-template <int EPI>
+template <int EPI, bool PRE>
 __global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
     constexpr int NB = 64, FN = 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -428,24 +474,36 @@ __global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
     const int zpx = C3_BM;                                                // zero pixel of each k-chunk image
 
     // ---- A panel: pixels p0 .. p0+255, all K channels (masked unconditional loads; rows >= P are zero)
-    for (int i0 = 0; i0 < KC * C3_BM * 8; i0 += 256 * 8) {
-        u16x8_t v[8];
+    constexpr int J = PRE ? 4 : 8;
+    for (int i0 = 0; i0 < KC * C3_BM * 8; i0 += 256 * J) {
+        u16x8_t v[J], tv[PRE ? J : 1];
+        PreCoef pc;
+        if constexpr (PRE) {                      // i0 / 2048 = this iteration's k-chunk (J * 256 <= 2048)
+            const int kc0 = i0 / (C3_BM * 8);
+            pre_coef(a, (kc0 < KC ? kc0 : KC - 1) * 64 + (tid & 7) * 8, pc);
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < J; ++j) {
             const int i = i0 + j * 256 + tid;                 // = (kc * 256 + px) * 8 + q
             const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
             const long gp = (long)p0 + px;
-            const bool ok = i < KC * C3_BM * 8 && gp < a.P;
             const long gc = gp < a.P ? gp : a.P - 1;
             const int kk = kc < KC ? kc : KC - 1;
-            const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + kk * 64 + q * 8);
-            const unsigned short m = ok ? 0xFFFF : 0;
-            v[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+            v[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + kk * 64 + q * 8);
+            if constexpr (PRE) tv[j] = *reinterpret_cast<const u16x8_t*>(a.pre_t + gc * a.C + kk * 64 + q * 8);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < J; ++j) {
             const int i = i0 + j * 256 + tid;
             const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
+            const long gp = (long)p0 + px;
+            const bool ok = i < KC * C3_BM * 8 && gp < a.P;
+            if constexpr (PRE) {
+                v[j] = pre_apply(pc, v[j], tv[j]);
+                if (a.pre_out && grp == 0 && ok) *reinterpret_cast<u16x8_t*>(a.pre_out + gp * a.C + kc * 64 + q * 8) = v[j];
+            }
+            const unsigned short m = ok ? 0xFFFF : 0;
+            v[j] = v[j] & (u16x8_t){m, m, m, m, m, m, m, m};
             if (kc < KC) *reinterpret_cast<u16x8_t*>(panel + kc * (C3_BM + 1) * 64 + halo_off(px, q)) = v[j];
         }
     }
@@ -562,31 +620,62 @@ int c3r_launch(const C3Args& a, hipStream_t st) {
     PDNN_LAUNCH_RET;
 }
 
-template <int NB, int EPI>
+template <int NB, int EPI, bool PRE>
 int c3_launch(const C3Args& a, hipStream_t st) {
     static int attr_done = 0;
     const int sm = c3_smem<NB>(a.W);
     if (sm > attr_done) {
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  sm);
         attr_done = sm;
     }
-    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
+}
+
+template <int NB, bool PRE>
+int c3_dispatch(const C3Args& a, int epi, hipStream_t st) {
+    switch (epi) {
+        case C3_BNB: return c3_launch<NB, C3_BNB, PRE>(a, st);
+        case C3_STATS: return c3_launch<NB, C3_STATS, PRE>(a, st);
+        case C3_RES: return c3_launch<NB, C3_RES, PRE>(a, st);
+        default: return c3_launch<NB, C3_PLAIN, PRE>(a, st);
+    }
 }
 
 }  // namespace
 
 
 
-template <int EPI>
+template <int EPI, bool PRE>
 int p1_launch(const C3Args& a, int sm, hipStream_t st) {
     static int attr_done = 0;
     if (sm > attr_done) {
-        (void)hipFuncSetAttribute((const void*)conv1x1_panel_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        (void)hipFuncSetAttribute((const void*)conv1x1_panel_kernel<EPI, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  sm);
         attr_done = sm;
     }
-    hipLaunchKernelGGL((conv1x1_panel_kernel<EPI>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    hipLaunchKernelGGL((conv1x1_panel_kernel<EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
+}
+
+template <bool PRE>
+int p1_dispatch(const C3Args& a, int epi, int sm, hipStream_t st) {
+    switch (epi) {
+        case C3_BNB: return p1_launch<C3_BNB, PRE>(a, sm, st);
+        case C3_STATS: return p1_launch<C3_STATS, PRE>(a, sm, st);
+        case C3_RES: return p1_launch<C3_RES, PRE>(a, sm, st);
+        default: return p1_launch<C3_PLAIN, PRE>(a, sm, st);
+    }
+}
+
+// the PRE prologue's operands (all or none; t: [P][C] like x, the rest fp32 [C], gamma optional)
+static bool set_pre(C3Args& a, const bf16_t* t, const float* mean, const float* invstd, const float* gamma,
+             const float* dgamma, const float* dbeta, bf16_t* out) {
+    a.pre_t = t; a.pre_mean = mean; a.pre_invstd = invstd; a.pre_gamma = gamma;
+    a.pre_dgamma = dgamma; a.pre_dbeta = dbeta; a.pre_out = out;
+    if (!t) return !out;
+    return mean && invstd && dgamma && dbeta;
 }
 static int c3_force() { return pg::tune().conv3x3_force; }
 
@@ -632,10 +721,14 @@ PDNN_API int pdnn_conv3x3_flip(const bf16_t* w, bf16_t* wt, int K, int C, hipStr
 
 // y[P][N] = conv3x3(x, w) with pad 1, stride 1 (w: [N][3][3][C]); epilogue: stats (fwd BN statistics),
 // bn_x (BN-backward mask + sums), res (residual add), else plain.  nb: 0 = automatic, 64 / 128 forced.
+// pre_*: optional BN-backward operand prologue (x = gm; the conv's operand is dt = bn_bwd_apply(gm, pre_t),
+// also written to pre_out if given): the apply pass of the layer below fused into the loads.
 PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int C, int N,
                           float* stats, const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x,
                           const float* bn_mean,
                           const float* bn_invstd, const float* bn_mscale, const float* bn_mshift, int nb,
+                          const bf16_t* pre_t, const float* pre_mean, const float* pre_invstd,
+                          const float* pre_gamma, const float* pre_dgamma, const float* pre_dbeta, bf16_t* pre_out,
                           hipStream_t st) {
     if (!pdnn_conv3x3_supported(Nimg, H, W, C, N)) return (int)hipErrorInvalidValue;
     C3Args a{};
@@ -646,16 +739,19 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     a.halo_max = c3_halo_max(W);
     a.stats = stats; a.res = res; a.rmask = res_mask;
     if (res_mask && !res) return (int)hipErrorInvalidValue;
+    if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
+        return (int)hipErrorInvalidValue;
+    const bool pre = pre_t != nullptr;
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
-    const int epi0 = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    if (bn_x && !stats) return (int)hipErrorInvalidValue;
     // 64 -> 64 channels: the weight-resident persistent kernel (nb = 1; measured slower than the streaming
     // kernel at ResNet-50 stage 1, 125 / 173 vs 104 / 142 us fwd / dgrad, gpurun_out/r3_04: one wave per SIMD
     // exposes the LDS latency of the unrolled tap sequence)
-    if (nb == 1 && C == 64 && N == 64 && c3_halo_max(W) * 8 <= C3R_HREG * 256 &&
+    if (nb == 1 && !pre && C == 64 && N == 64 && c3_halo_max(W) * 8 <= C3R_HREG * 256 &&
         c3r_smem(W) <= 160 * 1024) {
         a.ntiles = 1;
-        if (bn_x && !stats) return (int)hipErrorInvalidValue;
-        switch (epi0) {
+        switch (epi) {
             case C3_BNB: return c3r_launch<C3_BNB>(a, st);
             case C3_STATS: return c3r_launch<C3_STATS>(a, st);
             case C3_RES: return c3r_launch<C3_RES>(a, st);
@@ -665,22 +761,8 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     if (nb == 0 || nb == 1) nb = N % 128 == 0 ? 128 : 64;
     if (nb == 128 && (N % 128 || c3_smem<128>(W) > 80 * 1024)) nb = 64;
     a.ntiles = N / nb;
-    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
-    if (bn_x && !stats) return (int)hipErrorInvalidValue;
-    if (nb == 128) {
-        switch (epi) {
-            case C3_BNB: return c3_launch<128, C3_BNB>(a, st);
-            case C3_STATS: return c3_launch<128, C3_STATS>(a, st);
-            case C3_RES: return c3_launch<128, C3_RES>(a, st);
-            default: return c3_launch<128, C3_PLAIN>(a, st);
-        }
-    }
-    switch (epi) {
-        case C3_BNB: return c3_launch<64, C3_BNB>(a, st);
-        case C3_STATS: return c3_launch<64, C3_STATS>(a, st);
-        case C3_RES: return c3_launch<64, C3_RES>(a, st);
-        default: return c3_launch<64, C3_PLAIN>(a, st);
-    }
+    if (nb == 128) return pre ? c3_dispatch<128, true>(a, epi, st) : c3_dispatch<128, false>(a, epi, st);
+    return pre ? c3_dispatch<64, true>(a, epi, st) : c3_dispatch<64, false>(a, epi, st);
 }
 
 // 1x1 / stride-1 conv on the pixel-panel kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128}, N % 64 == 0.
@@ -692,7 +774,9 @@ PDNN_API int pdnn_conv1x1_panel_supported(long P, int K, int N) {
 PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, long P, int K, int N, float* stats,
                                 const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x, const float* bn_mean,
                                 const float* bn_invstd, const float* bn_mscale, const float* bn_mshift,
-                                hipStream_t st) {
+                                const bf16_t* pre_t, const float* pre_mean, const float* pre_invstd,
+                                const float* pre_gamma, const float* pre_dgamma, const float* pre_dbeta,
+                                bf16_t* pre_out, hipStream_t st) {
     if (!pdnn_conv1x1_panel_supported(P, K, N) || (bn_x && !stats) || (res_mask && !res))
         return (int)hipErrorInvalidValue;
     C3Args a{};
@@ -700,6 +784,8 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     a.tiles = (int)cdiv(P, C3_BM);
     a.stats = stats; a.res = res; a.rmask = res_mask;
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+    if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
+        return (int)hipErrorInvalidValue;
     // column groups: split the output columns over blocks only until the grid covers ~2 blocks per CU
     const int chunks = N / 64;
     int g = 1;
@@ -707,12 +793,7 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     a.ntiles = g;
     const int sm = (K / 64) * (C3_BM + 1) * 128 + 2 * 64 * 128;
     const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
-    switch (epi) {
-        case C3_BNB: return p1_launch<C3_BNB>(a, sm, st);
-        case C3_STATS: return p1_launch<C3_STATS>(a, sm, st);
-        case C3_RES: return p1_launch<C3_RES>(a, sm, st);
-        default: return p1_launch<C3_PLAIN>(a, sm, st);
-    }
+    return pre_t ? p1_dispatch<true>(a, epi, sm, st) : p1_dispatch<false>(a, epi, sm, st);
 }
 
 PDNN_API int pdnn_conv1x1_panel_stats_rows(long P) { return (int)cdiv(P, C3_BM) * 4; }

@@ -38,7 +38,7 @@ _SIGS = {
     "pdnn_conv_dgrad_stats_rows": [I, I, I, I, I, I, I],
     "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "pdnn_gemm_stats_rows": [I],
-    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
+    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
@@ -47,7 +47,7 @@ _SIGS = {
     "pdnn_tune_get": [ctypes.c_char_p],
     "pdnn_tune_list": [ctypes.c_char_p, I],
     "pdnn_tune_error": [],
-    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P],
+    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
     "pdnn_set_glds_mode": [I],

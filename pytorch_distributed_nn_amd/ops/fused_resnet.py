@@ -193,6 +193,20 @@ def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, si
     return dt, dgamma, dbeta
 
 
+def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p):
+    """dgrad with the fused BN-backward epilogue, stopped before the apply pass: -> (gm, dgamma, dbeta,
+    returned grads).  The apply then runs inside the next data gradient's operand loads (_dgrad_pre)."""
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh))
+    (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
+    return gm, dgamma, dbeta, ret
+
+
+def _pre_ok(t, wk, st, pad):
+    """Whether the consumer of dt = bn_bwd_apply(gm, t) (data gradient of the conv with weight wk) takes the
+    apply as its operand prologue."""
+    return tuning.get("bwd_pre") == 1 and K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
+
+
 def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p):
     """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
     one apply pass produces dt (the gradient w.r.t. the BN input t)."""
@@ -307,21 +321,42 @@ class BottleneckFn(torch.autograd.Function):
             dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
         else:
             dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
-        dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5])
-        dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
-        dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, stride, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
-        dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)
+        bn1 = (t1, m1, i1, s1, h1)
+        if _pre_ok(t2, k2, stride, 1):
+            # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad
+            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5])
+            dt2 = torch.empty_like(t2)
+            gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2))
+            del gm2
+            dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
+        else:
+            dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5])
+            dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
+            gm1, slab1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1, bn=bn1)
+        (dg1, db1), (rg1, rb1) = sink.bn(slab1, slab1.shape[0] // 2, P[1], P[2])
+        pre1 = None
+        if _pre_ok(t1, k1, 1, 0):
+            dt1 = torch.empty_like(t1)
+            pre1 = (t1, m1, i1, g1, dg1, db1, dt1)
+            dy1 = gm1
+        else:
+            C1 = t1.shape[-1]
+            dt1 = K.bn_bwd_apply(gm1.view(-1, C1), t1.view(-1, C1), m1, i1, g1, dg1, db1, mode=0)[0].view(t1.shape)
+            dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)
+            dy1 = dt1
         if down:
             dtd = dtd.view(td.shape)
             dwd = sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
-            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0)
+            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, pre=pre1)
             # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
             # reach, so no zero-filled full-size buffer and no extra full read/write pass
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
-            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3, dwd, rgd, rbd)
         else:
-            dx = K.conv_dgrad(dt1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=mb if MASKED_RES else None)
-            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3)
+            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=mb if MASKED_RES else None,
+                              pre=pre1)
+        if pre1 is not None:
+            dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)       # dt1 written by conv1's data gradient
+        grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3) + ((dwd, rgd, rbd) if down else ())
         sink.done()
         return (dx, None, None, None) + grads
 
@@ -380,17 +415,25 @@ class BasicBlockFn(torch.autograd.Function):
             gres = gout                                     # masked by conv1's data-gradient epilogue
         dt2 = dt2.view(t2.shape)
         dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, 1, 1)
-        dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
-        dw1 = sink.wgrad(P[0], x, dt1, 3, 3, stride, 1)
+        if _pre_ok(t1, k1, stride, 1):
+            # BN1's apply inside conv1's data-gradient operand loads (dt1 written there for the wgrad)
+            gm1, dg1, db1, (rg1, rb1) = _dgrad_bn_gm(dt2, k2, t1, 1, 1, m1, i1, s1, h1, sink, P[1], P[2])
+            dt1 = torch.empty_like(t1)
+            pre1, dy1 = (t1, m1, i1, g1, dg1, db1, dt1), gm1
+        else:
+            dt1, rg1, rb1 = _fused_dgrad_bn(dt2, k2, t1, 1, 1, m1, i1, s1, h1, g1, sink, P[1], P[2])
+            dw1 = sink.wgrad(P[0], x, dt1, 3, 3, stride, 1)
+            pre1, dy1 = None, dt1
         if down:
             dtd = dtd.view(td.shape)
             dwd = sink.wgrad(P[6], x, dtd, 1, 1, stride, 0)
-            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1)
+            dx = K.conv_dgrad(dy1, k1, x.shape, stride, 1, pre=pre1)
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)      # shortcut, in place
-            grads = (dw1, rg1, rb1, dw2, rg2, rb2, dwd, rgd, rbd)
         else:
-            dx = K.conv_dgrad(dt1, k1, x.shape, stride, 1, res=gres.view(x.shape), res_mask=mb)
-            grads = (dw1, rg1, rb1, dw2, rg2, rb2)
+            dx = K.conv_dgrad(dy1, k1, x.shape, stride, 1, res=gres.view(x.shape), res_mask=mb, pre=pre1)
+        if pre1 is not None:
+            dw1 = sink.wgrad(P[0], x, dt1, 3, 3, stride, 1)
+        grads = (dw1, rg1, rb1, dw2, rg2, rb2) + ((dwd, rgd, rbd) if down else ())
         sink.done()
         return (dx, None, None, None) + grads
 

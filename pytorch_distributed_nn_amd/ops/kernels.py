@@ -206,8 +206,22 @@ def _panel_ok(P, K, N, R, S, st, pad):
             and lib().pdnn_conv1x1_panel_supported(P, K, N) == 1)
 
 
-def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None):
-    """y[P][N] = x[P][K] . w[N][K]^T on the panel kernel; epilogues as conv3x3 / conv_dgrad."""
+def _pre_args(pre, x):
+    """pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out or None): the BN-backward apply of the layer whose
+    gradient gm is ``x`` (dt = bn_bwd_apply(gm, t), mode 0) fused into the operand loads."""
+    if pre is None:
+        return (None,) * 7
+    t, mean, inv, gamma, dg, db, dt_out = pre
+    _bf16_c(t, "pre.t")
+    _chk(t.numel() == x.numel(), "pre: t must have the operand's shape")
+    if dt_out is not None:
+        _chk(dt_out.numel() == x.numel() and dt_out.dtype == BF16 and dt_out.is_contiguous(), "pre: dt_out")
+    return tuple(ptr(v) for v in (t, mean, inv, gamma, dg, db, dt_out))
+
+
+def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None):
+    """y[P][N] = x[P][K] . w[N][K]^T on the panel kernel; epilogues as conv3x3 / conv_dgrad; pre: the
+    BN-backward operand prologue (_pre_args)."""
     P, Kc = x2d.shape
     N = w2d.shape[0]
     y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
@@ -218,7 +232,7 @@ def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, 
     if bn is not None:
         t, mean, inv, msc, msh = bn
     call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
     return y, slab
 
 
@@ -230,7 +244,7 @@ def conv3x3_flip(w):
     return wt
 
 
-def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None):
+def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, pre=None):
     """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
     conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
     Nimg, H, W, C = x.shape
@@ -243,7 +257,7 @@ def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None):
     if bn is not None:
         t, mean, inv, msc, msh = bn
     call("pdnn_conv3x3", ptr(x), ptr(w), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), _C3["nb"], stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), _C3["nb"], *_pre_args(pre, x), stream())
     return y, slab
 
 
@@ -273,7 +287,16 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     return y, stats
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None):
+def dgrad_pre_ok(dy_shape, w_shape, st, pad):
+    """Whether conv_dgrad takes ``pre=`` (the BN-backward apply fused into its operand loads) for this
+    conv: the halo 3x3 kernel and the K = 64 panel kernel."""
+    N, Ho, Wo, K = dy_shape
+    Kw, R, S, C = w_shape
+    return (_conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad)
+            or (K == 64 and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
+
+
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None):
     """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
     conv only the pixels its taps reach are touched, the others keep ``res``).
 
@@ -283,7 +306,11 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
 
     res_mask: uint8 [N*H*W][C/8] ReLU bits (bn_apply's mask): the residual is added only where its bit is set,
     i.e. res * mask -- the identity branch's gradient computed here instead of materialised by the BN
-    backward (stride 1 only)."""
+    backward (stride 1 only).
+
+    pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out): ``dy`` is the masked gradient gm of a BatchNorm
+    whose backward apply (bn_bwd_apply mode 0) runs inside this conv's operand loads; dt_out (optional)
+    receives that dt for the weight gradient.  Only where dgrad_pre_ok()."""
     _bf16_c(dy, "conv_dgrad.dy")
     N, H, W, C = x_shape
     _bf16_c(w, "conv_dgrad.w")
@@ -306,7 +333,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
              "conv_dgrad: res_mask needs res, stride 1, uint8 [N*H*W][C/8], out not aliasing res")
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
-        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask)
+        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask, pre=pre)
         return (y, slab) if bn is not None else y
     # panel data gradient only for K = 64 (ResNet stage 1): at K = 128 -> 512 the implicit-GEMM engine was faster
     # (154 vs 176 us, gpurun_out/r3_08)
@@ -315,9 +342,10 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)),
                                 res=None if res is None else res.view(-1, C), res_mask=res_mask,
                                 bn=None if bn is None else (bn[0].view(-1, C),) + tuple(bn[1:]),
-                                out=None if out is None else out.view(-1, C))
+                                out=None if out is None else out.view(-1, C), pre=pre)
         y = y.view(N, H, W, C)
         return (y, slab) if bn is not None else y
+    _chk(pre is None, "conv_dgrad: pre= needs the halo 3x3 or K = 64 panel kernel (dgrad_pre_ok)")
     dx = out if out is not None else torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
     slab = None
     t = mean = inv = msc = msh = None

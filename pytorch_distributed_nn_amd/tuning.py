@@ -12,6 +12,8 @@ materialize_a2     1        Bottleneck: write a2 = relu(bn2(t2)) once instead of
                             (9,240 -> 9,596 img/s, gpurun_out/r3_05)
 conv3x3            1        3x3 / stride-1 convs on the LDS-halo kernel (+2.5%, gpurun_out/r3_07)
 panel1x1           1        1x1 / stride-1 convs with K <= 128 on the pixel-panel kernel (+1.1%, r3_08)
+bwd_pre            1        BatchNorm-backward apply (dt = k*gm + A*t + B) fused into the operand loads of
+                            the consuming halo 3x3 / K=64 panel data gradient, dt written once for the wgrad
 direct_grad        1        fused ops accumulate weight gradients straight into the flat arena
 opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream during the backward
 =================  =======  ===========================================================================
@@ -20,7 +22,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "direct_grad": 1, "opt_overlap": 0}
+DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "direct_grad": 1, "opt_overlap": 0}
 
 _VALUES = dict(DEFAULTS)
 

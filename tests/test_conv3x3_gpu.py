@@ -145,3 +145,76 @@ def test_conv1x1_panel_dgrad(K, shape):
     xhat = ((t.float() - mean) * inv).reshape(-1, C)
     assert torch.allclose(s[0], gmf.sum(0), rtol=1e-3, atol=1e-3 * gmf.abs().sum(0).max().item())
     assert torch.allclose(s[1], (gmf * xhat).sum(0), rtol=1e-3, atol=1e-3 * (gmf * xhat).abs().sum(0).max().item())
+
+
+# ------------------------------------------- BN-backward apply fused into the operand loads (pre=)
+def _pre_operands(shape_nhwc, gamma=True):
+    Ko = shape_nhwc[-1]
+    gm = torch.randn(*shape_nhwc, device="cuda").to(BF)
+    t = torch.randn(*shape_nhwc, device="cuda").to(BF)
+    mean, inv = torch.randn(Ko, device="cuda") * 0.1, torch.rand(Ko, device="cuda") + 0.5
+    g = torch.rand(Ko, device="cuda") + 0.5 if gamma else None
+    dg, db = torch.randn(Ko, device="cuda") * 50, torch.randn(Ko, device="cuda") * 50
+    return gm, t, mean, inv, g, dg, db
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3x3_dgrad_pre_matches_separate_apply(K, nb, shape):
+    """dx = conv3x3_dgrad(bn_bwd_apply(gm, t)) with the apply in the halo loads: dt_out bitwise equal to the
+    apply kernel's output, dx bitwise equal to the dgrad of that dt (same kernel and tile), for the plain,
+    residual and fused-BN epilogues."""
+    N, H, W, C, Ko = shape
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(BF)
+    gm, t, mean, inv, g, dg, db = _pre_operands((N, H, W, Ko), gamma=(Ko % 128 == 0))
+    dt_ref = K.bn_bwd_apply(gm.view(-1, Ko), t.view(-1, Ko), mean, inv, g, dg, db, mode=0)[0].view_as(gm)
+    assert K.dgrad_pre_ok(gm.shape, w.shape, 1, 1)
+    exact = nb != 1          # nb=1: the plain dgrad runs the weight-resident kernel, pre= the streaming one
+    chk = (lambda a, b: torch.equal(a, b)) if exact else (lambda a, b: rel(a, b) < 1e-2)
+    dt_out = torch.empty_like(gm)
+    dx = K.conv_dgrad(gm, w, (N, H, W, C), 1, 1, pre=(t, mean, inv, g, dg, db, dt_out))
+    assert torch.equal(dt_out, dt_ref)
+    assert chk(dx, K.conv_dgrad(dt_ref, w, (N, H, W, C), 1, 1))
+    res = torch.randn(N, H, W, C, device="cuda").to(BF)
+    keep = torch.rand(N * H * W, C, device="cuda") > 0.5
+    bits = (keep.view(-1, C // 8, 8).to(torch.int32) << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1)
+    bits = bits.to(torch.uint8).contiguous()
+    dxr = K.conv_dgrad(gm, w, (N, H, W, C), 1, 1, res=res, res_mask=bits, pre=(t, mean, inv, g, dg, db, None))
+    assert chk(dxr, K.conv_dgrad(dt_ref, w, (N, H, W, C), 1, 1, res=res, res_mask=bits))
+    t1 = torch.randn(N, H, W, C, device="cuda").to(BF)
+    m1, i1 = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    s1, h1 = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    g1, sl1 = K.conv_dgrad(gm, w, (N, H, W, C), 1, 1, bn=(t1, m1, i1, s1, h1), pre=(t, mean, inv, g, dg, db, None))
+    g1r, sl1r = K.conv_dgrad(dt_ref, w, (N, H, W, C), 1, 1, bn=(t1, m1, i1, s1, h1))
+    assert chk(g1, g1r)
+    if exact:
+        assert torch.equal(sl1, sl1r)
+
+
+@pytest.mark.parametrize("shape", PANEL)
+def test_conv1x1_panel_pre_matches_separate_apply(K, shape):
+    """The panel kernel's operand prologue (K in {64, 128}): same bits as apply-then-conv."""
+    N, H, W, Kc, C = shape
+    w = (torch.randn(Kc, 1, 1, C, device="cuda") * 0.1).to(BF)
+    gm, t, mean, inv, g, dg, db = _pre_operands((N, H, W, Kc))
+    dt_ref = K.bn_bwd_apply(gm.view(-1, Kc), t.view(-1, Kc), mean, inv, g, dg, db, mode=0)[0]
+    wt = K.transpose_bf16(w.view(Kc, C))
+    dt_out = torch.empty_like(gm)
+    y, _ = K.conv1x1_panel(gm.view(-1, Kc), wt, pre=(t, mean, inv, g, dg, db, dt_out))
+    y_ref, _ = K.conv1x1_panel(dt_ref, wt)
+    assert torch.equal(dt_out.view(-1, Kc), dt_ref)
+    assert torch.equal(y, y_ref)
+    res = torch.randn(N * H * W, C, device="cuda").to(BF)
+    yr, _ = K.conv1x1_panel(gm.view(-1, Kc), wt, res=res, pre=(t, mean, inv, g, dg, db, None))
+    assert torch.equal(yr, K.conv1x1_panel(dt_ref, wt, res=res)[0])
+    if Kc == 64:       # routed through conv_dgrad (the K = 64 panel data gradient)
+        assert K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
+        dx = K.conv_dgrad(gm, w, (N, H, W, C), 1, 0, pre=(t, mean, inv, g, dg, db, None))
+        assert torch.equal(dx.view(-1, C), y_ref)
+
+
+def test_dgrad_pre_rejected_on_gemm_engine(K):
+    gm, t, mean, inv, g, dg, db = _pre_operands((2, 8, 8, 256))
+    w = (torch.randn(256, 1, 1, 64, device="cuda") * 0.1).to(BF)
+    assert not K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
+    with pytest.raises(ValueError):
+        K.conv_dgrad(gm, w, (2, 8, 8, 64), 1, 0, pre=(t, mean, inv, g, dg, db, None))

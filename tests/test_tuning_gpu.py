@@ -70,12 +70,12 @@ def test_kernel_entry_alternatives(K, key, value):
         K.tune_set(key, old)
 
 
-def _resnet_grads():
+def _resnet_grads(arch="resnet50"):
     from pytorch_distributed_nn_amd.models import build_model
     from pytorch_distributed_nn_amd.ops import functional as OF
     from pytorch_distributed_nn_amd.optim import flatten_module
     torch.manual_seed(0)
-    m = build_model("resnet50").cuda()
+    m = build_model(arch).cuda()
     fp = flatten_module(m)
     g = torch.Generator().manual_seed(5)
     x = torch.randn(4, 3, 64, 64, generator=g).cuda().to(BF)
@@ -86,18 +86,20 @@ def _resnet_grads():
     return fp.grad.clone()
 
 
-@pytest.mark.parametrize("key", ["side_wgrad", "materialize_a2", "conv3x3", "panel1x1"])
-def test_python_entry_alternatives(K, key):
+@pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("materialize_a2", "resnet50"),
+                                      ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("bwd_pre", "resnet50"),
+                                      ("bwd_pre", "resnet18")])
+def test_python_entry_alternatives(K, key, arch):
     """The model-level switches change only the schedule / kernel choice: same gradients (bf16 noise)."""
     from pytorch_distributed_nn_amd import tuning
-    base = _resnet_grads()
+    base = _resnet_grads(arch)
     old = tuning.set(key, 0)
     if key == "conv3x3":
         K.set_conv3x3_mode(0)
     if key == "panel1x1":
         K.set_panel_mode(0)
     try:
-        alt = _resnet_grads()
+        alt = _resnet_grads(arch)
     finally:
         tuning.set(key, old)
         K.set_conv3x3_mode(1)
