@@ -81,6 +81,14 @@ __device__ __forceinline__ u16x8_t pre_apply(const PreCoef& pc, const u16x8_t& g
     return pack8(o);
 }
 
+// v if ok else 0, as four 32-bit ANDs (a u16x8 AND with a 16-bit mask vector lowers to per-half sdwa/perm ops)
+__device__ __forceinline__ u16x8_t mask16(const u16x8_t& v, bool ok) {
+    const uint32_t m = ok ? 0xFFFFFFFFu : 0u;
+    uint4 u = __builtin_bit_cast(uint4, v);
+    u.x &= m; u.y &= m; u.z &= m; u.w &= m;
+    return __builtin_bit_cast(u16x8_t, u);
+}
+
 __device__ __forceinline__ u16x8_t c3_zero8() {
     u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
     return z;
@@ -275,8 +283,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
                     if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
                         *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 8) = v[j];
                 }
-                const unsigned short m = okj[j] ? 0xFFFF : 0;     // masked, not selected: keeps the load unconditional
-                v[j] = v[j] & (u16x8_t){m, m, m, m, m, m, m, m};
+                v[j] = mask16(v[j], okj[j]);     // masked, not selected: keeps the load unconditional
             }
 #pragma unroll
             for (int j = 0; j < J; ++j) {
@@ -369,8 +376,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
             const bool ok = i < nch && gp >= 0 && gp < a.P;
             const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
             const u16x8_t ld = *reinterpret_cast<const u16x8_t*>(a.x + gc * 64 + (i & 7) * 8);
-            const unsigned short m = ok ? 0xFFFF : 0;
-            hreg[j] = ld & (u16x8_t){m, m, m, m, m, m, m, m};
+            hreg[j] = mask16(ld, ok);
         }
     };
     auto put = [&](int tile) {                   // registers -> LDS halo (past the halo: the zero pixel)
@@ -502,8 +508,7 @@ __global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
                 v[j] = pre_apply(pc, v[j], tv[j]);
                 if (a.pre_out && grp == 0 && ok) *reinterpret_cast<u16x8_t*>(a.pre_out + gp * a.C + kc * 64 + q * 8) = v[j];
             }
-            const unsigned short m = ok ? 0xFFFF : 0;
-            v[j] = v[j] & (u16x8_t){m, m, m, m, m, m, m, m};
+            v[j] = mask16(v[j], ok);
             if (kc < KC) *reinterpret_cast<u16x8_t*>(panel + kc * (C3_BM + 1) * 64 + halo_off(px, q)) = v[j];
         }
     }
@@ -574,6 +579,122 @@ __global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         }
+        if (more) {
+            store_b((s + 1) & 1);
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// 1x1 / stride-1 convs with K = 64 * KC <= 256 input channels, A-stationary: each wave holds the MFMA
+// fragments of its 64 pixels x all K channels in VGPRs for the whole block (KC = 4: 128 VGPRs), so the
+// activations are read once, straight from global memory in fragment order, and never pass through LDS;
+// only the weights stream, NB output columns per step, through a double-buffered LDS image (next step's
+// weights fetched into registers under this step's MFMAs, one barrier per step).  LDS traffic is then
+// one B fragment per 4 MFMAs, the panel kernel's A-from-LDS reads and its 64 KB+ A panel are gone, and
+// K = 256 fits (ResNet-50 stage-3 conv3 forward / conv1 data gradient: 50176 x 256 -> 1024).
+// PRE: the BatchNorm-backward apply runs on the fragments as they are loaded (once per pixel tile).
+// ---------------------------------------------------------------------------------------------------
+template <int KC, int NB, int EPI, bool PRE>
+__global__ void __launch_bounds__(256, 2) conv1x1_areg_kernel(C3Args a) {
+    constexpr int FN = NB / 16, NKS = 2 * KC, K = 64 * KC;
+    constexpr int BPT = NB * KC * 8 / 256;               // 16-byte weight pieces per thread per step
+    static_assert(BPT >= 1 && NB * KC * 8 % 256 == 0, "weight step must cover the block");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const bbuf = reinterpret_cast<bf16_t*>(smem);     // [2][KC][NB][64] K-major kimg_off images
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int groups = a.ntiles;
+    const int t = xcd_remap(blockIdx.x, a.tiles * groups);
+    const int tile = t / groups, grp = t - tile * groups;
+    const int steps = (a.N / NB) / groups;
+    const int c00 = grp * steps;
+    const int p0 = tile * C3_BM;
+
+    u16x8_t rb[BPT];
+    auto load_b = [&](int s) {
+        const int n0 = (c00 + s) * NB;
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const int li = tid + 256 * i, row = li / (KC * 8), rem = li - row * (KC * 8);
+            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * K + rem * 8);
+        }
+    };
+    auto store_b = [&](int buf) {
+        bf16_t* B = bbuf + buf * (KC * NB * 64);
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const int li = tid + 256 * i, row = li / (KC * 8), rem = li - row * (KC * 8);
+            *reinterpret_cast<u16x8_t*>(B + (rem >> 3) * (NB * 64) + kimg_off(row, rem & 7)) = rb[i];
+        }
+    };
+    load_b(0);
+
+    // this wave's activation fragments: pixel (wave*64 + fm*16 + lane&15), channels ks*32 + (lane>>4)*8 .. +8
+    bool pv[4];
+    long prow[4];
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+        const int p = p0 + wave * 64 + fm * 16 + (lane & 15);
+        pv[fm] = p < a.P;
+        prow[fm] = (long)(pv[fm] ? p : a.P - 1) * K;
+    }
+    bf16x8_t af[NKS][4];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int k = ks * 32 + (lane >> 4) * 8;
+        u16x8_t v[4], tv[PRE ? 4 : 1];
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            v[fm] = *reinterpret_cast<const u16x8_t*>(a.x + prow[fm] + k);
+            if constexpr (PRE) tv[fm] = *reinterpret_cast<const u16x8_t*>(a.pre_t + prow[fm] + k);
+        }
+        PreCoef pc;
+        if constexpr (PRE) pre_coef(a, k, pc);
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            if constexpr (PRE) {
+                v[fm] = pre_apply(pc, v[fm], tv[fm]);
+                if (a.pre_out && grp == 0 && pv[fm]) *reinterpret_cast<u16x8_t*>(a.pre_out + prow[fm] + k) = v[fm];
+            }
+            // rows past P hold row P-1's values: their outputs are neither stored nor counted in the statistics
+            af[ks][fm] = __builtin_bit_cast(bf16x8_t, v[fm]);
+        }
+    }
+    store_b(0);
+    __syncthreads();
+
+    for (int s = 0; s < steps; ++s) {
+        const bool more = s + 1 < steps;
+        if (more) load_b(s + 1);                 // under this step's MFMAs
+        const bf16_t* B = bbuf + (s & 1) * (KC * NB * 64);
+        f32x4_t acc[4][FN];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        // weight fragments one k-step ahead; the scheduling barrier keeps the compiler from hoisting every
+        // k-step's LDS reads to the top (that costs 4 * FN * NKS VGPRs, and spills next to the A fragments)
+        bf16x8_t bcur[FN], bnxt[FN];
+#pragma unroll
+        for (int f = 0; f < FN; ++f) bcur[f] = frag_kmajor(B, f * 16 + (lane & 15), 0, lane);
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            if (ks + 1 < NKS) {
+#pragma unroll
+                for (int f = 0; f < FN; ++f)
+                    bnxt[f] = frag_kmajor(B + ((ks + 1) >> 1) * (NB * 64), f * 16 + (lane & 15), (ks + 1) & 1, lane);
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bcur[fn], af[ks][fm], acc[fm][fn], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int f = 0; f < FN; ++f) bcur[f] = bnxt[f];
+        }
+        c3_epilogue<NB, EPI>(a, acc, tile, p0, (c00 + s) * NB, wave, lane, pv);
         if (more) {
             store_b((s + 1) & 1);
             __syncthreads();
@@ -667,6 +788,36 @@ int p1_dispatch(const C3Args& a, int epi, int sm, hipStream_t st) {
         case C3_RES: return p1_launch<C3_RES, PRE>(a, sm, st);
         default: return p1_launch<C3_PLAIN, PRE>(a, sm, st);
     }
+}
+
+template <int KC, int NB, int EPI, bool PRE>
+int areg_launch(const C3Args& a, hipStream_t st) {
+    constexpr int sm = 2 * KC * NB * 128;
+    hipLaunchKernelGGL((conv1x1_areg_kernel<KC, NB, EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    PDNN_LAUNCH_RET;
+}
+
+template <int KC, int NB, bool PRE>
+int areg_dispatch(const C3Args& a, int epi, hipStream_t st) {
+    switch (epi) {
+        case C3_BNB: return areg_launch<KC, NB, C3_BNB, PRE>(a, st);
+        case C3_STATS: return areg_launch<KC, NB, C3_STATS, PRE>(a, st);
+        case C3_RES: return areg_launch<KC, NB, C3_RES, PRE>(a, st);
+        default: return areg_launch<KC, NB, C3_PLAIN, PRE>(a, st);
+    }
+}
+
+// K = 64 / 128 / 256 -> (KC, NB) = (1, 64) / (2, 64) / (4, 32): <= ~190 VGPRs, two blocks per CU
+template <bool PRE>
+int areg_run(C3Args& a, int K, int epi, hipStream_t st) {
+    const int nb = K == 256 ? 32 : 64;
+    const int chunks = a.N / nb;
+    int g = 1;
+    while (g < chunks && (long)a.tiles * g < 512 && chunks % (2 * g) == 0) g *= 2;
+    a.ntiles = g;
+    if (K == 64) return areg_dispatch<1, 64, PRE>(a, epi, st);
+    if (K == 128) return areg_dispatch<2, 64, PRE>(a, epi, st);
+    return areg_dispatch<4, 32, PRE>(a, epi, st);
 }
 
 // the PRE prologue's operands (all or none; t: [P][C] like x, the rest fp32 [C], gamma optional)
@@ -768,7 +919,8 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
 // 1x1 / stride-1 conv on the pixel-panel kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128}, N % 64 == 0.
 // Epilogues as pdnn_conv3x3.  Returns hipErrorInvalidValue for shapes it does not take.
 PDNN_API int pdnn_conv1x1_panel_supported(long P, int K, int N) {
-    return (K == 64 || K == 128) && N % 64 == 0 && N >= 64 && P > 0 && P < (1L << 30) ? 1 : 0;
+    const bool k_ok = K == 64 || K == 128 || (K == 256 && pg::tune().areg >= 1);
+    return k_ok && N % 64 == 0 && N >= 64 && P > 0 && P < (1L << 30) ? 1 : 0;
 }
 
 PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, long P, int K, int N, float* stats,
@@ -786,13 +938,15 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
     if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
         return (int)hipErrorInvalidValue;
+    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    // K = 256 always on the A-stationary kernel (the panel's A image would not leave room for 2 blocks per CU)
+    if (K == 256 || pg::tune().areg >= 2) return pre_t ? areg_run<true>(a, K, epi, st) : areg_run<false>(a, K, epi, st);
     // column groups: split the output columns over blocks only until the grid covers ~2 blocks per CU
     const int chunks = N / 64;
     int g = 1;
     while (g < chunks && (long)a.tiles * g < 512 && chunks % (2 * g) == 0) g *= 2;
     a.ntiles = g;
     const int sm = (K / 64) * (C3_BM + 1) * 128 + 2 * 64 * 128;
-    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
     return pre_t ? p1_dispatch<true>(a, epi, sm, st) : p1_dispatch<false>(a, epi, sm, st);
 }
 

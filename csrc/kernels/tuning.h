@@ -29,7 +29,9 @@ namespace pg {
     X(staged_store, 1, "128-row kernel: bf16 epilogue stores staged through LDS (full rows)")                \
     X(lowk_bn64, 24, "GEMMs of <= this many K-steps take the 128x64 tile (r2_42-44 sweep: 24)")             \
     X(split_blocks, 512, "split-K weight gradients: target blocks (r2 sweep: 256/384 -2%/-1%, 768 equal)")   \
-    X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")
+    X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                           \
+    X(areg, 2, "A-stationary 1x1 kernel: 0 off, 1 for K = 256 (LDS panel for K <= 128), 2 for every K <= 256 " \
+               "(r3_15: 9,844 vs 9,780 / 9,690 img/s for 1 / 0)")
 
 struct Tune {
 #define PDNN_TUNE_FIELD(n, d, doc) int n = d;

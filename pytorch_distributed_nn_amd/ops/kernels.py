@@ -287,13 +287,20 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     return y, stats
 
 
+def _panel_dgrad_k(K):
+    """Data gradients (dx[P][C] = dy[P][K] . W) on the panel / A-stationary kernels: K = 64 (ResNet stage 1),
+    K = 256 and, with the A-stationary kernel for every K (tuning areg = 2), K = 128.  The LDS-panel kernel
+    lost to the implicit-GEMM engine at K = 128 (176 vs 154 us, gpurun_out/r3_08)."""
+    return K in (64, 256) or (K == 128 and tune_get("areg") >= 2)
+
+
 def dgrad_pre_ok(dy_shape, w_shape, st, pad):
     """Whether conv_dgrad takes ``pre=`` (the BN-backward apply fused into its operand loads) for this
     conv: the halo 3x3 kernel and the K = 64 panel kernel."""
     N, Ho, Wo, K = dy_shape
     Kw, R, S, C = w_shape
     return (_conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad)
-            or (K == 64 and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
+            or (_panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
 
 
 def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None):
@@ -335,9 +342,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
         y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask, pre=pre)
         return (y, slab) if bn is not None else y
-    # panel data gradient only for K = 64 (ResNet stage 1): at K = 128 -> 512 the implicit-GEMM engine was faster
-    # (154 vs 176 us, gpurun_out/r3_08)
-    if K == 64 and _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
+    if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
         # dx[P][C] = dy[P][K] . W[K][C]: the panel kernel with the transposed weight W^T [C][K]
         y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)),
                                 res=None if res is None else res.view(-1, C), res_mask=res_mask,

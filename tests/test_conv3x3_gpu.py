@@ -100,11 +100,19 @@ def test_conv3x3_matches_gemm_engine_bitwise_stats_layout(K):
 
 # ------------------------------------------------------------------- 1x1 pixel-panel kernel (K in {64, 128})
 PANEL = [(2, 56, 56, 64, 256), (3, 28, 28, 128, 512), (1, 7, 7, 128, 2048), (2, 9, 11, 64, 64), (5, 14, 14, 64, 1024),
-         (1, 1, 3, 128, 128)]
+         (1, 1, 3, 128, 128), (4, 14, 14, 256, 1024), (3, 9, 7, 256, 64), (1, 1, 1, 256, 128), (2, 28, 28, 256, 64)]
+
+
+@pytest.fixture(params=[1, 2], ids=["areg-k256", "areg-all"])
+def areg(request, K):
+    """tuning areg: 1 = A-stationary kernel for K = 256 only (panel for K <= 128), 2 = for every K"""
+    old = K.tune_set("areg", request.param)
+    yield request.param
+    K.tune_set("areg", old)
 
 
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_fwd_stats(K, shape):
+def test_conv1x1_panel_fwd_stats(K, areg, shape):
     N, H, W, C, Ko = shape
     x = torch.randn(N, H, W, C, device="cuda").to(BF)
     w = (torch.randn(Ko, 1, 1, C, device="cuda") * 0.1).to(BF)
@@ -119,7 +127,7 @@ def test_conv1x1_panel_fwd_stats(K, shape):
 
 
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_dgrad(K, shape):
+def test_conv1x1_panel_dgrad(K, areg, shape):
     """dx = dy . W (K = dy channels in {64, 128}) plain / masked residual / fused BN backward."""
     N, H, W, Kc, C = shape            # dy has Kc channels, dx has C
     x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
@@ -191,7 +199,7 @@ def test_conv3x3_dgrad_pre_matches_separate_apply(K, nb, shape):
 
 
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_pre_matches_separate_apply(K, shape):
+def test_conv1x1_panel_pre_matches_separate_apply(K, areg, shape):
     """The panel kernel's operand prologue (K in {64, 128}): same bits as apply-then-conv."""
     N, H, W, Kc, C = shape
     w = (torch.randn(Kc, 1, 1, C, device="cuda") * 0.1).to(BF)
@@ -206,15 +214,15 @@ def test_conv1x1_panel_pre_matches_separate_apply(K, shape):
     res = torch.randn(N * H * W, C, device="cuda").to(BF)
     yr, _ = K.conv1x1_panel(gm.view(-1, Kc), wt, res=res, pre=(t, mean, inv, g, dg, db, None))
     assert torch.equal(yr, K.conv1x1_panel(dt_ref, wt, res=res)[0])
-    if Kc == 64:       # routed through conv_dgrad (the K = 64 panel data gradient)
+    if Kc in (64, 256):       # routed through conv_dgrad (the K = 64 / 256 panel data gradient)
         assert K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
         dx = K.conv_dgrad(gm, w, (N, H, W, C), 1, 0, pre=(t, mean, inv, g, dg, db, None))
         assert torch.equal(dx.view(-1, C), y_ref)
 
 
 def test_dgrad_pre_rejected_on_gemm_engine(K):
-    gm, t, mean, inv, g, dg, db = _pre_operands((2, 8, 8, 256))
-    w = (torch.randn(256, 1, 1, 64, device="cuda") * 0.1).to(BF)
+    gm, t, mean, inv, g, dg, db = _pre_operands((2, 8, 8, 512))
+    w = (torch.randn(512, 1, 1, 64, device="cuda") * 0.1).to(BF)
     assert not K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
     with pytest.raises(ValueError):
         K.conv_dgrad(gm, w, (2, 8, 8, 64), 1, 0, pre=(t, mean, inv, g, dg, db, None))

@@ -13,7 +13,7 @@ ALT = {
     "glds": [0, 2], "glds_min_tiles": [1, 1 << 20], "glds_fwd_k": [64], "glds_dgrad_n": [64], "glds_dgrad_k": [64],
     "glds_persistent": [1], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "pp_fp8": [0], "pp_conv_min_n": [64],
     "pp_conv_fwd_k": [64], "pp_conv_dgrad_k": [64], "pp_conv_bnb_k": [64], "staged_store": [0], "lowk_bn64": [0, 4],
-    "split_blocks": [64, 2048], "conv3x3_force": [1],
+    "split_blocks": [64, 2048], "conv3x3_force": [1], "areg": [0, 1],
 }
 
 
@@ -28,7 +28,7 @@ def _battery(K):
     x, w = rn(1000, 512), rn(776, 512, sc=0.05)
     assert rel(K.gemm_nt(x, w), x.float() @ w.float().t()) < 1e-2
     for (N, H, C, Ko, R, st, pad) in [(2, 14, 128, 128, 3, 1, 1), (2, 14, 128, 128, 3, 2, 1), (2, 14, 64, 256, 1, 1, 0),
-                                      (2, 8, 256, 512, 1, 1, 0), (3, 7, 512, 512, 3, 1, 1)]:
+                                      (2, 8, 256, 512, 1, 1, 0), (2, 14, 128, 512, 1, 1, 0), (2, 8, 512, 128, 1, 1, 0), (3, 7, 512, 512, 3, 1, 1)]:
         xi = torch.randn(N, C, H, H, device="cuda", generator=g, requires_grad=True)
         wk = rn(Ko, R, R, C, sc=0.05)
         y = F.conv2d(xi, wk.float().permute(0, 3, 1, 2), None, st, pad)
