@@ -55,6 +55,18 @@ def main():
         row["conv1_fwd"] = timeit(lambda: K.conv_fwd(x4, k1, 1, 0, want_stats=True))
         row["conv3_dgrad_bn"] = timeit(lambda: K.conv_dgrad(dt3, k3, t2.shape, 1, 0, bn=(t2, mean, inv, sc, sh)))
         row["conv1_dgrad_res"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4))
+        bits = torch.randint(0, 256, (N * H * H, C4 // 8), device=d, dtype=torch.uint8)
+        row["conv1_dgrad_res_mask"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4, res_mask=bits))
+        if K.dgrad_pre_ok(dt1.shape, k1.shape, 1, 0):
+            # the Bottleneck's conv1 data gradient: BN1's backward apply in the operand loads, dt1 written
+            g1, dg, db = torch.rand(C, device=d) + 0.5, torch.randn(C, device=d), torch.randn(C, device=d)
+            dt_out = torch.empty_like(dt1)
+            pre = (t2, mean, inv, g1, dg, db, dt_out)
+            row["conv1_dgrad_pre"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, pre=pre))
+            row["conv1_dgrad_pre_res_mask"] = timeit(
+                lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4, res_mask=bits, pre=pre))
+            row["conv1_dgrad_pre_nowrite"] = timeit(
+                lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4, res_mask=bits, pre=pre[:6] + (None,)))
         print(json.dumps(row), flush=True)
         for k, v in row.items():
             if k not in ("H", "C"):
