@@ -650,25 +650,59 @@ __global__ void __launch_bounds__(256, 2) conv1x1_areg_kernel(C3Args a) {
         prow[fm] = (long)(pv[fm] ? p : a.P - 1) * K;
     }
     bf16x8_t af[NKS][4];
+    if constexpr (!PRE) {
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-        const int k = ks * 32 + (lane >> 4) * 8;
-        u16x8_t v[4], tv[PRE ? 4 : 1];
+        for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            v[fm] = *reinterpret_cast<const u16x8_t*>(a.x + prow[fm] + k);
-            if constexpr (PRE) tv[fm] = *reinterpret_cast<const u16x8_t*>(a.pre_t + prow[fm] + k);
-        }
-        PreCoef pc;
-        if constexpr (PRE) pre_coef(a, k, pc);
-#pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            if constexpr (PRE) {
-                v[fm] = pre_apply(pc, v[fm], tv[fm]);
-                if (a.pre_out && grp == 0 && pv[fm]) *reinterpret_cast<u16x8_t*>(a.pre_out + prow[fm] + k) = v[fm];
+            for (int fm = 0; fm < 4; ++fm)
+                // rows past P hold row P-1's values: their outputs are neither stored nor counted in the statistics
+                af[ks][fm] = __builtin_bit_cast(
+                    bf16x8_t, *reinterpret_cast<const u16x8_t*>(a.x + prow[fm] + ks * 32 + (lane >> 4) * 8));
+    } else {
+        // BN-backward coefficients of all K channels computed once per block into LDS (after the weight
+        // buffers), then the fragments are loaded GB k-steps at a time (gm and t of all of them in flight
+        // together) and transformed: per-k-step global coefficient loads serialised the prologue
+        float* coef = reinterpret_cast<float*>(bbuf + 2 * KC * NB * 64);      // [3][K]: k, A, B
+        {
+            const float invL = (float)(1.0 / (double)a.P);
+            for (int c = tid; c < K; c += 256) {
+                const float is = a.pre_invstd[c], kk = (a.pre_gamma ? a.pre_gamma[c] : 1.f) * is;
+                const float dg = a.pre_dgamma[c] * invL, db = a.pre_dbeta[c] * invL;
+                coef[c] = kk;
+                coef[K + c] = -kk * is * dg;
+                coef[2 * K + c] = kk * (a.pre_mean[c] * is * dg - db);
             }
-            // rows past P hold row P-1's values: their outputs are neither stored nor counted in the statistics
-            af[ks][fm] = __builtin_bit_cast(bf16x8_t, v[fm]);
+        }
+        __syncthreads();
+        constexpr int GB = KC == 4 ? 2 : (KC == 2 ? 4 : 2);
+#pragma unroll
+        for (int g0 = 0; g0 < NKS; g0 += GB) {
+            u16x8_t v[GB][4], tv[GB][4];
+#pragma unroll
+            for (int kk = 0; kk < GB; ++kk)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) {
+                    const long off = prow[fm] + (g0 + kk) * 32 + (lane >> 4) * 8;
+                    v[kk][fm] = *reinterpret_cast<const u16x8_t*>(a.x + off);
+                    tv[kk][fm] = *reinterpret_cast<const u16x8_t*>(a.pre_t + off);
+                }
+#pragma unroll
+            for (int kk = 0; kk < GB; ++kk) {
+                const int k = (g0 + kk) * 32 + (lane >> 4) * 8;
+                PreCoef pc;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    pc.k[j] = coef[k + j];
+                    pc.A[j] = coef[K + k + j];
+                    pc.B[j] = coef[2 * K + k + j];
+                }
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) {
+                    const u16x8_t d = pre_apply(pc, v[kk][fm], tv[kk][fm]);
+                    if (a.pre_out && grp == 0 && pv[fm]) *reinterpret_cast<u16x8_t*>(a.pre_out + prow[fm] + k) = d;
+                    af[g0 + kk][fm] = __builtin_bit_cast(bf16x8_t, d);
+                }
+            }
         }
     }
     store_b(0);
@@ -802,7 +836,7 @@ int p1_dispatch(const C3Args& a, int epi, int sm, hipStream_t st) {
 
 template <int KC, int NB, int EPI, bool PRE>
 int areg_launch(const C3Args& a, hipStream_t st) {
-    constexpr int sm = 2 * KC * NB * 128;
+    constexpr int sm = 2 * KC * NB * 128 + (PRE ? 3 * 64 * KC * 4 : 0);
     hipLaunchKernelGGL((conv1x1_areg_kernel<KC, NB, EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }
