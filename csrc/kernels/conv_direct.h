@@ -1,0 +1,179 @@
+// Shared pieces of the direct (non-implicit-GEMM) convolution kernels: conv3x3.hip (LDS-halo 3x3, pixel
+// panel and A-stationary 1x1) and stem.hip (7x7 / stride-2 stem).  Argument block, operand masking, the
+// LDS halo swizzle, the BatchNorm-backward operand prologue and the common epilogue (plain / residual /
+// BN statistics / fused BN backward) -- one slab row pair per (pixel tile, wave), 64 pixels each.
+#pragma once
+#include "gemm_common.h"
+#include "tuning.h"
+
+namespace {
+using namespace pg;
+
+constexpr int C3_BM = 256;
+enum { C3_PLAIN = 0, C3_STATS = 1, C3_BNB = 2, C3_RES = 3 };
+
+struct C3Args {
+    const bf16_t* x;     // [P][C]  NHWC input
+    const bf16_t* w;     // [N][3][3][C]
+    bf16_t* y;           // [P][N]
+    int Nimg, H, W, C, N, P;
+    FastDiv dW, dH;
+    int tiles, ntiles;
+    int halo_max;        // pixels of the largest halo (LDS layout)
+    float* stats;
+    const bf16_t* res;
+    const uint8_t* rmask;  // C3_RES: residual masked by these ReLU bits ([P][N/8] bytes), or null
+    const bf16_t* ep_x;
+    const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
+    // PRE operand prologue (BatchNorm backward apply of the layer whose gradient is the input): the staged
+    // operand is dt = k*gm + A*t + B per channel (pdnn_bn_bwd_apply's formula, same rounding) with gm = x;
+    // the own pixels' dt is also written to pre_out (the weight gradient's operand)
+    const bf16_t* pre_t;
+    const float *pre_mean, *pre_invstd, *pre_gamma, *pre_dgamma, *pre_dbeta;
+    bf16_t* pre_out;
+};
+
+// per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)
+struct PreCoef {
+    float k[8], A[8], B[8];
+};
+__device__ __forceinline__ void pre_coef(const C3Args& a, int c, PreCoef& pc) {
+    const float invL = (float)(1.0 / (double)a.P);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float is = a.pre_invstd[c + j], k = (a.pre_gamma ? a.pre_gamma[c + j] : 1.f) * is;
+        const float dg = a.pre_dgamma[c + j] * invL, db = a.pre_dbeta[c + j] * invL;
+        pc.k[j] = k;
+        pc.A[j] = -k * is * dg;
+        pc.B[j] = k * (a.pre_mean[c + j] * is * dg - db);
+    }
+}
+__device__ __forceinline__ u16x8_t pre_apply(const PreCoef& pc, const u16x8_t& gv, const u16x8_t& tv) {
+    float gm[8], t[8], o[8];
+    unpack8(gv, gm);
+    unpack8(tv, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(pc.k[j], gm[j], fmaf(t[j], pc.A[j], pc.B[j]));
+    return pack8(o);
+}
+
+// v if ok else 0, as four 32-bit ANDs (a u16x8 AND with a 16-bit mask vector lowers to per-half sdwa/perm ops)
+__device__ __forceinline__ u16x8_t mask16(const u16x8_t& v, bool ok) {
+    const uint32_t m = ok ? 0xFFFFFFFFu : 0u;
+    uint4 u = __builtin_bit_cast(uint4, v);
+    u.x &= m; u.y &= m; u.z &= m; u.w &= m;
+    return __builtin_bit_cast(u16x8_t, u);
+}
+
+__device__ __forceinline__ u16x8_t c3_zero8() {
+    u16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+    return z;
+}
+
+// halo image: pixel hp = 128 bytes (64 channels), 16-byte chunk q stored at q ^ ((hp >> 1) & 7)
+__device__ __forceinline__ int halo_off(int hp, int q) {   // bf16 elements
+    return hp * 64 + ((q ^ ((hp >> 1) & 7)) << 3);
+}
+
+// ---------------- epilogue: lane holds y[pixel m = wave*64 + fm*16 + (lane&15)][n = fn*16 + 4*(lane>>4) + j]
+template <int NB, int EPI>
+__device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile, int p0, int n0,
+                                            int wave, int lane, const bool (&pv)[4]) {
+    constexpr int FN = NB / 16;
+    const int lg = lane >> 4;
+    long orow[4];
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
+    // processed one fragment pair (fn, fn+1) at a time: only that pair's loads / packed results are live
+#pragma unroll
+    for (int fp = 0; fp < FN / 2; ++fp) {
+        uint32_t pk[4][2][2];
+        // C3_RES mask bits of this pair's 32 channels: ONE aligned 32-bit load per pixel (bit c = channel
+        // n0 + 32*fp + c), not a byte load per fragment (that doubled the epilogue's memory instructions:
+        // ResNet-50 stage-1 conv1 data gradient 239 -> 341 us with the mask, gpurun_out/r3_18)
+        uint32_t mw[4];
+        if constexpr (EPI == C3_RES) {
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+                mw[fm] = a.rmask ? *reinterpret_cast<const uint32_t*>(a.rmask + (((pv[fm] ? orow[fm] : 0) + n0 + 32 * fp) >> 3))
+                                 : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int fn = 2 * fp + h;
+            const int n = n0 + fn * 16 + 4 * lg;
+            u16x4_t tv[4];
+            if constexpr (EPI == C3_BNB || EPI == C3_RES) {
+                const bf16_t* src = EPI == C3_BNB ? a.ep_x : a.res;
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    tv[fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(src + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
+            }
+            float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+            float bmu[4], bis[4], bms[4], bmh[4];
+            if constexpr (EPI == C3_BNB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bmu[j] = a.ep_mean[n + j]; bis[j] = a.ep_invstd[n + j];
+                    bms[j] = a.ep_mscale[n + j]; bmh[j] = a.ep_mshift[n + j];
+                }
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) {
+                const bool ok = pv[fm];
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j];
+                if constexpr (EPI == C3_RES) {
+                    const uint32_t mb = mw[fm] >> (16 * h + 4 * lg);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(tv[fm][j]) : 0.f;
+                }
+                if constexpr (EPI == C3_BNB) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float tt = bf2f(tv[fm][j]);
+                        const float gm = (ok && fmaf(tt, bms[j], bmh[j]) > 0.f) ? bf2f(f2bf(v[j])) : 0.f;
+                        v[j] = gm;
+                        s[j] += gm;
+                        q[j] += ok ? gm * (tt - bmu[j]) * bis[j] : 0.f;
+                    }
+                } else if constexpr (EPI == C3_STATS) {
+                    if (ok) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float r = bf2f(f2bf(v[j]));
+                            s[j] += r;
+                            q[j] += r * r;
+                        }
+                    }
+                }
+                pk[fm][h][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                pk[fm][h][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            }
+            if constexpr (EPI == C3_STATS || EPI == C3_BNB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    s[j] = row16_sum(s[j]);
+                    q[j] = row16_sum(q[j]);
+                }
+                if ((lane & 15) == 0) {
+                    float* ps = a.stats + (long)(tile * 4 + wave) * 2 * a.N + n;
+                    float* pq = ps + a.N;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { ps[j] = s[j]; pq[j] = q[j]; }
+                }
+            }
+        }
+        // permlane16_swap pairs the two fragments: every lane then holds 8 consecutive channels (16 bytes)
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[fm][0][0], pk[fm][1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[fm][0][1], pk[fm][1][1], false, false);
+            const int n = n0 + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
+            if (pv[fm]) *reinterpret_cast<uint4*>(a.y + orow[fm] + n) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+    }
+}
+
+}  // namespace

@@ -50,6 +50,9 @@ _SIGS = {
     "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
+    "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
+    "pdnn_stem_stats_rows": [L],
+    "pdnn_bn_relu_maxpool": [P, P, P, P, P, I, I, I, I, I, I, P],
     "pdnn_set_glds_mode": [I],
     "pdnn_set_pp_mode": [I],
     "pdnn_set_pp_bn": [I],

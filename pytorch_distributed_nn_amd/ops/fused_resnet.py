@@ -447,22 +447,35 @@ class StemFn(torch.autograd.Function):
     def forward(ctx, x, conf, bufs, shadows, w, gamma, beta):
         stride, pad, pool, training, mom, eps = conf
         kpad = shadows[0]
-        t, m, i, s, h = _conv_bn(x, kpad, stride, pad, None, training, (gamma, beta), bufs, mom, eps)
-        C = t.shape[-1]
-        a, mb = K.bn_apply(t.view(-1, C), s, h, relu=True, want_mask=training)
-        a = a.view(t.shape)
-        if pool:
-            y, idx = K.maxpool_fwd(a, 3, 2, 1)
+        direct = pool and K.stem_ok(x.shape, kpad.shape, stride, pad)
+        if direct:
+            # direct 7x7/s2 kernel, then BN + ReLU + max-pool in one pass over t; the backward recomputes the
+            # ReLU mask from t (mask mode 2), so neither the activation nor its mask is stored
+            t, slab = K.stem_conv(x, kpad, want_stats=training)
+            M = t.numel() // t.shape[-1]
+            if training:
+                m, i, s, h = _bn_train(slab, M, (gamma, beta), bufs, mom, eps)
+            else:
+                m, i, s, h = _bn_eval((gamma, beta), bufs, eps)
+            y, idx = K.bn_relu_maxpool(t, s, h)
+            mb = None
         else:
-            y, idx = a, None
-        ctx.save_for_backward(x, t, mb, idx, m, i, gamma)      # ReLU mask bits, not the activation
+            t, m, i, s, h = _conv_bn(x, kpad, stride, pad, None, training, (gamma, beta), bufs, mom, eps)
+            C = t.shape[-1]
+            a, mb = K.bn_apply(t.view(-1, C), s, h, relu=True, want_mask=training)
+            a = a.view(t.shape)
+            if pool:
+                y, idx = K.maxpool_fwd(a, 3, 2, 1)
+            else:
+                y, idx = a, None
+        ctx.save_for_backward(x, t, mb, idx, m, i, gamma, s if direct else None, h if direct else None)
         ctx.conf = (stride, pad, pool, w.shape, kpad.shape)
         ctx.params = (w, gamma, beta)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, t, mb, idx, m, i, gamma = ctx.saved_tensors
+        x, t, mb, idx, m, i, gamma, s, h = ctx.saved_tensors
         stride, pad, pool, wshape, kshape = ctx.conf
         gy = gy.contiguous()
         ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy
@@ -470,8 +483,12 @@ class StemFn(torch.autograd.Function):
         P = ctx.params
         ctx.params = None
         sink = _Sink()
-        dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
-                              bn_params=(P[1], P[2]))
+        if mb is None:          # direct stem: ReLU mask recomputed from t (t * s + h > 0)
+            dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 2, msrc=t.view(-1, C), msc=s, msh=h,
+                                  sink=sink, bn_params=(P[1], P[2]))
+        else:
+            dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
+                                  bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
         if kshape[3] == wshape[1]:
             dw = sink.wgrad(P[0], x, dt, kshape[1], kshape[2], stride, pad)

@@ -471,6 +471,41 @@ def bn_bwd_apply(g, x, mean, invstd, gamma, dgamma, dbeta, mode=0, msrc=None, ms
 
 
 # ----------------------------------------------------------------------------------- pooling
+def stem_ok(x_shape, w_shape, st, pad):
+    """The ImageNet stem conv (7x7 / stride 2 / pad 3, 8 padded input channels, 64 outputs) on the direct
+    stem kernel (csrc/kernels/stem.hip)."""
+    return (tuple(w_shape) == (64, 7, 7, 8) and x_shape[-1] == 8 and st == 2 and pad == 3
+            and _tuning.get("stem") == 1)
+
+
+def stem_conv(x, w, want_stats=True):
+    """t = conv7x7/s2/p3(x) (x NHWC bf16 with 8 channels, w bf16 [64][7][7][8]) + BN partial statistics."""
+    _bf16_c(x, "stem.x")
+    _bf16_c(w, "stem.w")
+    N, H, W, C = x.shape
+    _chk(C == 8 and tuple(w.shape) == (64, 7, 7, 8), "stem_conv: x [N][H][W][8], w [64][7][7][8]")
+    Ho, Wo = conv_out_hw(H, W, 7, 7, 2, 3)
+    y = torch.empty(N, Ho, Wo, 64, device=x.device, dtype=BF16)
+    slab = None
+    if want_stats:
+        slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
+    call("pdnn_stem_conv", ptr(x), ptr(w), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
+    return y, slab
+
+
+def bn_relu_maxpool(t, scale, shift):
+    """(y, idx) = maxpool3x3/s2/p1(relu(t * scale + shift)) without materialising the activation; bitwise
+    equal to bn_apply(relu=True) followed by maxpool_fwd."""
+    _bf16_c(t, "bn_relu_maxpool.t")
+    N, H, W, C = t.shape
+    _chk(C % 8 == 0, "bn_relu_maxpool: C % 8")
+    Ho, Wo = conv_out_hw(H, W, 3, 3, 2, 1)
+    y = torch.empty(N, Ho, Wo, C, device=t.device, dtype=BF16)
+    idx = torch.empty(N, Ho, Wo, C, device=t.device, dtype=torch.uint8)
+    call("pdnn_bn_relu_maxpool", ptr(t), ptr(scale), ptr(shift), ptr(y), ptr(idx), N, H, W, C, Ho, Wo, stream())
+    return y, idx
+
+
 def maxpool_fwd(x, k, st, pad):
     _bf16_c(x, "maxpool.x")
     N, H, W, C = x.shape

@@ -88,7 +88,7 @@ def _resnet_grads(arch="resnet50"):
 
 @pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("materialize_a2", "resnet50"),
                                       ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("bwd_pre", "resnet50"),
-                                      ("bwd_pre", "resnet18")])
+                                      ("bwd_pre", "resnet18"), ("stem", "resnet50")])
 def test_python_entry_alternatives(K, key, arch):
     """The model-level switches change only the schedule / kernel choice: same gradients (bf16 noise)."""
     from pytorch_distributed_nn_amd import tuning
