@@ -112,6 +112,101 @@ __global__ void __launch_bounds__(256, 2) stem7_kernel(C3Args a, StemGeo g) {
     }
 }
 
+// The same conv reading the data loader's NCHW bf16 batch directly (3 channels, W even): per filter row r
+// the reduction runs over k = c*8 + j (c < 4, the 4th channel zero; j = 0..7 <-> input column 2*ox - 4 + j,
+// tap s = j - 1, j = 0 has zero weight), 32 deep = ONE MFMA k-step per filter row.  A lane's operand piece
+// is 8 consecutive input columns of one channel row -- 16 bytes, 4-byte aligned because 2*ox - 4 is even --
+// so the layer runs 7 k-steps instead of the NHWC form's 14 (channel padding 3 -> 8) and the NCHW -> NHWC
+// conversion pass leaves the critical path.  Lanes whose 8 columns cross the left / right image border
+// (3 output columns per row) load the nearest in-image 16 bytes, word-shifted.  All 7 rows in flight.
+// weight image of the NCHW stem: [7 r][64 n][32 k] bf16, 16-byte chunk q (4 per row) at q ^ ((n >> 1) & 3)
+__device__ __forceinline__ int w32_off(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3); }
+
+__global__ void __launch_bounds__(256, 2) stem7n_kernel(C3Args a, StemGeo g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const wimg = reinterpret_cast<bf16_t*>(smem);         // [7 r][64 n][32 k]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // weights [64][7][32] (k = c*8 + j, built by the host wrapper) -> per-row K-major images
+    for (int i = tid; i < STEM_R * 64 * 4; i += 256) {
+        const int r = i >> 8, n = (i >> 2) & 63, q = i & 3;
+        *reinterpret_cast<u16x8_t*>(wimg + r * 2048 + w32_off(n, q)) =
+            *reinterpret_cast<const u16x8_t*>(a.w + (n * STEM_R + r) * 32 + q * 8);
+    }
+    __syncthreads();
+    const int x8 = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
+    const int T8 = (a.tiles + 7) / 8;
+    const int t_end = min(a.tiles, (x8 + 1) * T8);
+    const int c = lane >> 4;                               // this lane's input channel (3: zero)
+    const long plane = (long)g.H * g.W;
+
+    for (int tile = x8 * T8 + l; tile < t_end; tile += G) {
+        const int p0 = tile * C3_BM;
+        bool pv[4];
+        const bf16_t* rowp[4];                            // filter row 0 of this lane's pixel, column `col`
+        int iy0[4], shw[4];
+        bool cok[4];
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            const int p = p0 + wave * 64 + fm * 16 + (lane & 15);
+            pv[fm] = p < a.P;
+            const int pp = pv[fm] ? p : a.P - 1;
+            const int q = (int)fdiv((uint32_t)pp, g.dWo);
+            const int ox = pp - q * g.Wo;
+            const int nimg = (int)fdiv((uint32_t)q, g.dHo);
+            const int oy = q - nimg * g.Ho;
+            const int lo = 2 * ox - 4;                     // column of j = 0
+            cok[fm] = pv[fm] && c < 3;
+            // border lanes (ox = 0, 1 and the last column) load the nearest in-image 16 bytes and shift them
+            // by whole 32-bit words (zeros shifted in): shw = +2 / +1 / -1 words, 0 inside
+            const int col = lo < 0 ? 0 : (lo + 8 > g.W ? g.W - 8 : lo);
+            shw[fm] = (col - lo) / 2;
+            iy0[fm] = 2 * oy - 3;
+            rowp[fm] = a.x + ((long)nimg * 3 + (c < 3 ? c : 0)) * plane + col;
+        }
+        auto load_row = [&](int r, u16x8_t (&dst)[4]) {
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) {
+                const int iy = iy0[fm] + r;
+                const bool rok = cok[fm] && (unsigned)iy < (unsigned)g.H;
+                const uint4 w = __builtin_bit_cast(uint4, *reinterpret_cast<const u16x8_t*>(rowp[fm] + (long)(rok ? iy : 0) * g.W));
+                const uint32_t m = rok ? 0xFFFFFFFFu : 0u;
+                const int sh = shw[fm];
+                uint4 o;
+                o.x = (sh == 0 ? w.x : sh == 1 ? 0u : sh == 2 ? 0u : w.y) & m;
+                o.y = (sh == 0 ? w.y : sh == 1 ? w.x : sh == 2 ? 0u : w.z) & m;
+                o.z = (sh == 0 ? w.z : sh == 1 ? w.y : sh == 2 ? w.x : w.w) & m;
+                o.w = (sh == 0 ? w.w : sh == 1 ? w.z : sh == 2 ? w.y : 0u) & m;
+                dst[fm] = __builtin_bit_cast(u16x8_t, o);
+            }
+        };
+        f32x4_t acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        // every filter row's pieces in flight at once (28 loads per lane): one memory latency per tile
+        u16x8_t v[STEM_R][4];
+#pragma unroll
+        for (int r = 0; r < STEM_R; ++r) load_row(r, v[r]);
+#pragma unroll
+        for (int r = 0; r < STEM_R; ++r) {
+            bf16x8_t bfr[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const int n = f * 16 + (lane & 15);
+                bfr[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(wimg + r * 2048 + w32_off(n, lane >> 4)));
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], __builtin_bit_cast(bf16x8_t, v[r][fm]),
+                                                                          acc[fm][fn], 0, 0, 0);
+        }
+        c3_epilogue<64, C3_STATS>(a, acc, tile, p0, 0, wave, lane, pv);
+    }
+}
+
 // y[n][ho][wo][c] = max over the 3x3 / stride-2 / pad-1 window of bf16(relu(t * scale + shift)), idx = the
 // first maximal window position (as maxpool_fwd_kernel); one thread per (output pixel, 8 channels).
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16_t* __restrict__ t,
@@ -205,6 +300,26 @@ PDNN_API int pdnn_stem_conv(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nim
     int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
     grid = (grid + 7) / 8 * 8;
     hipLaunchKernelGGL(stem7_kernel, dim3(grid), dim3(256), sm, st, a, g);
+    PDNN_LAUNCH_RET;
+}
+
+// The NCHW form: x [Nimg][3][H][W] bf16 (W even), w [64][7][32] bf16 (k = c*8 + j, see stem7n_kernel).
+PDNN_API int pdnn_stem_conv_nchw(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int Ho,
+                                 int Wo, float* stats, hipStream_t st) {
+    if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || W % 2 || W < 8 ||
+        (long)Nimg * Ho * Wo >= (1L << 31))
+        return (int)hipErrorInvalidValue;
+    C3Args a{};
+    a.x = x; a.w = w; a.y = y; a.C = 3; a.N = STEM_N;
+    a.P = Nimg * Ho * Wo;
+    a.tiles = (int)cdiv(a.P, C3_BM);
+    a.ntiles = 1;
+    a.stats = stats;
+    StemGeo g{H, W, Ho, Wo, make_fdiv_stem(Wo), make_fdiv_stem(Ho)};
+    const int sm = STEM_R * 64 * 32 * 2;              // 28 KB
+    int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
+    grid = (grid + 7) / 8 * 8;
+    hipLaunchKernelGGL(stem7n_kernel, dim3(grid), dim3(256), sm, st, a, g);
     PDNN_LAUNCH_RET;
 }
 

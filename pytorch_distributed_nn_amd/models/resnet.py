@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import functional as OF
+from ..ops import kernels as K
 from ..ops.fused_resnet import BasicBlockFn, BottleneckFn, StemFn, stem_shadow
 
 
@@ -242,12 +243,18 @@ class ResNetImageNet(_ResNetBase):
         return self
 
     def forward_nhwc(self, x):
-        xin = OF.nchw_to_nhwc_input(x)
         mom, eps = _bn_conf(self.bn1)
         self._count_bn_batches()
-        out = StemFn.apply(xin, (2, 3, True, self.training, mom, eps), [self.bn1.running_mean, self.bn1.running_var],
-                           [stem_shadow(self.conv1.weight, xin.shape[-1])], self.conv1.weight, self.bn1.weight,
-                           self.bn1.bias)
+        conf = (2, 3, True, self.training, mom, eps)
+        bufs = [self.bn1.running_mean, self.bn1.running_var]
+        params = (self.conv1.weight, self.bn1.weight, self.bn1.bias)
+        if K.stem_nchw_ok(x):
+            # the stem kernel reads the NCHW batch directly (csrc/kernels/stem.hip stem7n_kernel)
+            xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+            out = StemFn.apply(xb.contiguous(), conf, bufs, [K.stem_weight_nchw(self.conv1.weight)], *params)
+        else:
+            xin = OF.nchw_to_nhwc_input(x)
+            out = StemFn.apply(xin, conf, bufs, [stem_shadow(self.conv1.weight, xin.shape[-1])], *params)
         for b in self._blocks():
             out = b.forward_nhwc(out)
         feat = OF.global_avg_pool_nhwc(out)

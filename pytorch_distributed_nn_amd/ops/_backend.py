@@ -52,6 +52,7 @@ _SIGS = {
     "pdnn_conv1x1_panel_stats_rows": [L],
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_stem_stats_rows": [L],
+    "pdnn_stem_conv_nchw": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_bn_relu_maxpool": [P, P, P, P, P, I, I, I, I, I, I, P],
     "pdnn_set_glds_mode": [I],
     "pdnn_set_pp_mode": [I],

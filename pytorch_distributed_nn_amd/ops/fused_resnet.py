@@ -447,11 +447,32 @@ class StemFn(torch.autograd.Function):
     def forward(ctx, x, conf, bufs, shadows, w, gamma, beta):
         stride, pad, pool, training, mom, eps = conf
         kpad = shadows[0]
-        direct = pool and K.stem_ok(x.shape, kpad.shape, stride, pad)
+        nchw = kpad.dim() == 3          # shadow from K.stem_weight_nchw: x is the NCHW bf16 batch itself
+        direct = nchw or (pool and K.stem_ok(x.shape, kpad.shape, stride, pad))
+        ev = None
+        if nchw:
+            # the weight gradient (end of the backward) reads the NHWC copy: converted on the side stream,
+            # off the forward's critical path
+            side = _side_stream(x.device)
+            xin = x
+            if side is not None:
+                main = torch.cuda.current_stream(x.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    xin = K.nchw_to_nhwc(x, 8)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                x.record_stream(side)
+                xin.record_stream(main)
+            else:
+                xin = K.nchw_to_nhwc(x, 8)
+            t, slab = K.stem_conv_nchw(x, kpad, want_stats=training)
+            x = xin
         if direct:
             # direct 7x7/s2 kernel, then BN + ReLU + max-pool in one pass over t; the backward recomputes the
             # ReLU mask from t (mask mode 2), so neither the activation nor its mask is stored
-            t, slab = K.stem_conv(x, kpad, want_stats=training)
+            if not nchw:
+                t, slab = K.stem_conv(x, kpad, want_stats=training)
             M = t.numel() // t.shape[-1]
             if training:
                 m, i, s, h = _bn_train(slab, M, (gamma, beta), bufs, mom, eps)
@@ -469,7 +490,8 @@ class StemFn(torch.autograd.Function):
             else:
                 y, idx = a, None
         ctx.save_for_backward(x, t, mb, idx, m, i, gamma, s if direct else None, h if direct else None)
-        ctx.conf = (stride, pad, pool, w.shape, kpad.shape)
+        ctx.conf = (stride, pad, pool, w.shape, (w.shape[0], 7, 7, 8) if nchw else kpad.shape)
+        ctx.ev = ev
         ctx.params = (w, gamma, beta)
         return y
 
@@ -490,6 +512,9 @@ class StemFn(torch.autograd.Function):
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
                                   bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
+        if ctx.ev is not None:
+            torch.cuda.current_stream(x.device).wait_event(ctx.ev)     # NHWC copy made on the side stream
+            ctx.ev = None
         if kshape[3] == wshape[1]:
             dw = sink.wgrad(P[0], x, dt, kshape[1], kshape[2], stride, pad)
         else:

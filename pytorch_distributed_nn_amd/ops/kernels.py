@@ -475,7 +475,7 @@ def stem_ok(x_shape, w_shape, st, pad):
     """The ImageNet stem conv (7x7 / stride 2 / pad 3, 8 padded input channels, 64 outputs) on the direct
     stem kernel (csrc/kernels/stem.hip)."""
     return (tuple(w_shape) == (64, 7, 7, 8) and x_shape[-1] == 8 and st == 2 and pad == 3
-            and _tuning.get("stem") == 1)
+            and _tuning.get("stem") >= 1)
 
 
 def stem_conv(x, w, want_stats=True):
@@ -491,6 +491,35 @@ def stem_conv(x, w, want_stats=True):
         slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
     call("pdnn_stem_conv", ptr(x), ptr(w), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
     return y, slab
+
+
+def stem_nchw_ok(x):
+    """The stem conv reading the NCHW bf16 batch directly (3 channels, even width >= 8)."""
+    return (x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.shape[3] % 2 == 0 and x.shape[3] >= 8
+            and _tuning.get("stem") == 2)
+
+
+def stem_conv_nchw(x, w32, want_stats=True):
+    """t = conv7x7/s2/p3(x) for x NCHW bf16 [N][3][H][W]; w32 = stem_weight_nchw(w) bf16 [64][7][32]."""
+    _bf16_c(x, "stem.x")
+    _bf16_c(w32, "stem.w32")
+    N, C, H, W = x.shape
+    _chk(C == 3 and tuple(w32.shape) == (64, 7, 32), "stem_conv_nchw: x [N][3][H][W], w [64][7][32]")
+    Ho, Wo = conv_out_hw(H, W, 7, 7, 2, 3)
+    y = torch.empty(N, Ho, Wo, 64, device=x.device, dtype=BF16)
+    slab = None
+    if want_stats:
+        slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
+    call("pdnn_stem_conv_nchw", ptr(x), ptr(w32), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
+    return y, slab
+
+
+def stem_weight_nchw(w):
+    """[64][3][7][7] stem weight -> bf16 [64][7 r][32]: k = c*8 + j holds w[n][c][r][j-1] (j = 1..7, c < 3),
+    zero elsewhere (the reduction order of stem_conv_nchw)."""
+    k = torch.zeros(w.shape[0], 7, 4, 8, device=w.device, dtype=BF16)
+    k[:, :, :3, 1:] = w.detach().permute(0, 2, 1, 3).to(BF16)
+    return k.view(w.shape[0], 7, 32)
 
 
 def bn_relu_maxpool(t, scale, shift):

@@ -14,7 +14,8 @@ conv3x3            1        3x3 / stride-1 convs on the LDS-halo kernel (+2.5%, 
 panel1x1           1        1x1 / stride-1 convs with K <= 128 on the pixel-panel kernel (+1.1%, r3_08)
 bwd_pre            1        BatchNorm-backward apply (dt = k*gm + A*t + B) fused into the operand loads of
                             the consuming halo 3x3 / K=64 panel data gradient, dt written once for the wgrad
-stem               1        ImageNet stem: direct 7x7/s2 conv kernel + fused BN-apply/ReLU/max-pool (stem.hip)
+stem               2        ImageNet stem (stem.hip): 0 generic conv + bn_apply + max-pool, 1 direct 7x7/s2 kernel on
+                            the NHWC copy + fused BN-apply/ReLU/max-pool, 2 the same reading the NCHW batch
 direct_grad        1        fused ops accumulate weight gradients straight into the flat arena
 opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream during the backward
 =================  =======  ===========================================================================
@@ -23,7 +24,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 1, "direct_grad": 1, "opt_overlap": 0}
+DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0}
 
 _VALUES = dict(DEFAULTS)
 

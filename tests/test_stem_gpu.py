@@ -55,3 +55,64 @@ def test_bn_relu_maxpool_bitwise(K, shape):
     y_ref, idx_ref = K.maxpool_fwd(a, 3, 2, 1)
     assert torch.equal(y, y_ref)
     assert torch.equal(idx, idx_ref)
+
+
+@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 38, 52), (1, 8, 8), (4, 64, 64), (1, 9, 10)])
+def test_stem_conv_nchw_matches_fp32(K, shape):
+    """The stem conv straight from the NCHW bf16 batch (k = channel*8 + column, border columns word-shifted)."""
+    N, H, W = shape
+    x = torch.randn(N, 3, H, W, device="cuda").to(BF)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    assert K.stem_nchw_ok(x)
+    y, slab = K.stem_conv_nchw(x, K.stem_weight_nchw(w))
+    ref = F.conv2d(x.float(), w.to(BF).float(), None, 2, 3).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-2
+    yf = y.float().reshape(-1, 64)
+    s = slab.view(-1, 2, 64).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64), (2, 224, 224)])
+def test_stem_fn_modes_agree(K, shape):
+    """StemFn (conv + BN + ReLU + max-pool, and its backward) with the NCHW kernel (tuning stem = 2), the NHWC
+    direct kernel (1) and the generic path (0), same input and upstream gradient: outputs within bf16 rounding
+    (different summation orders flip a few last bits), parameter gradients aligned."""
+    from pytorch_distributed_nn_amd import tuning
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.ops.fused_resnet import StemFn, stem_shadow
+    N, H, W = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, 3, H, W, device="cuda").to(BF)
+    w = (torch.randn(64, 3, 7, 7, device="cuda") * 0.1).requires_grad_()
+    gamma = (torch.rand(64, device="cuda") + 0.5).requires_grad_()
+    beta = (torch.randn(64, device="cuda") * 0.1).requires_grad_()
+    gy = None
+    res = {}
+    for mode in (2, 1, 0):
+        old = tuning.set("stem", mode)
+        try:
+            bufs = [torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")]
+            conf = (2, 3, True, True, 0.1, 1e-5)
+            if mode == 2:
+                y = StemFn.apply(x.contiguous(), conf, bufs, [K.stem_weight_nchw(w)], w, gamma, beta)
+            else:
+                xin = OF.nchw_to_nhwc_input(x)
+                y = StemFn.apply(xin, conf, bufs, [stem_shadow(w, 8)], w, gamma, beta)
+            if gy is None:
+                gy = torch.randn_like(y.float()).to(BF)
+            dw, dg, db = torch.autograd.grad(y, (w, gamma, beta), gy)
+            torch.cuda.synchronize()
+            res[mode] = (y.float(), dw, dg, db, bufs)
+        finally:
+            tuning.set("stem", old)
+    y0, dw0, dg0, db0, b0 = res[0]
+    assert torch.equal(res[1][0], y0)               # NHWC direct kernel: same summation order as the engine
+    for mode in (2, 1):
+        y, dw, dg, db, b = res[mode]
+        assert (y - y0).abs().max() <= 2 ** -6 * y0.abs().max()       # a few last-bit flips at most
+        assert (y != y0).float().mean() < 1e-3
+        for a, r in ((dw, dw0), (dg, dg0), (db, db0)):
+            assert torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0) > 0.999
+        torch.testing.assert_close(b[0], b0[0], rtol=1e-3, atol=1e-4)     # running statistics

@@ -1,0 +1,55 @@
+"""Per-stream occupancy of one training step from a rocprofv3 --kernel-trace CSV (no PMC: real concurrency).
+
+python tools/stream_timeline.py TRACE.csv [--steps N]
+
+Splits the trace into steps at the optimizer kernel (sgd/adam), then per stream reports busy time (union of
+its kernel intervals), the gaps between consecutive kernels, and the largest gaps (what the compute stream
+waits on); finally the top kernels by time on the critical (compute) stream."""
+import argparse
+import csv
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    ks = sorted(({"s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"]), "q": (r["Queue_Id"], r["Stream_Id"]),
+                  "n": r["Kernel_Name"]} for r in rows), key=lambda k: k["s"])
+    opt = [k for k in ks if "sgd_kernel" in k["n"] or "adam_kernel" in k["n"]]
+    if len(opt) < 2:
+        print("need >= 2 optimizer kernels")
+        return
+    # last full step: between the last two optimizer kernels
+    t0, t1 = opt[-2]["e"], opt[-1]["e"]
+    step = [k for k in ks if k["s"] >= t0 and k["e"] <= t1]
+    print(f"step {(t1 - t0) / 1e3:.1f} us, {len(step)} kernels")
+    by = defaultdict(list)
+    for k in step:
+        by[k["q"]].append(k)
+    for q, kk in sorted(by.items(), key=lambda x: -len(x[1])):
+        busy, gaps, last = 0, [], None
+        for k in kk:
+            busy += k["e"] - k["s"]
+            if last is not None and k["s"] > last["e"]:
+                gaps.append((k["s"] - last["e"], last["n"][:60], k["n"][:60]))
+            last = k
+        tg = sum(g[0] for g in gaps)
+        print(f"queue/stream {q}: {len(kk)} kernels, busy {busy / 1e3:.1f} us, gaps {tg / 1e3:.1f} us "
+              f"({len(gaps)}; median {sorted(g[0] for g in gaps)[len(gaps) // 2] / 1e3 if gaps else 0:.1f} us)")
+        for g in sorted(gaps, reverse=True)[:5]:
+            print(f"   gap {g[0] / 1e3:7.1f} us  after {g[1]}  before {g[2]}")
+    main_q = max(by, key=lambda q: len(by[q]))
+    agg = defaultdict(lambda: [0, 0])
+    for k in by[main_q]:
+        agg[k["n"][:100]][0] += k["e"] - k["s"]
+        agg[k["n"][:100]][1] += 1
+    print(f"top kernels on {main_q}:")
+    for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:a.top]:
+        print(f"  {t / 1e3:8.1f} us {c:4d}  {n}")
+
+
+if __name__ == "__main__":
+    main()
