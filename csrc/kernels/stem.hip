@@ -28,6 +28,7 @@ struct StemGeo {
     FastDiv dWo, dHo;
 };
 
+template <int EPI>
 __global__ void __launch_bounds__(256, 2) stem7_kernel(C3Args a, StemGeo g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const wimg = reinterpret_cast<bf16_t*>(smem);         // [7 r][64 n][64 k] kimg_off images
@@ -108,7 +109,7 @@ __global__ void __launch_bounds__(256, 2) stem7_kernel(C3Args a, StemGeo g) {
                     for (int fm = 0; fm < 4; ++fm) cur[ks2][fm] = nxt[ks2][fm];
             }
         }
-        c3_epilogue<64, C3_STATS>(a, acc, tile, p0, 0, wave, lane, pv);
+        c3_epilogue<64, EPI>(a, acc, tile, p0, 0, wave, lane, pv);
     }
 }
 
@@ -122,6 +123,7 @@ __global__ void __launch_bounds__(256, 2) stem7_kernel(C3Args a, StemGeo g) {
 // weight image of the NCHW stem: [7 r][64 n][32 k] bf16, 16-byte chunk q (4 per row) at q ^ ((n >> 1) & 3)
 __device__ __forceinline__ int w32_off(int n, int q) { return n * 32 + ((q ^ ((n >> 1) & 3)) << 3); }
 
+template <int EPI>
 __global__ void __launch_bounds__(256, 2) stem7n_kernel(C3Args a, StemGeo g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const wimg = reinterpret_cast<bf16_t*>(smem);         // [7 r][64 n][32 k]
@@ -203,7 +205,7 @@ __global__ void __launch_bounds__(256, 2) stem7n_kernel(C3Args a, StemGeo g) {
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], __builtin_bit_cast(bf16x8_t, v[r][fm]),
                                                                           acc[fm][fn], 0, 0, 0);
         }
-        c3_epilogue<64, C3_STATS>(a, acc, tile, p0, 0, wave, lane, pv);
+        c3_epilogue<64, EPI>(a, acc, tile, p0, 0, wave, lane, pv);
     }
 }
 
@@ -278,7 +280,7 @@ FastDiv make_fdiv_stem(uint32_t d) {
 PDNN_API int pdnn_stem_stats_rows(long P) { return (int)cdiv(P, C3_BM) * 4; }
 
 // y[P][64] = conv7x7/s2/p3(x) for x [Nimg][H][W][8] bf16 (channels zero-padded), w [64][7][7][8] bf16;
-// stats: BN partial sums (pdnn_stem_stats_rows pairs) or null.
+// stats: BN partial sums (pdnn_stem_stats_rows pairs) or null (plain epilogue: eval mode).
 PDNN_API int pdnn_stem_conv(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int Ho, int Wo,
                             float* stats, hipStream_t st) {
     if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || (long)Nimg * Ho * Wo >= (1L << 31) ||
@@ -294,12 +296,14 @@ PDNN_API int pdnn_stem_conv(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nim
     const int sm = STEM_R * 64 * 64 * 2;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stem7_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        (void)hipFuncSetAttribute((const void*)stem7_kernel<C3_STATS>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        (void)hipFuncSetAttribute((const void*)stem7_kernel<C3_PLAIN>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
         attr = true;
     }
     int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
     grid = (grid + 7) / 8 * 8;
-    hipLaunchKernelGGL(stem7_kernel, dim3(grid), dim3(256), sm, st, a, g);
+    if (stats) hipLaunchKernelGGL(stem7_kernel<C3_STATS>, dim3(grid), dim3(256), sm, st, a, g);
+    else hipLaunchKernelGGL(stem7_kernel<C3_PLAIN>, dim3(grid), dim3(256), sm, st, a, g);
     PDNN_LAUNCH_RET;
 }
 
@@ -319,7 +323,8 @@ PDNN_API int pdnn_stem_conv_nchw(const bf16_t* x, const bf16_t* w, bf16_t* y, in
     const int sm = STEM_R * 64 * 32 * 2;              // 28 KB
     int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
     grid = (grid + 7) / 8 * 8;
-    hipLaunchKernelGGL(stem7n_kernel, dim3(grid), dim3(256), sm, st, a, g);
+    if (stats) hipLaunchKernelGGL(stem7n_kernel<C3_STATS>, dim3(grid), dim3(256), sm, st, a, g);
+    else hipLaunchKernelGGL(stem7n_kernel<C3_PLAIN>, dim3(grid), dim3(256), sm, st, a, g);
     PDNN_LAUNCH_RET;
 }
 

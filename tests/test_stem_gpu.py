@@ -116,3 +116,28 @@ def test_stem_fn_modes_agree(K, shape):
         for a, r in ((dw, dw0), (dg, dg0), (db, db0)):
             assert torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0) > 0.999
         torch.testing.assert_close(b[0], b0[0], rtol=1e-3, atol=1e-4)     # running statistics
+
+
+def test_stem_eval_mode_without_statistics(K):
+    """want_stats=False (eval-mode BatchNorm) takes the plain epilogue: same output, no slab."""
+    x = torch.randn(2, 3, 40, 48, device="cuda").to(BF)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    y1, s1 = K.stem_conv_nchw(x, K.stem_weight_nchw(w))
+    y0, s0 = K.stem_conv_nchw(x, K.stem_weight_nchw(w), want_stats=False)
+    assert s0 is None and torch.equal(y0, y1)
+    xin = K.nchw_to_nhwc(x, 8)
+    kpad = torch.nn.functional.pad(w.to(BF).permute(0, 2, 3, 1), (0, 5)).contiguous()
+    z1, _ = K.stem_conv(xin, kpad)
+    z0, t0 = K.stem_conv(xin, kpad, want_stats=False)
+    assert t0 is None and torch.equal(z0, z1)
+
+
+def test_resnet50_eval_forward_uses_direct_stem(K):
+    from pytorch_distributed_nn_amd.models import build_model
+    torch.manual_seed(0)
+    m = build_model("resnet50").cuda().eval()
+    x = torch.randn(2, 3, 64, 64, device="cuda").to(BF)
+    with torch.no_grad():
+        out = m(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
