@@ -47,7 +47,7 @@ _SIGS = {
     "pdnn_tune_get": [ctypes.c_char_p],
     "pdnn_tune_list": [ctypes.c_char_p, I],
     "pdnn_tune_error": [],
-    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],

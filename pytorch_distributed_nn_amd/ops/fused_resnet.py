@@ -217,6 +217,33 @@ def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p,
     return dt.view(t.shape), ret[0], ret[1]
 
 
+class _BnLink:
+    """Hand-off between two consecutive identity Bottlenecks (i -> i+1).  Block i's output BatchNorm backward
+    starts with a reduction over its incoming gradient, which is exactly what block i+1's conv1 data
+    gradient writes: that kernel's epilogue (conv_dgrad ``bn_mask``) also multiplies its output by block i's
+    ReLU mask and reduces block i's BN3 sums against t3, so block i skips its bn_bwd_reduce pass (one read
+    of the block output's gradient and of t3) and its residual needs no mask.  Block i only uses the slab
+    when the gradient it receives is the very tensor block i+1 produced (same storage, same version: no
+    other consumer's gradient was added); otherwise it re-masks and reduces as usual, which is exact
+    because re-applying the mask is idempotent.  The gradient returned for a block output is therefore
+    pre-multiplied by its ReLU mask (the same parameter gradients; an intermediate's ``.grad`` differs where
+    the ReLU is inactive)."""
+
+    __slots__ = ("t3", "mean", "invstd", "mask", "slab", "ptr", "version")
+
+    def __init__(self, t3, mean, invstd, mask):
+        self.t3, self.mean, self.invstd, self.mask = t3, mean, invstd, mask
+        self.slab = None
+        self.ptr = self.version = None
+
+    def take(self, g):
+        """The reduced BN slab if ``g`` is block i+1's untouched output gradient, else None."""
+        slab, self.slab = self.slab, None
+        if slab is not None and g.data_ptr() == self.ptr and g._version == self.version:
+            return slab
+        return None
+
+
 def _krsc_grad(dw):
     """fp32 [K][R][S][C] -> [K][C][R][S] view with channels_last strides (the parameter's layout)."""
     return dw.permute(0, 3, 1, 2)
@@ -278,6 +305,14 @@ class BottleneckFn(torch.autograd.Function):
             td = md = idd = None
             out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True, want_mask=training)
         out = out.view(t3.shape)
+        # hand-offs with the neighbouring identity blocks (tuning bn_link; _BnLink)
+        ctx.link_in = ctx.link_out = None
+        if training and not down and tuning.get("bn_link") and x.is_cuda:
+            link = getattr(x, "_pdnn_bn_link", None)
+            if link is not None and K.resbn_ok(tuple(t1.shape), tuple(k1.shape)):
+                ctx.link_in = link                  # this block's conv1 dgrad reduces the block below's BN3
+            ctx.link_out = _BnLink(t3, m3, i3, mb)
+            out._pdnn_bn_link = ctx.link_out
         # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
         ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2)
@@ -299,22 +334,32 @@ class BottleneckFn(torch.autograd.Function):
         P = ctx.params
         ctx.params = None
         sink = _Sink(gout.device)
-        slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
-                                             x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
-        (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
-        if down:
-            (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
-            dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
-                                         x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
-                                         dbeta2=dbd)
-            gres = None
-        elif MASKED_RES:
-            # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
-            # materialised here: one activation-sized write less per block
-            dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb)
-            gres = gout
+        link_in, link_out = ctx.link_in, ctx.link_out
+        ctx.link_in = ctx.link_out = None
+        slab3 = link_out.take(gout) if link_out is not None else None
+        gres_mask = mb if MASKED_RES else None
+        if slab3 is not None:
+            # the block above masked gout and reduced this BN's sums in its conv1 data gradient (_BnLink)
+            (dg3, db3), (rg3, rb3) = sink.bn(slab3, slab3.shape[0] // 2, P[7], P[8])
+            dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=0)
+            gres, gres_mask = gout, None
         else:
-            dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
+            slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
+                                                 x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
+            (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
+            if down:
+                (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
+                dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
+                                             x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
+                                             dbeta2=dbd)
+                gres = None
+            elif MASKED_RES:
+                # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
+                # materialised here: one activation-sized write less per block
+                dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb)
+                gres = gout
+            else:
+                dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
         if a2 is not None:
@@ -351,9 +396,14 @@ class BottleneckFn(torch.autograd.Function):
             # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
             # reach, so no zero-filled full-size buffer and no extra full read/write pass
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
+        elif link_in is not None:
+            # also the block below's BN3 reduction (its mask applied to dx): see _BnLink
+            dx, lslab = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1,
+                                     bn=(link_in.t3, link_in.mean, link_in.invstd, None, None),
+                                     bn_mask=link_in.mask)
+            link_in.slab, link_in.ptr, link_in.version = lslab, dx.data_ptr(), dx._version
         else:
-            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=mb if MASKED_RES else None,
-                              pre=pre1)
+            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1)
         if pre1 is not None:
             dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)       # dt1 written by conv1's data gradient
         grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3) + ((dwd, rgd, rbd) if down else ())

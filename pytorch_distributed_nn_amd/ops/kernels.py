@@ -219,9 +219,10 @@ def _pre_args(pre, x):
     return tuple(ptr(v) for v in (t, mean, inv, gamma, dg, db, dt_out))
 
 
-def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None):
+def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None, bn_mask=None):
     """y[P][N] = x[P][K] . w[N][K]^T on the panel kernel; epilogues as conv3x3 / conv_dgrad; pre: the
-    BN-backward operand prologue (_pre_args)."""
+    BN-backward operand prologue (_pre_args); bn_mask: the residual + BN-backward-reduce epilogue
+    (conv_dgrad's ``bn_mask``)."""
     P, Kc = x2d.shape
     N = w2d.shape[0]
     y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
@@ -232,7 +233,7 @@ def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, 
     if bn is not None:
         t, mean, inv, msc, msh = bn
     call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), ptr(bn_mask), *_pre_args(pre, x2d), stream())
     return y, slab
 
 
@@ -303,7 +304,17 @@ def dgrad_pre_ok(dy_shape, w_shape, st, pad):
             or (_panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None):
+def resbn_ok(dy_shape, w_shape):
+    """Whether conv_dgrad takes ``bn_mask=`` (the residual epilogue that also reduces the BatchNorm backward
+    of the block below): 1x1 / stride-1 data gradients on the A-stationary kernel with K = 64 / 128 (at K = 256
+    the extra epilogue operands push that kernel into scratch)."""
+    N, Ho, Wo, K = dy_shape
+    Kw, R, S, C = w_shape
+    return (K in (64, 128) and C % 64 == 0 and R == 1 and S == 1
+            and _panel_ok(N * Ho * Wo, K, C, R, S, 1, 0))
+
+
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None, bn_mask=None):
     """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
     conv only the pixels its taps reach are touched, the others keep ``res``).
 
@@ -317,7 +328,12 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
 
     pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out): ``dy`` is the masked gradient gm of a BatchNorm
     whose backward apply (bn_bwd_apply mode 0) runs inside this conv's operand loads; dt_out (optional)
-    receives that dt for the weight gradient.  Only where dgrad_pre_ok()."""
+    receives that dt for the weight gradient.  Only where dgrad_pre_ok().
+
+    bn_mask (with res and bn = (t, mean, invstd, None, None)): the output is the gradient of the BLOCK BELOW's
+    pre-ReLU sum, gm = (dx + res * res_mask) * bn_mask (bn_mask: that block's output ReLU bits), and the slab
+    holds the partial sums of gm and gm * (t - mean) * invstd of its BatchNorm (t = its BN input): its
+    bn_bwd_reduce pass runs here.  Returns (gm, slab).  Only where resbn_ok()."""
     _bf16_c(dy, "conv_dgrad.dy")
     N, H, W, C = x_shape
     _bf16_c(w, "conv_dgrad.w")
@@ -338,6 +354,14 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         _chk(res is not None and st == 1 and res_mask.dtype == torch.uint8 and res_mask.is_contiguous()
              and res_mask.numel() * 8 == N * H * W * C and (out is None or out.data_ptr() != res.data_ptr()),
              "conv_dgrad: res_mask needs res, stride 1, uint8 [N*H*W][C/8], out not aliasing res")
+    if bn_mask is not None:
+        _chk(res is not None and bn is not None and out is None and st == 1 and pad == 0
+             and resbn_ok(dy.shape, w.shape) and bn_mask.dtype == torch.uint8 and bn_mask.is_contiguous()
+             and bn_mask.numel() * 8 == N * H * W * C, "conv_dgrad: bn_mask needs res, bn, resbn_ok shapes")
+        y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)), res=res.view(-1, C),
+                                res_mask=res_mask, bn=(bn[0].view(-1, C), bn[1], bn[2], None, None), pre=pre,
+                                bn_mask=bn_mask)
+        return y.view(N, H, W, C), slab
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
         y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask, pre=pre)
@@ -376,6 +400,13 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
         out = torch.zeros(K, R, S, C, device=x.device, dtype=F32)
     _chk(out.shape == (K, R, S, C) and out.is_contiguous() and out.dtype == F32, "conv_wgrad: out [K][R][S][C] fp32")
     sc, sh = pro if pro is not None else (None, None)
+    P = N * H * W
+    if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _tuning.get("wgrad1x1_pp_pix")
+            and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
+        # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs): the short
+        # reductions of ResNet stages 3-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33: 67 -> 62 us, 64 -> 47 us)
+        pp_wgrad(dy.view(P, K), x.view(P, C), out.view(K, C))
+        return out
     call("pdnn_conv_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
          stream())
     return out

@@ -18,13 +18,20 @@ stem               2        ImageNet stem (stem.hip): 0 generic conv + bn_apply 
                             the NHWC copy + fused BN-apply/ReLU/max-pool, 2 the same reading the NCHW batch
 direct_grad        1        fused ops accumulate weight gradients straight into the flat arena
 opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream during the backward
+bn_link            0        consecutive identity Bottlenecks: the upper block's conv1 data gradient also masks its
+                            output and reduces the lower block's BN3 backward sums (no bn_bwd_reduce pass there);
+                            off: 10,209-10,237 vs 10,285-10,309 img/s (gpurun_out/r3_35)
+wgrad1x1_pp_pix    50176    1x1 / stride-1 weight gradients with at most this many pixels on the ping-pong
+                            engine (ResNet-50 stages 3-4 at bs 256; the longer stage-1/2 reductions lose there,
+                            tools/bench_wgrad1x1.py); 0 = off
 =================  =======  ===========================================================================
 """
 from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0}
+DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
+            "wgrad1x1_pp_pix": 50176}
 
 _VALUES = dict(DEFAULTS)
 

@@ -110,9 +110,10 @@ def test_side_stream_wgrad_matches_serial(monkeypatch, flat):
     g = torch.Generator().manual_seed(1)
     data = [(torch.randn(4, 3, 96, 96, generator=g).cuda().to(torch.bfloat16), torch.randint(0, 1000, (4,), generator=g).cuda())
             for _ in range(2)]
+    from pytorch_distributed_nn_amd import tuning
     grads = []
-    for side, m, o in zip(("1", "0", "0"), ms, opts):
-        monkeypatch.setenv("PDNN_SIDE_WGRAD", side)
+    for side, m, o in zip((1, 0, 0), ms, opts):
+        old = tuning.set("side_wgrad", side)
         for x, y in data:
             if o is not None:
                 o.zero_grad()
@@ -120,6 +121,7 @@ def test_side_stream_wgrad_matches_serial(monkeypatch, flat):
                 m.zero_grad()
             OF.cross_entropy(m(x), y).backward()
         torch.cuda.synchronize()
+        tuning.set("side_wgrad", old)
         grads.append(torch.cat([p.grad.float().flatten() for p in m.parameters()]))
     floor = rel(grads[2], grads[1])          # serial vs serial: fp32 atomics ordering
     r = rel(grads[0], grads[1])
