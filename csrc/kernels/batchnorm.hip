@@ -208,6 +208,128 @@ __global__ void __launch_bounds__(NT) bn_slab_final_kernel(const float* __restri
     }
 }
 
+// One-launch finalize: the level-1 blocks of a column hand their partial rows to the column's LAST-arriving
+// block, which sums them and runs the epilogue (cdna_hip_programming.md §6 Guideline 16, counter form): the
+// partial rows are stored write-through (sc1, so no release fence and no L2 write-back of the conv output
+// that just filled it -- the cost that sank a __threadfence() version), the storing wave drains them
+// (vmcnt(0)) before one lane draws a ticket with an agent-scope atomic, and the last arriver acquires once
+// and reads the rows with sc1 loads.  `cnt` holds one zeroed counter per column; the last arriver puts it
+// back to zero, so a pool of counters is reused across calls without a memset launch.
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ void st_sc1(float* p, float4 v) {     // 16 bytes as two 8-byte sc1 stores
+    gu64* g = (gu64*)p;
+    __hip_atomic_store(g, (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld_sc1(const float* p) {
+    const gu64* g = (const gu64*)p;
+    const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float4(__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
+                       __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32)));
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(NT) bn_slab_fused_kernel(const float* __restrict__ slab, int rows, int C,
+                                                           float* work, unsigned* cnt, Epi epi) {
+    const int col = blockIdx.x, RB = gridDim.y, y = blockIdx.y;
+    const int ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
+    const int c0 = col * 64 + ch * 4;
+    const bool on = c0 < C;
+    __shared__ double redd[2][16][64];
+    float4* red = reinterpret_cast<float4*>(&redd[0][0][0]);    // level-1 view: [2][16][16] float4
+    __shared__ int last;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+    if (on) {
+        const int stride = RB * 16;
+        int r = y * 16 + lane;
+        for (; r + 3 * stride < rows; r += 4 * stride) {
+            float4 a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + j * stride)) * C + c0);
+                b[j] = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + j * stride) + 1) * C + c0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s.x += a[j].x; s.y += a[j].y; s.z += a[j].z; s.w += a[j].w;
+                q.x += b[j].x; q.y += b[j].y; q.z += b[j].z; q.w += b[j].w;
+            }
+        }
+        for (; r < rows; r += stride) {
+            const float4 a0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r) * C + c0);
+            const float4 b0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r + 1) * C + c0);
+            s.x += a0.x; s.y += a0.y; s.z += a0.z; s.w += a0.w;
+            q.x += b0.x; q.y += b0.y; q.z += b0.z; q.w += b0.w;
+        }
+    }
+    red[lane * 16 + ch] = s;
+    red[256 + lane * 16 + ch] = q;
+    __syncthreads();
+    if (threadIdx.x < 64) {                  // wave 0: lanes 0..15 publish this block's row, lane 0 draws the ticket
+        if (lane == 0 && on) {
+            float4 a = red[ch], b = red[256 + ch];
+            for (int k = 1; k < 16; ++k) {
+                const float4 u = red[k * 16 + ch], v = red[256 + k * 16 + ch];
+                a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+                b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+            }
+            st_sc1(work + (long)(2 * y) * C + c0, a);
+            st_sc1(work + (long)(2 * y + 1) * C + c0, b);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the storing wave drains its sc1 stores
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add((gu32*)(cnt + col), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = t == (unsigned)(RB - 1);
+        }
+    }
+    __syncthreads();                          // also: every wave is done with the level-1 LDS view
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    double sd[4] = {0, 0, 0, 0}, qd[4] = {0, 0, 0, 0};
+    if (on) {
+        int r = lane;
+        for (; r + 48 < RB; r += 64) {
+            float4 a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = ld_sc1(work + (long)(2 * (r + 16 * j)) * C + c0);
+                b[j] = ld_sc1(work + (long)(2 * (r + 16 * j) + 1) * C + c0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sd[0] += a[j].x; sd[1] += a[j].y; sd[2] += a[j].z; sd[3] += a[j].w;
+                qd[0] += b[j].x; qd[1] += b[j].y; qd[2] += b[j].z; qd[3] += b[j].w;
+            }
+        }
+        for (; r < RB; r += 16) {
+            const float4 a = ld_sc1(work + (long)(2 * r) * C + c0);
+            const float4 b = ld_sc1(work + (long)(2 * r + 1) * C + c0);
+            sd[0] += a.x; sd[1] += a.y; sd[2] += a.z; sd[3] += a.w;
+            qd[0] += b.x; qd[1] += b.y; qd[2] += b.z; qd[3] += b.w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { redd[0][lane][ch * 4 + j] = sd[j]; redd[1][lane][ch * 4 + j] = qd[j]; }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int c = col * 64 + threadIdx.x;
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { a += redd[0][k][threadIdx.x]; b += redd[1][k][threadIdx.x]; }
+        if (c < C) epi(c, a, b);
+        if (threadIdx.x == 0) __hip_atomic_store((gu32*)(cnt + col), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 inline unsigned fin_rows(int rows) {       // level-1 blocks per column: >= 4 slab rows per thread
     int rb = rows / (16 * 4);
     if (rows <= 64) return 0;                // few rows: level 2 reads the slab directly
@@ -534,14 +656,20 @@ PDNN_API int pdnn_bn_fin_work(int rows, int C) {
 #endif
 }
 
-// work: >= pdnn_bn_fin_work(rows, C) floats of scratch for the level-1 reduction
+// work: >= pdnn_bn_fin_work(rows, C) floats of scratch for the level-1 reduction; cnt (optional): C/64 zeroed
+// counters -> one launch (bn_slab_fused_kernel), left zeroed
 PDNN_API int pdnn_bn_finalize(const float* slab, int rows, int C, double L, float eps, float momentum,
                               const float* gamma, const float* beta, float* run_mean, float* run_var,
                               float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
-                              float* work, hipStream_t st) {
+                              float* work, unsigned* cnt, hipStream_t st) {
 #if PDNN_BN_WIDE_FIN
     const FinFwd epi{L, eps, momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out};
     const unsigned rb = fin_rows(rows);
+    if (rb && cnt) {
+        hipLaunchKernelGGL(bn_slab_fused_kernel<FinFwd>, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work,
+                           cnt, epi);
+        PDNN_LAUNCH_RET;
+    }
     if (rb) hipLaunchKernelGGL(bn_slab_level1_kernel, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work);
     hipLaunchKernelGGL(bn_slab_final_kernel<FinFwd>, dim3((C + 63) / 64), dim3(NT), 0, st, rb ? work : slab,
                        rb ? (int)rb : rows, C, epi);
@@ -611,10 +739,16 @@ PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C,
 // dgamma/dbeta of this backward (consumed by bn_bwd_apply); gacc/bacc (optional): also added into the
 // parameters' gradient accumulators.
 PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dgamma, float* dbeta,
-                                  int accumulate, float* work, float* gacc, float* bacc, hipStream_t st) {
+                                  int accumulate, float* work, float* gacc, float* bacc, unsigned* cnt,
+                                  hipStream_t st) {
 #if PDNN_BN_WIDE_FIN
     const FinBwd epi{dgamma, dbeta, accumulate, gacc, bacc};
     const unsigned rb = fin_rows(rows);
+    if (rb && cnt) {
+        hipLaunchKernelGGL(bn_slab_fused_kernel<FinBwd>, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work,
+                           cnt, epi);
+        PDNN_LAUNCH_RET;
+    }
     if (rb) hipLaunchKernelGGL(bn_slab_level1_kernel, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work);
     hipLaunchKernelGGL(bn_slab_final_kernel<FinBwd>, dim3((C + 63) / 64), dim3(NT), 0, st, rb ? work : slab,
                        rb ? (int)rb : rows, C, epi);

@@ -418,6 +418,29 @@ def _fin_work(rows, C, device):
     return torch.empty(n, device=device, dtype=F32) if n > 0 else None
 
 
+# Zeroed counters for the one-launch BN finalize (batchnorm.hip bn_slab_fused_kernel): each call takes the
+# next C/64 slots of a per-device ring; the kernel's last-arriving block puts its counters back to zero, so
+# no memset is needed per call.  A slot comes round again only after _CNT_SLOTS / (C/64) calls (thousands of
+# launches, several training steps), long after the kernel that last used it finished on its stream.
+_CNT_SLOTS = 1 << 16
+_CNT = {}
+
+
+def _fin_counters(C, device):
+    if not _tuning.get("bn_fused_fin"):
+        return None
+    key = device.index
+    ent = _CNT.get(key)
+    if ent is None:
+        ent = _CNT[key] = [torch.zeros(_CNT_SLOTS, device=device, dtype=torch.int32), 0]
+    buf, pos = ent
+    n = (C + 63) // 64
+    if pos + n > _CNT_SLOTS:
+        pos = 0
+    ent[1] = pos + n
+    return buf[pos:pos + n]
+
+
 def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
     C = slab.shape[1]
     mean = torch.empty(C, device=slab.device, dtype=F32)
@@ -425,8 +448,9 @@ def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
     scale = torch.empty_like(mean)
     shift = torch.empty_like(mean)
     work = _fin_work(rows, C, slab.device)
+    cnt = _fin_counters(C, slab.device) if work is not None else None
     call("pdnn_bn_finalize", ptr(slab), rows, C, float(L), float(eps), float(momentum), ptr(gamma), ptr(beta),
-         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(work), stream())
+         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(work), ptr(cnt), stream())
     return mean, invstd, scale, shift
 
 
@@ -482,9 +506,10 @@ def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=N
         dgamma = torch.empty(C, device=slab.device, dtype=F32)
         dbeta = torch.empty_like(dgamma)
     work = _fin_work(rows, C, slab.device)
+    cnt = _fin_counters(C, slab.device) if work is not None else None
     ga, ba = acc if acc is not None else (None, None)
     call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), ptr(ga),
-         ptr(ba), stream())
+         ptr(ba), ptr(cnt), stream())
     return dgamma, dbeta
 
 

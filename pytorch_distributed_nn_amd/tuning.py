@@ -21,6 +21,8 @@ opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream duri
 bn_link            0        consecutive identity Bottlenecks: the upper block's conv1 data gradient also masks its
                             output and reduces the lower block's BN3 backward sums (no bn_bwd_reduce pass there);
                             off: 10,209-10,237 vs 10,285-10,309 img/s (gpurun_out/r3_35)
+bn_fused_fin       1        BatchNorm slab finalize in one launch (level-1 blocks hand their rows to the last
+                            arriver through a counter, batchnorm.hip bn_slab_fused_kernel) instead of two
 wgrad1x1_pp_pix    50176    1x1 / stride-1 weight gradients with at most this many pixels on the ping-pong
                             engine (ResNet-50 stages 3-4 at bs 256; the longer stage-1/2 reductions lose there,
                             tools/bench_wgrad1x1.py); 0 = off
@@ -31,7 +33,7 @@ from __future__ import annotations
 import os
 
 DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
-            "wgrad1x1_pp_pix": 50176}
+            "wgrad1x1_pp_pix": 50176, "bn_fused_fin": 1}
 
 _VALUES = dict(DEFAULTS)
 

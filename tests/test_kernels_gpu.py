@@ -149,12 +149,21 @@ def test_conv_wgrad(K, shape, pro):
     assert rel(dw, w.grad.permute(0, 2, 3, 1)) < 5e-3
 
 
-@pytest.mark.parametrize("rows,C", [(1, 64), (7, 8), (64, 200), (65, 64), (1000, 2048), (12544, 64), (3137, 1024)])
-def test_bn_slab_finalize(K, rows, C):
-    """Wide-grid slab finalize (level-1 pass + per-column fp64 epilogue) against fp64 torch sums;
-    three calls in a row (no state carried between calls)."""
+@pytest.fixture(params=[1, 0], ids=["fused-fin", "two-launch-fin"])
+def fused_fin(request):
+    from pytorch_distributed_nn_amd import tuning
+    old = tuning.set("bn_fused_fin", request.param)
+    yield request.param
+    tuning.set("bn_fused_fin", old)
+
+
+@pytest.mark.parametrize("rows,C", [(1, 64), (7, 8), (64, 200), (65, 64), (129, 64), (1000, 2048), (12544, 64),
+                                    (3137, 1024), (40000, 256)])
+def test_bn_slab_finalize(K, rows, C, fused_fin):
+    """Wide-grid slab finalize (level-1 pass + per-column fp64 epilogue; one launch with the counter hand-off
+    or two) against fp64 torch sums; several calls in a row (the hand-off's counters must come back zeroed)."""
     L = float(rows * 64)
-    for it in range(3):
+    for it in range(4):
         slab = torch.rand(rows, 2, C, device="cuda") * 64
         slab[:, 1] += slab[:, 0] ** 2 / 64 + 1.0            # sum of squares consistent with a positive var
         slab = slab.reshape(rows * 2, C)
@@ -174,6 +183,28 @@ def test_bn_slab_finalize(K, rows, C):
         assert torch.allclose(db.double(), sd[0] + 2.0, rtol=1e-5)
         assert torch.allclose(dg.double(), sd[1] + 1.0, rtol=1e-5)
         assert torch.allclose(acc[0].double(), sd[1], rtol=1e-5) and torch.allclose(acc[1].double(), sd[0], rtol=1e-5)
+
+
+def test_bn_fused_finalize_two_streams_many_calls(K):
+    """200 one-launch finalizes alternating between two streams with no synchronisation between them (the
+    counter ring hands each call its own counters), every result against fp64 sums."""
+    from pytorch_distributed_nn_amd import tuning
+    assert tuning.get("bn_fused_fin") == 1
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    streams[1].wait_stream(streams[0])
+    outs = []
+    for i in range(200):
+        rows, C = (3136, 256) if i % 3 else (12544, 64)
+        st = streams[i % 2]
+        with torch.cuda.stream(st):
+            slab = torch.rand(rows * 2, C, device="cuda")
+            dg, db = K.bn_bwd_finalize(slab, rows)
+        outs.append((slab, dg, db))
+    torch.cuda.synchronize()
+    for slab, dg, db in outs:
+        rows, C = slab.shape[0] // 2, slab.shape[1]
+        sd = slab.view(rows, 2, C).double().sum(0)
+        assert torch.allclose(db.double(), sd[0], rtol=1e-5) and torch.allclose(dg.double(), sd[1], rtol=1e-5)
 
 
 def test_bn_train_fwd_bwd(K):
