@@ -886,6 +886,31 @@ PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
     return best;
 }
 
+// K-splits for the long-reduction weight gradients of 1x1 convs (K = pixels, 10^4..10^5 slices, few output
+// tiles): minimise  max(latency term, operand-traffic term) + slab term  [us], fitted to the ResNet-50 stage-2..4
+// shapes (tools/bench_wgrad1x1.py, gpurun_out/r3_38): ~0.65 us per slice per item round plus ~10 slices of
+// per-item overhead, operand bytes at ~6 TB/s, fp32 slab written and re-read at ~4 TB/s; up to 256 splits.
+PDNN_API int pdnn_pp_wgrad_splits_long(int M, int N, int K) {
+    using namespace pg;
+    GemmArgs a{};
+    a.M = M; a.N = N; a.K = K;
+    const int bn = pick_bn(a, false);
+    const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
+    const int cus = device_cus();
+    const int nsl = K / PP_SK;
+    // operand bytes: a tile wider than the matrix re-reads clamped rows from L2, so count the real extent
+    const double mem = (double)tiles * nsl * ((M < PP_BM ? M : PP_BM) + (N < bn ? N : bn)) * 64 / 6e6;
+    int best = 1;
+    double bt = 1e300;
+    for (int s = 1; s <= 256; ++s) {
+        if (nsl % s || (s > 1 && nsl / s < 16)) continue;
+        const double lat = (double)cdiv(tiles * s, cus) * (nsl / s + 10) * 0.65;
+        const double t = (lat > mem ? lat : mem) + (s > 1 ? 2.0 * s * M * N * 4 / 4e6 : 0.0);
+        if (t < bt) { bt = t; best = s; }
+    }
+    return best;
+}
+
 // phase trace buffer for the next pp launches (null = off): 2 * grid * 64 int64 timestamps (100 MHz)
 PDNN_API void pdnn_set_pp_trace(long long* buf) { pg::g_pp_trace = buf; }
 

@@ -60,6 +60,7 @@ _SIGS = {
     "pdnn_set_pp_trace": [P],
     "pdnn_pp_wgrad": [P, L, P, L, P, L, I, I, I, F, P, I, P],
     "pdnn_pp_wgrad_splits": [I, I, I],
+    "pdnn_pp_wgrad_splits_long": [I, I, I],
     "pdnn_pp_gemm_nt_splitk": [P, L, P, L, P, L, I, I, I, P, I, P],
     "pdnn_pp_splitk_splits": [I, I, I],
     "pdnn_transpose_bf16": [P, L, P, L, I, I, P],

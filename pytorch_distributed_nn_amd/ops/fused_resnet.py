@@ -193,12 +193,33 @@ def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, si
     return dt, dgamma, dbeta
 
 
-def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p):
+def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, wprep=None):
     """dgrad with the fused BN-backward epilogue, stopped before the apply pass: -> (gm, dgamma, dbeta,
     returned grads).  The apply then runs inside the next data gradient's operand loads (_dgrad_pre)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh))
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     return gm, dgamma, dbeta, ret
+
+
+def _prep_dgrad_weights(x, specs):
+    """Make the data gradients' transformed weights (K.dgrad_weight: flipped 3x3, transposed 1x1) in the
+    forward, on the side stream, which is idle there: the backward then finds them ready instead of running
+    ~30 small transform kernels on its critical path.  specs: [(dy_shape, w, x_shape, st, pad)].
+    -> (list of weights or None, event the backward waits on) or None without a side stream."""
+    side = _side_stream(x.device)
+    if side is None or not tuning.get("wprep"):
+        return None
+    main = torch.cuda.current_stream(x.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        ws = [K.dgrad_weight(*sp) for sp in specs]
+        ev = torch.cuda.Event()
+        ev.record(side)
+    for sp, w in zip(specs, ws):
+        sp[1].record_stream(side)
+        if w is not None:
+            w.record_stream(main)
+    return ws, ev
 
 
 def _pre_ok(t, wk, st, pad):
@@ -207,10 +228,10 @@ def _pre_ok(t, wk, st, pad):
     return tuning.get("bwd_pre") == 1 and K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
 
 
-def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p):
+def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None):
     """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
     one apply pass produces dt (the gradient w.r.t. the BN input t)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh))
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     C = t.shape[-1]
     dt, _, _ = K.bn_bwd_apply(gm.view(-1, C), t.view(-1, C), mean, inv, gamma, dgamma, dbeta, mode=0)
@@ -313,6 +334,11 @@ class BottleneckFn(torch.autograd.Function):
                 ctx.link_in = link                  # this block's conv1 dgrad reduces the block below's BN3
             ctx.link_out = _BnLink(t3, m3, i3, mb)
             out._pdnn_bn_link = ctx.link_out
+        ctx.wprep = None
+        if training:
+            ctx.wprep = _prep_dgrad_weights(x, [(tuple(t3.shape), k3, tuple(t2.shape), 1, 0),
+                                                (tuple(t2.shape), k2, tuple(t1.shape), stride, 1),
+                                                (tuple(t1.shape), k1, tuple(x.shape), 1, 0)])
         # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
         ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2)
@@ -336,6 +362,11 @@ class BottleneckFn(torch.autograd.Function):
         sink = _Sink(gout.device)
         link_in, link_out = ctx.link_in, ctx.link_out
         ctx.link_in = ctx.link_out = None
+        w3p = w2p = w1p = None
+        if ctx.wprep is not None:
+            (w3p, w2p, w1p), ev = ctx.wprep
+            torch.cuda.current_stream(gout.device).wait_event(ev)
+            ctx.wprep = None
         slab3 = link_out.take(gout) if link_out is not None else None
         gres_mask = mb if MASKED_RES else None
         if slab3 is not None:
@@ -369,15 +400,16 @@ class BottleneckFn(torch.autograd.Function):
         bn1 = (t1, m1, i1, s1, h1)
         if _pre_ok(t2, k2, stride, 1):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad
-            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5])
+            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p)
             dt2 = torch.empty_like(t2)
-            gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2))
+            gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2),
+                                      wprep=w2p)
             del gm2
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
         else:
-            dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5])
+            dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p)
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
-            gm1, slab1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1, bn=bn1)
+            gm1, slab1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1, bn=bn1, wprep=w2p)
         (dg1, db1), (rg1, rb1) = sink.bn(slab1, slab1.shape[0] // 2, P[1], P[2])
         pre1 = None
         if _pre_ok(t1, k1, 1, 0):
@@ -392,7 +424,7 @@ class BottleneckFn(torch.autograd.Function):
         if down:
             dtd = dtd.view(td.shape)
             dwd = sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
-            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, pre=pre1)
+            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, pre=pre1, wprep=w1p)
             # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
             # reach, so no zero-filled full-size buffer and no extra full read/write pass
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
@@ -400,10 +432,11 @@ class BottleneckFn(torch.autograd.Function):
             # also the block below's BN3 reduction (its mask applied to dx): see _BnLink
             dx, lslab = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1,
                                      bn=(link_in.t3, link_in.mean, link_in.invstd, None, None),
-                                     bn_mask=link_in.mask)
+                                     bn_mask=link_in.mask, wprep=w1p)
             link_in.slab, link_in.ptr, link_in.version = lslab, dx.data_ptr(), dx._version
         else:
-            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1)
+            dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1,
+                              wprep=w1p)
         if pre1 is not None:
             dw1 = sink.wgrad(P[0], x, dt1, 1, 1, 1, 0)       # dt1 written by conv1's data gradient
         grads = (dw1, rg1, rb1, dw2, rg2, rb2, dw3, rg3, rb3) + ((dwd, rgd, rbd) if down else ())

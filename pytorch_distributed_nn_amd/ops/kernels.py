@@ -314,7 +314,25 @@ def resbn_ok(dy_shape, w_shape):
             and _panel_ok(N * Ho * Wo, K, C, R, S, 1, 0))
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None, bn_mask=None):
+def dgrad_weight(dy_shape, w, x_shape, st, pad, bn_mask=False):
+    """The transformed weight conv_dgrad builds on entry for this data gradient (tap-flipped transposed 3x3
+    weight for the halo kernel, transposed 1x1 weight for the panel / A-stationary kernel), or None when its
+    route takes the weight as is.  Pass it back as ``conv_dgrad(..., wprep=...)``: the fused blocks make it
+    in the forward on the side stream, off the backward's critical path."""
+    N, Ho, Wo, K = dy_shape
+    _, H, W, C = x_shape
+    Kw, R, S, C2 = w.shape
+    if bn_mask:
+        return transpose_bf16(w.view(K, C))
+    if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
+        return conv3x3_flip(w)
+    if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad):
+        return transpose_bf16(w.view(K, C))
+    return None
+
+
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None, bn_mask=None,
+               wprep=None):
     """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
     conv only the pixels its taps reach are touched, the others keep ``res``).
 
@@ -329,6 +347,8 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
     pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out): ``dy`` is the masked gradient gm of a BatchNorm
     whose backward apply (bn_bwd_apply mode 0) runs inside this conv's operand loads; dt_out (optional)
     receives that dt for the weight gradient.  Only where dgrad_pre_ok().
+
+    wprep: dgrad_weight()'s result for this call (else it is made here).
 
     bn_mask (with res and bn = (t, mean, invstd, None, None)): the output is the gradient of the BLOCK BELOW's
     pre-ReLU sum, gm = (dx + res * res_mask) * bn_mask (bn_mask: that block's output ReLU bits), and the slab
@@ -358,17 +378,18 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         _chk(res is not None and bn is not None and out is None and st == 1 and pad == 0
              and resbn_ok(dy.shape, w.shape) and bn_mask.dtype == torch.uint8 and bn_mask.is_contiguous()
              and bn_mask.numel() * 8 == N * H * W * C, "conv_dgrad: bn_mask needs res, bn, resbn_ok shapes")
-        y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)), res=res.view(-1, C),
-                                res_mask=res_mask, bn=(bn[0].view(-1, C), bn[1], bn[2], None, None), pre=pre,
-                                bn_mask=bn_mask)
+        y, slab = conv1x1_panel(dy.view(-1, K), wprep if wprep is not None else transpose_bf16(w.view(K, C)),
+                                res=res.view(-1, C), res_mask=res_mask, bn=(bn[0].view(-1, C), bn[1], bn[2], None, None),
+                                pre=pre, bn_mask=bn_mask)
         return y.view(N, H, W, C), slab
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
-        y, slab = conv3x3(dy, conv3x3_flip(w), res=res, bn=bn, out=out, res_mask=res_mask, pre=pre)
+        y, slab = conv3x3(dy, wprep if wprep is not None else conv3x3_flip(w), res=res, bn=bn, out=out,
+                          res_mask=res_mask, pre=pre)
         return (y, slab) if bn is not None else y
     if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
         # dx[P][C] = dy[P][K] . W[K][C]: the panel kernel with the transposed weight W^T [C][K]
-        y, slab = conv1x1_panel(dy.view(-1, K), transpose_bf16(w.view(K, C)),
+        y, slab = conv1x1_panel(dy.view(-1, K), wprep if wprep is not None else transpose_bf16(w.view(K, C)),
                                 res=None if res is None else res.view(-1, C), res_mask=res_mask,
                                 bn=None if bn is None else (bn[0].view(-1, C),) + tuple(bn[1:]),
                                 out=None if out is None else out.view(-1, C), pre=pre)
@@ -403,9 +424,9 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     P = N * H * W
     if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _tuning.get("wgrad1x1_pp_pix")
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
-        # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs): the short
-        # reductions of ResNet stages 3-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33: 67 -> 62 us, 64 -> 47 us)
-        pp_wgrad(dy.view(P, K), x.view(P, C), out.view(K, C))
+        # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs, split count from
+        # the long-reduction model): ResNet stages 2-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33, r3_38)
+        pp_wgrad(dy.view(P, K), x.view(P, C), out.view(K, C), splits=lib().pdnn_pp_wgrad_splits_long(K, C, P))
         return out
     call("pdnn_conv_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
          stream())

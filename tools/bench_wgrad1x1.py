@@ -11,6 +11,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_nn_amd import tuning              # noqa: E402
 from pytorch_distributed_nn_amd.ops import kernels as K   # noqa: E402
 
 STAGES = [(56, 64), (28, 128), (14, 256), (7, 512)]
@@ -40,11 +41,13 @@ def main():
             flop = 2.0 * M * cin * ko
             out = torch.zeros(ko, 1, 1, cin, device=d)
             row = {"H": H, "conv": name, "Ko": ko, "C": cin}
+            old = tuning.set("wgrad1x1_pp_pix", 0)          # the 128-row implicit-GEMM engine
             row["reg_us"] = timeit(lambda: K.conv_wgrad(x, dy, 1, 1, 1, 0, out=out))
             ref = K.conv_wgrad(x, dy, 1, 1, 1, 0).view(ko, cin)
+            tuning.set("wgrad1x1_pp_pix", old)
             o2 = torch.zeros(ko, cin, device=d)
             x2, dy2 = x.view(M, cin), dy.view(M, ko)
-            auto = K.lib().pdnn_pp_wgrad_splits(ko, cin, M)
+            auto = K.lib().pdnn_pp_wgrad_splits_long(ko, cin, M)
             row["pp_auto_splits"] = auto
             best = None
             for s in sorted({auto, 8, 16, 32, 64, 128, 256}):
