@@ -1,0 +1,324 @@
+// Direct weight gradient of a 3x3 / stride-1 / pad-1 convolution on MFMA (gfx950):
+//   dW[ko][r][s][c] = sum over output pixels p of dy[p][ko] * x[p + (r - 1, s - 1)][c]
+// (reference layers: pytorch_code/model_ops/resnet.py:19-21,44-48, every 3x3 conv of the ResNets).
+//
+// The implicit-GEMM engine (gemm_mfma.hip, A_MNMAJOR x B_IM2COL with split-K atomics) gathers the im2col
+// operand from global memory per k-row with two divisions per load, re-reads every input element 9 times
+// through L2, and at 2 blocks/CU its one-step register prefetch leaves each K-step waiting on memory:
+// 150-350 us per ResNet-50 3x3 layer on the weight-gradient side stream (profiles/resnet50_bs256_timeline_r3b).
+//
+// Here a block owns one (64 ko x 64 c) chunk pair of the output and a contiguous run of 256-pixel tiles.
+// Per tile it stages (a) the dy tile [256 px][64 ko] and (b) the HALO of the tile's input rows (the same
+// contiguous NHWC range the forward halo kernel stages, conv3x3.hip) into LDS, then runs the 9 taps as
+// shifted reads of the one halo: both operands reach MFMA through the CDNA4 transpose read
+// (ds_read_b64_tr_b16), so the pixel dimension -- the reduction -- lands in the fragments' k without any
+// transpose pass, and a tap that falls outside the image (padding, or the neighbouring image of a tile that
+// straddles two) reads the zero pixel at the end of the halo.  The next tile's dy and halo are fetched into
+// registers while the current tile computes (one block of 8 waves per CU, two barriers per tile).
+// Accumulation stays in registers across all of the block's tiles (wave w: 16 input channels x 32 output
+// channels x 9 taps = 18 fragments); each block writes its partial [64][9][64] once to a workspace slab,
+// and a second kernel adds the partials of every chunk pair into dW (the arena's fp32 gradient, +=).
+#include "conv_direct.h"
+
+namespace {
+using namespace pg;
+
+constexpr int W3_NT = 512;
+constexpr int W3_BM = 256;           // pixels per tile
+constexpr int W3_HMAX = 512;         // largest supported halo source range (pixels): 8 chunks per thread
+constexpr int W3_PB = 160;           // bytes per halo pixel (64 channels + 32 B skew): 8 consecutive pixels
+                                     // tile the 64 LDS banks, so the transpose reads of 16 pixel rows are 2-way
+
+struct W3Args {
+    const bf16_t* x;     // [P][C]
+    const bf16_t* dy;    // [P][Ko]
+    float* ws;           // [gridDim.x][64 ko][9][64 c] partials
+    int H, W, C, Ko, P;
+    FastDiv dW, dH;
+    int tiles, cch, G, hrows;
+};
+int g_w3_abl = 0;
+
+// Halo layout (per tile): the tile's input rows from one above its first to one below its last, each
+// image's rows bracketed by an all-zero row above and below, every row padded by a zero pixel left and
+// right (pitch WT + 2).  Tap (r, s) of output pixel (y, x) is then halo pixel (hrow(y) + r - 1, x + s) at a
+// FIXED offset from the pixel's base for every pixel of the tile: the 9 taps are 9 immediate offsets of one
+// address (no per-tap validity, select or swizzle arithmetic; that VALU work was 3x the MFMA time).
+//   hrow(gr) = gr - gstart + 2 (img(gr) - img(gstart)) + 1,  gstart = first row - 1 (global row index over
+//   the whole batch; img(-1) = -1).
+template <int WT, int ABL>
+__global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
+    constexpr int PITCH = WT + 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const dimg = reinterpret_cast<bf16_t*>(smem);        // [256 px][64 ko], mimg_off<64> swizzle
+    char* const halo = smem + W3_BM * 64 * 2;                     // [hrows][PITCH] pixels of W3_PB bytes
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pair = blockIdx.x / a.G, part = blockIdx.x - pair * a.G;
+    const int ko0 = (pair / a.cch) * 64, c0 = (pair % a.cch) * 64;
+    const int t0 = (int)((long)part * a.tiles / a.G), t1 = (int)((long)(part + 1) * a.tiles / a.G);
+    const int hbytes = a.hrows * PITCH * W3_PB;
+
+    // wave roles: input channels [16 fn, +16), output-channel fragments fmb, fmb + 1 (32 ko), all 9 taps
+    const int fn = wave & 3, fmb = (wave >> 2) * 2;
+    f32x4_t acc[2][9];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int DCH = W3_BM * 8 / W3_NT;      // 4 dy chunks per thread
+    constexpr int HCH = W3_HMAX * 8 / W3_NT;    // 8 halo source chunks per thread
+    u16x8_t rd[DCH], rh[HCH];
+    int nch = 0;                                // source chunks of the tile held in rh
+    uint32_t okm = 0;                           // validity of rd (bits 0..3) and rh (bits 4..11): masked at the
+                                                // LDS store, so the loads stay in flight under the MFMAs
+    int s_gstart = 0, s_istart = 0;             // halo origin of the tile held in the registers
+
+    auto geo = [&](int t, int& p0, int& plast, int& gstart, int& istart) {
+        p0 = t * W3_BM;
+        plast = min(a.P, p0 + W3_BM) - 1;
+        gstart = (int)fdiv((uint32_t)p0, a.dW) - 1;
+        istart = gstart < 0 ? -1 : (int)fdiv((uint32_t)gstart, a.dH);
+    };
+    auto load_regs = [&](int t) {
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        s_gstart = gstart;
+        s_istart = istart;
+#pragma unroll
+        for (int j = 0; j < DCH; ++j) {
+            const int i = tid + j * W3_NT, row = i >> 3;
+            const int p = p0 + row;
+            const bool ok = p < a.P;
+            rd[j] = *reinterpret_cast<const u16x8_t*>(a.dy + (long)(ok ? p : plast) * a.Ko + ko0 + (i & 7) * 8);
+            okm = ok ? (okm | (1u << j)) : (okm & ~(1u << j));
+        }
+        const int gr1 = (int)fdiv((uint32_t)plast, a.dW);
+        nch = (gr1 + 2 - gstart) * WT * 8;      // rows gstart .. gr1 + 1
+        const long gp0 = (long)gstart * WT;
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            const long gp = gp0 + (i >> 3);
+            const bool ok = i < nch && gp >= 0 && gp < a.P;
+            const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+            rh[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+            okm = ok ? (okm | (16u << j)) : (okm & ~(16u << j));
+        }
+    };
+    // zero the whole halo (padding pixels and bracket rows move with every tile), then, after a barrier, the data
+    auto zero_halo = [&]() {
+        for (int o = tid * 16; o < hbytes; o += W3_NT * 16) *reinterpret_cast<u16x8_t*>(halo + o) = c3_zero8();
+    };
+    auto store_lds = [&]() {
+#pragma unroll
+        for (int j = 0; j < DCH; ++j) {
+            const int i = tid + j * W3_NT;
+            *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(rd[j], (okm >> j) & 1);
+        }
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            if (((okm >> (4 + j)) & 1) != 0) {
+                const int gp = s_gstart * WT + (i >> 3);           // >= 0 and < P here
+                const int gr = (int)fdiv((uint32_t)gp, a.dW);
+                const int xx = gp - gr * WT;
+                const int img = (int)fdiv((uint32_t)gr, a.dH);
+                const int hrow = gr - s_gstart + 2 * (img - s_istart) + 1;
+                *reinterpret_cast<u16x8_t*>(halo + (hrow * PITCH + xx + 1) * W3_PB + (i & 7) * 16) = rh[j];
+            }
+        }
+    };
+
+    // this lane's transpose-read coordinates: rows k = 32 ks + 8 g + q (+4), input channels 16 fn + 4 pq .. +3
+    const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+    const int cbyte = (fn * 16 + 4 * pq) * 2;
+
+    if (t0 < t1) {
+        load_regs(t0);
+        zero_halo();
+    }
+    __syncthreads();
+    if (t0 < t1) store_lds();
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+        const bool more = t + 1 < t1;
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        if (more && !(ABL & 4)) load_regs(t + 1);               // under this tile's MFMAs
+#pragma unroll 1
+        for (int ks = 0; ks < W3_BM / 32; ++ks) {
+            bf16x8_t af[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) af[f] = frag_mnmajor<64>(dimg, (fmb + f) * 16, ks, lane);
+            // byte address of tap (0, 0) for the two pixels of this lane's transpose reads; pixels past P read
+            // real (finite) halo data against an all-zero dy row
+            int base[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int p = min(p0 + ks * 32 + 8 * g + q + 4 * h, plast);
+                const int gr = (int)fdiv((uint32_t)p, a.dW);
+                const int xx = p - gr * WT;
+                const int img = (int)fdiv((uint32_t)gr, a.dH);
+                const int hrow = gr - gstart + 2 * (img - istart) + 1;
+                base[h] = ((hrow - 1) * PITCH + xx) * W3_PB + cbyte;
+            }
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                constexpr int dummy = 0;
+                (void)dummy;
+                const int off = ((tap / 3) * PITCH + tap % 3) * W3_PB;
+                bf16x8_t xf;
+                if constexpr ((ABL & 2) != 0) {
+                    xf = af[tap & 1];
+                    asm volatile("" ::"v"(base[0]), "v"(base[1]));
+                } else {
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[0] + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[1] + off));
+                    typedef __attribute__((ext_vector_type(8))) short s16x8;
+                    const s16x8 xv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    xf = __builtin_bit_cast(bf16x8_t, xv);
+                }
+                if constexpr ((ABL & 1) != 0) {
+                    asm volatile("" ::"v"(xf), "v"(af[0]), "v"(af[1]));
+                } else {
+#pragma unroll
+                    for (int f = 0; f < 2; ++f)
+                        acc[f][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], xf, acc[f][tap], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();                          // every wave is done reading this tile's images
+        if (more && !(ABL & 4)) {
+            zero_halo();
+            __syncthreads();
+            store_lds();
+            __syncthreads();
+        }
+    }
+    // partial of this block: lane holds dW[ko = 16 (fmb + f) + 4 g + j][tap][c = 16 fn + (lane & 15)]
+    float* ws = a.ws + (long)blockIdx.x * (64 * 9 * 64);
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ko = (fmb + f) * 16 + 4 * g + j;
+                ws[(ko * 9 + tap) * 64 + fn * 16 + (lane & 15)] = acc[f][tap][j];
+            }
+}
+
+// dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64); one thread per 4 channels
+__global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                                                    int Ko, int C, int cch, int G) {
+    const long total = (long)Ko * 9 * (C / 4);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int c = (int)(i % (C / 4)) * 4;
+        const long r = i / (C / 4);
+        const int tap = (int)(r % 9), ko = (int)(r / 9);
+        const int pair = (ko >> 6) * cch + (c >> 6);
+        const float* src = ws + ((long)pair * G * 64 + (ko & 63)) * 576 + tap * 64 + (c & 63);
+        constexpr long BS = 64L * 9 * 64;         // floats per block partial
+        float4 s = *reinterpret_cast<const float4*>(dw + ((long)ko * 9 + tap) * C + c);
+        int b = 0;
+        for (; b + 8 <= G; b += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(src + (b + j) * BS);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
+        }
+        for (; b < G; ++b) {
+            const float4 v = *reinterpret_cast<const float4*>(src + b * BS);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(dw + ((long)ko * 9 + tap) * C + c) = s;
+    }
+}
+
+// halo rows of the padded layout: source rows R = ceil((BM - 1 + W - 1) / W) + 3, plus a zero row above and
+// below every image they touch, plus one
+int w3_hrows(int H, int W) {
+    const int R = (W3_BM - 1 + W - 1) / W + 1 + 2;
+    const int imgs = (R + H - 1) / H + 1;
+    return R + 2 * imgs + 1;
+}
+int w3_smem(int H, int W) { return W3_BM * 64 * 2 + w3_hrows(H, W) * (W + 2) * W3_PB; }
+
+void w3_plan(int P, int C, int Ko, int& tiles, int& cch, int& G) {
+    tiles = (P + W3_BM - 1) / W3_BM;
+    cch = C / 64;
+    const int pairs = (Ko / 64) * cch;
+    G = (256 + pairs - 1) / pairs;               // ~one block per CU in total
+    if (G > tiles) G = tiles;
+    if (G < 1) G = 1;
+}
+
+FastDiv w3_fdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d ? d : 1;
+    uint32_t l = 0;
+    while ((1ull << l) < f.d) ++l;
+    f.s = l;
+    f.m = (uint32_t)((((1ull << l) - f.d) << 32) / f.d + 1);
+    return f;
+}
+}  // namespace
+
+PDNN_API void pdnn_set_w3_ablate(int v) { g_w3_abl = v; }
+
+// Whether the direct kernel takes this 3x3 / stride-1 / pad-1 weight gradient (image widths 7/14/28/56: the
+// ResNet stages; the tap offsets are compile-time immediates).
+PDNN_API int pdnn_conv3x3_wgrad_supported(int Nimg, int H, int W, int C, int Ko) {
+    if (C % 64 || Ko % 64 || C < 64 || Ko < 64 || H < 1) return 0;
+    if (W != 7 && W != 14 && W != 28 && W != 56) return 0;
+    if ((long)Nimg * H * W >= (1L << 31) / 2) return 0;
+    if (((W3_BM - 1 + W - 1) / W + 3) * W > W3_HMAX) return 0;
+    return w3_smem(H, W) <= 160 * 1024 ? 1 : 0;
+}
+
+// floats of workspace pdnn_conv3x3_wgrad needs
+PDNN_API int pdnn_conv3x3_wgrad_ws(int Nimg, int H, int W, int C, int Ko) {
+    int tiles, cch, G;
+    w3_plan(Nimg * H * W, C, Ko, tiles, cch, G);
+    return (Ko / 64) * cch * G * 64 * 9 * 64;
+}
+
+// dw [Ko][3][3][C] fp32 += weight gradient of y = conv3x3(x, w) (stride 1, pad 1) given dy [P][Ko]
+PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C, int Ko,
+                                float* ws, hipStream_t st) {
+    if (!pdnn_conv3x3_wgrad_supported(Nimg, H, W, C, Ko) || !ws) return (int)hipErrorInvalidValue;
+    W3Args a{};
+    a.x = x; a.dy = dy; a.ws = ws;
+    a.H = H; a.W = W; a.C = C; a.Ko = Ko; a.P = Nimg * H * W;
+    a.dW = w3_fdiv(W); a.dH = w3_fdiv(H);
+    w3_plan(a.P, C, Ko, a.tiles, a.cch, a.G);
+    a.hrows = w3_hrows(H, W);
+    const int abl = g_w3_abl & 7;
+    const int sm = w3_smem(H, W);
+    const int grid = (Ko / 64) * a.cch * a.G;
+    static int attr_done = 0;
+    const bool set = sm > attr_done;
+    if (set) attr_done = sm;
+#define W3_GO(WT, A)                                                                                             \
+    do {                                                                                                         \
+        if (set) (void)hipFuncSetAttribute((const void*)conv3x3_wgrad_kernel<WT, A>,                              \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
+        hipLaunchKernelGGL((conv3x3_wgrad_kernel<WT, A>), dim3(grid), dim3(W3_NT), sm, st, a);                   \
+    } while (0)
+#define W3_W(WT)                                                                                                 \
+    switch (abl) {                                                                                               \
+        case 1: W3_GO(WT, 1); break; case 2: W3_GO(WT, 2); break; case 3: W3_GO(WT, 3); break;                   \
+        case 4: W3_GO(WT, 4); break; case 5: W3_GO(WT, 5); break; case 6: W3_GO(WT, 6); break;                   \
+        case 7: W3_GO(WT, 7); break; default: W3_GO(WT, 0);                                                      \
+    }
+    if (W == 56) { W3_W(56) } else if (W == 28) { W3_W(28) } else if (W == 14) { W3_W(14) } else { W3_W(7) }
+#undef W3_W
+#undef W3_GO
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(stream_grid((long)Ko * 9 * (C / 4), 256)), dim3(256), 0, st,
+                       (const float*)ws, dw, Ko, C, a.cch, a.G);
+    PDNN_LAUNCH_RET;
+}

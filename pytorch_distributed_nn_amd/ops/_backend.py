@@ -42,6 +42,10 @@ _SIGS = {
     "pdnn_conv3x3_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
+    "pdnn_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, P],
+    "pdnn_conv3x3_wgrad_supported": [I, I, I, I, I],
+    "pdnn_conv3x3_wgrad_ws": [I, I, I, I, I],
+    "pdnn_set_w3_ablate": [I],
     "pdnn_conv3x3_force": [I],
     "pdnn_tune_set": [ctypes.c_char_p, I],
     "pdnn_tune_get": [ctypes.c_char_p],

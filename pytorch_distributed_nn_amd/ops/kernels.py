@@ -422,6 +422,12 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     _chk(out.shape == (K, R, S, C) and out.is_contiguous() and out.dtype == F32, "conv_wgrad: out [K][R][S][C] fp32")
     sc, sh = pro if pro is not None else (None, None)
     P = N * H * W
+    if (pro is None and R == 3 and S == 3 and st == 1 and pad == 1 and _tuning.get("wgrad3x3")
+            and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, K) == 1):
+        # direct kernel: LDS halo + transpose reads, partials per block, then one reduce (conv3x3_wgrad.hip)
+        ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
+        call("pdnn_conv3x3_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), stream())
+        return out
     if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _tuning.get("wgrad1x1_pp_pix")
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
         # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs, split count from

@@ -226,3 +226,33 @@ def test_dgrad_pre_rejected_on_gemm_engine(K):
     assert not K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
     with pytest.raises(ValueError):
         K.conv_dgrad(gm, w, (2, 8, 8, 64), 1, 0, pre=(t, mean, inv, g, dg, db, None))
+
+
+# ------------------------------------------- direct 3x3 weight gradient (conv3x3_wgrad.hip)
+WGRAD3 = [(4, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (5, 7, 7, 512, 512), (3, 9, 56, 64, 192),
+          (2, 5, 14, 128, 64), (7, 3, 7, 64, 128), (1, 4, 7, 64, 64), (2, 13, 28, 192, 64)]
+
+
+@pytest.mark.parametrize("shape", WGRAD3)
+def test_conv3x3_wgrad_direct(K, shape):
+    """dW of a 3x3 / stride-1 / pad-1 conv on the direct halo kernel against fp32 torch, accumulated into an
+    existing gradient (+=), including tiles straddling image boundaries and partial last tiles."""
+    from pytorch_distributed_nn_amd import tuning
+    N, H, W, C, Ko = shape
+    assert K.lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, Ko) == 1
+    x = torch.randn(N, H, W, C, device="cuda").to(BF)
+    dy = torch.randn(N, H, W, Ko, device="cuda").to(BF)
+    wr = torch.zeros(Ko, C, 3, 3, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, None, 1, 1)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    ref = wr.grad.permute(0, 2, 3, 1)                      # [Ko][3][3][C]
+    base = torch.randn(Ko, 3, 3, C, device="cuda")
+    old = tuning.set("wgrad3x3", 1)
+    try:
+        out = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())
+        tuning.set("wgrad3x3", 0)
+        out_gemm = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())
+    finally:
+        tuning.set("wgrad3x3", old)
+    assert rel(out - base, ref) < 5e-3
+    assert rel(out, out_gemm) < 5e-3
