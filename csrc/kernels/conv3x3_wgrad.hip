@@ -209,31 +209,47 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
             }
 }
 
-// dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64); one thread per 4 channels
+// dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64).  A block covers 32 consecutive
+// float4 outputs (one 512-byte row run) with 8 partial groups: thread (o, pg) sums partials pg, pg + 8, ...
+// (8 loads in flight), then the 8 groups are combined through LDS.  (One thread per output summing all G
+// partials was a G/8-deep latency chain: 92 us at stage 1, G = 256.)
 __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                                                     int Ko, int C, int cch, int G) {
+    __shared__ float4 red[8][32];
+    const int o = threadIdx.x & 31, pg = threadIdx.x >> 5;
     const long total = (long)Ko * 9 * (C / 4);
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int c = (int)(i % (C / 4)) * 4;
+    const long i = (long)blockIdx.x * 32 + o;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int c = 0, tap = 0, ko = 0;
+    if (i < total) {
+        c = (int)(i % (C / 4)) * 4;
         const long r = i / (C / 4);
-        const int tap = (int)(r % 9), ko = (int)(r / 9);
+        tap = (int)(r % 9);
+        ko = (int)(r / 9);
         const int pair = (ko >> 6) * cch + (c >> 6);
         const float* src = ws + ((long)pair * G * 64 + (ko & 63)) * 576 + tap * 64 + (c & 63);
         constexpr long BS = 64L * 9 * 64;         // floats per block partial
-        float4 s = *reinterpret_cast<const float4*>(dw + ((long)ko * 9 + tap) * C + c);
-        int b = 0;
-        for (; b + 8 <= G; b += 8) {
+        int b = pg;
+        for (; b + 56 < G; b += 64) {
             float4 v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(src + (b + j) * BS);
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(src + (b + 8 * j) * BS);
 #pragma unroll
             for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
         }
-        for (; b < G; ++b) {
+        for (; b < G; b += 8) {
             const float4 v = *reinterpret_cast<const float4*>(src + b * BS);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
-        *reinterpret_cast<float4*>(dw + ((long)ko * 9 + tap) * C + c) = s;
+    }
+    red[pg][o] = s;
+    __syncthreads();
+    if (pg == 0 && i < total) {
+#pragma unroll
+        for (int k = 1; k < 8; ++k) { const float4 v = red[k][o]; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+        float4* d = reinterpret_cast<float4*>(dw + ((long)ko * 9 + tap) * C + c);
+        const float4 cur = *d;
+        *d = make_float4(cur.x + s.x, cur.y + s.y, cur.z + s.z, cur.w + s.w);
     }
 }
 
@@ -318,7 +334,7 @@ PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, in
 #undef W3_GO
     const int e = (int)hipGetLastError();
     if (e) return e;
-    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(stream_grid((long)Ko * 9 * (C / 4), 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3((unsigned)cdiv((long)Ko * 9 * (C / 4), 32)), dim3(256), 0, st,
                        (const float*)ws, dw, Ko, C, a.cch, a.G);
     PDNN_LAUNCH_RET;
 }

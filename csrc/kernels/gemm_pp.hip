@@ -541,8 +541,6 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_kernel(const float* __rest
         const long off = (long)m * ldc + c, soff = (long)m * N + c;       // slab rows are N wide
         float4 s = accumulate ? *reinterpret_cast<const float4*>(out + off) : make_float4(0.f, 0.f, 0.f, 0.f);
         int z = 0;
-        // 8 splits' loads in flight per batch: a split-by-split chain exposed one memory latency per split
-        // (32 splits: 32 us per call for a 1 MB output)
         for (; z + 8 <= splits; z += 8) {
             float4 v[8];
 #pragma unroll
@@ -553,6 +551,49 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_kernel(const float* __rest
         for (; z < splits; ++z) {
             const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + soff);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(out + off) = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) pp_slab_reduce_wide_kernel(const float* __restrict__ slab, long sz, int splits,
+                                                             float* __restrict__ out, int M, int N, long ldc,
+                                                             int accumulate) {
+    // a block covers 32 consecutive float4 outputs with 8 split groups: thread (o, zg) sums splits zg, zg + 8, ...
+    // (8 loads in flight), the groups are combined through LDS.  One thread per output summing every split was
+    // a splits/8-deep latency chain on a grid of only M*N/1024 blocks (31-49 us per 1x1 conv weight gradient).
+    __shared__ float4 red[8][32];
+    const int o = threadIdx.x & 31, zg = threadIdx.x >> 5;
+    const int n4 = N >> 2;
+    const long total = (long)M * n4;
+    const long i = (long)blockIdx.x * 32 + o;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    long off = 0;
+    if (i < total) {
+        const int m = (int)(i / n4), c = (int)(i - (long)m * n4) * 4;
+        off = (long)m * ldc + c;
+        const long soff = (long)m * N + c;        // slab rows are N wide
+        int z = zg;
+        for (; z + 56 < splits; z += 64) {
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(slab + (z + 8 * j) * sz + soff);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
+        }
+        for (; z < splits; z += 8) {
+            const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + soff);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    }
+    red[zg][o] = s;
+    __syncthreads();
+    if (zg == 0 && i < total) {
+#pragma unroll
+        for (int k = 1; k < 8; ++k) { const float4 v = red[k][o]; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+        if (accumulate) {
+            const float4 cur = *reinterpret_cast<const float4*>(out + off);
+            s.x += cur.x; s.y += cur.y; s.z += cur.z; s.w += cur.w;
         }
         *reinterpret_cast<float4*>(out + off) = s;
     }
@@ -825,8 +866,13 @@ PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb,
     a.C = ws; a.ldc = N; a.sC1 = (long)M * N;
     int e = launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, splits, st);
     if (e) return e;
-    hipLaunchKernelGGL(pp_slab_reduce_kernel, dim3(stream_grid((long)M * N / 4, 256)), dim3(256), 0, st,
-                       (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
+    // many splits (the long conv-weight-gradient reductions): split-parallel reduce; few (GPT-2): per-output
+    if (splits >= 16)
+        hipLaunchKernelGGL(pp_slab_reduce_wide_kernel, dim3((unsigned)cdiv((long)M * N / 4, 32)), dim3(256), 0, st,
+                           (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
+    else
+        hipLaunchKernelGGL(pp_slab_reduce_kernel, dim3(stream_grid((long)M * N / 4, 256)), dim3(256), 0, st,
+                           (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
     PDNN_LAUNCH_RET;
 }
 

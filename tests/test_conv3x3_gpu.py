@@ -75,9 +75,11 @@ def test_conv3x3_dgrad_bn_and_res(K, nb, shape):
     mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
     msc, msh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
     gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), 1, 1, bn=(t, mean, inv, msc, msh))
-    mask = (t.float() * msc + msh) > 0
+    z = t.float() * msc + msh
+    mask = z > 0
     gm_ref = dx_ref * mask
-    assert rel(gm, gm_ref) < 1.5e-2
+    far = z.abs() > 1e-3          # the kernel's fma and torch's mul+add may round a ~0 pre-activation apart
+    assert rel(gm[far], gm_ref[far]) < 1.5e-2
     s = slab.view(-1, 2, C).sum(0)
     gmf = gm.float().reshape(-1, C)
     xhat = ((t.float() - mean) * inv).reshape(-1, C)
@@ -146,8 +148,10 @@ def test_conv1x1_panel_dgrad(K, areg, shape):
     mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
     msc, msh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
     gm, slab = K.conv_dgrad(dy, w, (N, H, W, C), 1, 0, bn=(t, mean, inv, msc, msh))
-    mask = (t.float() * msc + msh) > 0
-    assert rel(gm, dx_ref * mask) < 1.5e-2
+    z = t.float() * msc + msh
+    mask = z > 0
+    far = z.abs() > 1e-3          # the kernel's fma and torch's mul+add may round a ~0 pre-activation apart
+    assert rel(gm[far], (dx_ref * mask)[far]) < 1.5e-2
     s = slab.view(-1, 2, C).sum(0)
     gmf = gm.float().reshape(-1, C)
     xhat = ((t.float() - mean) * inv).reshape(-1, C)
