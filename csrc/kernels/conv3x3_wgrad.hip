@@ -209,16 +209,18 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
             }
 }
 
-// dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64).  A block covers 32 consecutive
-// float4 outputs (one 512-byte row run) with 8 partial groups: thread (o, pg) sums partials pg, pg + 8, ...
-// (8 loads in flight), then the 8 groups are combined through LDS.  (One thread per output summing all G
-// partials was a G/8-deep latency chain: 92 us at stage 1, G = 256.)
+// dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64).  A block covers OUT = 256 / PG
+// consecutive float4 outputs with PG partial groups (PG ~ G / 8, so every thread sums ~8 partials with all its
+// loads in flight); the groups are combined through LDS.  (One thread per output summing all G partials was a
+// G/8-deep latency chain: 92 us at stage 1, G = 256.)
+template <int PG>
 __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                                                     int Ko, int C, int cch, int G) {
-    __shared__ float4 red[8][32];
-    const int o = threadIdx.x & 31, pg = threadIdx.x >> 5;
+    constexpr int OUT = 256 / PG;
+    __shared__ float4 red[PG][OUT];
+    const int o = threadIdx.x % OUT, pg = threadIdx.x / OUT;
     const long total = (long)Ko * 9 * (C / 4);
-    const long i = (long)blockIdx.x * 32 + o;
+    const long i = (long)blockIdx.x * OUT + o;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     int c = 0, tap = 0, ko = 0;
     if (i < total) {
@@ -230,23 +232,25 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* 
         const float* src = ws + ((long)pair * G * 64 + (ko & 63)) * 576 + tap * 64 + (c & 63);
         constexpr long BS = 64L * 9 * 64;         // floats per block partial
         int b = pg;
-        for (; b + 56 < G; b += 64) {
+        for (; b + 7 * PG < G; b += 8 * PG) {
             float4 v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(src + (b + 8 * j) * BS);
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float4*>(src + (b + PG * j) * BS);
 #pragma unroll
             for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
         }
-        for (; b < G; b += 8) {
+        for (; b < G; b += PG) {
             const float4 v = *reinterpret_cast<const float4*>(src + b * BS);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
     }
-    red[pg][o] = s;
-    __syncthreads();
+    if constexpr (PG > 1) {
+        red[pg][o] = s;
+        __syncthreads();
+    }
     if (pg == 0 && i < total) {
 #pragma unroll
-        for (int k = 1; k < 8; ++k) { const float4 v = red[k][o]; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+        for (int k = 1; k < PG; ++k) { const float4 v = red[k][o]; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
         float4* d = reinterpret_cast<float4*>(dw + ((long)ko * 9 + tap) * C + c);
         const float4 cur = *d;
         *d = make_float4(cur.x + s.x, cur.y + s.y, cur.z + s.z, cur.w + s.w);
@@ -334,7 +338,15 @@ PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, in
 #undef W3_GO
     const int e = (int)hipGetLastError();
     if (e) return e;
-    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3((unsigned)cdiv((long)Ko * 9 * (C / 4), 32)), dim3(256), 0, st,
-                       (const float*)ws, dw, Ko, C, a.cch, a.G);
+    const long outs = (long)Ko * 9 * (C / 4);
+#define W3_R(PG) hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel<PG>, dim3((unsigned)cdiv(outs, 256 / PG)), dim3(256), 0, st, \
+                                    (const float*)ws, dw, Ko, C, a.cch, a.G)
+    if (a.G >= 256) W3_R(32);
+    else if (a.G >= 128) W3_R(16);
+    else if (a.G >= 64) W3_R(8);
+    else if (a.G >= 32) W3_R(4);
+    else if (a.G >= 16) W3_R(2);
+    else W3_R(1);
+#undef W3_R
     PDNN_LAUNCH_RET;
 }

@@ -1,0 +1,12 @@
+#!/bin/bash
+# split-parallel reduce kernels (pp slab, 3x3 wgrad partials): tests, step, GPT-2
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r3_52
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv3x3_gpu.py -k wgrad > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for i in 1 2 3; do timeout -k 10 200 python -u bench.py --steps 30 --no-ddp-rehearsal > $O/b$i.log 2>&1 || exit 1; echo "[b$i] $(grep -o '"value": [0-9.]*' $O/b$i.log)"; done
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o r50 --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 3 --no-ddp-rehearsal > $O/prof.log 2>&1 || exit 1
+echo done
