@@ -26,13 +26,16 @@ using namespace pg;
 constexpr int W3_NT = 512;
 constexpr int W3_BM = 256;           // pixels per tile
 constexpr int W3_HMAX = 512;         // largest supported halo source range (pixels): 8 chunks per thread
+constexpr int W3_PS = 64 * 9 * 64 + 64;   // floats per block partial, padded by 256 B: unpadded (147456 B =
+                                            // 9 * 16 KB) every partial of an output sat in one HBM channel and the
+                                            // reduce crawled (117 us at stage 2)
 constexpr int W3_PB = 160;           // bytes per halo pixel (64 channels + 32 B skew): 8 consecutive pixels
                                      // tile the 64 LDS banks, so the transpose reads of 16 pixel rows are 2-way
 
 struct W3Args {
     const bf16_t* x;     // [P][C]
     const bf16_t* dy;    // [P][Ko]
-    float* ws;           // [gridDim.x][64 ko][9][64 c] partials
+    float* ws;           // [gridDim.x][64 ko][9][64 c] partials, W3_PS floats apart
     int H, W, C, Ko, P;
     FastDiv dW, dH;
     int tiles, cch, G, hrows;
@@ -197,7 +200,7 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
         }
     }
     // partial of this block: lane holds dW[ko = 16 (fmb + f) + 4 g + j][tap][c = 16 fn + (lane & 15)]
-    float* ws = a.ws + (long)blockIdx.x * (64 * 9 * 64);
+    float* ws = a.ws + (long)blockIdx.x * W3_PS;
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
@@ -229,8 +232,8 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_reduce_kernel(const float* 
         tap = (int)(r % 9);
         ko = (int)(r / 9);
         const int pair = (ko >> 6) * cch + (c >> 6);
-        const float* src = ws + ((long)pair * G * 64 + (ko & 63)) * 576 + tap * 64 + (c & 63);
-        constexpr long BS = 64L * 9 * 64;         // floats per block partial
+        const float* src = ws + (long)pair * G * W3_PS + (ko & 63) * 576 + tap * 64 + (c & 63);
+        constexpr long BS = W3_PS;
         int b = pg;
         for (; b + 7 * PG < G; b += 8 * PG) {
             float4 v[8];
@@ -302,7 +305,7 @@ PDNN_API int pdnn_conv3x3_wgrad_supported(int Nimg, int H, int W, int C, int Ko)
 PDNN_API int pdnn_conv3x3_wgrad_ws(int Nimg, int H, int W, int C, int Ko) {
     int tiles, cch, G;
     w3_plan(Nimg * H * W, C, Ko, tiles, cch, G);
-    return (Ko / 64) * cch * G * 64 * 9 * 64;
+    return (Ko / 64) * cch * G * W3_PS;
 }
 
 // dw [Ko][3][3][C] fp32 += weight gradient of y = conv3x3(x, w) (stride 1, pad 1) given dy [P][Ko]

@@ -847,7 +847,8 @@ PP_F5(B_KMAJOR) PP_F5(B_MNMAJOR)
 #undef PP_I
 
 // pp_wgrad: out[M][N] (fp32) += alpha * A[K][M]^T . B[K][N] with split-K partial slabs in `ws`
-// (>= splits * M * N floats) reduced by a second kernel; splits == 1 accumulates in place.
+// (>= pdnn_pp_wgrad_ws(M, N, splits) floats) reduced by a second kernel; splits == 1 accumulates in place.
+PDNN_API long pdnn_pp_wgrad_ws(int M, int N, int splits) { return splits > 1 ? (long)splits * ((long)M * N + 64) : 0; }
 PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* out, long ldc, int M, int N,
                            int K, float alpha, float* ws, int splits, hipStream_t st) {
     using namespace pg;
@@ -863,21 +864,24 @@ PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb,
         return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
     }
     if (!ws) return (int)hipErrorInvalidValue;
-    a.C = ws; a.ldc = N; a.sC1 = (long)M * N;
+    // slab stride padded by 256 B (pdnn_pp_wgrad_ws): with power-of-two M*N every split of an output falls in
+    // the same HBM channel and the reduce crawls
+    const long sz = (long)M * N + 64;
+    a.C = ws; a.ldc = N; a.sC1 = sz;
     int e = launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, splits, st);
     if (e) return e;
     // many splits (the long conv-weight-gradient reductions): split-parallel reduce; few (GPT-2): per-output
     if (splits >= 16)
         hipLaunchKernelGGL(pp_slab_reduce_wide_kernel, dim3((unsigned)cdiv((long)M * N / 4, 32)), dim3(256), 0, st,
-                           (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
+                           (const float*)ws, sz, splits, out, M, N, ldc, 1);
     else
         hipLaunchKernelGGL(pp_slab_reduce_kernel, dim3(stream_grid((long)M * N / 4, 256)), dim3(256), 0, st,
-                           (const float*)ws, (long)M * N, splits, out, M, N, ldc, 1);
+                           (const float*)ws, sz, splits, out, M, N, ldc, 1);
     PDNN_LAUNCH_RET;
 }
 
 // Y[M][N] (bf16) = X[M][K] . W[N][K]^T for a very long reduction: 256 x 256 tiles, K split over `splits`
-// work items writing fp32 slabs in `ws` (>= splits * M * N floats), summed into bf16 by a second kernel.
+// work items writing fp32 slabs in `ws` (>= splits * (M * N + 64) floats), summed into bf16 by a second kernel.
 PDNN_API int pdnn_pp_gemm_nt_splitk(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t* Y, long ldy, int M,
                                     int N, int K, float* ws, int splits, hipStream_t st) {
     using namespace pg;
@@ -887,11 +891,12 @@ PDNN_API int pdnn_pp_gemm_nt_splitk(const bf16_t* X, long ldx, const bf16_t* W, 
     const int nsl = K / PP_SK;
     while (nsl % splits) --splits;
     a.ktiles_per_split = nsl / splits;
-    a.C = ws; a.ldc = N; a.sC1 = (long)M * N;
+    const long sz = (long)M * N + 64;             // padded slab stride (see pdnn_pp_wgrad)
+    a.C = ws; a.ldc = N; a.sC1 = sz;
     int e = launch_bn<A_KMAJOR, B_KMAJOR, E_F32>(a, 256, splits, st);
     if (e) return e;
     hipLaunchKernelGGL(pp_slab_reduce_bf16_kernel, dim3(stream_grid((long)M * N / 4, 256)), dim3(256), 0, st,
-                       (const float*)ws, (long)M * N, splits, Y, M, N, ldy);
+                       (const float*)ws, sz, splits, Y, M, N, ldy);
     PDNN_LAUNCH_RET;
 }
 

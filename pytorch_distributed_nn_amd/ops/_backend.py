@@ -57,6 +57,8 @@ _SIGS = {
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_stem_stats_rows": [L],
     "pdnn_stem_conv_nchw": [P, P, P, I, I, I, I, I, P, P],
+    "pdnn_stem_wgrad_nchw": [P, P, P, I, I, I, I, I, P, P],
+    "pdnn_stem_wgrad_ws": [I, I, I],
     "pdnn_bn_relu_maxpool": [P, P, P, P, P, I, I, I, I, I, I, P],
     "pdnn_set_glds_mode": [I],
     "pdnn_set_pp_mode": [I],
@@ -64,6 +66,7 @@ _SIGS = {
     "pdnn_set_pp_trace": [P],
     "pdnn_pp_wgrad": [P, L, P, L, P, L, I, I, I, F, P, I, P],
     "pdnn_pp_wgrad_splits": [I, I, I],
+    "pdnn_pp_wgrad_ws": [I, I, I],
     "pdnn_pp_wgrad_splits_long": [I, I, I],
     "pdnn_pp_gemm_nt_splitk": [P, L, P, L, P, L, I, I, I, P, I, P],
     "pdnn_pp_splitk_splits": [I, I, I],

@@ -533,7 +533,12 @@ class StemFn(torch.autograd.Function):
         nchw = kpad.dim() == 3          # shadow from K.stem_weight_nchw: x is the NCHW bf16 batch itself
         direct = nchw or (pool and K.stem_ok(x.shape, kpad.shape, stride, pad))
         ev = None
-        if nchw:
+        xn = None
+        if nchw and tuning.get("stem_wgrad_nchw"):
+            # the weight gradient reads the NCHW batch itself (stem_wgrad.hip): no NHWC copy at all
+            t, slab = K.stem_conv_nchw(x, kpad, want_stats=training)
+            xn = x
+        elif nchw:
             # the weight gradient (end of the backward) reads the NHWC copy: converted on the side stream,
             # off the forward's critical path
             side = _side_stream(x.device)
@@ -573,6 +578,7 @@ class StemFn(torch.autograd.Function):
             else:
                 y, idx = a, None
         ctx.save_for_backward(x, t, mb, idx, m, i, gamma, s if direct else None, h if direct else None)
+        ctx.nchw_wgrad = xn is not None
         ctx.conf = (stride, pad, pool, w.shape, (w.shape[0], 7, 7, 8) if nchw else kpad.shape)
         ctx.ev = ev
         ctx.params = (w, gamma, beta)
@@ -595,6 +601,15 @@ class StemFn(torch.autograd.Function):
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
                                   bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
+        if ctx.nchw_wgrad:
+            # x is the NCHW batch: the direct NCHW weight-gradient kernel
+            dw = K.stem_wgrad_nchw(x, dt)
+            acc = sink.acc(P[0])
+            if acc is not None:
+                acc[0].add_(dw)
+                dw = None
+            sink.done()
+            return None, None, None, None, dw, dg, db
         if ctx.ev is not None:
             torch.cuda.current_stream(x.device).wait_event(ctx.ev)     # NHWC copy made on the side stream
             ctx.ev = None

@@ -65,7 +65,8 @@ def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None):
     if splits is None:
         splits = lib().pdnn_pp_wgrad_splits(M, N, K_)
     if splits > 1 and ws is None:
-        ws = torch.empty(splits * M * N, device=x.device, dtype=F32)
+        ws = torch.empty(splits * (M * N + 64), device=x.device, dtype=F32)     # pdnn_pp_wgrad_ws
+    _chk(splits <= 1 or ws.numel() >= splits * (M * N + 64), "pp_wgrad: workspace of splits * (M*N + 64) floats")
     call("pdnn_pp_wgrad", ptr(x), x.stride(0), ptr(y), y.stride(0), ptr(out), out.stride(0), M, N, K_,
          float(alpha), ptr(ws), int(splits), stream())
     return out
@@ -81,7 +82,8 @@ def gemm_nt_splitk(x, w, splits=None, ws=None):
     if splits is None:
         splits = lib().pdnn_pp_splitk_splits(M, N, Kd)
     if ws is None:
-        ws = torch.empty(splits * M * N, device=x.device, dtype=F32)
+        ws = torch.empty(splits * (M * N + 64), device=x.device, dtype=F32)
+    _chk(ws.numel() >= splits * (M * N + 64), "gemm_nt_splitk: workspace of splits * (M*N + 64) floats")
     out = torch.empty(M, N, device=x.device, dtype=BF16)
     call("pdnn_pp_gemm_nt_splitk", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), out.stride(0), M, N, Kd,
          ptr(ws), int(splits), stream())
@@ -595,6 +597,20 @@ def stem_conv_nchw(x, w32, want_stats=True):
         slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
     call("pdnn_stem_conv_nchw", ptr(x), ptr(w32), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
     return y, slab
+
+
+def stem_wgrad_nchw(x, dt):
+    """Weight gradient of stem_conv_nchw: x NCHW bf16 [N][3][H][W], dt bf16 [N][Ho][Wo][64] -> fp32 [64][3][7][7]
+    (a view of the kernel's [64][7 r][32 k] result, k = c*8 + j, tap s = j - 1)."""
+    _bf16_c(x, "stem_wgrad.x")
+    _bf16_c(dt, "stem_wgrad.dt")
+    N, C, H, W = x.shape
+    Ho, Wo = conv_out_hw(H, W, 7, 7, 2, 3)
+    _chk(C == 3 and tuple(dt.shape) == (N, Ho, Wo, 64), "stem_wgrad_nchw: x [N][3][H][W], dt [N][Ho][Wo][64]")
+    ws = torch.empty(lib().pdnn_stem_wgrad_ws(N, Ho, Wo), device=x.device, dtype=F32)
+    dw32 = torch.empty(64, 7, 32, device=x.device, dtype=F32)
+    call("pdnn_stem_wgrad_nchw", ptr(x), ptr(dt), ptr(dw32), N, H, W, Ho, Wo, ptr(ws), stream())
+    return dw32.view(64, 7, 4, 8)[:, :, :3, 1:].permute(0, 2, 1, 3)
 
 
 def stem_weight_nchw(w):

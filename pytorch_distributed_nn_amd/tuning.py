@@ -23,6 +23,8 @@ bn_link            0        consecutive identity Bottlenecks: the upper block's 
                             off: 10,209-10,237 vs 10,285-10,309 img/s (gpurun_out/r3_35)
 bn_fused_fin       1        BatchNorm slab finalize in one launch (level-1 blocks hand their rows to the last
                             arriver through a counter, batchnorm.hip bn_slab_fused_kernel) instead of two
+stem_wgrad_nchw    1        ImageNet stem weight gradient straight from the NCHW batch (stem_wgrad.hip) instead of the
+                            implicit-GEMM im2col over a channel-padded NHWC copy
 wgrad3x3           1        3x3 / stride-1 weight gradients on the direct halo kernel (conv3x3_wgrad.hip) instead of
                             the implicit-GEMM engine
 wprep              1        the data gradients' transformed weights (flipped 3x3, transposed 1x1) made in the forward
@@ -37,7 +39,7 @@ from __future__ import annotations
 import os
 
 DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
-            "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1}
+            "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1, "stem_wgrad_nchw": 1}
 
 _VALUES = dict(DEFAULTS)
 

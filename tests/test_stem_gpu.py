@@ -141,3 +141,18 @@ def test_resnet50_eval_forward_uses_direct_stem(K):
         out = m(x)
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64), (2, 224, 224), (3, 30, 18), (1, 9, 8)])
+def test_stem_wgrad_nchw_matches_fp32(K, shape):
+    """Weight gradient of the NCHW stem (stem_wgrad.hip: NCHW batch read directly, transpose-read reduction over
+    the pixels) against fp32 torch, including partial last tiles and border columns."""
+    N, H, W = shape
+    x = torch.randn(N, 3, H, W, device="cuda").to(BF)
+    w = torch.zeros(64, 3, 7, 7, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float(), w, None, 2, 3)
+    dt = torch.randn(*y.permute(0, 2, 3, 1).shape, device="cuda").to(BF)
+    y.backward(dt.float().permute(0, 3, 1, 2))
+    dw = K.stem_wgrad_nchw(x, dt.contiguous())
+    assert dw.shape == (64, 3, 7, 7)
+    assert rel(dw, w.grad) < 5e-3, rel(dw, w.grad)
