@@ -7,11 +7,12 @@
 // The implicit-GEMM engine ran this as an im2col weight gradient over the channel-padded NHWC copy
 // (K = 7*7*8, 62% of the MFMA work and loads on padding, per-chunk divisions in the gather): 534 us at the very
 // end of the backward with the rest of the GPU idle (profiles/resnet50_bs256_timeline_r3b.txt).  Here a block
-// takes a run of 128-pixel tiles; per tile it stages dt [128 px][64 n] and the seven A_r [128 px][32 k] images
+// takes a run of 96-pixel tiles; per tile it stages dt [96 px][64 n] and the seven A_r [96 px][32 k] images
 // (each lane loads 8 input columns of one channel row for one pixel: 16 bytes, word-shifted at the image
 // border, exactly like the forward) into LDS, and reduces over the pixels through transpose reads
 // (ds_read_b64_tr_b16) of both: 8 waves, wave w owns n-fragment (w & 3), k-half (w >> 2) for all 7 filter
-// rows.  The next tile is fetched into registers under the current tile's MFMAs.  Per-block partials
+// rows.  The next tile is fetched into registers under the current tile's MFMAs; 96-pixel tiles keep the LDS at
+// 66 KB so two blocks share a CU (one block of 128-pixel tiles: 329 us, load-latency bound).  Per-block partials
 // [64][7][32] go to a workspace; a second kernel sums them.
 #include "conv_direct.h"
 
@@ -19,7 +20,7 @@ namespace {
 using namespace pg;
 
 constexpr int SW_NT = 512;
-constexpr int SW_BM = 128;                 // pixels per tile
+constexpr int SW_BM = 96;                  // pixels per tile (LDS 66 KB: two blocks per CU)
 constexpr int SW_R = 7;
 constexpr int SW_AP = 80;                  // bytes per pixel row of an A_r image (64 + 16 skew: 2-way tr reads)
 constexpr int SW_PS = 64 * SW_R * 32 + 64; // floats per block partial (padded by 256 B)
@@ -32,10 +33,10 @@ struct SWArgs {
     FastDiv dWo, dHo;
 };
 
-__global__ void __launch_bounds__(SW_NT, 1) stem_wgrad_kernel(SWArgs a) {
+__global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* const dimg = reinterpret_cast<bf16_t*>(smem);                 // [128 px][64 n], mimg_off<64>
-    char* const aimg = smem + SW_BM * 64 * 2;                              // [7][128 px][SW_AP bytes]
+    bf16_t* const dimg = reinterpret_cast<bf16_t*>(smem);                 // [96 px][64 n], mimg_off<64>
+    char* const aimg = smem + SW_BM * 64 * 2;                              // [7][96 px][SW_AP bytes]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t0 = (int)((long)blockIdx.x * a.tiles / a.G), t1 = (int)((long)(blockIdx.x + 1) * a.tiles / a.G);
     const int fm = wave & 3, kh = wave >> 2;
@@ -44,8 +45,8 @@ __global__ void __launch_bounds__(SW_NT, 1) stem_wgrad_kernel(SWArgs a) {
 #pragma unroll
     for (int r = 0; r < SW_R; ++r) acc[r] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // staging roles: dt chunks i = tid, tid + 512 (pixel i >> 3, chunk i & 7); A: pixel tid >> 2, channel tid & 3,
-    // all 7 filter rows
+    // staging roles: dt chunks i = tid, tid + 512 (pixel i >> 3, chunk i & 7; i < 768); A: pixel tid >> 2 (< 96),
+    // channel tid & 3, all 7 filter rows
     u16x8_t rd[2], ra[SW_R];
     uint32_t okm = 0;                          // bits 0-1: dt chunk valid (masked at the LDS store)
     const long plane = (long)a.H * a.W;
@@ -55,11 +56,11 @@ __global__ void __launch_bounds__(SW_NT, 1) stem_wgrad_kernel(SWArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + j * SW_NT, p = p0 + (i >> 3);
-            const bool ok = p < a.P;
+            const bool ok = p < a.P && i < SW_BM * 8;
             rd[j] = *reinterpret_cast<const u16x8_t*>(a.dt + (long)(ok ? p : plast) * 64 + (i & 7) * 8);
             okm = ok ? (okm | (1u << j)) : (okm & ~(1u << j));
         }
-        const int p = min(p0 + (tid >> 2), plast), c = tid & 3;
+        const int p = min(p0 + min(tid >> 2, SW_BM - 1), plast), c = tid & 3;
         const int q = (int)fdiv((uint32_t)p, a.dWo);
         const int ox = p - q * a.Wo;
         const int img = (int)fdiv((uint32_t)q, a.dHo);
@@ -86,12 +87,15 @@ __global__ void __launch_bounds__(SW_NT, 1) stem_wgrad_kernel(SWArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + j * SW_NT;
-            *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(rd[j], (okm >> j) & 1);
+            if (i < SW_BM * 8)
+                *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(rd[j], (okm >> j) & 1);
         }
         // the A values are finite for every pixel (clamped to the last one): dt's zero rows cancel them
+        if (tid < SW_BM * 4) {
 #pragma unroll
-        for (int r = 0; r < SW_R; ++r)
-            *reinterpret_cast<u16x8_t*>(aimg + (r * SW_BM + (tid >> 2)) * SW_AP + (tid & 3) * 16) = ra[r];
+            for (int r = 0; r < SW_R; ++r)
+                *reinterpret_cast<u16x8_t*>(aimg + (r * SW_BM + (tid >> 2)) * SW_AP + (tid & 3) * 16) = ra[r];
+        }
     };
 
     // transpose-read coordinates: rows (pixels) k = 32 ks + 8 g + q (+4), columns (k index) 16 kh + 4 pq .. +3
@@ -178,7 +182,7 @@ FastDiv sw_fdiv(uint32_t d) {
 
 int sw_blocks(long P) {
     const long tiles = (P + SW_BM - 1) / SW_BM;
-    return (int)(tiles < 256 ? tiles : 256);
+    return (int)(tiles < 512 ? tiles : 512);     // two per CU
 }
 }  // namespace
 
