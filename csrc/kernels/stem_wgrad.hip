@@ -27,17 +27,35 @@ constexpr int SW_PS = 64 * SW_R * 32 + 64; // floats per block partial (padded b
 
 struct SWArgs {
     const bf16_t* x;     // [Nimg][3][H][W]
-    const bf16_t* dt;    // [P][64]
+    const bf16_t* dt;    // [P][64]; with PRE: the max-pool gradient ga, dt = bn_bwd_apply(ga, t) (mask mode 2)
     float* ws;           // partials
     int H, W, Ho, Wo, P, tiles, G;
     FastDiv dWo, dHo;
+    // PRE: the stem BatchNorm's backward apply fused into the dt staging (dt never materialised)
+    const bf16_t* t;     // [P][64] BN input
+    const float *mean, *invstd, *gamma, *dgamma, *dbeta, *mscale, *mshift;
 };
 
+template <bool PRE>
 __global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const dimg = reinterpret_cast<bf16_t*>(smem);                 // [96 px][64 n], mimg_off<64>
     char* const aimg = smem + SW_BM * 64 * 2;                              // [7][96 px][SW_AP bytes]
+    float* const coef = reinterpret_cast<float*>(aimg + SW_R * SW_BM * SW_AP);   // PRE: [5][64] k, A, B, ms, mh
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if constexpr (PRE) {
+        if (tid < 64) {
+            const float invL = (float)(1.0 / (double)a.P);
+            const float is = a.invstd[tid], k = (a.gamma ? a.gamma[tid] : 1.f) * is;
+            const float dg = a.dgamma[tid] * invL, db = a.dbeta[tid] * invL;
+            coef[tid] = k;
+            coef[64 + tid] = -k * is * dg;
+            coef[128 + tid] = k * (a.mean[tid] * is * dg - db);
+            coef[192 + tid] = a.mscale[tid];
+            coef[256 + tid] = a.mshift[tid];
+        }
+        __syncthreads();
+    }
     const int t0 = (int)((long)blockIdx.x * a.tiles / a.G), t1 = (int)((long)(blockIdx.x + 1) * a.tiles / a.G);
     const int fm = wave & 3, kh = wave >> 2;
 
@@ -47,7 +65,7 @@ __global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
 
     // staging roles: dt chunks i = tid, tid + 512 (pixel i >> 3, chunk i & 7; i < 768); A: pixel tid >> 2 (< 96),
     // channel tid & 3, all 7 filter rows
-    u16x8_t rd[2], ra[SW_R];
+    u16x8_t rd[2], ra[SW_R], rt[PRE ? 2 : 1];
     uint32_t okm = 0;                          // bits 0-1: dt chunk valid (masked at the LDS store)
     const long plane = (long)a.H * a.W;
     auto load_regs = [&](int t) {
@@ -58,6 +76,7 @@ __global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
             const int i = tid + j * SW_NT, p = p0 + (i >> 3);
             const bool ok = p < a.P && i < SW_BM * 8;
             rd[j] = *reinterpret_cast<const u16x8_t*>(a.dt + (long)(ok ? p : plast) * 64 + (i & 7) * 8);
+            if constexpr (PRE) rt[j] = *reinterpret_cast<const u16x8_t*>(a.t + (long)(ok ? p : plast) * 64 + (i & 7) * 8);
             okm = ok ? (okm | (1u << j)) : (okm & ~(1u << j));
         }
         const int p = min(p0 + min(tid >> 2, SW_BM - 1), plast), c = tid & 3;
@@ -87,8 +106,22 @@ __global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + j * SW_NT;
-            if (i < SW_BM * 8)
-                *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(rd[j], (okm >> j) & 1);
+            if (i < SW_BM * 8) {
+                u16x8_t v = rd[j];
+                if constexpr (PRE) {     // dt = k * gm + A * t + B, gm = ga * [t * ms + mh > 0] (bn_bwd_apply mode 2)
+                    const float* cf = coef + (i & 7) * 8;
+                    float gm[8], tv[8], o[8];
+                    unpack8(rd[j], gm);
+                    unpack8(rt[j], tv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float g0 = fmaf(tv[e], cf[192 + e], cf[256 + e]) > 0.f ? gm[e] : 0.f;
+                        o[e] = fmaf(cf[e], g0, fmaf(tv[e], cf[64 + e], cf[128 + e]));
+                    }
+                    v = pack8(o);
+                }
+                *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(v, (okm >> j) & 1);
+            }
         }
         // the A values are finite for every pixel (clamped to the last one): dt's zero rows cancel them
         if (tid < SW_BM * 4) {
@@ -190,25 +223,35 @@ int sw_blocks(long P) {
 PDNN_API int pdnn_stem_wgrad_ws(int Nimg, int Ho, int Wo) { return sw_blocks((long)Nimg * Ho * Wo) * SW_PS; }
 
 // dw32 [64][7][32] fp32 (overwritten; k = c*8 + j as pdnn_stem_conv_nchw's weight) = weight gradient of the
-// NCHW stem given dt [Nimg*Ho*Wo][64] bf16 (the gradient w.r.t. its output)
+// NCHW stem given dt [Nimg*Ho*Wo][64] bf16 (the gradient w.r.t. its output).  t != null: `dt` is the gradient
+// ga of the stem's BN+ReLU output and the BN backward apply (mode 2: ReLU mask recomputed from t) runs in the
+// staging, so dt is never written.
 PDNN_API int pdnn_stem_wgrad_nchw(const bf16_t* x, const bf16_t* dt, float* dw32, int Nimg, int H, int W, int Ho,
-                                  int Wo, float* ws, hipStream_t st) {
+                                  int Wo, float* ws, const bf16_t* t, const float* mean, const float* invstd,
+                                  const float* gamma, const float* dgamma, const float* dbeta, const float* mscale,
+                                  const float* mshift, hipStream_t st) {
     if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || W % 2 || W < 8 || !ws ||
         (long)Nimg * Ho * Wo >= (1L << 31))
         return (int)hipErrorInvalidValue;
+    const bool pre = t != nullptr;
+    if (pre && !(mean && invstd && dgamma && dbeta && mscale && mshift)) return (int)hipErrorInvalidValue;
     SWArgs a{};
     a.x = x; a.dt = dt; a.ws = ws;
     a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.P = Nimg * Ho * Wo;
     a.tiles = (int)cdiv(a.P, SW_BM);
     a.G = sw_blocks(a.P);
     a.dWo = sw_fdiv(Wo); a.dHo = sw_fdiv(Ho);
-    const int sm = SW_BM * 64 * 2 + SW_R * SW_BM * SW_AP;
+    a.t = t; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.dgamma = dgamma; a.dbeta = dbeta;
+    a.mscale = mscale; a.mshift = mshift;
+    const int sm = SW_BM * 64 * 2 + SW_R * SW_BM * SW_AP + (pre ? 5 * 64 * 4 : 0);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, sm + 5 * 64 * 4);
+        (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, sm + 5 * 64 * 4);
         attr = true;
     }
-    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(a.G), dim3(SW_NT), sm, st, a);
+    if (pre) hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(a.G), dim3(SW_NT), sm, st, a);
+    else hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(a.G), dim3(SW_NT), sm, st, a);
     const int e = (int)hipGetLastError();
     if (e) return e;
     hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((64 * SW_R * 32 / 4 + 7) / 8), dim3(256), 0, st,

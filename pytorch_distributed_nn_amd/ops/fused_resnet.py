@@ -594,6 +594,18 @@ class StemFn(torch.autograd.Function):
         P = ctx.params
         ctx.params = None
         sink = _Sink()
+        if ctx.nchw_wgrad and mb is None:
+            # the BN backward's apply runs inside the NCHW weight-gradient kernel's staging: dt never written
+            slab, _, rows = K.bn_bwd_reduce(ga.view(-1, C), t.view(-1, C), m, i, mode=2, msrc=t.view(-1, C), mscale=s,
+                                           mshift=h)
+            (dg_, db_), (dg, db) = sink.bn(slab, rows, P[1], P[2])
+            dw = K.stem_wgrad_nchw(x, ga, pre=(t, m, i, gamma, dg_, db_, s, h))
+            acc = sink.acc(P[0])
+            if acc is not None:
+                acc[0].add_(dw)
+                dw = None
+            sink.done()
+            return None, None, None, None, dw, dg, db
         if mb is None:          # direct stem: ReLU mask recomputed from t (t * s + h > 0)
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 2, msrc=t.view(-1, C), msc=s, msh=h,
                                   sink=sink, bn_params=(P[1], P[2]))
@@ -601,15 +613,6 @@ class StemFn(torch.autograd.Function):
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
                                   bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
-        if ctx.nchw_wgrad:
-            # x is the NCHW batch: the direct NCHW weight-gradient kernel
-            dw = K.stem_wgrad_nchw(x, dt)
-            acc = sink.acc(P[0])
-            if acc is not None:
-                acc[0].add_(dw)
-                dw = None
-            sink.done()
-            return None, None, None, None, dw, dg, db
         if ctx.ev is not None:
             torch.cuda.current_stream(x.device).wait_event(ctx.ev)     # NHWC copy made on the side stream
             ctx.ev = None

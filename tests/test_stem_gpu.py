@@ -156,3 +156,22 @@ def test_stem_wgrad_nchw_matches_fp32(K, shape):
     dw = K.stem_wgrad_nchw(x, dt.contiguous())
     assert dw.shape == (64, 3, 7, 7)
     assert rel(dw, w.grad) < 5e-3, rel(dw, w.grad)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64), (3, 30, 18)])
+def test_stem_wgrad_nchw_fused_bn_apply(K, shape):
+    """The BN-backward apply (mask mode 2) inside the NCHW stem weight-gradient staging == apply pass + kernel."""
+    N, H, W = shape
+    x = torch.randn(N, 3, H, W, device="cuda").to(BF)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    ga = torch.randn(N, Ho, Wo, 64, device="cuda").to(BF)
+    t = torch.randn(N, Ho, Wo, 64, device="cuda").to(BF)
+    mean, inv = torch.randn(64, device="cuda") * 0.1, torch.rand(64, device="cuda") + 0.5
+    gamma = torch.rand(64, device="cuda") + 0.5
+    dg, db = torch.randn(64, device="cuda") * 50, torch.randn(64, device="cuda") * 50
+    s, h = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.3
+    dt = K.bn_bwd_apply(ga.view(-1, 64), t.view(-1, 64), mean, inv, gamma, dg, db, mode=2, msrc=t.view(-1, 64),
+                        mscale=s, mshift=h)[0].view_as(ga)
+    ref = K.stem_wgrad_nchw(x, dt)
+    out = K.stem_wgrad_nchw(x, ga, pre=(t, mean, inv, gamma, dg, db, s, h))
+    assert rel(out, ref) < 1e-5, rel(out, ref)
