@@ -156,6 +156,101 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16_t* __restric
     }
 }
 
+// ResNet stem backward, max-pool gather + the BatchNorm-backward statistics in one pass (3x3 / s2 / p1
+// window, even H = 2*Ho, W = 2*Wo).  A thread owns the 2x2 input patch (2ho..2ho+1, 2wo..2wo+1) of one
+// 8-channel group: those four pixels receive only from outputs (ho..ho+1, wo..wo+1) — 4 dy / idx loads per
+// 4 pixels instead of ~9 — so the patch's 4 dy, 4 idx and 4 pre-BN t loads all issue together.  It writes
+// ga = the pooled gradient (bf16) and accumulates the BN-backward sums of mask mode 2 (gm = ga where
+// t*mscale + mshift > 0): sum(gm), sum(gm * (t - mean) * invstd), per-block partial rows in the slab layout
+// of bn_bwd_reduce ([rows][2][C]).  Replaces maxpool_bwd (write ga) + bn_bwd_reduce<2> (read ga and t
+// again) on the serial tail of the ResNet backward.
+__global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+    const bf16_t* __restrict__ tin, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ mscale, const float* __restrict__ mshift, float* __restrict__ slab, int N, int Ho,
+    int Wo, int C) {
+    __shared__ float red[2][NT * 8];
+    const int CG = C >> 3, W = 2 * Wo;
+    const int total = N * Ho * Wo * CG;
+    const int t0 = blockIdx.x * NT + threadIdx.x;
+    const int cg = t0 % CG;                              // fixed per thread: the grid stride is a multiple of CG
+    float mu[8], is[8], ms[8], mh[8], s[8], q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = cg * 8 + j;
+        mu[j] = mean[c]; is[j] = invstd[c]; ms[j] = mscale[c]; mh[j] = mshift[c];
+        s[j] = 0.f; q[j] = 0.f;
+    }
+    for (int i = t0; i < total; i += gridDim.x * NT) {
+        int r = i / CG;
+        const int wo = r % Wo; r /= Wo;
+        const int ho = r % Ho;
+        const int n = r / Ho;
+        const bool wn = wo + 1 < Wo, hn = ho + 1 < Ho;
+        uint2 pk[2][2];
+        u16x8_t gv[2][2], tv[2][2];
+#pragma unroll
+        for (int da = 0; da < 2; ++da)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const long o = ((long)(n * Ho + ho + da) * Wo + wo + db) * C + cg * 8;
+                const bool ok = (da == 0 || hn) && (db == 0 || wn);
+                pk[da][db] = make_uint2(0xffffffffu, 0xffffffffu);    // no window index matches 0xff
+                gv[da][db] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+                if (ok) {
+                    pk[da][db] = *reinterpret_cast<const uint2*>(idx + o);
+                    gv[da][db] = *reinterpret_cast<const u16x8_t*>(dy + o);
+                }
+                tv[da][db] = *reinterpret_cast<const u16x8_t*>(
+                    tin + ((long)(n * 2 * Ho + 2 * ho + da) * W + 2 * wo + db) * C + cg * 8);
+            }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                // pixel (2ho+a, 2wo+b) receives from output (ho+da, wo+db) at window row a+1-2da (col b+1-2db):
+                // da = 0 always (row a+1), da = 1 only for a = 1 (row 0)
+                float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int da = 0; da <= a; ++da)
+#pragma unroll
+                    for (int db = 0; db <= b; ++db) {
+                        const uint32_t want = (uint32_t)((a + 1 - 2 * da) * 3 + (b + 1 - 2 * db));
+                        float g[8];
+                        unpack8(gv[da][db], g);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const uint32_t word = j < 4 ? pk[da][db].x : pk[da][db].y;
+                            if (((word >> (8 * (j & 3))) & 0xffu) == want) acc[j] += g[j];
+                        }
+                    }
+                const u16x8_t packed = pack8(acc);
+                *reinterpret_cast<u16x8_t*>(dx + ((long)(n * 2 * Ho + 2 * ho + a) * W + 2 * wo + b) * C + cg * 8) =
+                    packed;
+                float g[8], tv8[8];
+                unpack8(packed, g);                          // the stored (bf16) gradient, as a separate pass reads it
+                unpack8(tv[a][b], tv8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float gm = fmaf(tv8[j], ms[j], mh[j]) > 0.f ? g[j] : 0.f;
+                    s[j] += gm;
+                    q[j] += gm * (tv8[j] - mu[j]) * is[j];
+                }
+            }
+    }
+    const int t = threadIdx.x, RPI = NT / CG;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][t * 8 + j] = s[j]; red[1][t * 8 + j] = q[j]; }
+    __syncthreads();
+    for (int cc = t; cc < C; cc += NT) {
+        const int gg = cc >> 3, j = cc & 7;
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + gg) * 8 + j]; b += red[1][(k * CG + gg) * 8 + j]; }
+        slab[(long)(2 * blockIdx.x) * C + cc] = a;
+        slab[(long)(2 * blockIdx.x + 1) * C + cc] = b;
+    }
+}
+
 // Global average pool [N][HW][C] -> [N][C] (fp32 accumulate).  One block per (n, 2048-channel slab).
 __global__ void __launch_bounds__(NT) avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          int HW, int C) {
@@ -226,6 +321,28 @@ PDNN_API int pdnn_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
     else
         hipLaunchKernelGGL((maxpool_bwd_kernel<0, 0>), dim3(stream_grid(work, NT)), dim3(NT), 0, s, dy, idx, dx, N, H, W,
                            C, Ho, Wo, k, st, pad);
+    PDNN_LAUNCH_RET;
+}
+
+// partial rows of the fused stem max-pool backward's BN slab ([rows][2][C] floats); 0 = shape unsupported
+PDNN_API int pdnn_maxpool_bwd_bnred_rows(int N, int Ho, int Wo, int C) {
+    if (C % 8 || C > 2048 || NT % (C / 8)) return 0;
+    if ((long)N * 4 * Ho * Wo * C >= (1L << 31)) return 0;
+    const long work = (long)N * Ho * Wo * (C / 8);
+    long g = (work + NT - 1) / NT;
+    return (int)(g < 1 ? 1 : g > 768 ? 768 : g);         // one wave of blocks: 140 VGPRs = 3 blocks per CU
+}
+
+// dy [N][Ho][Wo][C], idx its window bytes, t [N][2Ho][2Wo][C] (pre-BN) -> dx (pooled gradient, same shape
+// as t) + the mode-2 BN-backward slab (pdnn_maxpool_bwd_bnred_rows rows).  3x3 / s2 / p1 window only.
+PDNN_API int pdnn_maxpool_bwd_bnred(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, const bf16_t* t,
+                                    const float* mean, const float* invstd, const float* mscale,
+                                    const float* mshift, float* slab, int N, int Ho, int Wo, int C,
+                                    hipStream_t s) {
+    const int rows = pdnn_maxpool_bwd_bnred_rows(N, Ho, Wo, C);
+    if (!rows) return 2;
+    hipLaunchKernelGGL(maxpool_bwd_bnred_kernel, dim3(rows), dim3(NT), 0, s, dy, idx, dx, t, mean, invstd, mscale,
+                       mshift, slab, N, Ho, Wo, C);
     PDNN_LAUNCH_RET;
 }
 

@@ -83,6 +83,8 @@ _SIGS = {
     "pdnn_bn_bwd_apply": [P, P, L, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_maxpool_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],
     "pdnn_maxpool_bwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "pdnn_maxpool_bwd_bnred": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "pdnn_maxpool_bwd_bnred_rows": [I, I, I, I],
     "pdnn_avgpool_fwd": [P, P, I, I, I, P],
     "pdnn_avgpool_bwd": [P, P, I, I, I, P],
     "pdnn_xent_fwd": [P, L, I, I, P, I, P, P, P, P, I, P],

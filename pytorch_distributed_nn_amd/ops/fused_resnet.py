@@ -589,15 +589,20 @@ class StemFn(torch.autograd.Function):
         x, t, mb, idx, m, i, gamma, s, h = ctx.saved_tensors
         stride, pad, pool, wshape, kshape = ctx.conf
         gy = gy.contiguous()
-        ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy
         C = t.shape[-1]
         P = ctx.params
         ctx.params = None
         sink = _Sink()
         if ctx.nchw_wgrad and mb is None:
-            # the BN backward's apply runs inside the NCHW weight-gradient kernel's staging: dt never written
-            slab, _, rows = K.bn_bwd_reduce(ga.view(-1, C), t.view(-1, C), m, i, mode=2, msrc=t.view(-1, C), mscale=s,
-                                           mshift=h)
+            # the BN backward's apply runs inside the NCHW weight-gradient kernel's staging: dt never written;
+            # its statistics come out of the max-pool gather's pass
+            fused = K.maxpool_bwd_bnred(gy, idx, t, m, i, s, h) if pool and tuning.get("pool_bnred") else None
+            if fused is not None:
+                ga, slab, rows = fused
+            else:
+                ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy
+                slab, _, rows = K.bn_bwd_reduce(ga.view(-1, C), t.view(-1, C), m, i, mode=2, msrc=t.view(-1, C),
+                                               mscale=s, mshift=h)
             (dg_, db_), (dg, db) = sink.bn(slab, rows, P[1], P[2])
             dw = K.stem_wgrad_nchw(x, ga, pre=(t, m, i, gamma, dg_, db_, s, h))
             acc = sink.acc(P[0])
@@ -606,6 +611,7 @@ class StemFn(torch.autograd.Function):
                 dw = None
             sink.done()
             return None, None, None, None, dw, dg, db
+        ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy
         if mb is None:          # direct stem: ReLU mask recomputed from t (t * s + h > 0)
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 2, msrc=t.view(-1, C), msc=s, msh=h,
                                   sink=sink, bn_params=(P[1], P[2]))

@@ -659,6 +659,24 @@ def maxpool_bwd(dy, idx, x_shape, k, st, pad):
     return dx
 
 
+def maxpool_bwd_bnred(dy, idx, t, mean, invstd, mscale, mshift):
+    """Stem backward: 3x3/s2/p1 max-pool gather fused with the mode-2 BN-backward reduce (mask = t*mscale +
+    mshift > 0).  -> (ga [N,2Ho,2Wo,C], slab, rows) like maxpool_bwd + bn_bwd_reduce(mode=2); None when the
+    shape is not covered (odd H/W, C not dividing the block)."""
+    N, H, W, C = t.shape
+    _, Ho, Wo, _ = dy.shape
+    if H != 2 * Ho or W != 2 * Wo:
+        return None
+    rows = lib().pdnn_maxpool_bwd_bnred_rows(N, Ho, Wo, C)
+    if rows <= 0:
+        return None
+    ga = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
+    slab = torch.empty(2 * rows, C, device=dy.device, dtype=F32)
+    call("pdnn_maxpool_bwd_bnred", ptr(dy.contiguous()), ptr(idx), ptr(ga), ptr(t), ptr(mean), ptr(invstd),
+         ptr(mscale), ptr(mshift), ptr(slab), N, Ho, Wo, C, stream())
+    return ga, slab, rows
+
+
 def avgpool_fwd(x):
     _bf16_c(x, "avgpool.x")
     N, H, W, C = x.shape

@@ -175,3 +175,32 @@ def test_stem_wgrad_nchw_fused_bn_apply(K, shape):
     ref = K.stem_wgrad_nchw(x, dt)
     out = K.stem_wgrad_nchw(x, ga, pre=(t, mean, inv, gamma, dg, db, s, h))
     assert rel(out, ref) < 1e-5, rel(out, ref)
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 16, 10, 64), (1, 2, 2, 16), (2, 8, 6, 8)])
+def test_maxpool_bwd_bnred_matches_two_passes(K, shape):
+    """The stem's fused max-pool gather + mode-2 BN-backward reduce (pool.hip maxpool_bwd_bnred_kernel): the
+    pooled gradient is bitwise maxpool_bwd's, the summed slab matches bn_bwd_reduce(mode=2) on it."""
+    N, H, W, C = shape
+    t = torch.randn(N, H, W, C, device="cuda").to(BF)
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.5
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    y, idx = K.bn_relu_maxpool(t, sc, sh)
+    gy = torch.randn_like(y.float()).to(BF)
+    ga_ref = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1)
+    slab_ref, _, rows_ref = K.bn_bwd_reduce(ga_ref.view(-1, C), t.view(-1, C), mean, inv, mode=2,
+                                            msrc=t.view(-1, C), mscale=sc, mshift=sh)
+    out = K.maxpool_bwd_bnred(gy, idx, t, mean, inv, sc, sh)
+    assert out is not None
+    ga, slab, rows = out
+    assert torch.equal(ga, ga_ref)
+    a = slab.view(rows, 2, C).double().sum(0)
+    b = slab_ref.view(rows_ref, 2, C).double().sum(0)
+    torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+
+
+def test_maxpool_bwd_bnred_declines_odd_sizes(K):
+    t = torch.randn(1, 9, 8, 64, device="cuda").to(BF)
+    y, idx = K.bn_relu_maxpool(t, torch.ones(64, device="cuda"), torch.zeros(64, device="cuda"))
+    z = torch.zeros(64, device="cuda")
+    assert K.maxpool_bwd_bnred(y, idx, t, z, z, z, z) is None

@@ -42,6 +42,26 @@ def main():
         for g in sorted(gaps, reverse=True)[:5]:
             print(f"   gap {g[0] / 1e3:7.1f} us  after {g[1]}  before {g[2]}")
     main_q = max(by, key=lambda q: len(by[q]))
+    # classify the compute stream's gaps: "dep" = the next kernel starts within 4 us of another stream's
+    # kernel ending (an event wait on it), "idle" = nothing else was running during the gap (host / launch
+    # bound), else "overlap" (another stream busy, no visible dependency)
+    others = [k for k in step if k["q"] != main_q]
+    cls = defaultdict(lambda: [0, 0])
+    kk = by[main_q]
+    for a_, b_ in zip(kk, kk[1:]):
+        g = b_["s"] - a_["e"]
+        if g <= 0:
+            continue
+        if any(0 <= b_["s"] - o["e"] <= 4000 for o in others):
+            c = "dep"
+        elif not any(o["s"] < b_["s"] and o["e"] > a_["e"] for o in others):
+            c = "idle"
+        else:
+            c = "overlap"
+        cls[c][0] += g
+        cls[c][1] += 1
+    print("compute-stream gaps by cause: " + ", ".join(f"{c} {t / 1e3:.1f} us ({n})" for c, (t, n) in
+                                                      sorted(cls.items())))
     agg = defaultdict(lambda: [0, 0])
     for k in by[main_q]:
         agg[k["n"][:100]][0] += k["e"] - k["s"]
