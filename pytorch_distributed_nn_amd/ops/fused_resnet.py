@@ -118,7 +118,7 @@ class _Sink:
         if self.side is None:
             return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
         main = torch.cuda.current_stream(x.device)
-        self.side.wait_stream(main)
+        K.stream_wait(self.side, main)
         self.forked = True
         with torch.cuda.stream(self.side):
             g = self._wgrad(w_p, x, dy, R, S, st, pad, pro)
@@ -147,7 +147,7 @@ class _Sink:
                 # stream): join before announcing them.  Side-aware hooks (DDP bucket launches) order their
                 # collectives after the side stream themselves (side_stream_if_active), so the compute
                 # stream is not held up.
-                torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+                K.stream_wait(torch.cuda.current_stream(self.side.device), self.side)
             else:
                 # nothing reads them before the optimizer: join once at the end of the backward, so a block's
                 # last weight gradients also overlap the next block's data-gradient chain
@@ -159,7 +159,7 @@ class _Sink:
 def _join_at_backward_end(side):
     # one callback per block (not a shared "already queued" flag, which an aborted backward would leave set)
     def join():
-        torch.cuda.current_stream(side.device).wait_stream(side)
+        K.stream_wait(torch.cuda.current_stream(side.device), side)
     torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
@@ -210,7 +210,7 @@ def _prep_dgrad_weights(x, specs):
     if side is None or not tuning.get("wprep"):
         return None
     main = torch.cuda.current_stream(x.device)
-    side.wait_stream(main)
+    K.stream_wait(side, main)
     with torch.cuda.stream(side):
         ws = [K.dgrad_weight(*sp) for sp in specs]
         ev = torch.cuda.Event()
@@ -285,7 +285,7 @@ class BottleneckFn(torch.autograd.Function):
         if side is not None:
             # the shortcut conv only depends on x: run it (and its BN statistics) beside conv1 -> conv2 -> conv3
             main = torch.cuda.current_stream(x.device)
-            side.wait_stream(main)
+            K.stream_wait(side, main)
             with torch.cuda.stream(side):
                 side_down = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]), bufs[6:8],
                                      mom, eps)
@@ -315,7 +315,7 @@ class BottleneckFn(torch.autograd.Function):
         C3 = t3.shape[-1]
         if down:
             if side_down is not None:
-                main.wait_stream(side)
+                K.stream_wait(main, side)
                 td, md, idd, sd, hd = side_down
             else:
                 td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]),

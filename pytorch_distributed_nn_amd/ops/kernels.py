@@ -659,6 +659,16 @@ def maxpool_bwd(dy, idx, x_shape, k, st, pad):
     return dx
 
 
+def stream_wait(waiter, signaler):
+    """``waiter.wait_stream(signaler)`` (same device) through a fence-free HIP event (streams.hip) when tuning
+    light_events is on: no system-scope cache write-back at each of the ~70 fork / join points of a step."""
+    if _tuning.get("light_events") and waiter.device == signaler.device:
+        with torch.cuda.device(waiter.device):
+            call("pdnn_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
+    else:
+        waiter.wait_stream(signaler)
+
+
 def maxpool_bwd_bnred(dy, idx, t, mean, invstd, mscale, mshift):
     """Stem backward: 3x3/s2/p1 max-pool gather fused with the mode-2 BN-backward reduce (mask = t*mscale +
     mshift > 0).  -> (ga [N,2Ho,2Wo,C], slab, rows) like maxpool_bwd + bn_bwd_reduce(mode=2); None when the

@@ -25,6 +25,9 @@ bn_fused_fin       1        BatchNorm slab finalize in one launch (level-1 block
                             arriver through a counter, batchnorm.hip bn_slab_fused_kernel) instead of two
 stem_wgrad_nchw    1        ImageNet stem weight gradient straight from the NCHW batch (stem_wgrad.hip) instead of the
                             implicit-GEMM im2col over a channel-padded NHWC copy
+light_events       1        cross-stream fork / join of the two-stream ResNet step through fence-free HIP events
+                            (streams.hip) instead of torch's Stream.wait_stream (system-scope release per marker);
+                            off: 10,604-10,615 vs 10,687-10,689 img/s (gpurun_out/r3_58)
 pool_bnred         1        stem backward: max-pool gather and the mode-2 BN-backward reduce in one pass
                             (pool.hip maxpool_bwd_bnred_kernel) instead of maxpool_bwd + bn_bwd_reduce
 wgrad3x3           1        3x3 / stride-1 weight gradients on the direct halo kernel (conv3x3_wgrad.hip) instead of
@@ -42,7 +45,7 @@ import os
 
 DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
             "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1, "stem_wgrad_nchw": 1,
-            "pool_bnred": 1}
+            "pool_bnred": 1, "light_events": 1}
 
 _VALUES = dict(DEFAULTS)
 
