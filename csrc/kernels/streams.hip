@@ -41,3 +41,33 @@ PDNN_API int pdnn_stream_wait(hipStream_t waiter, hipStream_t signaler) {
     if (e != hipSuccess) return (int)e;
     return (int)hipStreamWaitEvent(waiter, ev, 0);
 }
+
+// Experimental alternative fork (tools/fork_cost.py): a stream-ordered 32-bit write on `signaler` and a
+// wait-until->= on `waiter` over one word of signal memory per device (AQL barrier-value packet instead of a
+// marker + event).  Values increase monotonically per device.
+namespace {
+unsigned* g_sig[EV_DEVS];
+unsigned g_sig_next[EV_DEVS];
+}  // namespace
+
+PDNN_API int pdnn_stream_wait_value(hipStream_t waiter, hipStream_t signaler) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (dev < 0 || dev >= EV_DEVS) return (int)hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_sig[dev]) {
+        void* p = nullptr;
+        e = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory);   // signal memory: exactly 8 bytes
+        if (e != hipSuccess) return (int)e;
+        g_sig[dev] = static_cast<unsigned*>(p);
+        e = hipMemset(p, 0, 8);
+        if (e != hipSuccess) return (int)e;
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return (int)e;
+    }
+    const unsigned v = ++g_sig_next[dev];
+    e = hipStreamWriteValue32(signaler, g_sig[dev], v, 0);
+    if (e != hipSuccess) return (int)e;
+    return (int)hipStreamWaitValue32(waiter, g_sig[dev], v, hipStreamWaitValueGte, 0xffffffffu);
+}

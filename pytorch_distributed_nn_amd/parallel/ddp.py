@@ -381,7 +381,8 @@ class DistributedDataParallel(nn.Module):
         side = side_stream_if_active(self.flat.grad)
         if side is None:
             return self._launch_on(b, zero)
-        side.wait_stream(torch.cuda.current_stream(side.device))
+        from ..ops import kernels as K
+        K.stream_wait(side, torch.cuda.current_stream(side.device))
         with torch.cuda.stream(side):
             return self._launch_on(b, zero)
 
