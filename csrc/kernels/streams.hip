@@ -42,9 +42,10 @@ PDNN_API int pdnn_stream_wait(hipStream_t waiter, hipStream_t signaler) {
     return (int)hipStreamWaitEvent(waiter, ev, 0);
 }
 
-// Experimental alternative fork (tools/fork_cost.py): a stream-ordered 32-bit write on `signaler` and a
-// wait-until->= on `waiter` over one word of signal memory per device (AQL barrier-value packet instead of a
-// marker + event).  Values increase monotonically per device.
+// Experimental alternative fork (tools/fork_cost.py only): a stream-ordered 32-bit write on `signaler` and a
+// wait-until->= on `waiter` over one word of signal memory per device.  Values increase monotonically per
+// device.  Cheaper than an event in the tiny-kernel microbenchmark (11.7 vs 12.4 us per link), but the
+// ResNet-50 step ran 6-7% slower with it (gpurun_out/r3_61): not used by the framework.
 namespace {
 unsigned* g_sig[EV_DEVS];
 unsigned g_sig_next[EV_DEVS];
