@@ -100,7 +100,6 @@ class _Sink:
         self.side = _side_stream(device) if device is not None else None
         self.forked = False
         self.returned = False
-        self.pending = []           # deferred weight gradients: issued with the next fork (one marker for both)
 
     def acc(self, *ps):
         tg = [direct_grad(p) for p in ps]
@@ -115,19 +114,13 @@ class _Sink:
         dg, db = K.bn_bwd_finalize(slab, rows, acc=acc)
         return (dg, db), ((None, None) if acc is not None else (dg, db))
 
-    def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None, defer=False):
-        """defer: hold this (arena-accumulated) weight gradient back until the next fork of this block, so
-        the two share one cross-stream marker (~9 us on the compute stream each, tools/fork_cost.py)."""
+    def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
         if self.side is None:
             return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
-        if defer and direct_grad(w_p) is not None:
-            self.pending.append((w_p, x, dy, R, S, st, pad, pro))
-            return None
         return self._fork([(w_p, x, dy, R, S, st, pad, pro)])
 
     def _fork(self, jobs):
-        jobs = self.pending + jobs
-        self.pending = []
+        # (holding a weight gradient back to share the next fork's marker measured neutral: gpurun_out/r3_60)
         main = torch.cuda.current_stream(jobs[0][1].device)
         K.stream_wait(self.side, main)
         self.forked = True
@@ -154,8 +147,6 @@ class _Sink:
         return _krsc_grad(K.conv_wgrad(x, dy, R, S, st, pad, pro=pro))
 
     def done(self):
-        if self.pending:
-            self._fork([])
         if self.forked:
             self.forked = False
             if self.returned or not all(getattr(fn, "_pdnn_side_aware", False)
@@ -179,13 +170,14 @@ _JOINED = {}      # device index -> forks covered by the last end-of-backward jo
 
 def _join_at_backward_end(side):
     # one callback per block (not a shared "already queued" flag, which an aborted backward would leave set);
-    # the first to run joins every fork issued so far, the rest find nothing new and add no marker (tuning
-    # join_once; the callbacks all run after the last backward node, so the first join covers them all)
+    # the first to run joins every fork issued so far, the rest find nothing new and add no marker (the
+    # callbacks all run after the last backward node, so the first join covers them all; one join per block
+    # instead: -0.3%, gpurun_out/r3_60)
     dev = side.device.index
 
     def join():
         n = _FORKS.get(dev, 0)
-        if tuning.get("join_once") and _JOINED.get(dev) == n:
+        if _JOINED.get(dev) == n:
             return
         K.stream_wait(torch.cuda.current_stream(side.device), side)
         _JOINED[dev] = n
@@ -422,11 +414,10 @@ class BottleneckFn(torch.autograd.Function):
                 dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
         # conv3 (input = relu(bn2(t2)), virtual)
-        merge = tuning.get("fork_merge") == 1
         if a2 is not None:
-            dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0, defer=merge)
+            dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
         else:
-            dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2), defer=merge)
+            dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
         bn1 = (t1, m1, i1, s1, h1)
         if _pre_ok(t2, k2, stride, 1):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad

@@ -29,12 +29,9 @@ light_events       1        cross-stream fork / join of the two-stream ResNet st
                             (streams.hip) instead of torch's Stream.wait_stream (system-scope release per marker);
                             off: 10,604-10,615 vs 10,687-10,689 img/s (gpurun_out/r3_58); DDP path (bucket launches
                             fork too) 10,574-10,586 vs 10,692-10,695 (r3_60)
-fork_merge         0        Bottleneck backward: conv3's weight gradient held back to conv2's fork (one cross-stream
-                            marker instead of two per block); on: 10,840-10,857 vs 10,843-10,867 img/s (r3_60)
-join_once          1        end of the ResNet backward: one compute-stream join with the side stream instead of one per
-                            block; off: 10,818-10,827 vs 10,843-10,867 img/s (gpurun_out/r3_60)
 pool_bnred         1        stem backward: max-pool gather and the mode-2 BN-backward reduce in one pass
-                            (pool.hip maxpool_bwd_bnred_kernel) instead of maxpool_bwd + bn_bwd_reduce
+                            (pool.hip maxpool_bwd_bnred_kernel) instead of maxpool_bwd + bn_bwd_reduce;
+                            off: 10,644-10,656 vs 10,718-10,720 img/s (gpurun_out/r3_57)
 wgrad3x3           1        3x3 / stride-1 weight gradients on the direct halo kernel (conv3x3_wgrad.hip) instead of
                             the implicit-GEMM engine
 wprep              1        the data gradients' transformed weights (flipped 3x3, transposed 1x1) made in the forward
@@ -50,7 +47,7 @@ import os
 
 DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
             "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1, "stem_wgrad_nchw": 1,
-            "pool_bnred": 1, "light_events": 1, "fork_merge": 0, "join_once": 1}
+            "pool_bnred": 1, "light_events": 1}
 
 _VALUES = dict(DEFAULTS)
 

@@ -181,14 +181,15 @@ def _kofn(rank, world, k, sleep_ms, steps):
 
 
 def test_kofn_kill_straggler_short_circuits_and_averages_by_count():
-    """World 4, k = 3: rank 3 sleeps 20 ms per parameter (16 parameters: a 320 ms backward).  Once three
+    """World 4, k = 3: rank 3 sleeps 40 ms per parameter (16 parameters: a 640 ms backward).  Once three
     ranks finished, rank 3 abandons its backward; every bucket is averaged over the ranks that sent real
     gradients for it."""
-    out = run_world(_kofn, 4, (3, 20.0, 3), timeout=240)
+    out = run_world(_kofn, 4, (3, 40.0, 3), timeout=240)
     slow = out[3]
     assert all(a for a, _, _, _ in slow), slow                   # short-circuited every step
-    # far below the 0.32 s full backward (step 0 pays gloo's lazy connection setup on the fast ranks)
-    assert max(dt for _, dt, _, _ in slow[1:]) < 0.2, slow
+    # far below the 0.64 s full backward (step 0 pays gloo's lazy connection setup on the fast ranks; the
+    # margin leaves room for a loaded CI host, where 0.2 s against a 0.32 s backward flaked)
+    assert max(dt for _, dt, _, _ in slow[1:]) < 0.45, slow
     for r in range(4):
         for aborted, dt, err, counts in out[r]:
             assert err < 1e-5, (r, err)
