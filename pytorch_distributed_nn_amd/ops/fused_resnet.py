@@ -172,7 +172,8 @@ def _join_at_backward_end(side):
     # one callback per block (not a shared "already queued" flag, which an aborted backward would leave set);
     # the first to run joins every fork issued so far, the rest find nothing new and add no marker (the
     # callbacks all run after the last backward node, so the first join covers them all; one join per block
-    # instead: -0.3%, gpurun_out/r3_60)
+    # instead: -0.3%, gpurun_out/r3_60).  A final callback runs with backward()'s caller stream current (the
+    # stream the optimizer step follows on: tools/callback_stream_probe.py, gpurun_out/r3_64)
     dev = side.device.index
 
     def join():
