@@ -93,13 +93,16 @@ __global__ void __launch_bounds__(NT) xent_bwd_kernel(const T* __restrict__ logi
                                                       const int64_t* __restrict__ labels, int ignore,
                                                       const float* __restrict__ lse,
                                                       const float* __restrict__ gscale, float denom,
+                                                      const float* __restrict__ count,
                                                       T* __restrict__ dlogits, long ldd) {
     const long row = blockIdx.x;
     const T* x = logits + row * ld;
     T* d = dlogits + row * ldd;
     const int64_t y = labels[row];
     const bool ign = (y == ignore || y < 0 || y >= V);
-    const float sc = ign ? 0.f : (*gscale) / denom;
+    // count (optional): the forward's device-side count of non-ignored rows (mean reduction), so the caller
+    // needs no scalar kernels to form g / max(count, 1)
+    const float sc = ign ? 0.f : (*gscale) / (count ? fmaxf(*count, 1.f) : denom);
     const float l = lse[row];
     if (VEC) {
         const u16x8_t* x8 = reinterpret_cast<const u16x8_t*>(x);
@@ -146,18 +149,18 @@ PDNN_API int pdnn_xent_fwd(const void* logits, long ld, int rows, int V, const i
 }
 
 PDNN_API int pdnn_xent_bwd(const void* logits, long ld, int rows, int V, const int64_t* labels, int ignore,
-                           const float* lse, const float* gscale, float denom, void* dlogits, long ldd, int dtype,
-                           hipStream_t st) {
+                           const float* lse, const float* gscale, float denom, const float* count, void* dlogits,
+                           long ldd, int dtype, hipStream_t st) {
     const bool vec = dtype == 1 && V % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0 &&
                      ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 15) == 0;
     if (vec)
         hipLaunchKernelGGL((xent_bwd_kernel<bf16_t, true>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
-                           V, labels, ignore, lse, gscale, denom, (bf16_t*)dlogits, ldd);
+                           V, labels, ignore, lse, gscale, denom, count, (bf16_t*)dlogits, ldd);
     else if (dtype == 1)
         hipLaunchKernelGGL((xent_bwd_kernel<bf16_t, false>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)logits, ld,
-                           V, labels, ignore, lse, gscale, denom, (bf16_t*)dlogits, ldd);
+                           V, labels, ignore, lse, gscale, denom, count, (bf16_t*)dlogits, ldd);
     else
         hipLaunchKernelGGL((xent_bwd_kernel<float, false>), dim3(rows), dim3(NT), 0, st, (const float*)logits, ld,
-                           V, labels, ignore, lse, gscale, denom, (float*)dlogits, ldd);
+                           V, labels, ignore, lse, gscale, denom, count, (float*)dlogits, ldd);
     PDNN_LAUNCH_RET;
 }

@@ -355,10 +355,10 @@ class _XEnt(torch.autograd.Function):
             p[torch.arange(p.shape[0], device=p.device), target.clamp_min(0)] -= 1
             p = p * (target != ignore_index).unsqueeze(1) * g.unsqueeze(1)
             return p.to(logits.dtype), None, None, None
-        gs = g.reshape(1).float()
-        if reduction == "mean":
-            gs = gs / acc[1:2].clamp_min(1.0)
-        d = K.xent_bwd(logits, target, lse, gs, 1.0, ignore_index)
+        gs = g.reshape(1)
+        if gs.dtype != torch.float32:
+            gs = gs.float()
+        d = K.xent_bwd(logits, target, lse, gs, 1.0, ignore_index, count=acc[1:2] if reduction == "mean" else None)
         return d, None, None, None
 
 

@@ -717,12 +717,15 @@ def xent_fwd(logits, labels, ignore_index=-100):
     return loss, lse, acc
 
 
-def xent_bwd(logits, labels, lse, gscale_dev, denom, ignore_index=-100):
+def xent_bwd(logits, labels, lse, gscale_dev, denom, ignore_index=-100, count=None):
+    """d logits = softmax - onehot, times gscale_dev[0] / denom, or gscale_dev[0] / max(count[0], 1) with
+    ``count`` (fp32 device scalar: xent_fwd's count of non-ignored rows, the mean reduction)."""
     R, V = logits.shape
     d = torch.empty_like(logits)
     dt = 1 if logits.dtype == BF16 else 0
+    _chk(gscale_dev.dtype == F32 and gscale_dev.is_cuda, "xent_bwd: fp32 device gscale")
     call("pdnn_xent_bwd", ptr(logits), logits.stride(0), R, V, ptr(labels), int(ignore_index), ptr(lse),
-         ptr(gscale_dev), float(denom), ptr(d), d.stride(0), dt, stream())
+         ptr(gscale_dev), float(denom), ptr(count), ptr(d), d.stride(0), dt, stream())
     return d
 
 

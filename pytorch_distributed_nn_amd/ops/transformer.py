@@ -304,8 +304,10 @@ class LMHeadLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, xf, m, r, logits, targets, lse, acc, lnw, wte_k = ctx.saved_tensors
-        gs = g.reshape(1).float() / acc[1:2].clamp_min(1.0)
-        dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0)
+        gs = g.reshape(1)
+        if gs.dtype != torch.float32:
+            gs = gs.float()
+        dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0, count=acc[1:2])
         dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
         tte = direct_grad(ctx.wte) if ctx.head_direct else None
         if tte is not None:     # tied weight: the embedding backward adds its part and announces it

@@ -277,6 +277,10 @@ def test_xent(K, V):
     gs = torch.ones(1, device="cuda")
     d = K.xent_bwd(lg, y, lse, gs, 1.0)
     assert rel(d, lr.grad) < 1e-2
+    # mean reduction: the scale g / max(count, 1) formed in the kernel from the forward's device-side count
+    assert acc[1].item() == R - 1
+    dm = K.xent_bwd(lg, y, lse, gs, 1.0, count=acc[1:2])
+    assert rel(dm, lr.grad / (R - 1)) < 1e-2
 
 
 def test_sgd_adam(K):
