@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(SW_NT, 2) stem_wgrad_kernel(SWArgs a) {
 
 // out[i] = sum over the G block partials (fresh output, [64][7][32] fp32); 32 partial groups per 8 float4s
 __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
-                                                                int G) {
+                                                                int G, float* __restrict__ acc) {
     constexpr int PG = 32, OUT = 8, TOTAL = 64 * SW_R * 32 / 4;
     __shared__ float4 red[PG][OUT];
     const int o = threadIdx.x % OUT, pg = threadIdx.x / OUT;
@@ -199,7 +199,19 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* __r
     if (pg == 0 && i < TOTAL) {
 #pragma unroll
         for (int k = 1; k < PG; ++k) { const float4 v = red[k][o]; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
-        *reinterpret_cast<float4*>(out + 4 * i) = s;
+        if (acc) {
+            // accumulate straight into the parameter's gradient, [64][3][7][7] in channels-last memory
+            // (n*147 + r*21 + s*3 + c): element (n, r, k = c*8 + j) is tap s = j - 1 of channel c
+            const float e4[4] = {s.x, s.y, s.z, s.w};
+            const int nr = (4 * i) / 32, n = nr / SW_R, r = nr - n * SW_R;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = (4 * i + q) & 31, c = k >> 3, j = k & 7;
+                if (c < 3 && j >= 1) acc[n * 147 + r * 21 + (j - 1) * 3 + c] += e4[q];
+            }
+        } else {
+            *reinterpret_cast<float4*>(out + 4 * i) = s;
+        }
     }
 }
 
@@ -225,12 +237,13 @@ PDNN_API int pdnn_stem_wgrad_ws(int Nimg, int Ho, int Wo) { return sw_blocks((lo
 // dw32 [64][7][32] fp32 (overwritten; k = c*8 + j as pdnn_stem_conv_nchw's weight) = weight gradient of the
 // NCHW stem given dt [Nimg*Ho*Wo][64] bf16 (the gradient w.r.t. its output).  t != null: `dt` is the gradient
 // ga of the stem's BN+ReLU output and the BN backward apply (mode 2: ReLU mask recomputed from t) runs in the
-// staging, so dt is never written.
+// staging, so dt is never written.  acc != null: the result is added into acc (the parameter gradient,
+// [64][3][7][7] channels-last fp32) instead of written to dw32.
 PDNN_API int pdnn_stem_wgrad_nchw(const bf16_t* x, const bf16_t* dt, float* dw32, int Nimg, int H, int W, int Ho,
                                   int Wo, float* ws, const bf16_t* t, const float* mean, const float* invstd,
                                   const float* gamma, const float* dgamma, const float* dbeta, const float* mscale,
-                                  const float* mshift, hipStream_t st) {
-    if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || W % 2 || W < 8 || !ws ||
+                                  const float* mshift, float* acc, hipStream_t st) {
+    if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || W % 2 || W < 8 || !ws || (!dw32 && !acc) ||
         (long)Nimg * Ho * Wo >= (1L << 31))
         return (int)hipErrorInvalidValue;
     const bool pre = t != nullptr;
@@ -255,6 +268,6 @@ PDNN_API int pdnn_stem_wgrad_nchw(const bf16_t* x, const bf16_t* dt, float* dw32
     const int e = (int)hipGetLastError();
     if (e) return e;
     hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((64 * SW_R * 32 / 4 + 7) / 8), dim3(256), 0, st,
-                       (const float*)ws, dw32, a.G);
+                       (const float*)ws, dw32, a.G, acc);
     PDNN_LAUNCH_RET;
 }

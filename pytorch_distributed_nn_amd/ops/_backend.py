@@ -57,7 +57,7 @@ _SIGS = {
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_stem_stats_rows": [L],
     "pdnn_stem_conv_nchw": [P, P, P, I, I, I, I, I, P, P],
-    "pdnn_stem_wgrad_nchw": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_stem_wgrad_nchw": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_stem_wgrad_ws": [I, I, I],
     "pdnn_bn_relu_maxpool": [P, P, P, P, P, I, I, I, I, I, I, P],
     "pdnn_set_glds_mode": [I],

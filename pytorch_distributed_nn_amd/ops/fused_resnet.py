@@ -626,11 +626,16 @@ class StemFn(torch.autograd.Function):
                 slab, _, rows = K.bn_bwd_reduce(ga.view(-1, C), t.view(-1, C), m, i, mode=2, msrc=t.view(-1, C),
                                                mscale=s, mshift=h)
             (dg_, db_), (dg, db) = sink.bn(slab, rows, P[1], P[2])
-            dw = K.stem_wgrad_nchw(x, ga, pre=(t, m, i, gamma, dg_, db_, s, h))
+            pre = (t, m, i, gamma, dg_, db_, s, h)
             acc = sink.acc(P[0])
-            if acc is not None:
-                acc[0].add_(dw)
+            if acc is not None and acc[0].stride() == (147, 1, 21, 3):
+                K.stem_wgrad_nchw(x, ga, pre=pre, acc=acc[0])       # added straight into the arena
                 dw = None
+            else:
+                dw = K.stem_wgrad_nchw(x, ga, pre=pre)
+                if acc is not None:
+                    acc[0].add_(dw)
+                    dw = None
             sink.done()
             return None, None, None, None, dw, dg, db
         ga = K.maxpool_bwd(gy, idx, t.shape, 3, 2, 1) if pool else gy

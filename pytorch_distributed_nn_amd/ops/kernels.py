@@ -599,23 +599,30 @@ def stem_conv_nchw(x, w32, want_stats=True):
     return y, slab
 
 
-def stem_wgrad_nchw(x, dt, pre=None):
+def stem_wgrad_nchw(x, dt, pre=None, acc=None):
     """Weight gradient of stem_conv_nchw: x NCHW bf16 [N][3][H][W], dt bf16 [N][Ho][Wo][64] -> fp32 [64][3][7][7]
     (a view of the kernel's [64][7 r][32 k] result, k = c*8 + j, tap s = j - 1).  pre = (t, mean, invstd, gamma,
     dgamma, dbeta, mscale, mshift): ``dt`` is the gradient of the BN+ReLU output and the BN backward apply (ReLU
-    mask recomputed from t) runs inside the kernel's staging."""
+    mask recomputed from t) runs inside the kernel's staging.  acc: fp32 [64, 3, 7, 7] channels-last gradient the
+    result is added into (returns None)."""
     _bf16_c(x, "stem_wgrad.x")
     _bf16_c(dt, "stem_wgrad.dt")
     N, C, H, W = x.shape
     Ho, Wo = conv_out_hw(H, W, 7, 7, 2, 3)
     _chk(C == 3 and tuple(dt.shape) == (N, Ho, Wo, 64), "stem_wgrad_nchw: x [N][3][H][W], dt [N][Ho][Wo][64]")
     ws = torch.empty(lib().pdnn_stem_wgrad_ws(N, Ho, Wo), device=x.device, dtype=F32)
-    dw32 = torch.empty(64, 7, 32, device=x.device, dtype=F32)
+    if acc is not None:
+        _chk(acc.dtype == F32 and tuple(acc.shape) == (64, 3, 7, 7) and acc.stride() == (147, 1, 21, 3),
+             "stem_wgrad_nchw: acc fp32 [64,3,7,7] channels-last")
+    dw32 = torch.empty(64, 7, 32, device=x.device, dtype=F32) if acc is None else None
     pa = (None,) * 8 if pre is None else pre
     if pre is not None:
         _bf16_c(pre[0], "stem_wgrad.t")
         _chk(tuple(pre[0].shape) == tuple(dt.shape), "stem_wgrad_nchw: t like dt")
-    call("pdnn_stem_wgrad_nchw", ptr(x), ptr(dt), ptr(dw32), N, H, W, Ho, Wo, ptr(ws), *map(ptr, pa), stream())
+    call("pdnn_stem_wgrad_nchw", ptr(x), ptr(dt), ptr(dw32), N, H, W, Ho, Wo, ptr(ws), *map(ptr, pa), ptr(acc),
+         stream())
+    if acc is not None:
+        return None
     return dw32.view(64, 7, 4, 8)[:, :, :3, 1:].permute(0, 2, 1, 3)
 
 

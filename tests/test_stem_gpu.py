@@ -204,3 +204,16 @@ def test_maxpool_bwd_bnred_declines_odd_sizes(K):
     y, idx = K.bn_relu_maxpool(t, torch.ones(64, device="cuda"), torch.zeros(64, device="cuda"))
     z = torch.zeros(64, device="cuda")
     assert K.maxpool_bwd_bnred(y, idx, t, z, z, z, z) is None
+
+
+def test_stem_wgrad_nchw_accumulates_into_channels_last_grad(K):
+    """acc=: the reduce adds the weight gradient straight into a [64,3,7,7] channels-last fp32 gradient (the
+    flat arena's view of the stem weight) instead of returning it."""
+    x = torch.randn(3, 3, 30, 18, device="cuda").to(BF)
+    dt = torch.randn(3, 15, 9, 64, device="cuda").to(BF)
+    ref = K.stem_wgrad_nchw(x, dt)
+    base = torch.randn(64, 3, 7, 7, device="cuda").contiguous(memory_format=torch.channels_last)
+    acc = base.clone()
+    assert acc.stride() == (147, 1, 21, 3)
+    assert K.stem_wgrad_nchw(x, dt, acc=acc) is None
+    torch.testing.assert_close(acc, base + ref, rtol=1e-5, atol=1e-5)
