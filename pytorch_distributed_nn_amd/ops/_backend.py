@@ -86,6 +86,8 @@ _SIGS = {
     "pdnn_maxpool_bwd_bnred": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "pdnn_maxpool_bwd_bnred_rows": [I, I, I, I],
     "pdnn_stream_wait": [P, P],
+    "pdnn_bn_bwd_reduce_fin": [P, P, L, I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_bn_bwd_reduce_fin_groups": [L, I],
     "pdnn_stream_wait_value": [P, P],
     "pdnn_avgpool_fwd": [P, P, I, I, I, P],
     "pdnn_avgpool_bwd": [P, P, I, I, I, P],

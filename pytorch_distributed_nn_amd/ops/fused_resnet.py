@@ -114,6 +114,19 @@ class _Sink:
         dg, db = K.bn_bwd_finalize(slab, rows, acc=acc)
         return (dg, db), ((None, None) if acc is not None else (dg, db))
 
+    def bn_reduce(self, g2d, t2d, mean, inv, mode, bn_params, msrc=None, msc=None, msh=None, x2=None, mean2=None,
+                  inv2=None, bn_params2=None):
+        """bn_bwd_reduce + finalize of one BN (two with x2) in one launch (tuning bn_red_fin).  -> per BN
+        ((dgamma, dbeta) for bn_bwd_apply, (returned grads of gamma, beta))."""
+        acc = self.acc(*bn_params)
+        acc2 = self.acc(*bn_params2) if x2 is not None else None
+        (dg, db), second = K.bn_bwd_reduce_fin(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh,
+                                               x2=x2, mean2=mean2, invstd2=inv2, acc=acc, acc2=acc2)
+        out = [((dg, db), ((None, None) if acc is not None else (dg, db)))]
+        if x2 is not None:
+            out.append((second, ((None, None) if acc2 is not None else second)))
+        return out
+
     def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
         if self.side is None:
             return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
@@ -203,6 +216,12 @@ def _conv1x1_bn_fp8(x, w_param, meta, training, bn_params, bufs, mom, eps):
 
 
 def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
+    if sink is not None and tuning.get("bn_red_fin"):
+        ((dgamma, dbeta), (rg, rb)), = sink.bn_reduce(g2d, t2d, mean, inv, mode, bn_params, msrc=msrc, msc=msc,
+                                                      msh=msh)
+        dt, _, _ = K.bn_bwd_apply(g2d, t2d, mean, inv, gamma, dgamma, dbeta, mode=mode, msrc=msrc, mscale=msc,
+                                  mshift=msh)
+        return dt, rg, rb
     slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
     if sink is not None:
         (dgamma, dbeta), (rg, rb) = sink.bn(slab, rows, *bn_params)
@@ -397,11 +416,20 @@ class BottleneckFn(torch.autograd.Function):
             dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=0)
             gres, gres_mask = gout, None
         else:
-            slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
-                                                 x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
-            (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
+            if tuning.get("bn_red_fin"):
+                fins = sink.bn_reduce(g2d, t3_2d, m3, i3, 3, (P[7], P[8]), msrc=mb,
+                                      x2=td.view(-1, C3) if down else None, mean2=md, inv2=idd,
+                                      bn_params2=(P[10], P[11]) if down else None)
+                (dg3, db3), (rg3, rb3) = fins[0]
+                if down:
+                    (dgd, dbd), (rgd, rbd) = fins[1]
+            else:
+                slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
+                                                     x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
+                (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
+                if down:
+                    (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
             if down:
-                (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
                 dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
                                              x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                              dbeta2=dbd)

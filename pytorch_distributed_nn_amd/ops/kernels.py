@@ -455,15 +455,17 @@ _CNT_SLOTS = 1 << 16
 _CNT = {}
 
 
-def _fin_counters(C, device):
-    if not _tuning.get("bn_fused_fin"):
+def _fin_counters(C, device, n=None):
+    """n (optional): that many counters instead of one per 64-channel column."""
+    if n is None and not _tuning.get("bn_fused_fin"):
         return None
     key = device.index
     ent = _CNT.get(key)
     if ent is None:
         ent = _CNT[key] = [torch.zeros(_CNT_SLOTS, device=device, dtype=torch.int32), 0]
     buf, pos = ent
-    n = (C + 63) // 64
+    if n is None:
+        n = (C + 63) // 64
     if pos + n > _CNT_SLOTS:
         pos = 0
     ent[1] = pos + n
@@ -526,6 +528,32 @@ def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=Non
     call("pdnn_bn_bwd_reduce", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
          ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), stream())
     return slab, slab2, rows
+
+
+def bn_bwd_reduce_fin(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=None, x2=None, mean2=None,
+                      invstd2=None, acc=None, acc2=None):
+    """bn_bwd_reduce + bn_bwd_finalize in one launch (the reduce's last blocks finalize, batchnorm.hip
+    bwd_fuse_tail).  -> ((dgamma, dbeta), (dgamma2, dbeta2) or None); acc / acc2 = (gamma.grad, beta.grad)
+    also receive them (+=)."""
+    L, C = x.shape
+    dev = x.device
+    rows = lib().pdnn_bn_reduce_rows(L, C)
+    ng = lib().pdnn_bn_bwd_reduce_fin_groups(L, C)
+    npass = 2 if x2 is not None else 1
+    slab = torch.empty(2 * rows, C, device=dev, dtype=F32)
+    slab2 = torch.empty_like(slab) if x2 is not None else None
+    work = torch.empty(npass * ng * 2 * C, device=dev, dtype=F32)
+    cnt = _fin_counters(C, dev, n=ng + 1)
+    dg, db = torch.empty(C, device=dev, dtype=F32), torch.empty(C, device=dev, dtype=F32)
+    dg2 = db2 = None
+    if x2 is not None:
+        dg2, db2 = torch.empty(C, device=dev, dtype=F32), torch.empty(C, device=dev, dtype=F32)
+    ga, ba = acc if acc is not None else (None, None)
+    ga2, ba2 = acc2 if acc2 is not None else (None, None)
+    call("pdnn_bn_bwd_reduce_fin", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
+         ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), ptr(work), ptr(cnt), ptr(dg),
+         ptr(db), ptr(ga), ptr(ba), ptr(dg2), ptr(db2), ptr(ga2), ptr(ba2), stream())
+    return (dg, db), ((dg2, db2) if x2 is not None else None)
 
 
 def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=None):
