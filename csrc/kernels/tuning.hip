@@ -20,7 +20,7 @@ int* field(Tune& t, const char* name) {
 
 // Python-side entries of the same variable (pytorch_distributed_nn_amd/tuning.py) are accepted here
 bool python_key(const std::string& k) {
-    static const char* keys[] = {"side_wgrad", "materialize_a2", "conv3x3", "panel1x1", "bwd_pre", "stem", "direct_grad", "opt_overlap", "bn_link", "wgrad1x1_pp_pix", "bn_fused_fin", "wprep", "wgrad3x3", "stem_wgrad_nchw", "pool_bnred", "light_events", "bn_red_fin"};
+    static const char* keys[] = {"side_wgrad", "materialize_a2", "conv3x3", "panel1x1", "bwd_pre", "stem", "direct_grad", "opt_overlap", "bn_link", "wgrad1x1_pp_pix", "bn_fused_fin", "wprep", "wgrad3x3", "stem_wgrad_nchw", "pool_bnred", "light_events", "bn_red_fin", "wprep_once"};
     for (const char* p : keys)
         if (k == p) return true;
     return false;

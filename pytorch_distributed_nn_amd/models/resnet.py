@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from ..ops import functional as OF
 from ..ops import kernels as K
-from ..ops.fused_resnet import BasicBlockFn, BottleneckFn, StemFn, stem_shadow
+from ..ops.fused_resnet import BasicBlockFn, BottleneckFn, StemFn, side_forward, stem_shadow
 
 
 def _bn_conf(bn: nn.BatchNorm2d):
@@ -255,8 +255,9 @@ class ResNetImageNet(_ResNetBase):
         else:
             xin = OF.nchw_to_nhwc_input(x)
             out = StemFn.apply(xin, conf, bufs, [stem_shadow(self.conv1.weight, xin.shape[-1])], *params)
-        for b in self._blocks():
-            out = b.forward_nhwc(out)
+        with side_forward(out.device):
+            for b in self._blocks():
+                out = b.forward_nhwc(out)
         feat = OF.global_avg_pool_nhwc(out)
         return OF.linear(feat, self.fc.weight, self.fc.bias)
 

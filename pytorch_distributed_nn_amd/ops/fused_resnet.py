@@ -21,6 +21,7 @@ Fusion plan of a Bottleneck (x -> out):
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -242,6 +243,38 @@ def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, w
     return gm, dgamma, dbeta, ret
 
 
+_FWD_FORKED = set()   # devices whose side stream already waited on the compute stream in this model forward
+_WPREP_SEQ = [0]      # wprep events in issue order
+_WPREP_WAITED = {}    # device index -> highest wprep sequence number the compute stream has waited on
+
+
+@contextlib.contextmanager
+def side_forward(dev):
+    """Around a model's block loop (tuning wprep_once): the side stream waits on the compute stream ONCE (the
+    optimizer step that refreshed the weights is then behind it), so the blocks' weight transforms need no fork
+    of their own."""
+    side = _side_stream(dev) if dev.type == "cuda" else None
+    if side is None or not tuning.get("wprep") or not tuning.get("wprep_once"):
+        yield
+        return
+    K.stream_wait(side, torch.cuda.current_stream(dev))
+    _FWD_FORKED.add(dev.index)
+    try:
+        yield
+    finally:
+        _FWD_FORKED.discard(dev.index)
+
+
+def _wait_wprep(dev, ev, seq):
+    """The backward's wait for its block's transformed weights.  The side stream is in order, so waiting on the
+    latest wprep event covers every earlier one: with wprep_once only the first block of the backward (the
+    last of the forward) waits."""
+    if tuning.get("wprep_once") and _WPREP_WAITED.get(dev.index, -1) >= seq:
+        return
+    torch.cuda.current_stream(dev).wait_event(ev)
+    _WPREP_WAITED[dev.index] = max(seq, _WPREP_WAITED.get(dev.index, -1))
+
+
 def _prep_dgrad_weights(x, specs):
     """Make the data gradients' transformed weights (K.dgrad_weight: flipped 3x3, transposed 1x1) in the
     forward, on the side stream, which is idle there: the backward then finds them ready instead of running
@@ -251,7 +284,8 @@ def _prep_dgrad_weights(x, specs):
     if side is None or not tuning.get("wprep"):
         return None
     main = torch.cuda.current_stream(x.device)
-    K.stream_wait(side, main)
+    if x.device.index not in _FWD_FORKED:
+        K.stream_wait(side, main)
     with torch.cuda.stream(side):
         ws = [K.dgrad_weight(*sp) for sp in specs]
         ev = torch.cuda.Event()
@@ -260,7 +294,8 @@ def _prep_dgrad_weights(x, specs):
         sp[1].record_stream(side)
         if w is not None:
             w.record_stream(main)
-    return ws, ev
+    _WPREP_SEQ[0] += 1
+    return ws, (ev, _WPREP_SEQ[0])
 
 
 def _pre_ok(t, wk, st, pad):
@@ -405,8 +440,8 @@ class BottleneckFn(torch.autograd.Function):
         ctx.link_in = ctx.link_out = None
         w3p = w2p = w1p = None
         if ctx.wprep is not None:
-            (w3p, w2p, w1p), ev = ctx.wprep
-            torch.cuda.current_stream(gout.device).wait_event(ev)
+            (w3p, w2p, w1p), (ev, seq) = ctx.wprep
+            _wait_wprep(gout.device, ev, seq)
             ctx.wprep = None
         slab3 = link_out.take(gout) if link_out is not None else None
         gres_mask = mb if MASKED_RES else None

@@ -33,6 +33,9 @@ bn_red_fin         0        BatchNorm-backward reduce finalized by its own last 
                             bwd_fuse_tail) instead of a separate finalize launch (Bottleneck BN3 / BNd, _bn_back);
                             on: 10,711-10,728 vs 10,764-10,798 img/s (gpurun_out/r3_71: the single-block group sums
                             are latency-bound and the tail costs the reduce two VGPR waves)
+wprep_once         1        wprep: one side-stream fork per model forward and one compute-stream wait per backward (the
+                            latest transform event covers the earlier ones) instead of one of each per block;
+                            off: 10,819-10,821 vs 10,844-10,853 img/s (gpurun_out/r3_73)
 pool_bnred         1        stem backward: max-pool gather and the mode-2 BN-backward reduce in one pass
                             (pool.hip maxpool_bwd_bnred_kernel) instead of maxpool_bwd + bn_bwd_reduce;
                             off: 10,644-10,656 vs 10,718-10,720 img/s (gpurun_out/r3_57)
@@ -51,7 +54,7 @@ import os
 
 DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
             "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1, "stem_wgrad_nchw": 1,
-            "pool_bnred": 1, "light_events": 1, "bn_red_fin": 0}
+            "pool_bnred": 1, "light_events": 1, "bn_red_fin": 0, "wprep_once": 1}
 
 _VALUES = dict(DEFAULTS)
 
