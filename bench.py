@@ -58,10 +58,48 @@ def _ddp_rehearsal(a):
         r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         rec = json.loads(line)
-        return {"value": rec["value"], "ms_per_step": rec["ms_per_step"],
+        return {"value": rec["value"], "ms_per_step": rec["ms_per_step"], "comm": rec.get("comm"),
                 "note": "same step through DDP: bucket hooks + RCCL all-reduce over a 1-rank process group"}
     except Exception as e:       # never lose the headline line over the rehearsal
         return {"error": f"{type(e).__name__}: {e}"[:200]}
+
+
+def comm_diagnostics(net, step, n):
+    """{"bucket_mb", "fp32": {...}, "bf16": {...}}: per wire dtype, over ``n`` steps, the median per-bucket
+    all-reduce device time (gradients ready -> reduced), when each bucket was ready / done relative to the first
+    gradient hook, the exposed tail (last bucket done minus the backward's last kernel) and the BatchNorm-buffer
+    broadcast; max over ranks."""
+    import statistics
+    out = {"bucket_mb": [round(v, 3) for v in net.bucket_sizes_mb()], "world": net.world}
+    old = net.comm_dtype
+    for name, dt in (("fp32", None), ("bf16", torch.bfloat16)):
+        net.set_comm_dtype(dt)
+        net.comm_timing = True
+        net.comm_records()
+        for i in range(n):
+            step(i)
+        torch.cuda.synchronize()
+        net.comm_timing = False
+        recs = net.comm_records()
+        if not recs:
+            out[name] = None
+            continue
+        med = lambda xs: statistics.median(xs)          # noqa: E731
+        nb = len(recs[0]["bucket_ms"])
+        r = {"bucket_allreduce_ms": [round(med([x["bucket_ms"][b] for x in recs]), 3) for b in range(nb)],
+             "bucket_ready_ms": [round(med([x["bucket_ready_ms"][b] for x in recs]), 3) for b in range(nb)],
+             "bucket_done_ms": [round(med([x["bucket_done_ms"][b] for x in recs]), 3) for b in range(nb)],
+             "backward_end_ms": round(med([x["bwd_end_ms"] for x in recs]), 3),
+             "exposed_tail_ms": round(med([x["tail_ms"] for x in recs]), 3),
+             "bn_bcast_ms": (round(med([x["bn_bcast_ms"] for x in recs]), 3)
+                             if recs[0]["bn_bcast_ms"] is not None else None)}
+        if net.world > 1:       # max over ranks of the scalars (the slowest rank sets the step)
+            v = torch.tensor([r["exposed_tail_ms"], r["bn_bcast_ms"] or 0.0, r["backward_end_ms"]], device=net.flat.grad.device)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX, group=net.pg)
+            r["exposed_tail_ms"], r["bn_bcast_ms"], r["backward_end_ms"] = [round(x, 3) for x in v.tolist()]
+        out[name] = r
+    net.set_comm_dtype(old)
+    return out
 
 
 def main():
@@ -85,6 +123,8 @@ def main():
                     help="(internal) the 1-GPU DDP-path run: RCCL process group of one rank, every bucket all-reduced")
     ap.add_argument("--no-ddp-rehearsal", action="store_true",
                     help="at --gpus 1, skip the second measurement of the DDP code path")
+    ap.add_argument("--diag-steps", type=int, default=5,
+                    help="DDP path: extra steps after the timed region with per-bucket communication timing")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -188,6 +228,12 @@ def main():
         runtime.barrier()
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    comm = None
+    if use_ddp and not use_graph and isinstance(net, DistributedDataParallel) and dev.type == "cuda":
+        # after the timed region (it is not perturbed): a few more steps with device-event timing of every bucket
+        # all-reduce, the exposed tail and the BN-buffer broadcast -- fp32 wire, then bf16 wire
+        with ctx:
+            comm = comm_diagnostics(net, step, a.diag_steps)
     t = torch.tensor([dt], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -222,6 +268,7 @@ def main():
             "native_loaded": native_loaded(),
             "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
             "ddp_path_1gpu": ddp_rehearsal,
+            "comm": comm,
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
@@ -249,6 +296,7 @@ def main():
             "native_loaded": native_loaded(),
             "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
             "ddp_path_1gpu": ddp_rehearsal,
+            "comm": comm,
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",

@@ -59,6 +59,8 @@ def weight_fp8(p: torch.Tensor, krsc: bool = False):
     """(e4m3 weight [N][K] (conv: [K][R*S*C]), device inverse scale) cached per parameter version.
     Current scaling (exact amax of this version) in two launches: per-block amax partials, then a quantiser
     that reduces them itself (no fill, no single-thread scale kernel)."""
+    from ..optim.flat import await_param
+    await_param(p)                     # before the cache check: a PS bucket landing bumps the generation
     st = getattr(p, "_pdnn_fp8", None)
     ver = _weight_version(p)
     if st is not None and st[0] == ver:

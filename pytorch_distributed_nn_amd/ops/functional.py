@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..optim import flat
 from ..optim.flat import await_param, direct_grad, grad_ready
 from . import kernels as K
 
@@ -34,6 +35,7 @@ def weight_bf16(p: torch.Tensor, krsc: bool = False) -> torch.Tensor:
     if krsc and src.dim() == 4:
         src = src.permute(0, 2, 3, 1)
     out = src.to(BF16).contiguous()
+    flat.SHADOW_EPOCH[0] += 1          # a mid-forward re-cast on the compute stream (see flat.SHADOW_EPOCH)
     if sh is not None and sh.shape == out.shape:
         sh.copy_(out)
         p._pdnn_shadow_ver = p._version
@@ -44,6 +46,7 @@ def weight_bf16(p: torch.Tensor, krsc: bool = False) -> torch.Tensor:
 def weight_bf16_t(p: torch.Tensor) -> torch.Tensor:
     """bf16 transposed copy W^T [K][N] of a 2-D weight W [N][K] (the data-gradient GEMM's K-major B operand),
     cached per parameter version / flat-arena update generation, rebuilt by the in-tree transpose kernel."""
+    await_param(p)                     # before the cache check: a PS bucket landing bumps the generation
     fp = getattr(p, "_pdnn_flat", None)
     ver = (p._version, fp.generation if fp is not None else 0)
     st = getattr(p, "_pdnn_shadow_t", None)

@@ -27,7 +27,7 @@ import os
 import torch
 
 from .. import tuning
-from ..optim.flat import direct_grad, grad_ready
+from ..optim.flat import SHADOW_EPOCH, direct_grad, grad_ready
 from . import kernels as K
 from .functional import weight_bf16
 
@@ -243,7 +243,8 @@ def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, w
     return gm, dgamma, dbeta, ret
 
 
-_FWD_FORKED = set()   # devices whose side stream already waited on the compute stream in this model forward
+_FWD_FORKED = {}      # device index -> flat.SHADOW_EPOCH when the side stream last waited on the compute stream
+                      # in this model forward (a later mid-forward shadow re-cast needs a new fork)
 _WPREP_SEQ = [0]      # wprep events in issue order
 _WPREP_WAITED = {}    # device index -> highest wprep sequence number the compute stream has waited on
 
@@ -258,11 +259,11 @@ def side_forward(dev):
         yield
         return
     K.stream_wait(side, torch.cuda.current_stream(dev))
-    _FWD_FORKED.add(dev.index)
+    _FWD_FORKED[dev.index] = SHADOW_EPOCH[0]
     try:
         yield
     finally:
-        _FWD_FORKED.discard(dev.index)
+        _FWD_FORKED.pop(dev.index, None)
 
 
 def _wait_wprep(dev, ev, seq):
@@ -284,8 +285,13 @@ def _prep_dgrad_weights(x, specs):
     if side is None or not tuning.get("wprep"):
         return None
     main = torch.cuda.current_stream(x.device)
-    if x.device.index not in _FWD_FORKED:
+    idx = x.device.index
+    if _FWD_FORKED.get(idx) != SHADOW_EPOCH[0]:
+        # no fork in this forward yet, or a shadow slice was re-cast on the compute stream since the last one
+        # (a PS weight bucket that landed mid-forward): the transforms must read the fresh weights
         K.stream_wait(side, main)
+        if idx in _FWD_FORKED:
+            _FWD_FORKED[idx] = SHADOW_EPOCH[0]
     with torch.cuda.stream(side):
         ws = [K.dgrad_weight(*sp) for sp in specs]
         ev = torch.cuda.Event()

@@ -23,6 +23,11 @@ import torch
 from .. import tuning as _tuning
 
 ALIGN = 64
+# bumped by every bf16-shadow re-cast issued while a forward may be running (a PS weight bucket landing, an
+# on-the-fly re-cast of an externally modified weight): those casts run on the compute stream mid-forward,
+# so a side stream that forked from the compute stream earlier in the forward must fork again before it
+# reads the shadow (ops/fused_resnet._prep_dgrad_weights)
+SHADOW_EPOCH = [0]
 
 
 def _cl_strides(shape):
@@ -91,6 +96,7 @@ class FlatParams:
         else:
             self.shadow[start:end].copy_(self.data[start:end])
         self.generation += 1
+        SHADOW_EPOCH[0] += 1
         for p, o in zip(self.params, self.offsets):
             if start <= o < end:
                 p._pdnn_shadow_ver = p._version
@@ -183,6 +189,26 @@ def await_param(p):
     w = p.__dict__.get("_pdnn_await")
     if w is not None:
         w(p)
+
+
+class ParamUseMode(torch.overrides.TorchFunctionMode):
+    """While active and ``armed()`` is true, every torch op that takes an ``nn.Parameter`` first runs that
+    parameter's ``_pdnn_await`` (:func:`await_param`): the per-use hook of torch-op models, whose modules may
+    read ``lin.weight`` directly (so module forward hooks never fire).  The fused GPU ops call
+    :func:`await_param` themselves when they fetch a weight's bf16 shadow."""
+
+    def __init__(self, armed):
+        super().__init__()
+        self.armed = armed
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if self.armed():
+            for a in list(args) + list(kwargs.values()):
+                for t in (a if isinstance(a, (list, tuple)) else (a,)):
+                    if isinstance(t, torch.nn.Parameter):
+                        await_param(t)
+        return func(*args, **kwargs)
 
 
 def direct_grad(p):

@@ -50,7 +50,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.fused_resnet import side_stream_if_active
-from ..optim.flat import flatten_module, register_grad_ready_hook, reverse_buckets
+from ..optim.flat import ParamUseMode, flatten_module, register_grad_ready_hook, reverse_buckets
 
 
 class StepAborted(RuntimeError):
@@ -218,6 +218,8 @@ class DistributedDataParallel(nn.Module):
         # device-side per-bucket all-reduce latency (HIP events, read lazily: no host sync in the step)
         self.comm_timing = comm_timing
         self._ev_log = []
+        self._timing_stream = None
+        self._ev_bn = None
         self.comm_dtype = comm_dtype
         self.average = average
         self.kofn = None
@@ -243,9 +245,12 @@ class DistributedDataParallel(nn.Module):
         self.aborted_steps = 0
         self._reset()
         self.step_comm_log = []
+        self._in_fwd = False
+        self.abort_phase = None
         if self._comm and (num_aggregate > 0 or deadline_ms > 0):
             k = num_aggregate if num_aggregate > 0 else self.world
             self.kofn = _KofN(self, min(k, self.world), deadline_ms)
+            self._install_forward_checks()
 
     # ------------------------------------------------------------------ init broadcast (C-13)
     @torch.no_grad()
@@ -322,6 +327,36 @@ class DistributedDataParallel(nn.Module):
     def bucket_sizes_mb(self):
         return [(e - s) * 4 / 2 ** 20 for s, e, _ in self.buckets]
 
+    # ------------------------------------------------------------------ forward-phase short-circuit
+    def _install_forward_checks(self):
+        """k-of-n: a rank whose step is closed while it is still in its FORWARD abandons the step before its
+        next layer (the C++ worker checks before every forward layer too, worker_nn.h:56-64; the reference's
+        PyTorch worker polls the kill tag before each layer, lenet.py:168-178).  Checked at every parameter's
+        use through ``p._pdnn_await``: the fused GPU ops call it when they fetch a weight's bf16 shadow, and
+        :class:`~..optim.flat.ParamUseMode` around the forward calls it for torch ops taking a parameter."""
+        for p in self.flat.params:
+            if "_pdnn_await" not in p.__dict__:
+                p._pdnn_await = lambda _p: self._forward_check()
+
+    def _forward_check(self):
+        # during the forward of step self.step + 1 the watcher flags that step once it is closed elsewhere
+        if self._in_fwd and self.kofn is not None and self.kofn.abort_step == self.step + 1:
+            self._in_fwd = False
+            raise StepAborted(f"rank {self.rank} step {self.step + 1} (forward)")
+
+    def _abort_forward(self):
+        """The step was closed during this rank's forward: no backward runs, so take part in the step's
+        collectives here -- every bucket zero-filled, then the contributor counts -- exactly as an abort in the
+        backward would (_finish), leaving the count-correct average in the gradient arena."""
+        self._reset()
+        self._armed = True
+        self.step += 1
+        self._t0 = time.perf_counter()
+        self.kofn.begin(self.step)
+        self._aborted = True
+        self.abort_phase = "forward"
+        self._finish()
+
     # ------------------------------------------------------------------ per-backward state
     def _reset(self):
         self._ready = [0] * len(self.buckets)
@@ -335,9 +370,13 @@ class DistributedDataParallel(nn.Module):
         self._ev_start, self._ev_done = {}, {}
 
     def _arm(self):
+        self.abort_phase = None
         self._armed = True
         self.step += 1
         self._t0 = time.perf_counter()
+        if self.comm_timing and self.flat.grad.is_cuda:
+            self._ev_arm = torch.cuda.Event(enable_timing=True)
+            self._ev_arm.record()
         torch.autograd.Variable._execution_engine.queue_callback(self._finish)
         if self.kofn is not None:
             self.kofn.begin(self.step)
@@ -349,6 +388,7 @@ class DistributedDataParallel(nn.Module):
             self._arm()
         if self.kofn is not None and self.kofn.abort_step == self.step:
             self._aborted = True                 # closed by the k-th finisher / deadline: short-circuit
+            self.abort_phase = "backward"
             raise StepAborted(f"rank {self.rank} step {self.step}")
         b = self._pbucket[id(p)]
         self._ready[b] += 1
@@ -408,10 +448,24 @@ class DistributedDataParallel(nn.Module):
         if self.tracer is not None:
             self.tracer.instant(f"allreduce_bucket{b}", args={"mb": (e - s) * 4 / 2 ** 20})
         self.launch_order.append(b)
-        if self.comm_timing and view.is_cuda:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            self._ev_start[b] = ev
+        if self.comm_timing and view.is_cuda and getattr(self, "_ev_arm", None) is not None:
+            # the collective issued from a timing stream that has nothing else queued: its start event fires when
+            # the bucket's gradients are ready (the stream waits on the launching one), its end event when RCCL's
+            # kernel is done (the stream waits on RCCL's) -- per-bucket device time, no host sync in the step
+            if self._timing_stream is None:
+                self._timing_stream = torch.cuda.Stream(device=view.device)
+            cs = self._timing_stream
+            cs.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(cs):
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record(cs)
+                work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
+                work.wait()
+                ev1.record(cs)
+            t.record_stream(cs)
+            self._ev_start[b], self._ev_done[b] = ev0, ev1
+            self._works.append((b, work))
+            return
         self._works.append((b, dist.all_reduce(t, op=op, group=self.pg, async_op=True)))
 
     def _finish(self):
@@ -425,19 +479,25 @@ class DistributedDataParallel(nn.Module):
             # (otherwise no rank reports and the k-th-finisher close never fires)
             self.kofn.report_done(self.step)
         fp = self.flat
+        ev_bwd = None
+        if self.comm_timing and fp.grad.is_cuda and getattr(self, "_ev_arm", None) is not None:
+            # the backward's last kernels: compute stream, and the weight-gradient side stream if active
+            ev_bwd = [torch.cuda.Event(enable_timing=True)]
+            ev_bwd[0].record()
+            side = side_stream_if_active(fp.grad)
+            if side is not None:
+                ev_bwd.append(torch.cuda.Event(enable_timing=True))
+                ev_bwd[1].record(side)
         if self.straggler_mode:
             # per-bucket contributor counts: all-reduced after the buckets (same collective order everywhere)
             cnt = torch.tensor(self._contrib, dtype=torch.float32, device=fp.grad.device)
             self._works.append((-1, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
         for b, w in self._works:
             w.wait()
-            if self.comm_timing and b in self._ev_start:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()                          # the compute stream now waits on RCCL's stream
-                self._ev_done[b] = ev
-        if self.comm_timing and self._ev_start:
-            self._ev_log.append([(self._ev_start[b], self._ev_done[b]) for b in sorted(self._ev_start)
-                                 if b in self._ev_done])
+        if ev_bwd is not None and self._ev_start:
+            self._ev_log.append({"arm": self._ev_arm, "bwd": ev_bwd, "bn": self._ev_bn,
+                                 "buckets": [(b, self._ev_start[b], self._ev_done[b]) for b in sorted(self._ev_start)]})
+        self._ev_arm = self._ev_bn = None
         if self.comm_dtype is not None:
             for b, (s, e, _) in enumerate(self.buckets):
                 fp.grad[s:e].copy_(self._wire[b])
@@ -477,11 +537,30 @@ class DistributedDataParallel(nn.Module):
             self.kofn.stop()
 
     def forward(self, *args, **kwargs):
+        """Raises :class:`StepAborted` when k-of-n closed this step during the forward (after the step's
+        collectives have completed with a zero contribution from this rank): skip the loss and backward and
+        go on to the optimizer step, as after ``backward(loss)`` returned True."""
         if self.broadcast_buffers and self._comm and self.module.training:
             if self._fwd_count % self.buffer_sync_interval == 0:
-                self._broadcast_buffers()
+                if self.comm_timing and self.flat.grad.is_cuda:
+                    self._ev_bn = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    self._ev_bn[0].record()
+                    self._broadcast_buffers()
+                    self._ev_bn[1].record()
+                else:
+                    self._broadcast_buffers()
             self._fwd_count += 1
-        return self.module(*args, **kwargs)
+        if self.kofn is None or not (self.module.training and self._sync and torch.is_grad_enabled()):
+            return self.module(*args, **kwargs)
+        self._in_fwd = True
+        try:
+            with ParamUseMode(lambda: self.kofn.abort_step == self.step + 1):
+                return self.module(*args, **kwargs)
+        except StepAborted:
+            self._abort_forward()
+            raise
+        finally:
+            self._in_fwd = False
 
     def sync_buffers(self):
         """Broadcast rank 0's buffers now (e.g. before evaluation or a checkpoint: the last training forward
@@ -489,14 +568,36 @@ class DistributedDataParallel(nn.Module):
         self._broadcast_buffers()
 
     def comm_times_ms(self):
-        """Per step, per bucket: device time from the bucket's launch to its all-reduce completing (HIP
-        events on the compute stream around RCCL's stream-ordered collective), for the steps logged since
-        the last call (``comm_timing=True``).  Synchronises on the recorded events."""
+        """Per step, per bucket: device time of the bucket's all-reduce, from its gradients being ready to
+        RCCL's kernel completing (``comm_timing=True``), for the steps logged since the last call.  Synchronises
+        on the recorded events."""
+        return [r["bucket_ms"] for r in self.comm_records()]
+
+    def comm_records(self):
+        """Per logged step (``comm_timing=True``): ``bucket_ms`` (per bucket, ready -> all-reduced),
+        ``bucket_ready_ms`` / ``bucket_done_ms`` (from the first gradient hook), ``bwd_end_ms`` (last backward
+        kernel, both streams), ``tail_ms`` (last bucket done minus the backward's end: the exposed
+        communication) and ``bn_bcast_ms`` (the forward's BatchNorm-buffer broadcast).  Synchronises."""
         out = []
-        for evs in self._ev_log:
-            out.append([s.elapsed_time(e) for s, e in evs])
+        for r in self._ev_log:
+            arm = r["arm"]
+            arm.synchronize()
+            ready = [arm.elapsed_time(s) for _, s, _ in r["buckets"]]
+            done = [arm.elapsed_time(e) for _, _, e in r["buckets"]]
+            bwd = max(arm.elapsed_time(e) for e in r["bwd"])
+            rec = {"bucket_ms": [d - s for s, d in zip(ready, done)], "bucket_ready_ms": ready,
+                   "bucket_done_ms": done, "bwd_end_ms": bwd, "tail_ms": max(0.0, max(done) - bwd),
+                   "bn_bcast_ms": r["bn"][0].elapsed_time(r["bn"][1]) if r["bn"] is not None else None}
+            out.append(rec)
         self._ev_log = []
         return out
+
+    def set_comm_dtype(self, dtype):
+        """Switch the wire dtype between steps (None = the fp32 gradients themselves, torch.bfloat16 = a cast
+        copy per bucket)."""
+        self.comm_dtype = dtype
+        if dtype is not None:
+            self._wire = [torch.empty(e - s, dtype=dtype, device=self.flat.grad.device) for s, e, _ in self.buckets]
 
     @contextlib.contextmanager
     def no_sync(self):

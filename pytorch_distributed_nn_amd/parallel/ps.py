@@ -68,7 +68,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from ..optim.flat import flatten_module, register_grad_ready_hook, reverse_buckets
+from ..optim.flat import ParamUseMode, flatten_module, register_grad_ready_hook, reverse_buckets
 from ..utils.native import PSCoordinator, Store, StoreServer, StoreTimeout
 
 
@@ -76,32 +76,12 @@ class StepAborted(RuntimeError):
     """Raised inside a worker's backward to abandon a step (kill signal or a newer step)."""
 
 
-class _WeightUseMode(torch.overrides.TorchFunctionMode):
-    """Active during a PS worker's forward while weight buckets are still in flight: a torch op that takes
-    a parameter whose bucket has not landed yet waits for that bucket first (``p._pdnn_await``)."""
-
-    def __init__(self, pending):
-        super().__init__()
-        self.pending = pending
-
-    def __torch_function__(self, func, types, args=(), kwargs=None):
-        kwargs = kwargs or {}
-        if self.pending:
-            for a in list(args) + list(kwargs.values()):
-                for t in (a if isinstance(a, (list, tuple)) else (a,)):
-                    if isinstance(t, torch.nn.Parameter):
-                        w = t.__dict__.get("_pdnn_await")
-                        if w is not None:
-                            w(t)
-        return func(*args, **kwargs)
-
-
 class _StagedRecv:
     """irecv of a CUDA tensor over gloo through a host buffer (gloo's p2p moves host memory only)."""
 
-    def __init__(self, dst, src):
+    def __init__(self, dst, src, host=None):
         self.dst = dst
-        self.buf = torch.empty(dst.shape, dtype=dst.dtype, pin_memory=True)
+        self.buf = host if host is not None else torch.empty(dst.shape, dtype=dst.dtype, pin_memory=True)
         self.work = dist.irecv(self.buf, src)
 
     def wait(self):
@@ -209,8 +189,8 @@ class _Base:
     def _isend(self, t, dst):
         return _StagedSend(t, dst) if self._staged(t) else dist.isend(t, dst)
 
-    def _irecv(self, t, src):
-        return _StagedRecv(t, src) if self._staged(t) else dist.irecv(t, src)
+    def _irecv(self, t, src, host=None):
+        return _StagedRecv(t, src, host) if self._staged(t) else dist.irecv(t, src)
 
     def _recv(self, t, src):
         self._irecv(t, src).wait()
@@ -276,8 +256,11 @@ class PSMaster(_Base):
         # coordinator layers = buckets in reverse, so layer 0 is the LAST bucket (parameter 0: the sentinel)
         self.coord = PSCoordinator(self.n_workers, self.nb, cfg.n_to_collect, cfg.num_aggregate)
         self.opt = make_optimizer(self.flat.params, cfg)
-        big = max(e - s for s, e, _ in self.buckets)
-        self.stage = torch.zeros(big, dtype=torch.float32, device=self.flat.grad.device)
+        # one staging slot per (worker, bucket), allocated on first use and reused every step: a receive is
+        # posted the moment its arrival is announced, so the transfers of all workers overlap (the reference
+        # pre-posts P x (N-1) Irecv(ANY_SOURCE) and Waitany's over them, sync_replicas_master_nn.py:143-150,
+        # 275-284; the C++ master 100 per layer, sync_replicas_master_nn.h:163-186)
+        self._slots = {}
         self.qpos = 0                          # next arrival-queue entry to read
         self.log = []
         self.store.set("scheme", self.scheme)
@@ -294,11 +277,15 @@ class PSMaster(_Base):
         # end-of-step markers carry the worker's compute time (live TF-04 side channel) as a 4th field
         return int(f[0]), int(f[1]), int(f[2]), (float(f[3]) if len(f) > 3 else None)
 
-    def _receive(self, r, b):
-        s, e, _ = self.buckets[b]
-        buf = self.stage[: e - s]
-        self._recv(buf, r)
-        return buf
+    def _post_receive(self, r, b):
+        """Post the receive of worker r's bucket b into its staging slot -> (slot, work)."""
+        slot = self._slots.get((r, b))
+        if slot is None:
+            s, e, _ = self.buckets[b]
+            dev = torch.zeros(e - s, dtype=torch.float32, device=self.flat.grad.device)
+            host = torch.empty(e - s, dtype=torch.float32, pin_memory=True) if self._staged(dev) else None
+            slot = self._slots[(r, b)] = (dev, host)
+        return slot[0], self._irecv(slot[0], r, slot[1])
 
     def _save(self, step, final=False):
         from ..utils.observability import save_checkpoint
@@ -321,19 +308,33 @@ class PSMaster(_Base):
             tstep = time.perf_counter()
             closed, stale, ended = False, 0, set()
             ctimes = {}
+            inflight = []                                       # posted receives, in announcement order
+            xfer_ms = []                                        # per receive: post -> landed (overlapping)
 
             def take(timeout):
+                """Post a receive for every arrival announced so far (non-blocking queue reads; blocking up to
+                ``timeout`` only when nothing is in flight), then complete the oldest receive in flight and
+                offer it to the coordinator: all announced transfers run concurrently."""
                 nonlocal closed, stale
-                a = self._next_arrival(timeout)
-                if a is None:
+                got = False
+                while True:
+                    a = self._next_arrival(0 if (inflight or got) else timeout)
+                    if a is None:
+                        break
+                    got = True
+                    r, s, b, cms = a
+                    if b < 0:                                   # end-of-step marker of worker r
+                        if s == step:
+                            ended.add(r)
+                            ctimes[r] = cms
+                        continue
+                    g, work = self._post_receive(r, b)
+                    inflight.append((r, s, b, g, work, time.perf_counter()))
+                if not inflight:
                     return
-                r, s, b, cms = a
-                if b < 0:                                       # end-of-step marker of worker r
-                    if s == step:
-                        ended.add(r)
-                        ctimes[r] = cms
-                    return
-                g = self._receive(r, b)
+                r, s, b, g, work, tpost = inflight.pop(0)
+                work.wait()
+                xfer_ms.append((time.perf_counter() - tpost) * 1e3)
                 tms = (time.perf_counter() - t0) * 1e3
                 res = self.coord.offer(self.workers.index(r), self.nb - 1 - b, s, tms)
                 if res == PSCoordinator.ACCEPTED:
@@ -344,7 +345,7 @@ class PSMaster(_Base):
                 if self.coord.done():
                     closed = True
 
-            while not closed and len(ended) < self.n_workers:
+            while not closed and (len(ended) < self.n_workers or inflight):
                 timeout = -1
                 if cfg.interval_ms:
                     rest = cfg.interval_ms - (time.perf_counter() - tstep) * 1e3
@@ -354,12 +355,13 @@ class PSMaster(_Base):
                         and all(self.coord.count(li) >= 1 for li in range(self.nb))):
                     closed = True
             self.coord.close()                                  # later arrivals of this step are dropped
+            gather_ms = (time.perf_counter() - tstep) * 1e3
             # workers that did not deliver every bucket are killed (C-06, tag 77); published always so
             # every worker's watcher wakes for this step
             late = [w for i, w in enumerate(self.workers)
                     if not all(self.coord.contributed(li, i) for li in range(self.nb))]
             self.store.set(f"kill/{step}", json.dumps(late))
-            while len(ended) < self.n_workers:                  # receive (and drop) the late buckets, so
+            while len(ended) < self.n_workers or inflight:     # receive (and drop) the late buckets, so
                 take(-1)                                        # every p2p send of the step is matched
             # count-correct per-bucket average (fixes D3) + fused SGD (momentum, wd: fixes D9)
             counts = [self.coord.count(self.nb - 1 - b) for b in range(self.nb)]
@@ -374,8 +376,8 @@ class PSMaster(_Base):
                        if all(self.coord.contributed(li, i) for li in range(self.nb))]
             elapsed = sorted(v for v in ctimes.values() if v is not None)
             self.log.append({"step": step, "arrived": arrived, "count": min(counts), "bucket_counts": counts,
-                             "stale_dropped": stale, "gather_ms": (time.perf_counter() - tstep) * 1e3, "lr": lr,
-                             "compute_ms": elapsed})
+                             "stale_dropped": stale, "gather_ms": gather_ms, "lr": lr, "compute_ms": elapsed,
+                             "xfer_ms_sum": sum(xfer_ms), "receives": len(xfer_ms)})
             if cfg.log_compute_times:      # timeout_manager.py:48-70 "ELAPSED TIMES" line, live
                 print(f"Master: step {step} ELAPSED TIMES (ms, sorted over workers) "
                       f"{[round(v, 2) for v in elapsed]}", flush=True)
@@ -404,6 +406,8 @@ class PSWorker(_Base):
         self.cur = 0
         self.abort_step = -1
         self.done_step = 0
+        self._in_step = self._fwd_phase = self._aborted = False
+        self.abort_phase = None
         self._hooks = [register_grad_ready_hook(p, self._param_done) for p in self.flat.params]
         self._fwd_hooks = self._install_weight_waits()
         self.fwd_start = {}                 # step -> time the first module's forward began (timeline)
@@ -419,18 +423,31 @@ class PSWorker(_Base):
         self._watcher.start()
 
     def _install_weight_waits(self):
-        """Per-parameter waits: the first use of a parameter in the forward blocks on the weight bucket that
-        holds it and nothing else (the C++ worker's per-layer MPI_Wait just before computing the layer,
-        worker_nn.h:66-70).  A use is (a) the bf16 shadow fetch of every fused GPU op (``weight_bf16`` calls
+        """Per-parameter hooks run before each use of a parameter in the forward:
+
+        * the wait for the weight bucket that holds it and nothing else (pipelined push; the C++ worker's
+          per-layer MPI_Wait just before computing the layer, worker_nn.h:66-70);
+        * the forward-phase short-circuit: a worker the master has killed abandons the step before its next
+          layer (the C++ worker checks before EVERY forward layer as well as every backward layer,
+          worker_nn.h:56-64,77-84).
+
+        A use is (a) the bf16 shadow fetch of every fused GPU op (``weight_bf16`` calls
         :func:`~..optim.flat.await_param`), and (b) any torch op taking the parameter as an argument, caught
-        by :class:`_WeightUseMode` around the worker's forward."""
-        if not self.cfg.pipelined_push:
+        by :class:`~..optim.flat.ParamUseMode` around the worker's forward."""
+        if not (self.cfg.pipelined_push or self.cfg.shortcircuit or self.cfg.num_aggregate):
             return []
         for p in self.flat.params:
             p._pdnn_await = self._before_param
         return list(self.flat.params)
 
+    def _check_armed(self):
+        return bool(self._pending) or self.abort_step == self.cur
+
     def _before_param(self, p):
+        if self._in_step and self.abort_step == self.cur and not self._aborted:
+            self._aborted = True
+            self.abort_phase = "forward" if self._fwd_phase else "backward"
+            raise StepAborted(f"rank {self.rank} step {self.cur} (before a layer)")
         b = self.pbucket.get(id(p))
         if b is None or b not in self._pending:
             return
@@ -460,6 +477,7 @@ class PSWorker(_Base):
             return
         if self.abort_step == self.cur:                 # killed: skip the rest of the backward
             self._aborted = True
+            self.abort_phase = "backward"
             raise StepAborted(f"rank {self.rank} step {self.cur}")
         b = self.pbucket[id(p)]
         self._ready[b] += 1
@@ -496,9 +514,13 @@ class PSWorker(_Base):
             x, y = next(it)
             self.flat.zero_grad()
             self._ready, self._next, self._works, self._events, self._aborted = [0] * self.nb, 0, [], [], False
+            self.abort_phase = None
+            self._in_step = True
             try:
-                with _WeightUseMode(self._pending) if self.cfg.pipelined_push else _nullcontext():
+                self._fwd_phase = True
+                with ParamUseMode(self._check_armed) if self._fwd_hooks else _nullcontext():
                     out = self.model(x.to(self.device))
+                self._fwd_phase = False
                 self._wait_all_weights()                      # buckets no module claimed (and the backward's)
                 self.landed[s] = dict(self._land)
                 loss = self.loss_fn(out, y.to(self.device))
@@ -506,8 +528,12 @@ class PSWorker(_Base):
                 self.done_step = s
             except StepAborted:
                 self.aborted_steps += 1
+                self._wait_all_weights()        # a forward abort leaves weight receives posted: complete them
+            finally:
+                self._in_step = self._fwd_phase = False
             self.compute_records.append({"rank": self.rank, "step": s, "t_dequeue": t_deq,
                                          "t_finish": time.perf_counter(), "aborted": self.done_step != s,
+                                         "abort_phase": self.abort_phase,
                                          "compute_ms": 1e3 * (time.perf_counter() - t_deq)})
             # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped); it
             # carries the dequeue -> finish compute time, the master's live per-step ELAPSED TIMES

@@ -17,6 +17,7 @@ import time
 import torch
 
 from .ops import functional as OF
+from .parallel.ddp import StepAborted
 from .utils.observability import MetricsSink, Tracer, accuracy, load_checkpoint, save_checkpoint
 
 
@@ -78,13 +79,23 @@ class Trainer:
             self.step_no += 1
             return loss, self.graph_step.output, (0.0, time.perf_counter() - t0, 0.0)
         self.opt.zero_grad()
+        kofn = getattr(self.model, "kofn", None) is not None
         with self._span("forward"):
-            out = self.model(x)
-            loss = self.loss_fn(out, y)
+            try:
+                out = self.model(x)
+                loss = self.loss_fn(out, y)
+            except StepAborted:
+                # k-of-n DDP closed this step during the forward: the wrapper already took part in the step's
+                # collectives (zero contribution); no loss, no backward, the averaged gradient is applied below
+                if not kofn:
+                    raise
+                out = loss = None
         self._sync()
         t1 = time.perf_counter()
         with self._span("backward+allreduce"):
-            if getattr(self.model, "kofn", None) is not None:
+            if loss is None:
+                pass
+            elif kofn:
                 self.model.backward(loss)        # k-of-n DDP: a killed rank skips the rest of its backward
             else:
                 loss.backward()
@@ -101,20 +112,21 @@ class Trainer:
 
     # ----------------------------------------------------------------------------------------- loops
     def train(self, loader, epochs: int = 1, max_steps: int | None = None, steps_per_epoch: int | None = None,
-              batch_size: int | None = None, dataset_size: int | None = None):
+              batch_size: int | None = None, dataset_size: int | None = None, skip_consumed: bool = True):
         n_per_epoch = steps_per_epoch or (len(loader) if hasattr(loader, "__len__") else 100)
         it = iter(loader)
         done = False
         # a resumed run continues at its checkpoint: `epoch` is the epoch in progress (epoch-end checkpoints
         # store the NEXT epoch), and a mid-epoch checkpoint resumes after the steps that epoch already ran
         first_i = max(0, self.step_no - self.epoch * n_per_epoch)
+        # the loader is ONE stream across epochs (per-epoch reshuffles included) and a fresh loader restarts it
+        # at its first batch: consume every batch the checkpointed run trained on -- all earlier epochs too, not
+        # only this epoch's -- so the resumed run sees exactly the uninterrupted run's batches
+        for _ in range(self.step_no if skip_consumed else 0):
+            next(it)
         for ep in range(self.epoch, epochs):
             self.epoch = ep
             start, first_i = (first_i if first_i < n_per_epoch else 0), 0
-            for _ in range(start):
-                # mid-epoch resume: the loader restarts its stream, so consume the batches the checkpointed
-                # run already trained on; the step count, LR schedule and data then agree again
-                next(it)
             for i in range(start, n_per_epoch):
                 tf = time.perf_counter()
                 x, y = next(it)
@@ -127,7 +139,8 @@ class Trainer:
                 rec = {"step": self.step_no, "epoch": ep, "loss": None, "fetch_ms": 1e3 * fetch,
                        "forward_ms": 1e3 * tfw, "backward_ms": 1e3 * tbw, "opt_ms": 1e3 * topt,
                        "samples_per_s": bs * self.world / max(total, 1e-9)}
-                if self.step_no % self.log_interval == 0 or (max_steps and self.step_no >= max_steps):
+                if loss is not None and (self.step_no % self.log_interval == 0 or
+                                         (max_steps and self.step_no >= max_steps)):
                     lv = float(loss.detach())
                     if lv != lv or lv in (float("inf"), float("-inf")):      # TF trainer's NaN assert
                         raise FloatingPointError(f"Model diverged with loss = {lv} at step {self.step_no}")

@@ -80,3 +80,15 @@ def run_world(fn, world=2, args=(), timeout=180, device="cpu", backend="gloo", e
             if p.is_alive():
                 p.kill()
     return [out[r] for r in range(world)]
+
+
+def kofn_step(ddp, loss_fn):
+    """One k-of-n DDP step: forward + loss (``loss_fn()``) and ``ddp.backward``.  True when this rank was cut
+    short -- in its backward, or already in its forward (DDP.forward raises StepAborted after taking part in the
+    step's collectives)."""
+    from pytorch_distributed_nn_amd.parallel.ddp import StepAborted
+    try:
+        loss = loss_fn()
+    except StepAborted:
+        return True
+    return ddp.backward(loss)

@@ -1,7 +1,7 @@
 """DDP on CPU/gloo at world_size 2 (BASELINE.json config 1; SURVEY.md §7.4 tests/cpu_gloo)."""
 import torch
 
-from dist_utils import run_world
+from dist_utils import kofn_step, run_world
 
 
 def _ddp_vs_single(rank, world, model_name, shape, comm_dtype):
@@ -150,7 +150,7 @@ def _kofn(rank, world, k, sleep_ms, steps):
         local = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
         ddp.zero_grad()
         t0 = time.perf_counter()
-        aborted = ddp.backward(OF.cross_entropy(ddp(x), y))
+        aborted = kofn_step(ddp, lambda: OF.cross_entropy(ddp(x), y))
         dt = time.perf_counter() - t0
         contrib = torch.tensor(ddp.last_contrib)
         # expected: per bucket, the mean over the ranks that contributed real gradients
@@ -222,7 +222,7 @@ def _deadline(rank, world):
         x, y = torch.randn(16, 784), torch.randint(0, 10, (16,))
         ddp.zero_grad()
         t0 = time.perf_counter()
-        aborted = ddp.backward(OF.cross_entropy(ddp(x), y))
+        aborted = kofn_step(ddp, lambda: OF.cross_entropy(ddp(x), y))
         res.append((aborted, time.perf_counter() - t0, [float(v) for v in ddp.last_counts]))
     ddp.close()
     return res
@@ -254,7 +254,7 @@ def _deadline_after_fast_steps(rank, world):
         x, y = torch.randn(8, 784), torch.randint(0, 10, (8,))
         ddp.zero_grad()
         t0 = time.perf_counter()
-        aborted = ddp.backward(OF.cross_entropy(ddp(x), y))
+        aborted = kofn_step(ddp, lambda: OF.cross_entropy(ddp(x), y))
         res.append((aborted, time.perf_counter() - t0))
     ddp.close()
     return res
@@ -310,3 +310,53 @@ def test_world4_bit_identical_grads_and_launch_order():
     for orders, _, _ in out:
         assert orders == orders0
         assert all(o == list(range(nb)) for o in orders)           # strictly in bucket order
+
+
+def _kofn_fwd(rank, world):
+    import time
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel, StepAborted
+    def net():
+        torch.manual_seed(0)     # layers called as modules: forward pre-hooks record the layers a step entered
+        return torch.nn.Sequential(torch.nn.Linear(784, 256), torch.nn.ReLU(), torch.nn.Linear(256, 256),
+                                   torch.nn.ReLU(), torch.nn.Linear(256, 256), torch.nn.ReLU(),
+                                   torch.nn.Linear(256, 10))
+    m, ref = net(), net()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.5, first_bucket_cap_mb=0.05, num_aggregate=1)
+    linears = [mod for mod in m.modules() if isinstance(mod, torch.nn.Linear)]
+    entered = []
+    if rank == 1:                          # a slow FORWARD: 0.3 s before each layer
+        for i, mod in enumerate(linears):
+            mod.register_forward_pre_hook(lambda _m, _i, i=i: (entered.append((ddp.step + 1, i)), time.sleep(0.3)) and None)
+    res = []
+    for step in range(2):
+        g = torch.Generator().manual_seed(100 + step)
+        x, y = torch.randn(16, 784, generator=g), torch.randint(0, 10, (16,), generator=g)
+        ref.load_state_dict({k.replace("module.", ""): v for k, v in m.state_dict().items()})
+        ref.zero_grad()
+        OF.cross_entropy(ref(x), y).backward()
+        local0 = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])   # rank 0's gradient (same batch)
+        ddp.zero_grad()
+        try:
+            aborted = ddp.backward(OF.cross_entropy(ddp(x), y))
+        except StepAborted:
+            aborted = "forward"
+        got = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+        err = float((got - local0).abs().max() / local0.abs().max())
+        layers = [i for s, i in entered if s == ddp.step]
+        res.append((aborted, ddp.abort_phase, [float(v) for v in ddp.last_counts], err, len(layers), len(linears)))
+    ddp.close()
+    return res
+
+
+def test_kofn_rank_killed_in_forward_stops_before_next_layer():
+    """k = 1 of 2, rank 1's forward is slow (0.3 s per layer).  Rank 0 finishes and closes the
+    step; rank 1 abandons its FORWARD before the next layer (not only its backward), takes part in the step's
+    collectives with zero buckets, and both ranks end with rank 0's gradient (every bucket count 1)."""
+    out = run_world(_kofn_fwd, 2, (), timeout=240)
+    for r in range(2):
+        for aborted, phase, counts, err, n_entered, n_layers in out[r]:
+            assert counts == [1.0] * len(counts) and err < 1e-5, out[r]
+    for aborted, phase, counts, err, n_entered, n_layers in out[1]:
+        assert aborted == "forward" and phase == "forward" and n_entered <= 2 < n_layers, out[1]
+    assert all(a is False for a, *_ in out[0])

@@ -7,7 +7,7 @@ import copy
 import pytest
 import torch
 
-from dist_utils import run_world
+from dist_utils import kofn_step, run_world
 
 pytestmark = pytest.mark.gpu
 
@@ -127,7 +127,7 @@ def _rccl_kofn_job(rank, world):
         fref.zero_grad()
         OF.cross_entropy(ref(x), y).backward()
         net.zero_grad()
-        aborted = net.backward(OF.cross_entropy(net(x), y))
+        aborted = kofn_step(net, lambda: OF.cross_entropy(net(x), y))
         torch.cuda.synchronize()
         rel = ((net.flat.grad - fref.grad).norm() / fref.grad.norm()).item()
         out.append((aborted, rel, net.last_counts.cpu().tolist()))
@@ -210,3 +210,45 @@ def test_graphed_step_captures_rccl_collectives():
     for i, err, noise, le, lg in res:
         assert err < 3 * noise + 2e-3, res
         assert abs(le - lg) < 1e-2 * max(1.0, abs(lg)), res
+
+
+def _rccl_timing_job(rank, world):
+    """comm_timing on RCCL at world 1: every bucket's all-reduce gets a device time (ready -> reduced), the
+    exposed tail and the BN-buffer broadcast are measured, for the fp32 and the bf16 wire, and the timed
+    collectives still produce the plain gradients."""
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    m = build_model("resnet50").to(dev)
+    net = DistributedDataParallel(m, bucket_cap_mb=8.0, first_bucket_cap_mb=1.0)
+    x, y = torch.randn(8, 3, 64, 64, device=dev), torch.randint(0, 1000, (8,), device=dev)
+    net.zero_grad()
+    OF.cross_entropy(net(x), y).backward()
+    plain = net.flat.grad.clone()
+    out = {}
+    for name, dt in (("fp32", None), ("bf16", torch.bfloat16)):
+        net.set_comm_dtype(dt)
+        net.comm_timing = True
+        for _ in range(2):
+            net.zero_grad()
+            OF.cross_entropy(net(x), y).backward()
+        torch.cuda.synchronize()
+        net.comm_timing = False
+        recs = net.comm_records()
+        rel = ((net.flat.grad - plain).norm() / plain.norm()).item()
+        out[name] = (recs, rel)
+    return out, len(net.buckets)
+
+
+def test_ddp_comm_timing_records():
+    out, nb = run_world(_rccl_timing_job, 1, (), timeout=600, device=None, backend="nccl",
+                        env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
+    for name, (recs, rel) in out.items():
+        assert len(recs) == 2, name
+        for r in recs:
+            assert len(r["bucket_ms"]) == nb and all(0 <= v < 1e3 for v in r["bucket_ms"]), r
+            assert all(d >= s for s, d in zip(r["bucket_ready_ms"], r["bucket_done_ms"])), r
+            assert r["bwd_end_ms"] > 0 and r["tail_ms"] >= 0 and r["bn_bcast_ms"] is not None, r
+        assert rel < (1e-2 if name == "bf16" else 1e-5), (name, rel)

@@ -304,3 +304,80 @@ def test_ps_live_compute_times_in_master_log():
     for r in res[0][0]:
         assert len(r["compute_ms"]) == 2 and all(v > 0 for v in r["compute_ms"])
         assert r["compute_ms"] == sorted(r["compute_ms"])
+
+
+def _ps_fwd_kill_job(rank, world, out_dir, steps):
+    import time
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, PSMaster, PSWorker
+    torch.manual_seed(0)
+    # layers called as modules, so forward pre-hooks can record which layers a step entered
+    model = torch.nn.Sequential(torch.nn.Linear(784, 256), torch.nn.ReLU(), torch.nn.Linear(256, 256), torch.nn.ReLU(),
+                                torch.nn.Linear(256, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10))
+    x, y = _data()
+    cfg = PSConfig(num_aggregate=1, lr=0.05, max_steps=steps, out_dir=out_dir)
+    entered = []                               # (step, layer) of every forward layer the worker started
+    linears = [m for m in model.modules() if isinstance(m, torch.nn.Linear)]
+    if rank == 0:
+        role = PSMaster(model, cfg, torch.device("cpu"))
+        out = role.train()
+    else:
+        role = PSWorker(model, cfg, torch.device("cpu"), OF.cross_entropy)
+        if rank == 2:                          # the forward straggler: 0.3 s before each layer
+            for i, m in enumerate(linears):
+                m.register_forward_pre_hook(lambda mod, inp, i=i: (entered.append((role.cur, i)), time.sleep(0.3)) and None)
+
+        def batches():
+            i = 0
+            while True:
+                sl = slice((i * 32) % 512, (i * 32) % 512 + 32)
+                yield x[sl], y[sl]
+                i += 1
+        role.train(batches())
+        out = (role.compute_records, entered, len(linears))
+    role.close()
+    return out
+
+
+def test_ps_worker_killed_mid_forward_stops_before_next_layer():
+    """the C++ worker abandons the step before every FORWARD layer too (worker_nn.h:56-64).
+    k = 1 of 2: rank 2 spends 0.3 s before each layer, rank 1 finishes the whole step first, the master kills
+    rank 2, and rank 2 must stop before its next layer instead of finishing the forward."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_fwd_kill_job, 3, (out, 3), timeout=240)
+    recs, entered, n_layers = res[2]
+    killed = [r for r in recs if r["aborted"]]
+    assert killed and all(r["abort_phase"] == "forward" for r in killed), recs
+    for r in killed:
+        layers = [i for s, i in entered if s == r["step"]]
+        assert len(layers) <= 2 < n_layers, (r["step"], layers, n_layers)
+    assert all(r["count"] == 1 and r["arrived"] == [1] for r in res[0])
+
+
+def _ps_gather_job(rank, world, out_dir, steps):
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(784, 1024), torch.nn.ReLU(), torch.nn.Linear(1024, 1024),
+                                torch.nn.ReLU(), torch.nn.Linear(1024, 10))
+    x, y = _data()
+    cfg = PSConfig(lr=0.01, max_steps=steps, out_dir=out_dir, bucket_cap_mb=1.0, first_bucket_mb=0.25)
+
+    def batches():
+        while True:
+            yield x[:32], y[:32]
+    return run_ps(model, cfg, torch.device("cpu"), loss_fn=OF.cross_entropy, batches=batches())
+
+
+def test_ps_master_receives_workers_concurrently():
+    """the master posts each gradient receive the moment its arrival is announced (one
+    staging slot per (worker, bucket)) instead of one blocking receive at a time into one buffer: with 8
+    workers streaming ~7 MB each, the receives overlap -- the step's gather time is below the sum of the
+    individual transfer times."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_gather_job, 9, (out, 4), timeout=300)
+    log = res[0]
+    assert all(r["count"] == 8 for r in log)
+    assert all(r["receives"] == 8 * len(r["bucket_counts"]) for r in log)
+    overlapped = [r["xfer_ms_sum"] / r["gather_ms"] for r in log[1:]]
+    assert max(overlapped) > 1.5, [(r["gather_ms"], r["xfer_ms_sum"]) for r in log]

@@ -15,17 +15,20 @@ import copy
 import pytest
 import torch
 
-from dist_utils import run_world
+from dist_utils import kofn_step, run_world
 
 pytestmark = pytest.mark.gpu
 
 
-def _ddp_kill_job(rank, world):
+def _ddp_kill_job(rank, world, side):
     import time
+    from pytorch_distributed_nn_amd import tuning
     from pytorch_distributed_nn_amd.models import build_model
     from pytorch_distributed_nn_amd.ops import functional as OF
     from pytorch_distributed_nn_amd.optim.flat import flatten_module
     from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    # the schedule under test really is the one asked for (a stale knob name once ran one variant twice)
+    assert tuning.get("side_wgrad") == int(side), (tuning.get("side_wgrad"), side)
     torch.manual_seed(0)
     dev = torch.device("cuda")
     m = build_model("resnet50").to(dev)
@@ -52,7 +55,7 @@ def _ddp_kill_job(rank, world):
         torch.cuda.synchronize()
         slow["on"] = step == 0
         net.zero_grad()
-        aborted = net.backward(OF.cross_entropy(net(data[rank][0]), data[rank][1]))
+        aborted = kofn_step(net, lambda: OF.cross_entropy(net(data[rank][0]), data[rank][1]))
         torch.cuda.synchronize()
         counts = [int(c) for c in net.last_counts.cpu().tolist()]
         contrib = [None] * world                       # which buckets each rank delivered for real
@@ -69,7 +72,7 @@ def _ddp_kill_job(rank, world):
 
 @pytest.mark.parametrize("side", ["1", "0"], ids=["side-stream-wgrad", "serial-wgrad"])
 def test_ddp_kofn_kill_fused_resnet50_on_gpu(side):
-    res = run_world(_ddp_kill_job, 2, (), timeout=600, device=None, env={"PDNN_SIDE_WGRAD": side})
+    res = run_world(_ddp_kill_job, 2, (side,), timeout=600, device=None, env={"PDNN_TUNE": f"side_wgrad={side}"})
     (a0, c0, e0, f0), (a0n, c0n, e0n, f0n) = res[0]
     (a1, c1, e1, f1), (a1n, c1n, e1n, f1n) = res[1]
     assert not a0 and a1, res                          # the straggler was killed mid-backward
@@ -117,3 +120,41 @@ def test_ps_kofn_kill_with_cuda_tensors(tmp_path):
     assert torch.isfinite(w0).all()
     for r in res[1:]:
         assert torch.equal(r[1], w0)                                  # final push: consistent weights
+
+
+def _ps_resnet_job(rank, world, out_dir, pipelined):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.parallel.ps import PSConfig, run_ps
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = build_model("resnet50").to(dev)
+    cfg = PSConfig(comm_type="Bcast", lr=0.2, max_steps=3, out_dir=out_dir, pipelined_push=pipelined,
+                   bucket_cap_mb=8.0, first_bucket_mb=1.0, push_delay_ms=2.0 if pipelined else 0.0)
+
+    def batches():
+        i = 0
+        while True:
+            g = torch.Generator().manual_seed(100 + i)
+            yield torch.randn(4, 3, 64, 64, generator=g).to(dev), torch.randint(0, 1000, (4,), generator=g).to(dev)
+            i += 1
+
+    run_ps(model, cfg, dev, loss_fn=OF.cross_entropy, batches=batches())
+    return torch.cat([p.detach().float().flatten() for p in model.parameters()]).cpu()
+
+
+def test_ps_pipelined_push_fused_resnet50_matches_single_transfer(tmp_path):
+    """with the layer-pipelined weight push, weight buckets land -- and their bf16 shadow
+    slices are re-cast on the compute stream -- in the middle of the fused ResNet's forward, after the side
+    stream forked once for the data gradients' weight transforms.  Those transforms must see the fresh
+    weights: the pipelined run (a delay between buckets so they do land mid-forward) must train exactly like
+    the one-transfer run."""
+    w_pipe = run_world(_ps_resnet_job, 2, (str(tmp_path / "a"), True), timeout=600, device=None)[0]
+    w_one = run_world(_ps_resnet_job, 2, (str(tmp_path / "b"), False), timeout=600, device=None)[0]
+    from pytorch_distributed_nn_amd.models import build_model
+    torch.manual_seed(0)
+    w0 = torch.cat([p.detach().float().flatten() for p in build_model("resnet50").parameters()])
+    assert torch.isfinite(w_pipe).all()
+    d_pipe, d_one = w_pipe - w0, w_one - w0          # the three steps' updates (weights barely move otherwise)
+    err = ((d_pipe - d_one).norm() / d_one.norm()).item()
+    assert d_one.norm() > 0 and err < 1e-2, err

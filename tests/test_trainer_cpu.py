@@ -56,3 +56,31 @@ def test_resume_restores_weights(tmp_path):
     t2 = _trainer(tmp_path)
     t2.resume("auto")
     assert torch.equal(t2.model.weight, w)
+
+
+class _EpochLoader(_Loader):
+    """Per-epoch reshuffled stream (like data.DataLoader): a fresh iterator restarts at epoch 0's order."""
+
+    def __iter__(self):
+        data = torch.randn(self.n * self.bs, 8, generator=torch.Generator().manual_seed(1))
+        lab = torch.arange(self.n * self.bs) % 4
+        g = torch.Generator().manual_seed(2)
+        while True:
+            perm = torch.randperm(self.n * self.bs, generator=g)
+            for i in range(self.n):
+                idx = perm[i * self.bs:(i + 1) * self.bs]
+                yield data[idx], lab[idx]
+
+
+def test_resume_in_later_epoch_sees_the_uninterrupted_batches(tmp_path):
+    # ADVICE r3: a resume in epoch >= 1 must train on that epoch's order (not epoch 0's) and skip exactly the
+    # batches already consumed; the resumed run then ends bit-identical to the uninterrupted one
+    t = _trainer(tmp_path, checkpoint_interval=4)
+    t.train(_EpochLoader(), epochs=3)
+    ref = t.model.weight.detach().clone()
+    t2 = _trainer(tmp_path)
+    ck = t2.resume(str(tmp_path / "checkpoint_step4.pt"))
+    assert ck["step"] == 4 and ck["epoch"] == 1
+    t2.train(_EpochLoader(), epochs=3)
+    assert t2.step_no == 9
+    assert torch.equal(t2.model.weight, ref)
