@@ -176,14 +176,8 @@ def main():
     # (8,160-8,196 img/s; gpurun_out/r2_32)
     from pytorch_distributed_nn_amd import tuning
     side_overlap = not lm and not small and tuning.get("side_wgrad") == 1
-    # GPT-2 on one GPU: AdamW chunks run on a side stream during the backward (optim/overlap.py)
-    opt_overlap = lm and world == 1 and not use_ddp and tuning.get("opt_overlap") == 1
     use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1
-                                                                   and not side_overlap and not opt_overlap)
-    ov = None
-    if opt_overlap:
-        from pytorch_distributed_nn_amd.optim.overlap import BackwardOverlappedStep
-        ov = BackwardOverlappedStep(opt)
+                                                                   and not side_overlap)
     if use_graph:
         # whole step (fwd + bwd + optimizer [+ RCCL buckets if 'collectives']) replayed as one hipGraph
         from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
@@ -195,8 +189,6 @@ def main():
         if use_graph:
             return gstep(xs[i % 2], ys[i % 2])
         opt.zero_grad()
-        if ov is not None:
-            ov.arm()
         if lm:
             loss = net(xs[i % 2], ys[i % 2])
         else:
@@ -205,8 +197,7 @@ def main():
             net.backward(loss)
         else:
             loss.backward()
-        if ov is None:
-            opt.step()
+        opt.step()
         return loss
 
     # The side-stream ResNets run their compute stream at high priority (the side stream stays at the default,

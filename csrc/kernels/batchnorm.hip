@@ -440,85 +440,17 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
     }
 }
 
-// In-kernel finalize of bn_bwd_reduce (pdnn_bn_bwd_reduce_fin): instead of a bn_slab_fused launch after the
-// reduce, the reduce's own blocks finish the job with two ticket levels (the one-launch finalize's protocol:
-// write-through sc1 stores, drain, agent-scope ticket, acquire + sc1 loads in the last arriver, counters left
-// zeroed).  The last block of each group of BWF_GS blocks sums the group's partial rows into a level-1 row;
-// the last group to finish sums the level-1 rows in fp64 and runs the FinBwd epilogue (dgamma, dbeta and the
-// parameter-gradient accumulation).  Nothing waits on another block, so no residency assumption.
-constexpr int BWF_GS = 32;
-struct BwdFuse {
-    float* work;          // [npass][NG][2][C] level-1 rows
-    unsigned* cnt;        // NG + 1 zeroed counters
-    FinBwd e1, e2;
-};
-__device__ __forceinline__ void st1(float* p, float v) {
-    __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld1(const float* p) {
-    return __uint_as_float(__hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-__device__ void bwd_fuse_tail(const float* slab, const float* slab2, int C, int npass, const BwdFuse& fz) {
-    __shared__ int last;
-    const int G = gridDim.x, NG = (G + BWF_GS - 1) / BWF_GS, grp = blockIdx.x / BWF_GS;
-    const int g0 = grp * BWF_GS, g1 = min(G, g0 + BWF_GS);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // this thread's sc1 partial rows are done
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add((gu32*)(fz.cnt + grp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == (unsigned)(g1 - g0 - 1);
-    }
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-    for (int pass = 0; pass < npass; ++pass) {
-        const float* src = pass ? slab2 : slab;
-        float* w = fz.work + (long)pass * NG * 2 * C;
-        for (int cc = threadIdx.x; cc < C; cc += NT) {
-            float a = 0.f, b = 0.f;
-#pragma unroll 8
-            for (int r = g0; r < g1; ++r) { a += ld1(src + (long)(2 * r) * C + cc); b += ld1(src + (long)(2 * r + 1) * C + cc); }
-            st1(w + (long)(2 * grp) * C + cc, a);
-            st1(w + (long)(2 * grp + 1) * C + cc, b);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store((gu32*)(fz.cnt + grp), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned t = __hip_atomic_fetch_add((gu32*)(fz.cnt + NG), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == (unsigned)(NG - 1);
-    }
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-    for (int pass = 0; pass < npass; ++pass) {
-        const float* w = fz.work + (long)pass * NG * 2 * C;
-        for (int cc = threadIdx.x; cc < C; cc += NT) {
-            double a = 0.0, b = 0.0;
-#pragma unroll 8
-            for (int r = 0; r < NG; ++r) { a += ld1(w + (long)(2 * r) * C + cc); b += ld1(w + (long)(2 * r + 1) * C + cc); }
-            if (pass) fz.e2(cc, a, b);
-            else fz.e1(cc, a, b);
-        }
-    }
-    if (threadIdx.x == 0) __hip_atomic_store((gu32*)(fz.cnt + NG), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // mask modes for the backward: 0 none, 1 mask = (msrc > 0), 2 mask = (x*mscale + mshift > 0),
 // 3 mask = bit j of byte msrc[row][c/8] (written by bn_apply's MASK variant)
 // partial sums of gm and gm*xhat (xhat = (x-mean)*invstd) for one or two BNs sharing gm.
 // Specialised on the mask mode and the second BN so unused operands take no registers.
-template <int MODE, bool X2, bool FZ>
+template <int MODE, bool X2>
 __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const bf16_t* __restrict__ msrc, const float* __restrict__ mscale, const float* __restrict__ mshift,
     float* __restrict__ slab, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
-    const float* __restrict__ invstd2, float* __restrict__ slab2, BwdFuse fz) {
+    const float* __restrict__ invstd2, float* __restrict__ slab2) {
     __shared__ float red[2][NT * 8];
     const int CG = C >> 3, RPI = NT / CG;
     const int t = threadIdx.x, cg = t % CG, rr = t / CG, c = cg * 8;
@@ -589,17 +521,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
             const int gg = cc >> 3, j = cc & 7;
             float a = 0.f, b = 0.f;
             for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + gg) * 8 + j]; b += red[1][(k * CG + gg) * 8 + j]; }
-            if constexpr (FZ) {                  // in-kernel finalize: partial rows written through (sc1)
-                st1(out + (long)(2 * blockIdx.x) * C + cc, a);
-                st1(out + (long)(2 * blockIdx.x + 1) * C + cc, b);
-            } else {
-                out[(long)(2 * blockIdx.x) * C + cc] = a;
-                out[(long)(2 * blockIdx.x + 1) * C + cc] = b;
-            }
+            out[(long)(2 * blockIdx.x) * C + cc] = a;
+            out[(long)(2 * blockIdx.x + 1) * C + cc] = b;
         }
         __syncthreads();
     }
-    if constexpr (FZ) bwd_fuse_tail(slab, slab2, C, X2 ? 2 : 1, fz);
 }
 
 // sum partial rows -> dbeta (= sum gm), dgamma (= sum gm*xhat).  Optionally accumulate (+=).
@@ -792,19 +718,13 @@ PDNN_API int pdnn_bn_apply(const bf16_t* x, long L, int C, const float* scale, c
     PDNN_LAUNCH_RET;
 }
 
-static int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
+PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
                                 const float* invstd, int mode, const bf16_t* msrc, const float* mscale,
                                 const float* mshift, float* slab, const bf16_t* x2, const float* mean2,
-                                const float* invstd2, float* slab2, const BwdFuse& fz, hipStream_t st) {
+                                const float* invstd2, float* slab2, hipStream_t st) {
 #define PDNN_BWR(MODE, X2)                                                                                  \
-    do {                                                                                                    \
-        if (fz.cnt)                                                                                         \
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<MODE, X2, true>), dim3(reduce_grid(L, C)), dim3(NT), 0, st, \
-                               g, x, L, C, mean, invstd, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2, fz); \
-        else                                                                                                \
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<MODE, X2, false>), dim3(reduce_grid(L, C)), dim3(NT), 0, st, \
-                               g, x, L, C, mean, invstd, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2, fz); \
-    } while (0)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<MODE, X2>), dim3(reduce_grid(L, C)), dim3(NT), 0, st, g, x, L, C, \
+                       mean, invstd, msrc, mscale, mshift, slab, x2, mean2, invstd2, slab2)
     const bool hx2 = x2 != nullptr;
     switch (mode) {
         case 1: if (hx2) PDNN_BWR(1, true); else PDNN_BWR(1, false); break;
@@ -814,37 +734,6 @@ static int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* x, long L, int C,
     }
 #undef PDNN_BWR
     PDNN_LAUNCH_RET;
-}
-
-PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
-                                const float* invstd, int mode, const bf16_t* msrc, const float* mscale,
-                                const float* mshift, float* slab, const bf16_t* x2, const float* mean2,
-                                const float* invstd2, float* slab2, hipStream_t st) {
-    const BwdFuse fz{};
-    return bn_bwd_reduce_launch(g, x, L, C, mean, invstd, mode, msrc, mscale, mshift, slab, x2, mean2, invstd2,
-                                slab2, fz, st);
-}
-
-// level-1 groups of the in-kernel finalize (work holds npass * groups * 2 * C floats, cnt groups + 1 counters)
-PDNN_API int pdnn_bn_bwd_reduce_fin_groups(long L, int C) {
-    return (int)((reduce_grid(L, C) + BWF_GS - 1) / BWF_GS);
-}
-
-// bn_bwd_reduce + bn_bwd_finalize in one launch: (dgamma, dbeta) [, (dgamma2, dbeta2) with x2] written, and
-// also added into gacc/bacc (optional, the parameters' gradients).  cnt: zeroed, left zeroed.
-PDNN_API int pdnn_bn_bwd_reduce_fin(const bf16_t* g, const bf16_t* x, long L, int C, const float* mean,
-                                    const float* invstd, int mode, const bf16_t* msrc, const float* mscale,
-                                    const float* mshift, float* slab, const bf16_t* x2, const float* mean2,
-                                    const float* invstd2, float* slab2, float* work, unsigned* cnt, float* dgamma,
-                                    float* dbeta, float* gacc, float* bacc, float* dgamma2, float* dbeta2,
-                                    float* gacc2, float* bacc2, hipStream_t st) {
-    if (!work || !cnt || !dgamma || !dbeta || (x2 && (!slab2 || !dgamma2 || !dbeta2))) return (int)hipErrorInvalidValue;
-    BwdFuse fz{};
-    fz.work = work; fz.cnt = cnt;
-    fz.e1 = FinBwd{dgamma, dbeta, 0, gacc, bacc};
-    fz.e2 = FinBwd{dgamma2, dbeta2, 0, gacc2, bacc2};
-    return bn_bwd_reduce_launch(g, x, L, C, mean, invstd, mode, msrc, mscale, mshift, slab, x2, mean2, invstd2,
-                                slab2, fz, st);
 }
 
 // dgamma/dbeta of this backward (consumed by bn_bwd_apply); gacc/bacc (optional): also added into the

@@ -677,9 +677,6 @@ int areg_launch(const C3Args& a, hipStream_t st) {
 template <int KC, int NB, bool PRE>
 int areg_dispatch(const C3Args& a, int epi, hipStream_t st) {
     switch (epi) {
-        case C3_RESBN:       // K <= 128: at K = 256 the extra epilogue operands push the kernel into scratch
-            if constexpr (KC <= 2) return areg_launch<KC, NB, C3_RESBN, PRE>(a, st);
-            return (int)hipErrorInvalidValue;
         case C3_BNB: return areg_launch<KC, NB, C3_BNB, PRE>(a, st);
         case C3_STATS: return areg_launch<KC, NB, C3_STATS, PRE>(a, st);
         case C3_RES: return areg_launch<KC, NB, C3_RES, PRE>(a, st);
@@ -803,12 +800,9 @@ PDNN_API int pdnn_conv1x1_panel_supported(long P, int K, int N) {
     return k_ok && N % 64 == 0 && N >= 64 && P > 0 && P < (1L << 30) ? 1 : 0;
 }
 
-// bn_mask (with res and bn_x / bn_mean / bn_invstd; bn_mscale / bn_mshift unused): the C3_RESBN epilogue on the
-// A-stationary kernel -- y = (x.w^T + res * res_mask) * bn_mask and the BN-backward sums of y against bn_x.
 PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, long P, int K, int N, float* stats,
                                 const bf16_t* res, const uint8_t* res_mask, const bf16_t* bn_x, const float* bn_mean,
                                 const float* bn_invstd, const float* bn_mscale, const float* bn_mshift,
-                                const uint8_t* bn_mask,
                                 const bf16_t* pre_t, const float* pre_mean, const float* pre_invstd,
                                 const float* pre_gamma, const float* pre_dgamma, const float* pre_dbeta,
                                 bf16_t* pre_out, hipStream_t st) {
@@ -817,15 +811,13 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     C3Args a{};
     a.x = x; a.w = w; a.y = y; a.C = K; a.N = N; a.P = (int)P;
     a.tiles = (int)cdiv(P, C3_BM);
-    a.stats = stats; a.res = res; a.rmask = res_mask; a.rmask2 = bn_mask;
+    a.stats = stats; a.res = res; a.rmask = res_mask;
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
     if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
         return (int)hipErrorInvalidValue;
-    const bool resbn = bn_mask != nullptr;
-    if (resbn && !(res && bn_x && bn_mean && bn_invstd && N % 32 == 0)) return (int)hipErrorInvalidValue;
-    const int epi = resbn ? C3_RESBN : bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
+    const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
     // K = 256 always on the A-stationary kernel (the panel's A image would not leave room for 2 blocks per CU)
-    if (K == 256 || pg::tune().areg >= 2 || resbn)
+    if (K == 256 || pg::tune().areg >= 2)
         return pre_t ? areg_run<true>(a, K, epi, st) : areg_run<false>(a, K, epi, st);
     // column groups: split the output columns over blocks only until the grid covers ~2 blocks per CU
     const int chunks = N / 64;

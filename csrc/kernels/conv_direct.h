@@ -10,10 +10,7 @@ namespace {
 using namespace pg;
 
 constexpr int C3_BM = 256;
-// C3_RESBN: the residual epilogue of a block's input data gradient that also runs the BatchNorm-backward
-// reduction of the block BELOW: gm = (acc + res * rmask) * rmask2, stored, with slab sums of gm and
-// gm * (ep_x - ep_mean) * ep_invstd (rmask2 / ep_x: the ReLU bits and BN input of the block below's output)
-enum { C3_PLAIN = 0, C3_STATS = 1, C3_BNB = 2, C3_RES = 3, C3_RESBN = 4 };
+enum { C3_PLAIN = 0, C3_STATS = 1, C3_BNB = 2, C3_RES = 3 };
 
 struct C3Args {
     const bf16_t* x;     // [P][C]  NHWC input
@@ -26,7 +23,6 @@ struct C3Args {
     float* stats;
     const bf16_t* res;
     const uint8_t* rmask;  // C3_RES: residual masked by these ReLU bits ([P][N/8] bytes), or null
-    const uint8_t* rmask2; // C3_RESBN: output masked by these ReLU bits (same layout)
     const bf16_t* ep_x;
     const float *ep_mean, *ep_invstd, *ep_mscale, *ep_mshift;
     // PRE operand prologue (BatchNorm backward apply of the layer whose gradient is the input): the staged
@@ -35,6 +31,7 @@ struct C3Args {
     const bf16_t* pre_t;
     const float *pre_mean, *pre_invstd, *pre_gamma, *pre_dgamma, *pre_dbeta;
     bf16_t* pre_out;
+    const uint8_t* pre_mask;   // conv1x1_wide.hip PRE_MASK: the operand is masked by these ReLU bits first
 };
 
 // per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)
@@ -95,31 +92,25 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
         // C3_RES mask bits of this pair's 32 channels: ONE aligned 32-bit load per pixel (bit c = channel
         // n0 + 32*fp + c), not a byte load per fragment (that doubled the epilogue's memory instructions:
         // ResNet-50 stage-1 conv1 data gradient 239 -> 341 us with the mask, gpurun_out/r3_18)
-        constexpr bool RES = EPI == C3_RES || EPI == C3_RESBN;
-        uint32_t mw[4], mw2[4];
+        constexpr bool RES = EPI == C3_RES;
+        uint32_t mw[4];
         if constexpr (RES) {
 #pragma unroll
             for (int fm = 0; fm < 4; ++fm) {
                 const long mo = ((pv[fm] ? orow[fm] : 0) + n0 + 32 * fp) >> 3;
                 mw[fm] = a.rmask ? *reinterpret_cast<const uint32_t*>(a.rmask + mo) : 0xFFFFFFFFu;
-                if constexpr (EPI == C3_RESBN) mw2[fm] = *reinterpret_cast<const uint32_t*>(a.rmask2 + mo);
             }
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int fn = 2 * fp + h;
             const int n = n0 + fn * 16 + 4 * lg;
-            u16x4_t tv[4], xv[4];
+            u16x4_t tv[4];
             if constexpr (EPI == C3_BNB || RES) {
                 const bf16_t* src = EPI == C3_BNB ? a.ep_x : a.res;
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
                     tv[fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(src + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
-            }
-            if constexpr (EPI == C3_RESBN) {
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm)
-                    xv[fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(a.ep_x + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
             }
             // fused BN backward: q accumulates sum gm * t; sum gm * xhat = invstd * (sum gm t - mean * sum gm) is
             // formed at the flush, so mean / invstd are not live through the fragment loop (the K = 256
@@ -140,16 +131,6 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
                     const uint32_t mb = mw[fm] >> (16 * h + 4 * lg);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(tv[fm][j]) : 0.f;
-                }
-                if constexpr (EPI == C3_RESBN) {
-                    const uint32_t mb2 = mw2[fm] >> (16 * h + 4 * lg);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float gm = (ok && ((mb2 >> j) & 1)) ? bf2f(f2bf(v[j])) : 0.f;
-                        v[j] = gm;
-                        s[j] += gm;
-                        q[j] += gm * bf2f(xv[fm][j]);
-                    }
                 }
                 if constexpr (EPI == C3_BNB) {
 #pragma unroll
@@ -173,7 +154,7 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
                 pk[fm][h][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
                 pk[fm][h][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
             }
-            if constexpr (EPI == C3_STATS || EPI == C3_BNB || EPI == C3_RESBN) {
+            if constexpr (EPI == C3_STATS || EPI == C3_BNB) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     s[j] = row16_sum(s[j]);
@@ -182,7 +163,7 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
                 if ((lane & 15) == 0) {
                     float* ps = a.stats + (long)(tile * 4 + wave) * 2 * a.N + n;
                     float* pq = ps + a.N;
-                    if constexpr (EPI == C3_BNB || EPI == C3_RESBN) {
+                    if constexpr (EPI == C3_BNB) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) q[j] = (q[j] - a.ep_mean[n + j] * s[j]) * a.ep_invstd[n + j];
                     }

@@ -264,10 +264,9 @@ gemm_glds_kernel(GemmArgs a) {
     const int tiles_m = (a.M + GBM - 1) / GBM, tiles_n = (a.N + BN - 1) / BN;
     const int ntiles = tiles_m * tiles_n;
     const int ktiles = (a.K + BK - 1) / BK;
-    // Optionally persistent over output tiles (PDNN_GLDS_PERSISTENT=1; measured slower than the hardware
-    // dispatcher on every shape tried, so off by default): block b takes tiles
-    // b, b + G, ... (same XCD when G % 8 == 0), and issues the next tile's first K-step into the free LDS
-    // buffer before running this tile's epilogue, so short-K tiles overlap loads with stores.
+    // Grid-stride over output tiles (block b takes tiles b, b + G, ...; the launcher uses one block per tile: a
+    // persistent grid measured slower than the hardware dispatcher on every shape tried); the next tile's first
+    // K-step is issued into the free LDS buffer before this tile's epilogue.
     int cur = 0;
     bool pre = false;
     LA la;
@@ -557,7 +556,6 @@ inline int device_cus() {
     }
     return n;
 }
-inline int glds_persistent() { return tune().glds_persistent; }
 
 template <int AM, int BMODE, int EM, int BN, int DT = 0>
 int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {
@@ -570,12 +568,7 @@ int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, SM);
     }
     const int tiles = (int)(cdiv(a.M, GBM) * cdiv(a.N, BN));
-    int gx = tiles;
-    if (batch * splits == 1 && a.causal == 0 && glds_persistent()) {
-        const int slots = device_cus();                   // 1 block per CU (128 KiB LDS)
-        if (tiles > slots) gx = slots;
-    }
-    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN, DT>), dim3(gx, batch, splits), dim3(NTH), SM, st, a);
+    hipLaunchKernelGGL((gemm_glds_kernel<AM, BMODE, EM, BN, DT>), dim3(tiles, batch, splits), dim3(NTH), SM, st, a);
     PDNN_LAUNCH_RET;
 }
 

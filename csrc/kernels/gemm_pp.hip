@@ -157,16 +157,14 @@ __device__ __forceinline__ void pp_retire(int keep) {
 // multiple of 8, so an item keeps its block's XCD label).  The K-slices of consecutive items form one
 // continuous stream through the ring: the copies of the next item's first slices are in flight while the
 // current item finishes and stores its tile, so a tile boundary costs only the epilogue.
-// ABL (timing ablations, PDNN_PP_ABLATE with tools/pp_one.py; results are garbage): bit 0 = no MFMA,
-// bit 1 = no global->LDS copies in the loop, bit 2 = no LDS fragment reads (1..7)
 // FX (fusions, FX_* bits): A-operand BN-affine+ReLU prologue, BN partial statistics of the output,
 // BN-backward masking + statistics (the conv/1x1 paths of the ResNet blocks).
-template <class C, int AM, int BMODE, int EM, int ABL = 0, int FX = 0>
+template <class C, int AM, int BMODE, int EM, int FX = 0>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
     static_assert(!(FX & FX_PRO) || AK, "prologue: K-major A only");
     constexpr int NB = C::NB, D = NB - 1;
-    static_assert(!C::DT || (AK && BKm && !(FX & FX_PRO) && ABL == 0), "fp8: K-major operands, no prologue");
+    static_assert(!C::DT || (AK && BKm && !(FX & FX_PRO)), "fp8: K-major operands, no prologue");
     using LA = PPLoader<PP_BM, AK, C::SK>;
     using LB = PPLoader<C::BN, BKm, C::SK>;
     constexpr int NIT = LA::NI + LB::NI;
@@ -460,11 +458,6 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                 for (int f = 0; f < C::FN; ++f) bq[f] = frag8(B_, bcol + f * 16 + (lane & 15), lane);
 #pragma unroll
                 for (int f = 0; f < C::FM; ++f) aq[f] = frag8(A_, arow + f * 16 + (lane & 15), lane);
-            } else if constexpr ((ABL & 4) != 0) {
-#pragma unroll
-                for (int f = 0; f < C::FN; ++f) bfr[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)q, 1, 2, 3, 4, 5, 6, 7});
-#pragma unroll
-                for (int f = 0; f < C::FM; ++f) af[f] = __builtin_bit_cast(bf16x8_t, u16x8_t{(unsigned short)f, 1, 2, 3, 4, 5, 6, 7});
             } else {
 #pragma unroll
             for (int f = 0; f < C::FN; ++f) {
@@ -479,7 +472,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                 else af[f] = frag_mnmajor<PP_BM>(A_, arow + f * 16, 0, lane);
             }
             }
-            if (!(ABL & 2) && more) issue_next();
+            if (more) issue_next();
             if constexpr ((FX & FX_PRO) != 0) {
                 // this lane's 8 reduction indices of the slice: k = 32 s + 8 lg .. +7 (no split-K with FX_PRO)
                 const float* ps = ptab + s * PP_SK + 8 * (lane >> 4);
@@ -508,11 +501,6 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     for (int fn = 0; fn < C::FN; ++fn)
                         acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
                             bq[fn], aq[fm], acc[fm][fn], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
-            } else if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-                for (int f = 0; f < C::FM; ++f) asm volatile("" ::"v"(af[f]));
-#pragma unroll
-                for (int f = 0; f < C::FN; ++f) asm volatile("" ::"v"(bfr[f]));
             } else {
 #pragma unroll
             for (int fm = 0; fm < C::FM; ++fm)
@@ -653,34 +641,28 @@ int device_cus() {
 template <class C, int FX>
 constexpr int pp_smem() { return C::SMEM + ((FX & (FX_PRO | FX_BNB)) ? 2 * PP_PRO_MAXK * 4 : 0); }
 
-template <class C, int AM, int BMODE, int EM, int ABL, int FX = 0>
+template <class C, int AM, int BMODE, int EM, int FX = 0>
 void set_attr() {
     static bool attr = false;
     if (!attr) {
         attr = true;
         static_assert(pp_smem<C, FX>() <= 160 * 1024, "LDS");
-        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<C, AM, BMODE, EM, ABL, FX>,
+        (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<C, AM, BMODE, EM, FX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, pp_smem<C, FX>());
     }
 }
 
 template <class C, int AM, int BMODE, int EM, int FX = 0>
 int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
-    const int g_pp_ablate = tune().pp_ablate;
     const long items = cdiv(a.M, PP_BM) * cdiv(a.N, C::BN) * splits;
     const int cus = device_cus();
     const int grid = items <= cus ? (int)items : (cus / 8) * 8;     // persistent: one block per CU
     GemmArgs b = a;
     b.nb2 = splits;
     b.dbg = g_pp_trace;
-    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16 && FX == 0 && C::DT == 0) {
-#define PP_ABL_CASE(X) if (g_pp_ablate == X) { set_attr<C, AM, BMODE, EM, X>(); hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, X>), dim3(grid), dim3(512), C::SMEM, st, b); PDNN_LAUNCH_RET; }
-        PP_ABL_CASE(1) PP_ABL_CASE(2) PP_ABL_CASE(3) PP_ABL_CASE(4) PP_ABL_CASE(5) PP_ABL_CASE(6) PP_ABL_CASE(7)
-#undef PP_ABL_CASE
-    }
     constexpr int SM = pp_smem<C, FX>();
-    set_attr<C, AM, BMODE, EM, 0, FX>();
-    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, 0, FX>), dim3(grid), dim3(512), SM, st, b);
+    set_attr<C, AM, BMODE, EM, FX>();
+    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, FX>), dim3(grid), dim3(512), SM, st, b);
     PDNN_LAUNCH_RET;
 }
 
@@ -821,23 +803,18 @@ int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) 
 // hipcc (ROCm 7.2) emits the host launch stub of only the first implicitly instantiated specialisation of
 // a kernel template in an anonymous namespace: instantiate every specialisation used explicitly.
 #define PP_I(CFG, AM, BM_, EM) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::AM, pg::BM_, pg::EM, 0>(pg::GemmArgs);
-#define PP_A(CFG, X) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, X>(pg::GemmArgs);
-#define PP_A3(CFG) PP_A(CFG, 1) PP_A(CFG, 2) PP_A(CFG, 3) PP_A(CFG, 4) PP_A(CFG, 5) PP_A(CFG, 6) PP_A(CFG, 7)
-PP_A3(C96) PP_A3(C256) PP_A3(C256b)
-#undef PP_A3
-#undef PP_A
 #define PP_I2(CFG, AM, BM_) PP_I(CFG, AM, BM_, E_BF16) PP_I(CFG, AM, BM_, E_F32)
 PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR) PP_I2(C288, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_KMAJOR) PP_I2(C256, A_KMAJOR, B_KMAJOR) PP_I2(C256b, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_MNMAJOR) PP_I2(C256, A_KMAJOR, B_MNMAJOR)
 PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)
 #undef PP_I2
-#define PP_F(CFG, BM_, FX) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::BM_, pg::E_BF16, 0, FX>(pg::GemmArgs);
+#define PP_F(CFG, BM_, FX) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::BM_, pg::E_BF16, FX>(pg::GemmArgs);
 #define PP_F2(BM_, FX) PP_F(C128, BM_, FX) PP_F(C256, BM_, FX)
 #define PP_F5(BM_) PP_F(C128, BM_, 1) PP_F2(BM_, 2) PP_F(C128, BM_, 3) PP_F(C128, BM_, 4)
-#define PP_8(CFG) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 0, 0>(pg::GemmArgs); \
-    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_F32, 0, 0>(pg::GemmArgs); \
-    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 0, 2>(pg::GemmArgs);
+#define PP_8(CFG) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 0>(pg::GemmArgs); \
+    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_F32, 0>(pg::GemmArgs); \
+    template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::A_KMAJOR, pg::B_KMAJOR, pg::E_BF16, 2>(pg::GemmArgs);
 PP_8(C8_128) PP_8(C8_96)
 #undef PP_8
 PP_F5(B_KMAJOR) PP_F5(B_MNMAJOR)

@@ -17,11 +17,9 @@ namespace pg {
     X(glds_fwd_k, 1024, "implicit-GEMM conv forward on glds from this reduction length (r1: 512/1024/never tie)") \
     X(glds_dgrad_n, 1 << 30, "conv data gradient on glds from this many input channels (off: r1 whole-step -2.3%)") \
     X(glds_dgrad_k, 1 << 30, "conv data gradient on glds from this reduction length (off, as above)")         \
-    X(glds_persistent, 0, "glds engine as a persistent grid (off: within noise)")                           \
     X(pp, 1, "ping-pong engine for plain GEMMs: 0 off, 1 automatic, 2 whenever the operands allow (tests)")      \
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic)")                        \
     X(pp_fp8, 1, "fp8 GEMMs on the ping-pong engine (0: glds engine)")                                      \
-    X(pp_ablate, 0, "ping-pong engine ablations (profiles/pp_engine_ablations_r2a.txt; 0 = full engine)")   \
     X(pp_conv_min_n, 128, "1x1 stride-1 convs on the ping-pong engine from this output width")               \
     X(pp_conv_fwd_k, 1 << 30, "... forward from this reduction length (off: BN-stats epilogue slower there)")  \
     X(pp_conv_dgrad_k, 512, "... data gradient from this reduction length (r2_46: 512 vs 256 +0.5%)")        \

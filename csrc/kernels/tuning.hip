@@ -18,13 +18,9 @@ int* field(Tune& t, const char* name) {
     return nullptr;
 }
 
-// Python-side entries of the same variable (pytorch_distributed_nn_amd/tuning.py) are accepted here
-bool python_key(const std::string& k) {
-    static const char* keys[] = {"side_wgrad", "materialize_a2", "conv3x3", "panel1x1", "bwd_pre", "stem", "direct_grad", "opt_overlap", "bn_link", "wgrad1x1_pp_pix", "bn_fused_fin", "wprep", "wgrad3x3", "stem_wgrad_nchw", "pool_bnred", "light_events", "bn_red_fin", "wprep_once"};
-    for (const char* p : keys)
-        if (k == p) return true;
-    return false;
-}
+// keys of PDNN_TUNE that are not in this table: the Python side checks them against ITS table
+// (pytorch_distributed_nn_amd/tuning.py), so neither side keeps a copy of the other's key list
+std::string g_tune_unknown;
 
 Tune make() {
     Tune t;
@@ -43,7 +39,7 @@ Tune make() {
         if (eq == std::string::npos) { g_tune_error += "PDNN_TUNE: '" + item + "' is not key=value; "; continue; }
         int* f = field(t, k.c_str());
         if (f) *f = atoi(item.c_str() + eq + 1);
-        else if (!python_key(k)) g_tune_error += "PDNN_TUNE: unknown key '" + k + "'; ";
+        else g_tune_unknown += (g_tune_unknown.empty() ? "" : ",") + k;
     }
     return t;
 }
@@ -88,4 +84,10 @@ PDNN_API int pdnn_tune_list(char* buf, int n) {
 PDNN_API const char* pdnn_tune_error() {
     pg::tune();
     return pg::g_tune_error.c_str();
+}
+
+// comma-separated PDNN_TUNE keys this (kernel-side) table does not have
+PDNN_API const char* pdnn_tune_unknown() {
+    pg::tune();
+    return pg::g_tune_unknown.c_str();
 }

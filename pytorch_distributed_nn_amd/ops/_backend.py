@@ -51,9 +51,12 @@ _SIGS = {
     "pdnn_tune_get": [ctypes.c_char_p],
     "pdnn_tune_list": [ctypes.c_char_p, I],
     "pdnn_tune_error": [],
-    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_tune_unknown": [],
+    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
+    "pdnn_conv1x1_wide": [P, P, P, L, I, I] + [P] * 17,
+    "pdnn_conv1x1_wide_supported": [L, I, I],
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_stem_stats_rows": [L],
     "pdnn_stem_conv_nchw": [P, P, P, I, I, I, I, I, P, P],
@@ -86,8 +89,6 @@ _SIGS = {
     "pdnn_maxpool_bwd_bnred": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "pdnn_maxpool_bwd_bnred_rows": [I, I, I, I],
     "pdnn_stream_wait": [P, P],
-    "pdnn_bn_bwd_reduce_fin": [P, P, L, I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
-    "pdnn_bn_bwd_reduce_fin_groups": [L, I],
     "pdnn_stream_wait_value": [P, P],
     "pdnn_avgpool_fwd": [P, P, I, I, I, P],
     "pdnn_avgpool_bwd": [P, P, I, I, I, P],
@@ -167,8 +168,13 @@ def _load():
         fn.restype = ctypes.c_int
     if getattr(lib, "pdnn_tune_error", None) is not None:
         lib.pdnn_tune_error.restype = ctypes.c_char_p
+        lib.pdnn_tune_unknown.restype = ctypes.c_char_p
         err = lib.pdnn_tune_error().decode()
-        if err:                  # PDNN_TUNE names an entry that exists in neither table: fail loudly
+        from .. import tuning
+        unknown = [k for k in lib.pdnn_tune_unknown().decode().split(",") if k and k not in tuning.DEFAULTS]
+        if unknown:
+            err += f"PDNN_TUNE: unknown key(s) {unknown}; "
+        if err:                  # PDNN_TUNE is malformed or names an entry that exists in neither table: fail loudly
             _ERR = err
             return None
     _LIB = lib

@@ -115,19 +115,6 @@ class _Sink:
         dg, db = K.bn_bwd_finalize(slab, rows, acc=acc)
         return (dg, db), ((None, None) if acc is not None else (dg, db))
 
-    def bn_reduce(self, g2d, t2d, mean, inv, mode, bn_params, msrc=None, msc=None, msh=None, x2=None, mean2=None,
-                  inv2=None, bn_params2=None):
-        """bn_bwd_reduce + finalize of one BN (two with x2) in one launch (tuning bn_red_fin).  -> per BN
-        ((dgamma, dbeta) for bn_bwd_apply, (returned grads of gamma, beta))."""
-        acc = self.acc(*bn_params)
-        acc2 = self.acc(*bn_params2) if x2 is not None else None
-        (dg, db), second = K.bn_bwd_reduce_fin(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh,
-                                               x2=x2, mean2=mean2, invstd2=inv2, acc=acc, acc2=acc2)
-        out = [((dg, db), ((None, None) if acc is not None else (dg, db)))]
-        if x2 is not None:
-            out.append((second, ((None, None) if acc2 is not None else second)))
-        return out
-
     def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
         if self.side is None:
             return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
@@ -217,12 +204,6 @@ def _conv1x1_bn_fp8(x, w_param, meta, training, bn_params, bufs, mom, eps):
 
 
 def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
-    if sink is not None and tuning.get("bn_red_fin"):
-        ((dgamma, dbeta), (rg, rb)), = sink.bn_reduce(g2d, t2d, mean, inv, mode, bn_params, msrc=msrc, msc=msc,
-                                                      msh=msh)
-        dt, _, _ = K.bn_bwd_apply(g2d, t2d, mean, inv, gamma, dgamma, dbeta, mode=mode, msrc=msrc, mscale=msc,
-                                  mshift=msh)
-        return dt, rg, rb
     slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
     if sink is not None:
         (dgamma, dbeta), (rg, rb) = sink.bn(slab, rows, *bn_params)
@@ -235,10 +216,10 @@ def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, si
     return dt, dgamma, dbeta
 
 
-def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, wprep=None):
+def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, wprep=None, pre=None):
     """dgrad with the fused BN-backward epilogue, stopped before the apply pass: -> (gm, dgamma, dbeta,
     returned grads).  The apply then runs inside the next data gradient's operand loads (_dgrad_pre)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep, pre=pre)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     return gm, dgamma, dbeta, ret
 
@@ -310,41 +291,14 @@ def _pre_ok(t, wk, st, pad):
     return tuning.get("bwd_pre") == 1 and K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
 
 
-def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None):
+def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None, pre=None):
     """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
     one apply pass produces dt (the gradient w.r.t. the BN input t)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep, pre=pre)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     C = t.shape[-1]
     dt, _, _ = K.bn_bwd_apply(gm.view(-1, C), t.view(-1, C), mean, inv, gamma, dgamma, dbeta, mode=0)
     return dt.view(t.shape), ret[0], ret[1]
-
-
-class _BnLink:
-    """Hand-off between two consecutive identity Bottlenecks (i -> i+1).  Block i's output BatchNorm backward
-    starts with a reduction over its incoming gradient, which is exactly what block i+1's conv1 data
-    gradient writes: that kernel's epilogue (conv_dgrad ``bn_mask``) also multiplies its output by block i's
-    ReLU mask and reduces block i's BN3 sums against t3, so block i skips its bn_bwd_reduce pass (one read
-    of the block output's gradient and of t3) and its residual needs no mask.  Block i only uses the slab
-    when the gradient it receives is the very tensor block i+1 produced (same storage, same version: no
-    other consumer's gradient was added); otherwise it re-masks and reduces as usual, which is exact
-    because re-applying the mask is idempotent.  The gradient returned for a block output is therefore
-    pre-multiplied by its ReLU mask (the same parameter gradients; an intermediate's ``.grad`` differs where
-    the ReLU is inactive)."""
-
-    __slots__ = ("t3", "mean", "invstd", "mask", "slab", "ptr", "version")
-
-    def __init__(self, t3, mean, invstd, mask):
-        self.t3, self.mean, self.invstd, self.mask = t3, mean, invstd, mask
-        self.slab = None
-        self.ptr = self.version = None
-
-    def take(self, g):
-        """The reduced BN slab if ``g`` is block i+1's untouched output gradient, else None."""
-        slab, self.slab = self.slab, None
-        if slab is not None and g.data_ptr() == self.ptr and g._version == self.version:
-            return slab
-        return None
 
 
 def _krsc_grad(dw):
@@ -408,14 +362,6 @@ class BottleneckFn(torch.autograd.Function):
             td = md = idd = None
             out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=x.view(-1, C3), relu=True, want_mask=training)
         out = out.view(t3.shape)
-        # hand-offs with the neighbouring identity blocks (tuning bn_link; _BnLink)
-        ctx.link_in = ctx.link_out = None
-        if training and not down and tuning.get("bn_link") and x.is_cuda:
-            link = getattr(x, "_pdnn_bn_link", None)
-            if link is not None and K.resbn_ok(tuple(t1.shape), tuple(k1.shape)):
-                ctx.link_in = link                  # this block's conv1 dgrad reduces the block below's BN3
-            ctx.link_out = _BnLink(t3, m3, i3, mb)
-            out._pdnn_bn_link = ctx.link_out
         ctx.wprep = None
         if training:
             ctx.wprep = _prep_dgrad_weights(x, [(tuple(t3.shape), k3, tuple(t2.shape), 1, 0),
@@ -442,63 +388,62 @@ class BottleneckFn(torch.autograd.Function):
         P = ctx.params
         ctx.params = None
         sink = _Sink(gout.device)
-        link_in, link_out = ctx.link_in, ctx.link_out
-        ctx.link_in = ctx.link_out = None
         w3p = w2p = w1p = None
         if ctx.wprep is not None:
             (w3p, w2p, w1p), (ev, seq) = ctx.wprep
             _wait_wprep(gout.device, ev, seq)
             ctx.wprep = None
-        slab3 = link_out.take(gout) if link_out is not None else None
         gres_mask = mb if MASKED_RES else None
-        if slab3 is not None:
-            # the block above masked gout and reduced this BN's sums in its conv1 data gradient (_BnLink)
-            (dg3, db3), (rg3, rb3) = sink.bn(slab3, slab3.shape[0] // 2, P[7], P[8])
-            dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=0)
-            gres, gres_mask = gout, None
+        pre3 = None
+        slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
+                                             x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
+        (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
+        if down:
+            (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
+            dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
+                                         x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
+                                         dbeta2=dbd)
+            gres = None
+        elif MASKED_RES and a2 is not None and tuning.get("bn3_pre") and K.dgrad_pre_mask_ok(t3.shape, k3.shape):
+            # BN3's backward apply runs inside conv3's data-gradient operand loads (the long-reduction
+            # kernel reads gout, t3 and the ReLU bits, writes dt3 once for the weight gradient): no separate
+            # apply pass (read gout + t3, write dt3) and no re-read of dt3 by the data gradient
+            dt3 = torch.empty_like(t3)
+            pre3 = (t3, m3, i3, g3, dg3, db3, dt3, mb)
+            gres = gout
+        elif MASKED_RES:
+            # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
+            # materialised here: one activation-sized write less per block
+            dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb)
+            gres = gout
         else:
-            if tuning.get("bn_red_fin"):
-                fins = sink.bn_reduce(g2d, t3_2d, m3, i3, 3, (P[7], P[8]), msrc=mb,
-                                      x2=td.view(-1, C3) if down else None, mean2=md, inv2=idd,
-                                      bn_params2=(P[10], P[11]) if down else None)
-                (dg3, db3), (rg3, rb3) = fins[0]
-                if down:
-                    (dgd, dbd), (rgd, rbd) = fins[1]
-            else:
-                slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
-                                                     x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
-                (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
-                if down:
-                    (dgd, dbd), (rgd, rbd) = sink.bn(slabd, rows, P[10], P[11])
-            if down:
-                dt3, dtd, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb,
-                                             x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
-                                             dbeta2=dbd)
-                gres = None
-            elif MASKED_RES:
-                # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
-                # materialised here: one activation-sized write less per block
-                dt3, _, _ = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb)
-                gres = gout
-            else:
-                dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
+            dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
-        # conv3 (input = relu(bn2(t2)), virtual)
-        if a2 is not None:
-            dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
-        else:
-            dw3 = sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        dy3 = gout if pre3 is not None else dt3
+
+        def wgrad3():        # conv3 (input a2 = relu(bn2(t2)), or virtual through the prologue)
+            if a2 is not None:
+                return sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
+            return sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        if pre3 is None:
+            dw3 = wgrad3()
         bn1 = (t1, m1, i1, s1, h1)
         if _pre_ok(t2, k2, stride, 1):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad
-            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p)
+            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dy3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p,
+                                                     pre=pre3)
+            if pre3 is not None:
+                dw3 = wgrad3()                  # dt3 written by conv3's data gradient
             dt2 = torch.empty_like(t2)
             gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2),
                                       wprep=w2p)
             del gm2
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
         else:
-            dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p)
+            dt2, rg2, rb2 = _fused_dgrad_bn(dy3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p,
+                                            pre=pre3)
+            if pre3 is not None:
+                dw3 = wgrad3()
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
             gm1, slab1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1, bn=bn1, wprep=w2p)
         (dg1, db1), (rg1, rb1) = sink.bn(slab1, slab1.shape[0] // 2, P[1], P[2])
@@ -519,12 +464,6 @@ class BottleneckFn(torch.autograd.Function):
             # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
             # reach, so no zero-filled full-size buffer and no extra full read/write pass
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)
-        elif link_in is not None:
-            # also the block below's BN3 reduction (its mask applied to dx): see _BnLink
-            dx, lslab = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1,
-                                     bn=(link_in.t3, link_in.mean, link_in.invstd, None, None),
-                                     bn_mask=link_in.mask, wprep=w1p)
-            link_in.slab, link_in.ptr, link_in.version = lslab, dx.data_ptr(), dx._version
         else:
             dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, res=gres.view(x.shape), res_mask=gres_mask, pre=pre1,
                               wprep=w1p)

@@ -203,9 +203,16 @@ def set_panel_mode(mode: int) -> int:
     return old
 
 
-def _panel_ok(P, K, N, R, S, st, pad):
+def _wide_ok(P, K, N, fwd):
+    """1x1 / stride-1 convs with a long reduction (K >= 512) on the streaming kernel (conv1x1_wide.hip):
+    forwards (tuning wide1x1_fwd) and data gradients (wide1x1_dgrad)."""
+    return (K >= 512 and _tuning.get("wide1x1_fwd" if fwd else "wide1x1_dgrad") == 1
+            and lib().pdnn_conv1x1_wide_supported(P, K, N) == 1)
+
+
+def _panel_ok(P, K, N, R, S, st, pad, fwd=False):
     return (_P1["mode"] and R == 1 and S == 1 and st == 1 and pad == 0
-            and lib().pdnn_conv1x1_panel_supported(P, K, N) == 1)
+            and (lib().pdnn_conv1x1_panel_supported(P, K, N) == 1 or _wide_ok(P, K, N, fwd)))
 
 
 def _pre_args(pre, x):
@@ -213,7 +220,7 @@ def _pre_args(pre, x):
     gradient gm is ``x`` (dt = bn_bwd_apply(gm, t), mode 0) fused into the operand loads."""
     if pre is None:
         return (None,) * 7
-    t, mean, inv, gamma, dg, db, dt_out = pre
+    t, mean, inv, gamma, dg, db, dt_out = pre[:7]
     _bf16_c(t, "pre.t")
     _chk(t.numel() == x.numel(), "pre: t must have the operand's shape")
     if dt_out is not None:
@@ -221,10 +228,20 @@ def _pre_args(pre, x):
     return tuple(ptr(v) for v in (t, mean, inv, gamma, dg, db, dt_out))
 
 
-def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None, bn_mask=None):
-    """y[P][N] = x[P][K] . w[N][K]^T on the panel kernel; epilogues as conv3x3 / conv_dgrad; pre: the
-    BN-backward operand prologue (_pre_args); bn_mask: the residual + BN-backward-reduce epilogue
-    (conv_dgrad's ``bn_mask``)."""
+def _pre_mask(pre, x):
+    """The optional 8th entry of ``pre``: uint8 ReLU bits [P][K/8] masking the operand first (bn_bwd_apply mode 3:
+    x is the block output's gradient, not yet masked); only the long-reduction kernel takes it."""
+    if pre is None or len(pre) < 8 or pre[7] is None:
+        return None
+    m = pre[7]
+    _chk(m.dtype == torch.uint8 and m.is_contiguous() and m.numel() * 8 == x.numel(), "pre: mask [P][K/8] uint8")
+    return m
+
+
+def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None):
+    """y[P][N] = x[P][K] . w[N][K]^T on the panel / A-stationary kernels (K <= 256) or the long-reduction kernel
+    (K >= 512); epilogues as conv3x3 / conv_dgrad; pre: the BN-backward operand prologue (_pre_args, and the
+    operand mask of _pre_mask on the long-reduction kernel)."""
     P, Kc = x2d.shape
     N = w2d.shape[0]
     y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
@@ -234,8 +251,14 @@ def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, 
         slab = torch.empty(2 * lib().pdnn_conv1x1_panel_stats_rows(P), N, device=x2d.device, dtype=F32)
     if bn is not None:
         t, mean, inv, msc, msh = bn
+    mask = _pre_mask(pre, x2d)
+    if Kc >= 512:
+        call("pdnn_conv1x1_wide", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
+             ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), ptr(mask), stream())
+        return y, slab
+    _chk(mask is None, "conv1x1_panel: a masked operand (pre mask) needs K >= 512")
     call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), ptr(bn_mask), *_pre_args(pre, x2d), stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
     return y, slab
 
 
@@ -250,6 +273,7 @@ def conv3x3_flip(w):
 def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, pre=None):
     """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
     conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
+    _chk(_pre_mask(pre, x) is None, "conv3x3: a masked operand (pre mask) needs the long-reduction 1x1 kernel")
     Nimg, H, W, C = x.shape
     Ko = w.shape[0]
     y = out if out is not None else torch.empty(Nimg, H, W, Ko, device=x.device, dtype=BF16)
@@ -277,7 +301,7 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
     if pro is None and _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
         return conv3x3(x, w, want_stats=want_stats)
-    if pro is None and _panel_ok(N * H * W, C, K, R, S, st, pad):
+    if pro is None and _panel_ok(N * H * W, C, K, R, S, st, pad, fwd=True):
         y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats)
         return y.view(N, H, W, K), slab
     y = torch.empty(N, Ho, Wo, K, device=x.device, dtype=BF16)
@@ -293,8 +317,17 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
 def _panel_dgrad_k(K):
     """Data gradients (dx[P][C] = dy[P][K] . W) on the panel / A-stationary kernels: K = 64 (ResNet stage 1),
     K = 256 and, with the A-stationary kernel for every K (tuning areg = 2), K = 128.  The LDS-panel kernel
-    lost to the implicit-GEMM engine at K = 128 (176 vs 154 us, gpurun_out/r3_08)."""
-    return K in (64, 256) or (K == 128 and tune_get("areg") >= 2)
+    lost to the implicit-GEMM engine at K = 128 (176 vs 154 us, gpurun_out/r3_08).  K >= 512: the long-reduction
+    streaming kernel (conv1x1_wide.hip)."""
+    return K in (64, 256) or (K == 128 and tune_get("areg") >= 2) or (K >= 512 and _tuning.get("wide1x1_dgrad") == 1)
+
+
+def dgrad_pre_mask_ok(dy_shape, w_shape):
+    """Whether conv_dgrad takes ``pre=`` with the 8th (mask) entry: the operand is the block output's gradient,
+    masked by its ReLU bits inside the loads (bn_bwd_apply mode 3) -- the long-reduction kernel (K >= 512)."""
+    N, Ho, Wo, K = dy_shape
+    Kw, R, S, C = w_shape
+    return K >= 512 and R == 1 and S == 1 and _panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, 1, 0)
 
 
 def dgrad_pre_ok(dy_shape, w_shape, st, pad):
@@ -306,17 +339,7 @@ def dgrad_pre_ok(dy_shape, w_shape, st, pad):
             or (_panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
 
 
-def resbn_ok(dy_shape, w_shape):
-    """Whether conv_dgrad takes ``bn_mask=`` (the residual epilogue that also reduces the BatchNorm backward
-    of the block below): 1x1 / stride-1 data gradients on the A-stationary kernel with K = 64 / 128 (at K = 256
-    the extra epilogue operands push that kernel into scratch)."""
-    N, Ho, Wo, K = dy_shape
-    Kw, R, S, C = w_shape
-    return (K in (64, 128) and C % 64 == 0 and R == 1 and S == 1
-            and _panel_ok(N * Ho * Wo, K, C, R, S, 1, 0))
-
-
-def dgrad_weight(dy_shape, w, x_shape, st, pad, bn_mask=False):
+def dgrad_weight(dy_shape, w, x_shape, st, pad):
     """The transformed weight conv_dgrad builds on entry for this data gradient (tap-flipped transposed 3x3
     weight for the halo kernel, transposed 1x1 weight for the panel / A-stationary kernel), or None when its
     route takes the weight as is.  Pass it back as ``conv_dgrad(..., wprep=...)``: the fused blocks make it
@@ -324,8 +347,6 @@ def dgrad_weight(dy_shape, w, x_shape, st, pad, bn_mask=False):
     N, Ho, Wo, K = dy_shape
     _, H, W, C = x_shape
     Kw, R, S, C2 = w.shape
-    if bn_mask:
-        return transpose_bf16(w.view(K, C))
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         return conv3x3_flip(w)
     if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad):
@@ -333,8 +354,7 @@ def dgrad_weight(dy_shape, w, x_shape, st, pad, bn_mask=False):
     return None
 
 
-def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None, bn_mask=None,
-               wprep=None):
+def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=None, pre=None, wprep=None):
     """dx = conv_transpose(dy, w) (+ res).  ``out`` may alias ``res`` (in-place accumulation: for a strided
     conv only the pixels its taps reach are touched, the others keep ``res``).
 
@@ -348,14 +368,11 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
 
     pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out): ``dy`` is the masked gradient gm of a BatchNorm
     whose backward apply (bn_bwd_apply mode 0) runs inside this conv's operand loads; dt_out (optional)
-    receives that dt for the weight gradient.  Only where dgrad_pre_ok().
+    receives that dt for the weight gradient.  Only where dgrad_pre_ok().  An 8th entry, uint8 ReLU bits
+    [P][K/8] (bn_apply's mask): ``dy`` is the unmasked gradient and the mask is applied in the loads too
+    (bn_bwd_apply mode 3); only where dgrad_pre_mask_ok().
 
-    wprep: dgrad_weight()'s result for this call (else it is made here).
-
-    bn_mask (with res and bn = (t, mean, invstd, None, None)): the output is the gradient of the BLOCK BELOW's
-    pre-ReLU sum, gm = (dx + res * res_mask) * bn_mask (bn_mask: that block's output ReLU bits), and the slab
-    holds the partial sums of gm and gm * (t - mean) * invstd of its BatchNorm (t = its BN input): its
-    bn_bwd_reduce pass runs here.  Returns (gm, slab).  Only where resbn_ok()."""
+    wprep: dgrad_weight()'s result for this call (else it is made here)."""
     _bf16_c(dy, "conv_dgrad.dy")
     N, H, W, C = x_shape
     _bf16_c(w, "conv_dgrad.w")
@@ -376,14 +393,6 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         _chk(res is not None and st == 1 and res_mask.dtype == torch.uint8 and res_mask.is_contiguous()
              and res_mask.numel() * 8 == N * H * W * C and (out is None or out.data_ptr() != res.data_ptr()),
              "conv_dgrad: res_mask needs res, stride 1, uint8 [N*H*W][C/8], out not aliasing res")
-    if bn_mask is not None:
-        _chk(res is not None and bn is not None and out is None and st == 1 and pad == 0
-             and resbn_ok(dy.shape, w.shape) and bn_mask.dtype == torch.uint8 and bn_mask.is_contiguous()
-             and bn_mask.numel() * 8 == N * H * W * C, "conv_dgrad: bn_mask needs res, bn, resbn_ok shapes")
-        y, slab = conv1x1_panel(dy.view(-1, K), wprep if wprep is not None else transpose_bf16(w.view(K, C)),
-                                res=res.view(-1, C), res_mask=res_mask, bn=(bn[0].view(-1, C), bn[1], bn[2], None, None),
-                                pre=pre, bn_mask=bn_mask)
-        return y.view(N, H, W, C), slab
     if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
         y, slab = conv3x3(dy, wprep if wprep is not None else conv3x3_flip(w), res=res, bn=bn, out=out,
@@ -528,32 +537,6 @@ def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=Non
     call("pdnn_bn_bwd_reduce", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
          ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), stream())
     return slab, slab2, rows
-
-
-def bn_bwd_reduce_fin(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=None, x2=None, mean2=None,
-                      invstd2=None, acc=None, acc2=None):
-    """bn_bwd_reduce + bn_bwd_finalize in one launch (the reduce's last blocks finalize, batchnorm.hip
-    bwd_fuse_tail).  -> ((dgamma, dbeta), (dgamma2, dbeta2) or None); acc / acc2 = (gamma.grad, beta.grad)
-    also receive them (+=)."""
-    L, C = x.shape
-    dev = x.device
-    rows = lib().pdnn_bn_reduce_rows(L, C)
-    ng = lib().pdnn_bn_bwd_reduce_fin_groups(L, C)
-    npass = 2 if x2 is not None else 1
-    slab = torch.empty(2 * rows, C, device=dev, dtype=F32)
-    slab2 = torch.empty_like(slab) if x2 is not None else None
-    work = torch.empty(npass * ng * 2 * C, device=dev, dtype=F32)
-    cnt = _fin_counters(C, dev, n=ng + 1)
-    dg, db = torch.empty(C, device=dev, dtype=F32), torch.empty(C, device=dev, dtype=F32)
-    dg2 = db2 = None
-    if x2 is not None:
-        dg2, db2 = torch.empty(C, device=dev, dtype=F32), torch.empty(C, device=dev, dtype=F32)
-    ga, ba = acc if acc is not None else (None, None)
-    ga2, ba2 = acc2 if acc2 is not None else (None, None)
-    call("pdnn_bn_bwd_reduce_fin", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
-         ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), ptr(work), ptr(cnt), ptr(dg),
-         ptr(db), ptr(ga), ptr(ba), ptr(dg2), ptr(db2), ptr(ga2), ptr(ba2), stream())
-    return (dg, db), ((dg2, db2) if x2 is not None else None)
 
 
 def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=None):

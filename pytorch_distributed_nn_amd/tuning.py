@@ -6,6 +6,11 @@ both tables; the kernel library reports unknown ones when it loads).  Each defau
 =================  =======  ===========================================================================
 key                default  meaning (measurement)
 =================  =======  ===========================================================================
+wide1x1_fwd        1        1x1 / stride-1 forward convs with K >= 512 input channels on the long-reduction streaming
+                            kernel (conv1x1_wide.hip) instead of the implicit-GEMM engines
+wide1x1_dgrad      1        ... and the 1x1 / stride-1 data gradients with K >= 512
+bn3_pre            1        Bottleneck: BN3's backward apply (mode 3, the output ReLU bits) inside conv3's data-gradient
+                            operand loads on that kernel instead of a separate apply pass
 side_wgrad         1        conv weight gradients on a second HIP stream beside the data-gradient chain
                             (ResNet-50 +8.3%, profiles/resnet50_bs256_side_stream_r2.txt)
 materialize_a2     1        Bottleneck: write a2 = relu(bn2(t2)) once instead of conv3's operand prologue
@@ -17,10 +22,6 @@ bwd_pre            1        BatchNorm-backward apply (dt = k*gm + A*t + B) fused
 stem               2        ImageNet stem (stem.hip): 0 generic conv + bn_apply + max-pool, 1 direct 7x7/s2 kernel on
                             the NHWC copy + fused BN-apply/ReLU/max-pool, 2 the same reading the NCHW batch
 direct_grad        1        fused ops accumulate weight gradients straight into the flat arena
-opt_overlap        0        GPT-2 on one GPU: AdamW chunks on a side stream during the backward
-bn_link            0        consecutive identity Bottlenecks: the upper block's conv1 data gradient also masks its
-                            output and reduces the lower block's BN3 backward sums (no bn_bwd_reduce pass there);
-                            off: 10,209-10,237 vs 10,285-10,309 img/s (gpurun_out/r3_35)
 bn_fused_fin       1        BatchNorm slab finalize in one launch (level-1 blocks hand their rows to the last
                             arriver through a counter, batchnorm.hip bn_slab_fused_kernel) instead of two
 stem_wgrad_nchw    1        ImageNet stem weight gradient straight from the NCHW batch (stem_wgrad.hip) instead of the
@@ -29,10 +30,6 @@ light_events       1        cross-stream fork / join of the two-stream ResNet st
                             (streams.hip) instead of torch's Stream.wait_stream (system-scope release per marker);
                             off: 10,604-10,615 vs 10,687-10,689 img/s (gpurun_out/r3_58); DDP path (bucket launches
                             fork too) 10,574-10,586 vs 10,692-10,695 (r3_60)
-bn_red_fin         0        BatchNorm-backward reduce finalized by its own last blocks (two ticket levels, batchnorm.hip
-                            bwd_fuse_tail) instead of a separate finalize launch (Bottleneck BN3 / BNd, _bn_back);
-                            on: 10,711-10,728 vs 10,764-10,798 img/s (gpurun_out/r3_71: the single-block group sums
-                            are latency-bound and the tail costs the reduce two VGPR waves)
 wprep_once         1        wprep: one side-stream fork per model forward and one compute-stream wait per backward (the
                             latest transform event covers the earlier ones) instead of one of each per block;
                             off: 10,819-10,821 vs 10,844-10,853 img/s (gpurun_out/r3_73)
@@ -52,9 +49,9 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, "opt_overlap": 0, "bn_link": 0,
+DEFAULTS = {"wide1x1_fwd": 1, "wide1x1_dgrad": 1, "bn3_pre": 1, "side_wgrad": 1, "materialize_a2": 1, "conv3x3": 1, "panel1x1": 1, "bwd_pre": 1, "stem": 2, "direct_grad": 1, 
             "wgrad1x1_pp_pix": 200704, "bn_fused_fin": 1, "wprep": 1, "wgrad3x3": 1, "stem_wgrad_nchw": 1,
-            "pool_bnred": 1, "light_events": 1, "bn_red_fin": 0, "wprep_once": 1}
+            "pool_bnred": 1, "light_events": 1, "wprep_once": 1}
 
 _VALUES = dict(DEFAULTS)
 

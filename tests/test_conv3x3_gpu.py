@@ -225,8 +225,9 @@ def test_conv1x1_panel_pre_matches_separate_apply(K, areg, shape):
 
 
 def test_dgrad_pre_rejected_on_gemm_engine(K):
-    gm, t, mean, inv, g, dg, db = _pre_operands((2, 8, 8, 512))
-    w = (torch.randn(512, 1, 1, 64, device="cuda") * 0.1).to(BF)
+    # K = 192: neither the panel / A-stationary kernels (K <= 256 powers of two) nor the long-reduction one
+    gm, t, mean, inv, g, dg, db = _pre_operands((2, 8, 8, 192))
+    w = (torch.randn(192, 1, 1, 64, device="cuda") * 0.1).to(BF)
     assert not K.dgrad_pre_ok(gm.shape, w.shape, 1, 0)
     with pytest.raises(ValueError):
         K.conv_dgrad(gm, w, (2, 8, 8, 64), 1, 0, pre=(t, mean, inv, g, dg, db, None))

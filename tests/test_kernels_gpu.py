@@ -474,41 +474,3 @@ def test_conv_dgrad_masked_residual(K, shape):
     assert rel(dx, ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("L,C", [(300, 64), (200704, 64), (50176, 256), (12544, 2048)])
-@pytest.mark.parametrize("mode", [0, 2, 3])
-@pytest.mark.parametrize("x2", [False, True])
-def test_bn_bwd_reduce_fin_matches_two_passes(K, L, C, mode, x2):
-    """BN-backward reduce finalized by its own last blocks (two ticket levels) == bn_bwd_reduce +
-    bn_bwd_finalize, including the second BN and the accumulation into the parameter gradients; repeated so
-    the counters must come back zeroed."""
-    g = rnd(L, C)
-    x = rnd(L, C)
-    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
-    msrc = msc = msh = None
-    if mode == 2:
-        msrc, msc, msh = x, torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
-    elif mode == 3:
-        msrc = torch.randint(0, 256, (L, C // 8), device="cuda", dtype=torch.uint8)
-    xx = rnd(L, C) if x2 else None
-    m2, i2 = (torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5) if x2 else (None, None)
-    slab, slab2, rows = K.bn_bwd_reduce(g, x, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh, x2=xx,
-                                        mean2=m2, invstd2=i2)
-    dg_ref, db_ref = K.bn_bwd_finalize(slab, rows)
-    if x2:
-        dg2_ref, db2_ref = K.bn_bwd_finalize(slab2, rows)
-    for rep in range(3):
-        acc = (torch.ones(C, device="cuda"), torch.full((C,), 2.0, device="cuda"))
-        acc2 = (torch.ones(C, device="cuda"), torch.full((C,), 2.0, device="cuda")) if x2 else None
-        (dg, db), second = K.bn_bwd_reduce_fin(g, x, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh,
-                                               x2=xx, mean2=m2, invstd2=i2, acc=acc, acc2=acc2)
-        tol = dict(rtol=1e-4, atol=1e-3)
-        torch.testing.assert_close(dg, dg_ref, **tol)
-        torch.testing.assert_close(db, db_ref, **tol)
-        torch.testing.assert_close(acc[0], 1.0 + dg_ref, **tol)
-        torch.testing.assert_close(acc[1], 2.0 + db_ref, **tol)
-        if x2:
-            torch.testing.assert_close(second[0], dg2_ref, **tol)
-            torch.testing.assert_close(second[1], db2_ref, **tol)
-            torch.testing.assert_close(acc2[0], 1.0 + dg2_ref, **tol)
-        else:
-            assert second is None

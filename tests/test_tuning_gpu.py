@@ -8,10 +8,10 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 
-# kernel-side entries -> alternative values (pp_ablate is a timing-only ablation: it skips work on purpose)
+# kernel-side entries -> alternative values
 ALT = {
     "glds": [0, 2], "glds_min_tiles": [1, 1 << 20], "glds_fwd_k": [64], "glds_dgrad_n": [64], "glds_dgrad_k": [64],
-    "glds_persistent": [1], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "pp_fp8": [0], "pp_conv_min_n": [64],
+    "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "pp_fp8": [0], "pp_conv_min_n": [64],
     "pp_conv_fwd_k": [64], "pp_conv_dgrad_k": [64], "pp_conv_bnb_k": [64], "staged_store": [0], "lowk_bn64": [0, 4],
     "split_blocks": [64, 2048], "conv3x3_force": [1], "areg": [0, 1],
 }
@@ -56,7 +56,7 @@ def K():
 
 def test_table_lists_every_entry(K):
     keys = {k for k, *_ in K.tune_table()}
-    assert keys == set(ALT) | {"pp_ablate"}
+    assert keys == set(ALT)
     for k, v, d, doc in K.tune_table():
         assert v == d and doc, k          # the test process runs the defaults
 
