@@ -295,140 +295,6 @@ __global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// 1x1 / stride-1 convs with a short reduction (K = C_in <= 128) and a wide output: y[P][N] = x[P][K] . W^T.
-// The implicit-GEMM engine gives every 64-column output tile its own block, which re-fetches the A rows
-// and pays a full load -> MFMA -> epilogue latency chain for ONE k-step (ResNet-50 stage-1 conv3, K = 64
-// -> N = 256: 258 us against a ~100 us write floor, r3 trace).  Here a block owns 256 pixels: their A
-// panel ([256][K] bf16, <= 64 KB) is staged into LDS once, then the block walks its share of the output
-// columns in 64-wide chunks -- the weight tile of the next (chunk, k-chunk) step fetched into registers
-// under the current step's MFMAs, the epilogue of a chunk (BN statistics, stores) issued as soon as its
-// reduction ends.  Grid = pixel tiles x column groups (groups only when the pixel tiles alone cannot fill
-// the chip).  Same epilogues as the 3x3 kernel (stats / BN-backward / masked residual).
-// ---------------------------------------------------------------------------------------------------
-template <int EPI, bool PRE>
-__global__ void __launch_bounds__(256, 2) conv1x1_panel_kernel(C3Args a) {
-    constexpr int NB = 64, FN = 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* const panel = reinterpret_cast<bf16_t*>(smem);               // [K/64][257 px][64]
-    const int KC = a.C >> 6;
-    bf16_t* const bbuf = panel + KC * (C3_BM + 1) * 64;                  // [2][64][64]
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int groups = a.ntiles;                                          // column groups
-    const int t = xcd_remap(blockIdx.x, a.tiles * groups);
-    const int tile = t / groups, grp = t - tile * groups;
-    const int chunks = (a.N >> 6) / groups;                               // 64-column chunks of this block
-    const int c00 = grp * chunks;
-    const int p0 = tile * C3_BM;
-    const int zpx = C3_BM;                                                // zero pixel of each k-chunk image
-
-    // ---- A panel: pixels p0 .. p0+255, all K channels (masked unconditional loads; rows >= P are zero)
-    constexpr int J = PRE ? 4 : 8;
-    for (int i0 = 0; i0 < KC * C3_BM * 8; i0 += 256 * J) {
-        u16x8_t v[J], tv[PRE ? J : 1];
-        PreCoef pc;
-        if constexpr (PRE) {                      // i0 / 2048 = this iteration's k-chunk (J * 256 <= 2048)
-            const int kc0 = i0 / (C3_BM * 8);
-            pre_coef(a, (kc0 < KC ? kc0 : KC - 1) * 64 + (tid & 7) * 8, pc);
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int i = i0 + j * 256 + tid;                 // = (kc * 256 + px) * 8 + q
-            const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
-            const long gp = (long)p0 + px;
-            const long gc = gp < a.P ? gp : a.P - 1;
-            const int kk = kc < KC ? kc : KC - 1;
-            v[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + kk * 64 + q * 8);
-            if constexpr (PRE) tv[j] = *reinterpret_cast<const u16x8_t*>(a.pre_t + gc * a.C + kk * 64 + q * 8);
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int i = i0 + j * 256 + tid;
-            const int kc = i / (C3_BM * 8), px = (i >> 3) & (C3_BM - 1), q = i & 7;
-            const long gp = (long)p0 + px;
-            const bool ok = i < KC * C3_BM * 8 && gp < a.P;
-            if constexpr (PRE) {
-                v[j] = pre_apply(pc, v[j], tv[j]);
-                if (a.pre_out && grp == 0 && ok) *reinterpret_cast<u16x8_t*>(a.pre_out + gp * a.C + kc * 64 + q * 8) = v[j];
-            }
-            v[j] = mask16(v[j], ok);
-            if (kc < KC) *reinterpret_cast<u16x8_t*>(panel + kc * (C3_BM + 1) * 64 + halo_off(px, q)) = v[j];
-        }
-    }
-    if (tid < 8 * KC) *reinterpret_cast<u16x8_t*>(panel + (tid >> 3) * (C3_BM + 1) * 64 + zpx * 64 + (tid & 7) * 8) =
-        c3_zero8();
-
-    bool pv[4];
-    int hp[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        const int m = wave * 64 + f * 16 + (lane & 15);
-        pv[f] = p0 + m < a.P;
-        hp[f] = pv[f] ? m : zpx;
-    }
-
-    // weight tile of step s = (chunk s / KC, k-chunk s % KC): rows n, 64 k, K-major kimg_off image
-    u16x8_t rb[2];
-    auto load_b = [&](int s) {
-        const int n0 = (c00 + s / KC) * NB, k0 = (s % KC) * 64;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
-            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * a.C + k0 + q * 8);
-        }
-    };
-    auto store_b = [&](int buf) {
-        bf16_t* B = bbuf + buf * NB * 64;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
-            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
-        }
-    };
-    load_b(0);
-    store_b(0);
-    __syncthreads();
-    const int steps = chunks * KC;
-    f32x4_t acc[4][FN];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < steps; ++s) {
-        const bool more = s + 1 < steps;
-        if (more) load_b(s + 1);
-        const int kc = s % KC;
-        const bf16_t* A = panel + kc * (C3_BM + 1) * 64;
-        const bf16_t* B = bbuf + (s & 1) * NB * 64;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8_t af[4], bfr[FN];
-            const int q = ks * 4 + (lane >> 4);
-#pragma unroll
-            for (int f = 0; f < 4; ++f)
-                af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(A + halo_off(hp[f], q)));
-#pragma unroll
-            for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
-#pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-                for (int fn = 0; fn < FN; ++fn)
-                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
-        }
-        if (kc == KC - 1) {                       // this chunk's reduction is complete: epilogue, then restart
-            c3_epilogue<NB, EPI>(a, acc, tile, p0, (c00 + s / KC) * NB, wave, lane, pv);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-        if (more) {
-            store_b((s + 1) & 1);
-            __syncthreads();
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
 // 1x1 / stride-1 convs with K = 64 * KC <= 256 input channels, A-stationary: each wave holds the MFMA
 // fragments of its 64 pixels x all K channels in VGPRs for the whole block (KC = 4: 128 VGPRs), so the
 // activations are read once, straight from global memory in fragment order, and never pass through LDS;
@@ -645,28 +511,6 @@ int c3_dispatch(const C3Args& a, int epi, hipStream_t st) {
 
 
 
-template <int EPI, bool PRE>
-int p1_launch(const C3Args& a, int sm, hipStream_t st) {
-    static int attr_done = 0;
-    if (sm > attr_done) {
-        (void)hipFuncSetAttribute((const void*)conv1x1_panel_kernel<EPI, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  sm);
-        attr_done = sm;
-    }
-    hipLaunchKernelGGL((conv1x1_panel_kernel<EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
-    PDNN_LAUNCH_RET;
-}
-
-template <bool PRE>
-int p1_dispatch(const C3Args& a, int epi, int sm, hipStream_t st) {
-    switch (epi) {
-        case C3_BNB: return p1_launch<C3_BNB, PRE>(a, sm, st);
-        case C3_STATS: return p1_launch<C3_STATS, PRE>(a, sm, st);
-        case C3_RES: return p1_launch<C3_RES, PRE>(a, sm, st);
-        default: return p1_launch<C3_PLAIN, PRE>(a, sm, st);
-    }
-}
-
 template <int KC, int NB, int EPI, bool PRE>
 int areg_launch(const C3Args& a, hipStream_t st) {
     constexpr int sm = 2 * KC * NB * 128 + (PRE ? 3 * 64 * KC * 4 : 0);
@@ -793,10 +637,11 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     return pre ? c3_dispatch<64, true>(a, epi, st) : c3_dispatch<64, false>(a, epi, st);
 }
 
-// 1x1 / stride-1 conv on the pixel-panel kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128}, N % 64 == 0.
-// Epilogues as pdnn_conv3x3.  Returns hipErrorInvalidValue for shapes it does not take.
+// 1x1 / stride-1 conv on the A-stationary kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128, 256},
+// N % 64 == 0.  Epilogues as pdnn_conv3x3.  Returns hipErrorInvalidValue for shapes it does not take.  (An LDS
+// pixel-panel kernel for K <= 128 lost to it: r3_15, 9,844 vs 9,780 img/s; removed in round 4.)
 PDNN_API int pdnn_conv1x1_panel_supported(long P, int K, int N) {
-    const bool k_ok = K == 64 || K == 128 || (K == 256 && pg::tune().areg >= 1);
+    const bool k_ok = K == 64 || K == 128 || K == 256;
     return k_ok && N % 64 == 0 && N >= 64 && P > 0 && P < (1L << 30) ? 1 : 0;
 }
 
@@ -816,16 +661,7 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
         return (int)hipErrorInvalidValue;
     const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
-    // K = 256 always on the A-stationary kernel (the panel's A image would not leave room for 2 blocks per CU)
-    if (K == 256 || pg::tune().areg >= 2)
-        return pre_t ? areg_run<true>(a, K, epi, st) : areg_run<false>(a, K, epi, st);
-    // column groups: split the output columns over blocks only until the grid covers ~2 blocks per CU
-    const int chunks = N / 64;
-    int g = 1;
-    while (g < chunks && (long)a.tiles * g < 512 && chunks % (2 * g) == 0) g *= 2;
-    a.ntiles = g;
-    const int sm = (K / 64) * (C3_BM + 1) * 128 + 2 * 64 * 128;
-    return pre_t ? p1_dispatch<true>(a, epi, sm, st) : p1_dispatch<false>(a, epi, sm, st);
+    return pre_t ? areg_run<true>(a, K, epi, st) : areg_run<false>(a, K, epi, st);
 }
 
 PDNN_API int pdnn_conv1x1_panel_stats_rows(long P) { return (int)cdiv(P, C3_BM) * 4; }

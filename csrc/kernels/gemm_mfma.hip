@@ -642,23 +642,24 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
 #include "gemm_glds.h"
 
-// Engine selection reads the dispatch table (tuning.h: entries glds, glds_min_tiles, glds_fwd_k,
-// glds_dgrad_n / _k, with the measurements behind each default).
-// The 256-row tiles win once the grid fills most of the 256 CUs; with fewer tiles the 128-tile kernel's finer
-// grid (2 blocks/CU) has better wave quantisation.  Per layer (profiles/conv_layers_glds_vs_reg_r1.json) glds
-// wins the implicit-GEMM forward once the reduction is long and the data gradient unless both C and K are
-// small, but the glds data gradient's BN-backward epilogue tiles ran 2.3% slower in the whole step, so the
-// data gradient stays on the register-staged kernel (7,790 -> 7,970 img/s).
+// Engine selection (tuning.h entry glds: 0 off, 1 automatic, 2 whenever the operands allow).
+// The 256-row tiles win once the grid fills most of the 256 CUs (>= 192 output tiles: r1 sweep,
+// profiles/glds_threshold_sweep_r1.jsonl); with fewer tiles the 128-tile kernel's finer grid (2 blocks/CU) has
+// better wave quantisation.  Per layer (profiles/conv_layers_glds_r1.json) glds wins the implicit-GEMM forward
+// from a reduction of 1024 (512 / 1024 / never tied in r1) and the data gradient unless both C and K are small,
+// but the glds data gradient's BN-backward epilogue tiles ran 2.3% slower in the whole step, so the data gradient
+// stays on the register-staged kernel (7,790 -> 7,970 img/s).
+constexpr int kGldsMinTiles = 192;
+constexpr int kGldsFwdK = 1024;
 int glds_mode() { return tune().glds; }
 bool glds_enabled() { return glds_mode() != 0; }
-int glds_min_tiles() { return tune().glds_min_tiles; }
 template <int AM>
 bool glds_worth(const GemmArgs& a, int batch, int splits) {
     if (glds_mode() == 2) return true;
     const long tiles = cdiv(a.M, GBM) * cdiv(a.N, glds_bn(a.N)) * (long)batch * splits;
-    if (tiles < glds_min_tiles()) return false;
-    if constexpr (AM == A_CONV) return a.K >= tune().glds_fwd_k;
-    if constexpr (AM == A_CONVT) return a.N >= tune().glds_dgrad_n || a.K >= tune().glds_dgrad_k;
+    if (tiles < kGldsMinTiles) return false;
+    if constexpr (AM == A_CONV) return a.K >= kGldsFwdK;
+    if constexpr (AM == A_CONVT) return false;
     return true;
 }
 
@@ -672,13 +673,15 @@ FastDiv make_fdiv(uint32_t d) {
     return f;
 }
 
-// 1x1 stride-1 convs on the ping-pong engine (tuning.h pp_conv_*): the plain / residual data gradient wins
-// there from K >= 512; the forward with BN statistics and the data gradient with the BN-backward epilogue
-// are slower there than on the 128-row kernel (the fused epilogue roughly doubles the pp epilogue time).
-int pp_conv_min_n() { return tune().pp_conv_min_n; }
-int pp_conv_fwd_k() { return tune().pp_conv_fwd_k; }
-int pp_conv_dgrad_k() { return tune().pp_conv_dgrad_k; }
-int stage_store_mode() { return tune().staged_store; }
+// 1x1 stride-1 data gradients on the ping-pong engine: the plain / residual ones win there from K >= 512 with
+// >= 128 output columns (r2_46: 512 vs 256 +0.5%); the forward with BN statistics and the data gradient with
+// the BN-backward epilogue are slower there than on the 128-row kernel (the fused epilogue roughly doubles the
+// pp epilogue time), and K >= 512 1x1 convs are routed to the long-reduction kernel (conv1x1_wide.hip) first.
+constexpr int kPPConvMinN = 128;
+constexpr int kPPConvDgradK = 512;
+// 128-row kernel bf16 epilogue: 1 = stores staged through LDS (full rows), 0 = direct fragment stores (tests)
+int g_stage_store = 1;
+int stage_store_mode() { return g_stage_store; }
 
 template <int AM, int BMODE, int EM, bool PA, bool PB, int BNW>
 int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
@@ -701,9 +704,9 @@ int launch_w(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
     PDNN_LAUNCH_RET;
 }
 
-// lowk_bn64 = k: GEMMs of at most k K-steps use the 128x64 tile (fewer registers: more blocks per CU to hide
-// the load -> MFMA -> store latency of short reductions); 0 = off (r2_42-44 sweep in tuning.h)
-int lowk_bn64_mode() { return tune().lowk_bn64; }
+// GEMMs of at most this many K-steps use the 128x64 tile (fewer registers: more blocks per CU to hide the
+// load -> MFMA -> store latency of short reductions; r2_42-44 sweep: 24)
+constexpr int kLowKBn64 = 24;
 
 // the register-staged 128-row kernel only (the weight gradients' split-K atomics): N <= 64 -> 128x64 tile
 template <int AM, int BMODE, int EM, bool PA, bool PB>
@@ -724,7 +727,7 @@ int launch(const GemmArgs& a, int splits, hipStream_t st, int batch = 1) {
         }
     }
     if (a.N <= 64) return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
-    if (lowk_bn64_mode() && EM != E_ATOMIC && a.ktiles_per_split <= lowk_bn64_mode())
+    if (EM != E_ATOMIC && a.ktiles_per_split <= kLowKBn64)
         return launch_w<AM, BMODE, EM, PA, PB, 64>(a, splits, st, batch);
     return launch_w<AM, BMODE, EM, PA, PB, 128>(a, splits, st, batch);
 }
@@ -733,8 +736,9 @@ template <int BNW>
 int tiles_of(const GemmArgs& a) { return (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW)); }
 
 int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
-    // enough workgroups to cover 256 CUs twice (tuning.h split_blocks), but keep >= 4 K-steps per split
-    const int blocks = tune().split_blocks;
+    // enough workgroups to cover 256 CUs twice (r2 sweep: 256 / 384 -2% / -1%, 768 equal), but keep >= 4
+    // K-steps per split
+    const int blocks = 512;
     int want = (blocks + tiles - 1) / tiles;
     int s = want < max_splits ? want : max_splits;
     int cap = ktiles / 4;
@@ -774,8 +778,8 @@ static void ensure_attrs() {}
 // ------------------------------------------------------------------------------------------------
 
 PDNN_API int pdnn_set_staged_store(int mode) {
-    const int old = stage_store_mode();
-    tune().staged_store = mode;
+    const int old = g_stage_store;
+    g_stage_store = mode;
     return old;
 }
 
@@ -861,7 +865,7 @@ PDNN_API int pdnn_gemm_fp8(const uint8_t* X, long ldx, const uint8_t* W, long ld
     a.bias = bias; a.relu = act; a.ep_aux = aux; a.ep_res = res; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
     // ping-pong engine (fp8 slices of 128 bytes per row) unless tuning pp_fp8 = 0 / pp off: the glds engine
-    if (pp_mode_ref() && tune().pp_fp8 && M >= 16 && N >= 16)
+    if (pp_mode_ref() && M >= 16 && N >= 16)
         return pp_fp8_launch(a, out_f32 ? E_F32 : E_BF16, st);
     const int bn = glds_bn(N);
     if (out_f32) {
@@ -927,13 +931,6 @@ PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
-    if (R == 1 && S == 1 && st == 1 && pad == 0 && Ko >= pp_conv_min_n() && C >= pp_conv_fwd_k()) {
-        // 1x1 stride-1 conv = plain GEMM  y[M][Ko] = x[M][C] . w[Ko][C]^T: the ping-pong engine (prologue and
-        // BN statistics fused there too)
-        GemmArgs p = a;
-        p.lda = C;
-        if (pp_supported(p, A_KMAJOR, B_KMAJOR, E_BF16, 1, 1)) return pp_launch(p, A_KMAJOR, B_KMAJOR, E_BF16, stream);
-    }
     if (pro_scale) return launch<A_CONV, B_KMAJOR, E_BF16, true, false>(a, 1, stream);
     return launch<A_CONV, B_KMAJOR, E_BF16, false, false>(a, 1, stream);
 }
@@ -984,8 +981,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
                              hipStream_t stream) {
     if (res_mask && (st != 1 || C % 8 || !res || res == dx)) return (int)hipErrorInvalidValue;
     ensure_attrs();
-    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= pp_conv_min_n() &&
-        (bn_x ? Ko >= tune().pp_conv_bnb_k : Ko >= pp_conv_dgrad_k())) {
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= kPPConvMinN && !bn_x && Ko >= kPPConvDgradK) {
         // 1x1 stride-1: dx[M][C] = dy[M][Ko] . w[Ko][C] (w as a [k][n] matrix) on the ping-pong engine
         GemmArgs a{};
         a.M = Nimg * H * W; a.N = C; a.K = Ko;

@@ -232,11 +232,11 @@ _WPREP_WAITED = {}    # device index -> highest wprep sequence number the comput
 
 @contextlib.contextmanager
 def side_forward(dev):
-    """Around a model's block loop (tuning wprep_once): the side stream waits on the compute stream ONCE (the
-    optimizer step that refreshed the weights is then behind it), so the blocks' weight transforms need no fork
-    of their own."""
+    """Around a model's block loop: the side stream waits on the compute stream ONCE (the optimizer step that
+    refreshed the weights is then behind it), so the blocks' weight transforms need no fork of their own (one
+    fork per block: 10,819-10,821 vs 10,844-10,853 img/s, gpurun_out/r3_73)."""
     side = _side_stream(dev) if dev.type == "cuda" else None
-    if side is None or not tuning.get("wprep") or not tuning.get("wprep_once"):
+    if side is None:
         yield
         return
     K.stream_wait(side, torch.cuda.current_stream(dev))
@@ -249,9 +249,9 @@ def side_forward(dev):
 
 def _wait_wprep(dev, ev, seq):
     """The backward's wait for its block's transformed weights.  The side stream is in order, so waiting on the
-    latest wprep event covers every earlier one: with wprep_once only the first block of the backward (the
-    last of the forward) waits."""
-    if tuning.get("wprep_once") and _WPREP_WAITED.get(dev.index, -1) >= seq:
+    latest wprep event covers every earlier one: only the first block of the backward (the last of the forward)
+    waits."""
+    if _WPREP_WAITED.get(dev.index, -1) >= seq:
         return
     torch.cuda.current_stream(dev).wait_event(ev)
     _WPREP_WAITED[dev.index] = max(seq, _WPREP_WAITED.get(dev.index, -1))
@@ -263,7 +263,7 @@ def _prep_dgrad_weights(x, specs):
     ~30 small transform kernels on its critical path.  specs: [(dy_shape, w, x_shape, st, pad)].
     -> (list of weights or None, event the backward waits on) or None without a side stream."""
     side = _side_stream(x.device)
-    if side is None or not tuning.get("wprep"):
+    if side is None:
         return None
     main = torch.cuda.current_stream(x.device)
     idx = x.device.index
@@ -288,7 +288,7 @@ def _prep_dgrad_weights(x, specs):
 def _pre_ok(t, wk, st, pad):
     """Whether the consumer of dt = bn_bwd_apply(gm, t) (data gradient of the conv with weight wk) takes the
     apply as its operand prologue."""
-    return tuning.get("bwd_pre") == 1 and K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
+    return K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
 
 
 def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None, pre=None):
@@ -337,17 +337,13 @@ class BottleneckFn(torch.autograd.Function):
         C1 = t1.shape[-1]
         a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)
         t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
-        if tuning.get("materialize_a2"):
-            # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
-            # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
-            # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs
-            # 0.29 + 1.87 materialised)
-            C2 = t2.shape[-1]
-            a2 = K.bn_apply(t2.view(-1, C2), s2, h2, relu=True).view(t2.shape)
-            t3, m3, i3, s3, h3 = _conv_bn(a2, k3, 1, 0, None, training, (g3, b3), bufs[4:6], mom, eps)
-        else:
-            a2 = None
-            t3, m3, i3, s3, h3 = _conv_bn(t2, k3, 1, 0, (s2, h2), training, (g3, b3), bufs[4:6], mom, eps)
+        # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
+        # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
+        # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs
+        # 0.29 + 1.87 materialised)
+        C2 = t2.shape[-1]
+        a2 = K.bn_apply(t2.view(-1, C2), s2, h2, relu=True).view(t2.shape)
+        t3, m3, i3, s3, h3 = _conv_bn(a2, k3, 1, 0, None, training, (g3, b3), bufs[4:6], mom, eps)
         C3 = t3.shape[-1]
         if down:
             if side_down is not None:
@@ -404,7 +400,7 @@ class BottleneckFn(torch.autograd.Function):
                                          x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                          dbeta2=dbd)
             gres = None
-        elif MASKED_RES and a2 is not None and tuning.get("bn3_pre") and K.dgrad_pre_mask_ok(t3.shape, k3.shape):
+        elif MASKED_RES and tuning.get("bn3_pre") and K.dgrad_pre_mask_ok(t3.shape, k3.shape):
             # BN3's backward apply runs inside conv3's data-gradient operand loads (the long-reduction
             # kernel reads gout, t3 and the ReLU bits, writes dt3 once for the weight gradient): no separate
             # apply pass (read gout + t3, write dt3) and no re-read of dt3 by the data gradient
@@ -421,10 +417,8 @@ class BottleneckFn(torch.autograd.Function):
         dt3 = dt3.view(t3.shape)
         dy3 = gout if pre3 is not None else dt3
 
-        def wgrad3():        # conv3 (input a2 = relu(bn2(t2)), or virtual through the prologue)
-            if a2 is not None:
-                return sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
-            return sink.wgrad(P[6], t2, dt3, 1, 1, 1, 0, pro=(s2, h2))
+        def wgrad3():        # conv3 (input a2 = relu(bn2(t2)))
+            return sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
         if pre3 is None:
             dw3 = wgrad3()
         bn1 = (t1, m1, i1, s1, h1)
@@ -562,30 +556,11 @@ class StemFn(torch.autograd.Function):
         kpad = shadows[0]
         nchw = kpad.dim() == 3          # shadow from K.stem_weight_nchw: x is the NCHW bf16 batch itself
         direct = nchw or (pool and K.stem_ok(x.shape, kpad.shape, stride, pad))
-        ev = None
         xn = None
-        if nchw and tuning.get("stem_wgrad_nchw"):
+        if nchw:
             # the weight gradient reads the NCHW batch itself (stem_wgrad.hip): no NHWC copy at all
             t, slab = K.stem_conv_nchw(x, kpad, want_stats=training)
             xn = x
-        elif nchw:
-            # the weight gradient (end of the backward) reads the NHWC copy: converted on the side stream,
-            # off the forward's critical path
-            side = _side_stream(x.device)
-            xin = x
-            if side is not None:
-                main = torch.cuda.current_stream(x.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    xin = K.nchw_to_nhwc(x, 8)
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                x.record_stream(side)
-                xin.record_stream(main)
-            else:
-                xin = K.nchw_to_nhwc(x, 8)
-            t, slab = K.stem_conv_nchw(x, kpad, want_stats=training)
-            x = xin
         if direct:
             # direct 7x7/s2 kernel, then BN + ReLU + max-pool in one pass over t; the backward recomputes the
             # ReLU mask from t (mask mode 2), so neither the activation nor its mask is stored
@@ -610,7 +585,6 @@ class StemFn(torch.autograd.Function):
         ctx.save_for_backward(x, t, mb, idx, m, i, gamma, s if direct else None, h if direct else None)
         ctx.nchw_wgrad = xn is not None
         ctx.conf = (stride, pad, pool, w.shape, (w.shape[0], 7, 7, 8) if nchw else kpad.shape)
-        ctx.ev = ev
         ctx.params = (w, gamma, beta)
         return y
 
@@ -626,7 +600,7 @@ class StemFn(torch.autograd.Function):
         if ctx.nchw_wgrad and mb is None:
             # the BN backward's apply runs inside the NCHW weight-gradient kernel's staging: dt never written;
             # its statistics come out of the max-pool gather's pass
-            fused = K.maxpool_bwd_bnred(gy, idx, t, m, i, s, h) if pool and tuning.get("pool_bnred") else None
+            fused = K.maxpool_bwd_bnred(gy, idx, t, m, i, s, h) if pool else None
             if fused is not None:
                 ga, slab, rows = fused
             else:
@@ -654,9 +628,6 @@ class StemFn(torch.autograd.Function):
             dt, dg, db = _bn_back(ga.view(-1, C), t.view(-1, C), m, i, gamma, 3, msrc=mb, sink=sink,
                                   bn_params=(P[1], P[2]))
         dt = dt.view(t.shape)
-        if ctx.ev is not None:
-            torch.cuda.current_stream(x.device).wait_event(ctx.ev)     # NHWC copy made on the side stream
-            ctx.ev = None
         if kshape[3] == wshape[1]:
             dw = sink.wgrad(P[0], x, dt, kshape[1], kshape[2], stride, pad)
         else:

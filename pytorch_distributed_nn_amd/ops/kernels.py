@@ -150,7 +150,7 @@ def stats_rows(M: int) -> int:
 # 3x3 / stride-1 / pad-1 convs run on the LDS-halo kernel (csrc/kernels/conv3x3.hip): 1 = whenever the
 # shape is supported (default), 0 = the implicit-GEMM engine (tuning conv3x3 / set_conv3x3_mode)
 from .. import tuning as _tuning
-_C3 = {"mode": _tuning.get("conv3x3"), "nb": 0}
+_C3 = {"mode": 1, "nb": 0}
 
 
 def tune_set(key: str, value: int) -> int:
@@ -192,9 +192,9 @@ def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
             and lib().pdnn_conv3x3_supported(N, H, W, Cin, Cout) == 1)
 
 
-# 1x1 / stride-1 convs with K in {64, 128} run on the pixel-panel kernel (csrc/kernels/conv3x3.hip):
-# tuning panel1x1 = 0 / set_panel_mode(0) sends them back to the implicit-GEMM engines (A/B runs)
-_P1 = {"mode": _tuning.get("panel1x1")}
+# 1x1 / stride-1 convs with K in {64, 128, 256} run on the A-stationary kernel (csrc/kernels/conv3x3.hip), K >= 512
+# on the long-reduction one (conv1x1_wide.hip): set_panel_mode(0) sends them back to the implicit-GEMM engines
+_P1 = {"mode": 1}
 
 
 def set_panel_mode(mode: int) -> int:
@@ -315,11 +315,9 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
 
 
 def _panel_dgrad_k(K):
-    """Data gradients (dx[P][C] = dy[P][K] . W) on the panel / A-stationary kernels: K = 64 (ResNet stage 1),
-    K = 256 and, with the A-stationary kernel for every K (tuning areg = 2), K = 128.  The LDS-panel kernel
-    lost to the implicit-GEMM engine at K = 128 (176 vs 154 us, gpurun_out/r3_08).  K >= 512: the long-reduction
-    streaming kernel (conv1x1_wide.hip)."""
-    return K in (64, 256) or (K == 128 and tune_get("areg") >= 2) or (K >= 512 and _tuning.get("wide1x1_dgrad") == 1)
+    """Data gradients (dx[P][C] = dy[P][K] . W) on the A-stationary kernel (K in {64, 128, 256}) or the
+    long-reduction streaming kernel (K >= 512, conv1x1_wide.hip)."""
+    return K in (64, 128, 256) or (K >= 512 and _tuning.get("wide1x1_dgrad") == 1)
 
 
 def dgrad_pre_mask_ok(dy_shape, w_shape):
@@ -422,6 +420,11 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
     return (dx, slab) if bn is not None else dx
 
 
+# 1x1 / stride-1 weight gradients with at most this many pixels run on the ping-pong engine (ResNet-50 stages
+# 2-4 at bs 256; stage 1 loses there: tools/bench_wgrad1x1.py, gpurun_out/r3_38-40, stage 3/4 67/64 -> 57/48 us)
+_WGRAD1X1_PP_PIX = 200704
+
+
 def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     """fp32 dW [K][R][S][C] (accumulated into `out` if given, else fresh zeros)."""
     _bf16_c(x, "conv_wgrad.x")
@@ -433,13 +436,13 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     _chk(out.shape == (K, R, S, C) and out.is_contiguous() and out.dtype == F32, "conv_wgrad: out [K][R][S][C] fp32")
     sc, sh = pro if pro is not None else (None, None)
     P = N * H * W
-    if (pro is None and R == 3 and S == 3 and st == 1 and pad == 1 and _tuning.get("wgrad3x3")
+    if (pro is None and R == 3 and S == 3 and st == 1 and pad == 1
             and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, K) == 1):
         # direct kernel: LDS halo + transpose reads, partials per block, then one reduce (conv3x3_wgrad.hip)
         ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
         call("pdnn_conv3x3_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), stream())
         return out
-    if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _tuning.get("wgrad1x1_pp_pix")
+    if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _WGRAD1X1_PP_PIX
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
         # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs, split count from
         # the long-reduction model): ResNet stages 2-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33, r3_38)
@@ -466,8 +469,6 @@ _CNT = {}
 
 def _fin_counters(C, device, n=None):
     """n (optional): that many counters instead of one per 64-channel column."""
-    if n is None and not _tuning.get("bn_fused_fin"):
-        return None
     key = device.index
     ent = _CNT.get(key)
     if ent is None:
@@ -567,11 +568,21 @@ def bn_bwd_apply(g, x, mean, invstd, gamma, dgamma, dbeta, mode=0, msrc=None, ms
 
 
 # ----------------------------------------------------------------------------------- pooling
+# ImageNet stem router (tests compare the paths): 2 = the direct kernel reading the NCHW batch (default), 1 = the
+# direct kernel on a channel-padded NHWC copy, 0 = the implicit-GEMM conv + bn_apply + max-pool
+_STEM = {"mode": 2}
+
+
+def set_stem_mode(mode: int) -> int:
+    old = _STEM["mode"]
+    _STEM["mode"] = int(mode)
+    return old
+
+
 def stem_ok(x_shape, w_shape, st, pad):
     """The ImageNet stem conv (7x7 / stride 2 / pad 3, 8 padded input channels, 64 outputs) on the direct
     stem kernel (csrc/kernels/stem.hip)."""
-    return (tuple(w_shape) == (64, 7, 7, 8) and x_shape[-1] == 8 and st == 2 and pad == 3
-            and _tuning.get("stem") >= 1)
+    return tuple(w_shape) == (64, 7, 7, 8) and x_shape[-1] == 8 and st == 2 and pad == 3 and _STEM["mode"] >= 1
 
 
 def stem_conv(x, w, want_stats=True):
@@ -592,7 +603,7 @@ def stem_conv(x, w, want_stats=True):
 def stem_nchw_ok(x):
     """The stem conv reading the NCHW bf16 batch directly (3 channels, even width >= 8)."""
     return (x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.shape[3] % 2 == 0 and x.shape[3] >= 8
-            and _tuning.get("stem") == 2)
+            and _STEM["mode"] == 2)
 
 
 def stem_conv_nchw(x, w32, want_stats=True):
@@ -678,9 +689,10 @@ def maxpool_bwd(dy, idx, x_shape, k, st, pad):
 
 
 def stream_wait(waiter, signaler):
-    """``waiter.wait_stream(signaler)`` (same device) through a fence-free HIP event (streams.hip) when tuning
-    light_events is on: no system-scope cache write-back at each of the ~70 fork / join points of a step."""
-    if _tuning.get("light_events") and waiter.device == signaler.device:
+    """``waiter.wait_stream(signaler)`` (same device) through a fence-free HIP event (streams.hip): no
+    system-scope cache write-back at each of the ~70 fork / join points of a step (torch's wait_stream:
+    10,604-10,615 vs 10,687-10,689 img/s, gpurun_out/r3_58)."""
+    if waiter.device == signaler.device:
         with torch.cuda.device(waiter.device):
             call("pdnn_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
     else:

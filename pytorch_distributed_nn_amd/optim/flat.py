@@ -180,7 +180,7 @@ def flatten_module(module: torch.nn.Module, device=None, shadow=None) -> FlatPar
 # torch build skip those hooks for None gradients (probed once), :func:`grad_ready` runs them instead.
 # Only for parameters used ONCE per forward (a tied weight's contributions are summed by autograd).
 # ------------------------------------------------------------------------------------------------
-DIRECT_GRAD = bool(_tuning.get("direct_grad"))
+DIRECT_GRAD = True
 
 
 def await_param(p):

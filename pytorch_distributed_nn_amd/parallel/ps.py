@@ -408,6 +408,7 @@ class PSWorker(_Base):
         self.done_step = 0
         self._in_step = self._fwd_phase = self._aborted = False
         self.abort_phase = None
+        self.step_end = None                # optional callable(worker, step, x, y) after a completed backward
         self._hooks = [register_grad_ready_hook(p, self._param_done) for p in self.flat.params]
         self._fwd_hooks = self._install_weight_waits()
         self.fwd_start = {}                 # step -> time the first module's forward began (timeline)
@@ -526,6 +527,8 @@ class PSWorker(_Base):
                 loss = self.loss_fn(out, y.to(self.device))
                 loss.backward()
                 self.done_step = s
+                if self.step_end is not None:
+                    self.step_end(self, s, x, y)
             except StepAborted:
                 self.aborted_steps += 1
                 self._wait_all_weights()        # a forward abort leaves weight receives posted: complete them

@@ -105,16 +105,8 @@ PANEL = [(2, 56, 56, 64, 256), (3, 28, 28, 128, 512), (1, 7, 7, 128, 2048), (2, 
          (1, 1, 3, 128, 128), (4, 14, 14, 256, 1024), (3, 9, 7, 256, 64), (1, 1, 1, 256, 128), (2, 28, 28, 256, 64)]
 
 
-@pytest.fixture(params=[1, 2], ids=["areg-k256", "areg-all"])
-def areg(request, K):
-    """tuning areg: 1 = A-stationary kernel for K = 256 only (panel for K <= 128), 2 = for every K"""
-    old = K.tune_set("areg", request.param)
-    yield request.param
-    K.tune_set("areg", old)
-
-
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_fwd_stats(K, areg, shape):
+def test_conv1x1_panel_fwd_stats(K, shape):
     N, H, W, C, Ko = shape
     x = torch.randn(N, H, W, C, device="cuda").to(BF)
     w = (torch.randn(Ko, 1, 1, C, device="cuda") * 0.1).to(BF)
@@ -129,7 +121,7 @@ def test_conv1x1_panel_fwd_stats(K, areg, shape):
 
 
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_dgrad(K, areg, shape):
+def test_conv1x1_panel_dgrad(K, shape):
     """dx = dy . W (K = dy channels in {64, 128}) plain / masked residual / fused BN backward."""
     N, H, W, Kc, C = shape            # dy has Kc channels, dx has C
     x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
@@ -203,7 +195,7 @@ def test_conv3x3_dgrad_pre_matches_separate_apply(K, nb, shape):
 
 
 @pytest.mark.parametrize("shape", PANEL)
-def test_conv1x1_panel_pre_matches_separate_apply(K, areg, shape):
+def test_conv1x1_panel_pre_matches_separate_apply(K, shape):
     """The panel kernel's operand prologue (K in {64, 128}): same bits as apply-then-conv."""
     N, H, W, Kc, C = shape
     w = (torch.randn(Kc, 1, 1, C, device="cuda") * 0.1).to(BF)
@@ -242,7 +234,6 @@ WGRAD3 = [(4, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (5,
 def test_conv3x3_wgrad_direct(K, shape):
     """dW of a 3x3 / stride-1 / pad-1 conv on the direct halo kernel against fp32 torch, accumulated into an
     existing gradient (+=), including tiles straddling image boundaries and partial last tiles."""
-    from pytorch_distributed_nn_amd import tuning
     N, H, W, C, Ko = shape
     assert K.lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, Ko) == 1
     x = torch.randn(N, H, W, C, device="cuda").to(BF)
@@ -252,12 +243,5 @@ def test_conv3x3_wgrad_direct(K, shape):
     y.backward(dy.float().permute(0, 3, 1, 2))
     ref = wr.grad.permute(0, 2, 3, 1)                      # [Ko][3][3][C]
     base = torch.randn(Ko, 3, 3, C, device="cuda")
-    old = tuning.set("wgrad3x3", 1)
-    try:
-        out = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())
-        tuning.set("wgrad3x3", 0)
-        out_gemm = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())
-    finally:
-        tuning.set("wgrad3x3", old)
+    out = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())          # accumulates into out
     assert rel(out - base, ref) < 5e-3
-    assert rel(out, out_gemm) < 5e-3

@@ -149,17 +149,9 @@ def test_conv_wgrad(K, shape, pro):
     assert rel(dw, w.grad.permute(0, 2, 3, 1)) < 5e-3
 
 
-@pytest.fixture(params=[1, 0], ids=["fused-fin", "two-launch-fin"])
-def fused_fin(request):
-    from pytorch_distributed_nn_amd import tuning
-    old = tuning.set("bn_fused_fin", request.param)
-    yield request.param
-    tuning.set("bn_fused_fin", old)
-
-
 @pytest.mark.parametrize("rows,C", [(1, 64), (7, 8), (64, 200), (65, 64), (129, 64), (1000, 2048), (12544, 64),
                                     (3137, 1024), (40000, 256)])
-def test_bn_slab_finalize(K, rows, C, fused_fin):
+def test_bn_slab_finalize(K, rows, C):
     """Wide-grid slab finalize (level-1 pass + per-column fp64 epilogue; one launch with the counter hand-off
     or two) against fp64 torch sums; several calls in a row (the hand-off's counters must come back zeroed)."""
     L = float(rows * 64)
@@ -188,8 +180,6 @@ def test_bn_slab_finalize(K, rows, C, fused_fin):
 def test_bn_fused_finalize_two_streams_many_calls(K):
     """200 one-launch finalizes alternating between two streams with no synchronisation between them (the
     counter ring hands each call its own counters), every result against fp64 sums."""
-    from pytorch_distributed_nn_amd import tuning
-    assert tuning.get("bn_fused_fin") == 1
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     streams[1].wait_stream(streams[0])
     outs = []

@@ -76,10 +76,9 @@ def test_stem_conv_nchw_matches_fp32(K, shape):
 
 @pytest.mark.parametrize("shape", [(4, 64, 64), (2, 224, 224)])
 def test_stem_fn_modes_agree(K, shape):
-    """StemFn (conv + BN + ReLU + max-pool, and its backward) with the NCHW kernel (tuning stem = 2), the NHWC
+    """StemFn (conv + BN + ReLU + max-pool, and its backward) with the NCHW kernel (K.set_stem_mode 2), the NHWC
     direct kernel (1) and the generic path (0), same input and upstream gradient: outputs within bf16 rounding
     (different summation orders flip a few last bits), parameter gradients aligned."""
-    from pytorch_distributed_nn_amd import tuning
     from pytorch_distributed_nn_amd.ops import functional as OF
     from pytorch_distributed_nn_amd.ops.fused_resnet import StemFn, stem_shadow
     N, H, W = shape
@@ -91,7 +90,7 @@ def test_stem_fn_modes_agree(K, shape):
     gy = None
     res = {}
     for mode in (2, 1, 0):
-        old = tuning.set("stem", mode)
+        old = K.set_stem_mode(mode)
         try:
             bufs = [torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")]
             conf = (2, 3, True, True, 0.1, 1e-5)
@@ -106,7 +105,7 @@ def test_stem_fn_modes_agree(K, shape):
             torch.cuda.synchronize()
             res[mode] = (y.float(), dw, dg, db, bufs)
         finally:
-            tuning.set("stem", old)
+            K.set_stem_mode(old)
     y0, dw0, dg0, db0, b0 = res[0]
     assert torch.equal(res[1][0], y0)               # NHWC direct kernel: same summation order as the engine
     for mode in (2, 1):

@@ -9,12 +9,7 @@ pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 
 # kernel-side entries -> alternative values
-ALT = {
-    "glds": [0, 2], "glds_min_tiles": [1, 1 << 20], "glds_fwd_k": [64], "glds_dgrad_n": [64], "glds_dgrad_k": [64],
-    "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "pp_fp8": [0], "pp_conv_min_n": [64],
-    "pp_conv_fwd_k": [64], "pp_conv_dgrad_k": [64], "pp_conv_bnb_k": [64], "staged_store": [0], "lowk_bn64": [0, 4],
-    "split_blocks": [64, 2048], "conv3x3_force": [1], "areg": [0, 1],
-}
+ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1]}
 
 
 def rel(a, b):
@@ -86,9 +81,9 @@ def _resnet_grads(arch="resnet50"):
     return fp.grad.clone()
 
 
-@pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("materialize_a2", "resnet50"),
-                                      ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("bwd_pre", "resnet50"),
-                                      ("bwd_pre", "resnet18")])
+@pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("wide1x1_fwd", "resnet50"),
+                                      ("wide1x1_dgrad", "resnet50"), ("bn3_pre", "resnet50"),
+                                      ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("side_wgrad", "resnet18")])
 # (the stem entry is compared at the StemFn level in tests/test_stem_gpu.py: a 1-ulp flip in the stem output
 # -- the NCHW kernel's different summation order -- is amplified by this 4-image net's tiny BatchNorm batches
 # into O(1) gradient differences; modes 0 and 1 are bitwise equal, gpurun_out/r3_23)
@@ -96,7 +91,8 @@ def test_python_entry_alternatives(K, key, arch):
     """The model-level switches change only the schedule / kernel choice: same gradients (bf16 noise)."""
     from pytorch_distributed_nn_amd import tuning
     base = _resnet_grads(arch)
-    old = tuning.set(key, 0)
+    # conv3x3 / panel1x1: the routers' own switches (set_conv3x3_mode / set_panel_mode), not table entries
+    old = tuning.set(key, 0) if key in tuning.DEFAULTS else None
     if key == "conv3x3":
         K.set_conv3x3_mode(0)
     if key == "panel1x1":
@@ -104,7 +100,8 @@ def test_python_entry_alternatives(K, key, arch):
     try:
         alt = _resnet_grads(arch)
     finally:
-        tuning.set(key, old)
+        if old is not None:
+            tuning.set(key, old)
         K.set_conv3x3_mode(1)
         K.set_panel_mode(1)
     cos = torch.nn.functional.cosine_similarity(base, alt, dim=0).item()

@@ -44,18 +44,21 @@ def _sizes(lo: int, hi: int):
         s *= 4
 
 
-def _one(op: str, nbytes: int, dtype, dev, world: int, iters: int, warmup: int, sync):
+def _one(op: str, nbytes: int, dtype, dev, world: int, iters: int, warmup: int, sync, reduce_op="avg"):
     n = max(world, nbytes // torch.tensor([], dtype=dtype).element_size())
     n -= n % world
     x = torch.ones(n, dtype=dtype, device=dev)
     out = torch.empty(n // world, dtype=dtype, device=dev)
     full = torch.empty(n, dtype=dtype, device=dev)
+    # the DDP wrapper's op: AVG on RCCL (PreMulSum of 1/world -- a real reduction kernel even at world 1, where a
+    # SUM is a no-op RCCL skips: the r3 sweep timed exactly that no-op), SUM on gloo
+    rop = dist.ReduceOp.AVG if (reduce_op == "avg" and dev.type == "cuda") else dist.ReduceOp.SUM
 
     def run():
         if op == "all_reduce":
-            dist.all_reduce(x)
+            dist.all_reduce(x, op=rop)
         elif op == "reduce_scatter":
-            dist.reduce_scatter_tensor(out, x)
+            dist.reduce_scatter_tensor(out, x, op=rop)
         elif op == "all_gather":
             dist.all_gather_into_tensor(full, out)
         else:
@@ -65,11 +68,22 @@ def _one(op: str, nbytes: int, dtype, dev, world: int, iters: int, warmup: int, 
         run()
     sync()
     dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        run()
-    sync()
-    dt = (time.perf_counter() - t0) / iters
+    if dev.type == "cuda":
+        # device time of the collectives themselves: events on the current stream, which every RCCL launch joins
+        # and waits on (the host's launch latency does not enter)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            run()
+        e1.record()
+        e1.synchronize()
+        dt = e0.elapsed_time(e1) / 1e3 / iters
+    else:
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            run()
+        sync()
+        dt = (time.perf_counter() - t0) / iters
     t = torch.tensor([dt], dtype=torch.float64)
     if dev.type == "cuda":
         t = t.to(dev)
@@ -77,7 +91,8 @@ def _one(op: str, nbytes: int, dtype, dev, world: int, iters: int, warmup: int, 
     dt = float(t.item())
     size = n * x.element_size()
     algbw = size / dt / 1e9
-    return {"op": op, "dtype": str(dtype).replace("torch.", ""), "bytes": size, "us": round(dt * 1e6, 2),
+    return {"op": op, "reduce_op": reduce_op if op in ("all_reduce", "reduce_scatter") else None,
+            "dtype": str(dtype).replace("torch.", ""), "bytes": size, "us": round(dt * 1e6, 2),
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * FACTORS[op](world), 2), "world": world}
 
 
@@ -92,7 +107,7 @@ def run(args):
     for op in args.ops.split(","):
         for dt in dtypes:
             for nb in _sizes(args.min_bytes, args.max_bytes):
-                r = _one(op, nb, dt, dev, world, args.iters, args.warmup, sync)
+                r = _one(op, nb, dt, dev, world, args.iters, args.warmup, sync, args.reduce_op)
                 rows.append(r)
                 if env.rank == 0:
                     print(json.dumps(r), flush=True)
@@ -114,6 +129,8 @@ def main(argv=None):
     ap.add_argument("--min-bytes", type=int, default=64 * 1024)
     ap.add_argument("--max-bytes", type=int, default=256 * 2 ** 20)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--reduce-op", default="avg", choices=["avg", "sum"],
+                    help="reduction of all_reduce / reduce_scatter (avg = what DistributedDataParallel issues)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu", action="store_true", help="gloo on the CPU")
     ap.add_argument("--world", type=int, default=0, help="spawn this many local ranks (CPU rehearsal)")
