@@ -31,7 +31,6 @@ struct C3Args {
     const bf16_t* pre_t;
     const float *pre_mean, *pre_invstd, *pre_gamma, *pre_dgamma, *pre_dbeta;
     bf16_t* pre_out;
-    const uint8_t* pre_mask;   // conv1x1_wide.hip PRE_MASK: the operand is masked by these ReLU bits first
 };
 
 // per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)

@@ -55,7 +55,7 @@ _SIGS = {
     "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
-    "pdnn_conv1x1_wide": [P, P, P, L, I, I] + [P] * 17,
+    "pdnn_conv1x1_wide": [P, P, P, L, I, I] + [P] * 16,
     "pdnn_conv1x1_wide_supported": [L, I, I],
     "pdnn_stem_conv": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_stem_stats_rows": [L],

@@ -216,10 +216,10 @@ def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, si
     return dt, dgamma, dbeta
 
 
-def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, wprep=None, pre=None):
+def _dgrad_bn_gm(dy, wk, t, st, pad, mean, inv, sc, sh, sink, gamma_p, beta_p, wprep=None):
     """dgrad with the fused BN-backward epilogue, stopped before the apply pass: -> (gm, dgamma, dbeta,
     returned grads).  The apply then runs inside the next data gradient's operand loads (_dgrad_pre)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep, pre=pre)
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     return gm, dgamma, dbeta, ret
 
@@ -291,10 +291,10 @@ def _pre_ok(t, wk, st, pad):
     return K.dgrad_pre_ok(tuple(t.shape), tuple(wk.shape), st, pad)
 
 
-def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None, pre=None):
+def _fused_dgrad_bn(dy, wk, t, st, pad, mean, inv, sc, sh, gamma, sink, gamma_p, beta_p, wprep=None):
     """dgrad whose epilogue applies the ReLU mask of relu(bn(t)) and reduces the BN-backward sums; then
     one apply pass produces dt (the gradient w.r.t. the BN input t)."""
-    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep, pre=pre)
+    gm, slab = K.conv_dgrad(dy, wk, t.shape, st, pad, bn=(t, mean, inv, sc, sh), wprep=wprep)
     (dgamma, dbeta), ret = sink.bn(slab, slab.shape[0] // 2, gamma_p, beta_p)
     C = t.shape[-1]
     dt, _, _ = K.bn_bwd_apply(gm.view(-1, C), t.view(-1, C), mean, inv, gamma, dgamma, dbeta, mode=0)
@@ -390,7 +390,6 @@ class BottleneckFn(torch.autograd.Function):
             _wait_wprep(gout.device, ev, seq)
             ctx.wprep = None
         gres_mask = mb if MASKED_RES else None
-        pre3 = None
         slab3, slabd, rows = K.bn_bwd_reduce(g2d, t3_2d, m3, i3, mode=3, msrc=mb,
                                              x2=td.view(-1, C3) if down else None, mean2=md, invstd2=idd)
         (dg3, db3), (rg3, rb3) = sink.bn(slab3, rows, P[7], P[8])
@@ -400,13 +399,6 @@ class BottleneckFn(torch.autograd.Function):
                                          x2=td.view(-1, C3), mean2=md, invstd2=idd, gamma2=gd, dgamma2=dgd,
                                          dbeta2=dbd)
             gres = None
-        elif MASKED_RES and tuning.get("bn3_pre") and K.dgrad_pre_mask_ok(t3.shape, k3.shape):
-            # BN3's backward apply runs inside conv3's data-gradient operand loads (the long-reduction
-            # kernel reads gout, t3 and the ReLU bits, writes dt3 once for the weight gradient): no separate
-            # apply pass (read gout + t3, write dt3) and no re-read of dt3 by the data gradient
-            dt3 = torch.empty_like(t3)
-            pre3 = (t3, m3, i3, g3, dg3, db3, dt3, mb)
-            gres = gout
         elif MASKED_RES:
             # the identity branch's gradient gout * mask is added by conv1's data gradient (res_mask), not
             # materialised here: one activation-sized write less per block
@@ -415,29 +407,18 @@ class BottleneckFn(torch.autograd.Function):
         else:
             dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
-        dy3 = gout if pre3 is not None else dt3
-
-        def wgrad3():        # conv3 (input a2 = relu(bn2(t2)))
-            return sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)
-        if pre3 is None:
-            dw3 = wgrad3()
+        dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)       # conv3 (input a2 = relu(bn2(t2)))
         bn1 = (t1, m1, i1, s1, h1)
         if _pre_ok(t2, k2, stride, 1):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad
-            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dy3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p,
-                                                     pre=pre3)
-            if pre3 is not None:
-                dw3 = wgrad3()                  # dt3 written by conv3's data gradient
+            gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p)
             dt2 = torch.empty_like(t2)
             gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2),
                                       wprep=w2p)
             del gm2
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
         else:
-            dt2, rg2, rb2 = _fused_dgrad_bn(dy3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p,
-                                            pre=pre3)
-            if pre3 is not None:
-                dw3 = wgrad3()
+            dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p)
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
             gm1, slab1 = K.conv_dgrad(dt2, k2, t1.shape, stride, 1, bn=bn1, wprep=w2p)
         (dg1, db1), (rg1, rb1) = sink.bn(slab1, slab1.shape[0] // 2, P[1], P[2])

@@ -204,9 +204,11 @@ def set_panel_mode(mode: int) -> int:
 
 
 def _wide_ok(P, K, N, fwd):
-    """1x1 / stride-1 convs with a long reduction (K >= 512) on the streaming kernel (conv1x1_wide.hip):
-    forwards (tuning wide1x1_fwd) and data gradients (wide1x1_dgrad)."""
-    return (K >= 512 and _tuning.get("wide1x1_fwd" if fwd else "wide1x1_dgrad") == 1
+    """1x1 / stride-1 data gradients with a long reduction and a wide output (K >= 512, N >= 1024: ResNet-50's
+    stage-4 conv1 data gradients) on the streaming kernel (conv1x1_wide.hip; tuning wide1x1_dgrad): 81 vs 102 us
+    on the ping-pong engine.  Not the forwards or the conv3 data gradients (N <= 512), where the implicit-GEMM
+    engine stays ahead (gpurun_out/r4_02)."""
+    return (not fwd and K >= 512 and N >= 1024 and _tuning.get("wide1x1_dgrad") == 1
             and lib().pdnn_conv1x1_wide_supported(P, K, N) == 1)
 
 
@@ -220,7 +222,7 @@ def _pre_args(pre, x):
     gradient gm is ``x`` (dt = bn_bwd_apply(gm, t), mode 0) fused into the operand loads."""
     if pre is None:
         return (None,) * 7
-    t, mean, inv, gamma, dg, db, dt_out = pre[:7]
+    t, mean, inv, gamma, dg, db, dt_out = pre
     _bf16_c(t, "pre.t")
     _chk(t.numel() == x.numel(), "pre: t must have the operand's shape")
     if dt_out is not None:
@@ -228,20 +230,9 @@ def _pre_args(pre, x):
     return tuple(ptr(v) for v in (t, mean, inv, gamma, dg, db, dt_out))
 
 
-def _pre_mask(pre, x):
-    """The optional 8th entry of ``pre``: uint8 ReLU bits [P][K/8] masking the operand first (bn_bwd_apply mode 3:
-    x is the block output's gradient, not yet masked); only the long-reduction kernel takes it."""
-    if pre is None or len(pre) < 8 or pre[7] is None:
-        return None
-    m = pre[7]
-    _chk(m.dtype == torch.uint8 and m.is_contiguous() and m.numel() * 8 == x.numel(), "pre: mask [P][K/8] uint8")
-    return m
-
-
 def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None):
     """y[P][N] = x[P][K] . w[N][K]^T on the panel / A-stationary kernels (K <= 256) or the long-reduction kernel
-    (K >= 512); epilogues as conv3x3 / conv_dgrad; pre: the BN-backward operand prologue (_pre_args, and the
-    operand mask of _pre_mask on the long-reduction kernel)."""
+    (K >= 512); epilogues as conv3x3 / conv_dgrad; pre: the BN-backward operand prologue (_pre_args)."""
     P, Kc = x2d.shape
     N = w2d.shape[0]
     y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
@@ -251,12 +242,10 @@ def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, 
         slab = torch.empty(2 * lib().pdnn_conv1x1_panel_stats_rows(P), N, device=x2d.device, dtype=F32)
     if bn is not None:
         t, mean, inv, msc, msh = bn
-    mask = _pre_mask(pre, x2d)
     if Kc >= 512:
         call("pdnn_conv1x1_wide", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-             ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), ptr(mask), stream())
+             ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
         return y, slab
-    _chk(mask is None, "conv1x1_panel: a masked operand (pre mask) needs K >= 512")
     call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
          ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
     return y, slab
@@ -273,7 +262,6 @@ def conv3x3_flip(w):
 def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, pre=None):
     """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
     conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
-    _chk(_pre_mask(pre, x) is None, "conv3x3: a masked operand (pre mask) needs the long-reduction 1x1 kernel")
     Nimg, H, W, C = x.shape
     Ko = w.shape[0]
     y = out if out is not None else torch.empty(Nimg, H, W, Ko, device=x.device, dtype=BF16)
@@ -317,15 +305,7 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
 def _panel_dgrad_k(K):
     """Data gradients (dx[P][C] = dy[P][K] . W) on the A-stationary kernel (K in {64, 128, 256}) or the
     long-reduction streaming kernel (K >= 512, conv1x1_wide.hip)."""
-    return K in (64, 128, 256) or (K >= 512 and _tuning.get("wide1x1_dgrad") == 1)
-
-
-def dgrad_pre_mask_ok(dy_shape, w_shape):
-    """Whether conv_dgrad takes ``pre=`` with the 8th (mask) entry: the operand is the block output's gradient,
-    masked by its ReLU bits inside the loads (bn_bwd_apply mode 3) -- the long-reduction kernel (K >= 512)."""
-    N, Ho, Wo, K = dy_shape
-    Kw, R, S, C = w_shape
-    return K >= 512 and R == 1 and S == 1 and _panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, 1, 0)
+    return K in (64, 128, 256) or K >= 512
 
 
 def dgrad_pre_ok(dy_shape, w_shape, st, pad):
@@ -366,9 +346,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
 
     pre = (t, mean, invstd, gamma, dgamma, dbeta, dt_out): ``dy`` is the masked gradient gm of a BatchNorm
     whose backward apply (bn_bwd_apply mode 0) runs inside this conv's operand loads; dt_out (optional)
-    receives that dt for the weight gradient.  Only where dgrad_pre_ok().  An 8th entry, uint8 ReLU bits
-    [P][K/8] (bn_apply's mask): ``dy`` is the unmasked gradient and the mask is applied in the loads too
-    (bn_bwd_apply mode 3); only where dgrad_pre_mask_ok().
+    receives that dt for the weight gradient.  Only where dgrad_pre_ok().
 
     wprep: dgrad_weight()'s result for this call (else it is made here)."""
     _bf16_c(dy, "conv_dgrad.dy")

@@ -8,11 +8,8 @@ key                default  meaning (measurement)
 =================  =======  ===========================================================================
 side_wgrad         1        conv weight gradients on a second HIP stream beside the data-gradient chain
                             (ResNet-50 +8.3%, profiles/resnet50_bs256_side_stream_r2.txt); 0 = one stream
-wide1x1_fwd        1        1x1 / stride-1 forward convs with K >= 512 input channels on the long-reduction streaming
-                            kernel (conv1x1_wide.hip) instead of the implicit-GEMM engines
-wide1x1_dgrad      1        ... and the 1x1 / stride-1 data gradients with K >= 512
-bn3_pre            1        Bottleneck: BN3's backward apply (mode 3, the output ReLU bits) inside conv3's data-gradient
-                            operand loads on that kernel instead of a separate apply pass
+wide1x1_dgrad      1        1x1 / stride-1 data gradients with K >= 512 and >= 1024 outputs (ResNet-50 stage-4 conv1) on
+                            the long-reduction streaming kernel (conv1x1_wide.hip): 81 vs 102 us per layer (r4_02)
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there
@@ -22,7 +19,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_fwd": 1, "wide1x1_dgrad": 1, "bn3_pre": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1}
 
 _VALUES = dict(DEFAULTS)
 

@@ -81,8 +81,7 @@ def _resnet_grads(arch="resnet50"):
     return fp.grad.clone()
 
 
-@pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("wide1x1_fwd", "resnet50"),
-                                      ("wide1x1_dgrad", "resnet50"), ("bn3_pre", "resnet50"),
+@pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("wide1x1_dgrad", "resnet50"),
                                       ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("side_wgrad", "resnet18")])
 # (the stem entry is compared at the StemFn level in tests/test_stem_gpu.py: a 1-ulp flip in the stem output
 # -- the NCHW kernel's different summation order -- is amplified by this 4-image net's tiny BatchNorm batches

@@ -54,18 +54,13 @@ def main():
         row["conv3_fwd_plain"] = timeit(lambda: K.conv_fwd(a2, k3, 1, 0, want_stats=True))
         row["conv1_fwd"] = timeit(lambda: K.conv_fwd(x4, k1, 1, 0, want_stats=True))
         row["conv3_dgrad_bn"] = timeit(lambda: K.conv_dgrad(dt3, k3, t2.shape, 1, 0, bn=(t2, mean, inv, sc, sh)))
-        # the BN3 backward apply pass that produces dt3 from the block output's gradient, and the same apply
-        # fused into conv3's data-gradient operand loads (mode 3: gout masked by the output ReLU bits)
+        # the BN3 backward apply pass that produces dt3 from the block output's gradient
         t3 = torch.randn(N, H, H, C4, device=d).to(torch.bfloat16)
         ob = torch.randint(0, 256, (N * H * H, C4 // 8), device=d, dtype=torch.uint8)
         m3, i3, g3 = torch.zeros(C4, device=d), torch.ones(C4, device=d), torch.rand(C4, device=d) + 0.5
         dg3, db3 = torch.randn(C4, device=d), torch.randn(C4, device=d)
         row["bn3_apply"] = timeit(lambda: K.bn_bwd_apply(dt3.view(-1, C4), t3.view(-1, C4), m3, i3, g3, dg3, db3,
                                                          mode=3, msrc=ob))
-        if K.dgrad_pre_mask_ok(dt3.shape, k3.shape):
-            dt3o = torch.empty_like(dt3)
-            row["conv3_dgrad_bn_pre3"] = timeit(lambda: K.conv_dgrad(dt3, k3, t2.shape, 1, 0, bn=(t2, mean, inv, sc, sh),
-                                                                     pre=(t3, m3, i3, g3, dg3, db3, dt3o, ob)))
         row["conv1_dgrad_res"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4))
         bits = torch.randint(0, 256, (N * H * H, C4 // 8), device=d, dtype=torch.uint8)
         row["conv1_dgrad_res_mask"] = timeit(lambda: K.conv_dgrad(dt1, k1, x4.shape, 1, 0, res=x4, res_mask=bits))
