@@ -6,8 +6,9 @@ O=$GRAFT_REPO_ROOT/gpurun_out/r4_05
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_conv1x1_wide_gpu.py tests/test_trajectory_gpu.py tests/test_tuning_gpu.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -q --timeout 180 --timeout-method thread tests/test_conv1x1_wide_gpu.py tests/test_trajectory_gpu.py tests/test_tuning_gpu.py > $O/pytest.log 2>&1; rc=$?
 tail -1 $O/pytest.log
+[ $rc -le 1 ] || exit $rc        # test failures are reported, a crash / timeout ends the run
 timeout -k 10 200 python -u tools/bench_conv1x1.py > $O/c1_default.log 2>&1 || { tail -20 $O/c1_default.log; exit 1; }
 PDNN_TUNE=glds=2 timeout -k 10 200 python -u tools/bench_conv1x1.py > $O/c1_glds.log 2>&1 || { tail -20 $O/c1_glds.log; exit 1; }
 tail -n 1 $O/c1_default.log $O/c1_glds.log

@@ -13,6 +13,7 @@ implementation on CPU so the test-suite runs on the GPU-less dev box).
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 from pathlib import Path
 
@@ -177,8 +178,45 @@ def _load():
         if err:                  # PDNN_TUNE is malformed or names an entry that exists in neither table: fail loudly
             _ERR = err
             return None
-    _LIB = lib
+    _LIB = _Lib(lib)
     return _LIB
+
+
+class _Lib:
+    """The CDLL behind a per-name lookup cache.  Pure shape queries (``*_supported``, ``*_rows``, ``*_splits``,
+    ``*_ws``, ``*_work``, ``*_blocks``, ``*_groups``: integer arguments -> integer result) are memoised: the
+    fused blocks ask several per kernel launch, and at ResNet-50's stage 3-4 the step is bound by the host's
+    issue rate (gpurun_out/r4_04: the compute stream idles behind launches).  The memo is cleared whenever a
+    dispatch switch changes (clear_query_cache)."""
+
+    _PURE = ("_supported", "_rows", "_splits", "_splits_long", "_ws", "_work", "_blocks", "_groups")
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        self._fns = {}
+
+    def __getattr__(self, name):
+        f = self._fns.get(name)
+        if f is None:
+            f = getattr(self._cdll, name)
+            if name.endswith(self._PURE):
+                f = functools.lru_cache(maxsize=8192)(f)
+            elif name.startswith(("pdnn_set_", "pdnn_tune_set")) or name.endswith("_force"):
+                f = self._switch(f)              # a dispatch switch: the memoised answers may change
+            self._fns[name] = f
+        return f
+
+    def _switch(self, raw):
+        def call_and_clear(*args):
+            r = raw(*args)
+            self.clear_query_cache()
+            return r
+        return call_and_clear
+
+    def clear_query_cache(self):
+        for f in self._fns.values():
+            if hasattr(f, "cache_clear"):
+                f.cache_clear()
 
 
 def available() -> bool:
@@ -187,11 +225,17 @@ def available() -> bool:
 
 def lib():
     """The loaded kernel library; raises (never falls back) if it is unavailable."""
-    l = _load()
+    l = _LIB if _LIB is not None else _load()
     if l is None:
         raise RuntimeError(f"pytorch_distributed_nn_amd: HIP kernel library unavailable ({_ERR}). "
                            "Run `python -m pytorch_distributed_nn_amd._build` (hipcc, gfx950).")
     return l
+
+
+def clear_query_cache():
+    """Forget memoised shape queries (after a dispatch-table or routing switch changed)."""
+    if _LIB is not None:
+        _LIB.clear_query_cache()
 
 
 def stream(dev=None) -> int:

@@ -93,7 +93,7 @@ def test_flagship_resnet50_imagenet_trajectory_tracks_fp32():
     fused.fused = True
     flatten_module(fused)
     w0 = torch.cat([p.detach().float().flatten() for p in ref.parameters()]).cpu()
-    lr = 0.05
+    lr = 0.005               # 0.05 diverges on both sides (fp32 included) at this batch: chaotic, not comparable
     opt_r = torch.optim.SGD(ref.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
     opt_g = SGD(fused.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
     batches = [(x.cuda(), y.cuda()) for x, y in _task((64, 3, 112, 112), 10, 3)]
