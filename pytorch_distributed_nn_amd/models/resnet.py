@@ -128,6 +128,11 @@ class Bottleneck(_FusedBlockMixin, nn.Module):
 class _ResNetBase(nn.Module):
     fused = True   # GPU tensors run the fused HIP path
 
+    def awaits_params(self, x, *args, **kwargs):
+        """Whether this forward fetches every conv / linear weight through await_param itself (the fused GPU path:
+        bf16 shadows): then DistributedDataParallel's k-of-n forward needs no per-op ParamUseMode dispatch."""
+        return bool(getattr(x, "is_cuda", False) and self.fused)
+
     def _bn_modules(self):
         if not hasattr(self, "_bn_cache"):
             self._bn_cache = [m for m in self.modules() if isinstance(m, nn.BatchNorm2d)]

@@ -204,6 +204,7 @@ class _Lib:
             elif name.startswith(("pdnn_set_", "pdnn_tune_set")) or name.endswith("_force"):
                 f = self._switch(f)              # a dispatch switch: the memoised answers may change
             self._fns[name] = f
+            self.__dict__[name] = f              # later lookups bypass __getattr__
         return f
 
     def _switch(self, raw):
@@ -238,7 +239,15 @@ def clear_query_cache():
         _LIB.clear_query_cache()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEV = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream(dev=None) -> int:
+    """The current HIP stream handle (every launch passes it).  The raw-handle query skips the torch.cuda.Stream
+    object torch.cuda.current_stream() builds (dev/probes/host_prims.py)."""
+    if dev is None and _RAW_STREAM is not None:
+        return _RAW_STREAM(_CUR_DEV())
     return torch.cuda.current_stream(dev).cuda_stream
 
 
@@ -251,8 +260,7 @@ class HipError(RuntimeError):
 
 
 def call(name: str, *args):
-    fn = getattr(lib(), name)
-    rc = fn(*args)
+    rc = getattr(_LIB if _LIB is not None else lib(), name)(*args)
     if rc != 0:
         raise HipError(f"{name} failed with hipError {rc}")
     return rc

@@ -671,8 +671,11 @@ def stream_wait(waiter, signaler):
     system-scope cache write-back at each of the ~70 fork / join points of a step (torch's wait_stream:
     10,604-10,615 vs 10,687-10,689 img/s, gpurun_out/r3_58)."""
     if waiter.device == signaler.device:
-        with torch.cuda.device(waiter.device):
+        if waiter.device.index == torch.cuda.current_device():
             call("pdnn_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
+        else:
+            with torch.cuda.device(waiter.device):
+                call("pdnn_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
     else:
         waiter.wait_stream(signaler)
 
