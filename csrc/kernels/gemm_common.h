@@ -68,13 +68,19 @@ struct GemmArgs {
     long long* dbg;           // pp engine: per-block phase timestamps (tools/pp_one.py --trace), or null
 };
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-    const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
+// GELU (tanh form) through the hardware transcendentals: 0.5 (1 + tanh u) = 1 / (1 + exp(-2u)) = s, one v_exp_f32
+// and one v_rcp_f32 (~1 ulp each) instead of the library tanhf (~40 VALU ops with branches, which made the
+// GELU epilogue of a K = 768 GEMM cost as much as its MFMAs: GPT-2 fc forward 110 vs 56 us plain).
+// exp2 overflows to +inf for u << 0 (s -> 0) and underflows to 0 for u >> 0 (s -> 1): both limits exact.
+__device__ __forceinline__ float gelu_sig(float x) {
+    const float u = x * (0.7978845608028654f + 0.035677408136300125f * x * x);
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.885390081777927f * u));
 }
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sig(x); }
+// d/dx [x s(u)] = s + x * 2 s (1 - s) * u'(x),  u' = 0.79788 (1 + 3 * 0.044715 x^2)
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-    const float t = tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 0.134145f * x * x);
+    const float s = gelu_sig(x);
+    return s + 2.f * x * s * (1.f - s) * (0.7978845608028654f + 0.10703222440890037f * x * x);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -268,6 +268,37 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) s_[fn][j] = q_[fn][j] = 0.f;
             }
+            // Plain bf16 epilogues: the bias of this lane's columns is loaded once per item, and the residual /
+            // dGELU operand one fragment row ahead of its use.  Every load is issued before the stores of the
+            // rows after it (s_waitcnt vmcnt counts stores too on gfx9, so a load issued after a store waits for
+            // it) and unconditionally, from clamped addresses.  Loading both per fragment inside the row loop
+            // serialised ~FM x FN load latencies behind the stores: +13 us for the bias alone on the GPT-2 fc
+            // shape (dev/probes/epi_cost.py, gpurun_out/r4_13).
+            // (the 288-wide tile keeps the operand loads per fragment: its prefetch registers spilled to scratch;
+            // it runs the GPT-2 qkv GEMM, whose epilogue has only a bias)
+            constexpr bool PF = EM == E_BF16 && FX == 0;
+            constexpr bool PFO = PF && C::FN <= 8;
+            const bf16_t* const eop = PFO ? (a.ep_dgelu ? a.ep_dgelu : a.ep_res) : nullptr;   // prefetched operand
+            float4 bia[PF ? C::FN : 1];
+            u16x4_t nx[PFO ? C::FN : 1];
+            auto load_op = [&](int fm_) {      // PFO only
+                const long mm = min(m0 + arow + fm_ * 16 + lm, a.M - 1);
+#pragma unroll
+                for (int fn = 0; fn < C::FN; ++fn) {
+                    const int n = min(n0 + bcol + fn * 16 + 4 * lg, a.N - 4);
+                    nx[fn] = *reinterpret_cast<const u16x4_t*>(eop + mm * a.ldc + n);
+                }
+            };
+            if constexpr (PF) {
+#pragma unroll
+                for (int fn = 0; fn < C::FN; ++fn) {
+                    const int n = min(n0 + bcol + fn * 16 + 4 * lg, a.N - 4);
+                    bia[fn] = a.bias ? *reinterpret_cast<const float4*>(a.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+                }
+                if constexpr (PFO) {
+                    if (eop) load_op(0);
+                }
+            }
             static_for<0, C::FM>([&](auto FMC) {
                 constexpr int fm = decltype(FMC)::value;
                 // BN-backward epilogue: keep each fragment's loads inside its own iteration (hoisted loads of
@@ -277,6 +308,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                 const bool mv = m < a.M;
                 if constexpr (EM == E_BF16) {
                     uint32_t pk[C::FN][2];
+                    u16x4_t cu[PFO ? C::FN : 1];
+                    if constexpr (PFO) {
+                        if (eop) {
+#pragma unroll
+                            for (int fn = 0; fn < C::FN; ++fn) cu[fn] = nx[fn];
+                            if constexpr (fm + 1 < C::FM) load_op(fm + 1);
+                        }
+                    }
 #pragma unroll
                     for (int fn = 0; fn < C::FN; ++fn) {
                         const int n = n0 + bcol + fn * 16 + 4 * lg;
@@ -285,7 +324,11 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                         float v[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
-                        if (a.bias && n + 4 <= a.N) {
+                        if constexpr (PF) {
+                            if (a.bias) {
+                                v[0] += bia[fn].x; v[1] += bia[fn].y; v[2] += bia[fn].z; v[3] += bia[fn].w;
+                            }
+                        } else if (a.bias && n + 4 <= a.N) {
                             const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
                             v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
                         }
@@ -301,12 +344,16 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                             for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
                         }
                         if (a.ep_dgelu && ok) {
-                            const u16x4_t u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
+                            u16x4_t u;
+                            if constexpr (PFO) u = cu[fn];
+                            else u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
                         }
                         if (a.ep_res && ok) {
-                            const u16x4_t r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
+                            u16x4_t r;
+                            if constexpr (PFO) r = a.ep_dgelu ? *reinterpret_cast<const u16x4_t*>(a.ep_res + off) : cu[fn];
+                            else r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
                             const uint32_t mb = a.ep_rmask ? (uint32_t)(a.ep_rmask[off >> 3] >> (off & 4)) : 0xFu;
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(r[j]) : 0.f;
