@@ -18,10 +18,21 @@ What it does, and how it differs from the reference's design:
   (data_parallel_dist.py:211-267).
 * **Averaging** uses RCCL's native AVG reduction (one pass, no extra scale kernel); on gloo (CPU) it is
   SUM followed by a scale.
-* **Bucket sizing for xGMI**: each MI355X has 7 point-to-point xGMI links; a large bucket lets RCCL
-  spread one collective across many channels/links, small buckets are latency bound (~10-30 us per
-  collective).  Defaults: 1 MiB first bucket, 32 MiB afterwards (ResNet-50's 102 MB of fp32 gradients =
-  4-5 collectives) — sweep with ``tools/bench_allreduce.py``.
+* **Bucket sizing for xGMI** (defaults 1 MiB first bucket, 32 MiB afterwards).  A ring all-reduce of S bytes
+  over N ranks costs T(S) ~= a + 2(N-1)/N * S / B, with a the per-collective latency and B the per-rank bus
+  bandwidth.  Measured here (profiles/rccl_world1_r4.txt, device events, RCCL AVG): a ~= 12-18 us (the
+  64 KiB-4 MiB sizes all take 13-18 us), and the world-1 reduction kernel itself runs at ~700 GB/s fp32, so it
+  never binds.  At N = 8 each MI355X reaches its peers over 7 point-to-point xGMI links (~153 GB/s each per
+  direction); a ring is bound by one link per hop, so B ~= 150-300 GB/s depending on how many channels RCCL
+  spreads over the links.  Then a 32 MiB bucket takes ~= 15 + 1.75 * 33.5 MB / 200 GB/s ~= 310 us, latency
+  is < 5% of it, and ResNet-50's 102 MB of fp32 gradients is 4 collectives (+ the small first one) ~= 1.2 ms of
+  link time, against a ~15 ms backward that produces the buckets 1.3, 2.6, 5.7 and 15.7 ms after the first
+  gradient hook (bench.py ``comm`` block): every bucket but the last is hidden under the backward.  What is
+  exposed is the LAST bucket (stem + stage-1 parameters, 12.3 MiB, ready only when the backward ends): ~120 us
+  at N = 8 by the model above.  Smaller buckets would not shrink it (those parameters' gradients all arrive in
+  the backward's last ~1 ms) and would multiply the latency term; larger ones would delay the earlier buckets
+  past the point where they overlap.  The 1 MiB first bucket only starts the pipeline (it holds fc.bias: the
+  8 MB fc.weight does not fit).  Re-derive with ``tools/bench_allreduce.py`` at the real N.
 * **k-of-n straggler kill / backup workers in collective form** (PAR-DP-KILL / PAR-DP-BACKUP, SURVEY.md
   §5.3; reference: pytorch_code/sync_replicas_master_nn.py:172-186 kill on the k-th arrival,
   pytorch_code/model_ops/lenet.py:168-178 worker poll, MPI_code/src/distributed/worker_nn.h:59-84
@@ -31,7 +42,8 @@ What it does, and how it differs from the reference's design:
   the close key and raises a host flag; the gradient hooks poll that flag (a Python attribute, no RPC)
   and a rank that is still computing abandons the rest of its backward (``StepAborted`` stops autograd,
   so no further kernels are enqueued; on GPU the host is kept at most two buckets ahead of the device so
-  the decision reflects real GPU progress).  Collectives must stay matched, so the aborted rank still
+  the decision reflects real GPU progress; with no straggler the whole machinery costs < 1% of a ResNet-50
+  step, profiles/kofn_tax_r4.txt).  Collectives must stay matched, so the aborted rank still
   all-reduces every remaining bucket, zero-filled.  Each rank records per bucket whether it sent real
   gradients; that contribution vector is all-reduced after the buckets and every bucket is divided by
   ITS count — the count-correct average of the C++ master (sync_replicas_master_nn.h:125) per bucket,
