@@ -674,11 +674,13 @@ FastDiv make_fdiv(uint32_t d) {
 }
 
 // 1x1 stride-1 data gradients on the ping-pong engine: the plain / residual ones win there from K >= 512 with
-// >= 128 output columns (r2_46: 512 vs 256 +0.5%); the forward with BN statistics and the data gradient with
-// the BN-backward epilogue are slower there than on the 128-row kernel (the fused epilogue roughly doubles the
-// pp epilogue time), and K >= 512 1x1 convs are routed to the long-reduction kernel (conv1x1_wide.hip) first.
+// >= 128 output columns (r2_46: 512 vs 256 +0.5%); with the BN-backward epilogue (its BN input prefetched a
+// fragment row ahead, gemm_pp.hip) from K >= 1024: ResNet-50 conv3 data gradients 65 / 51 vs 81 / 69 us in stages
+// 3 / 4, but 111 vs 98 us at K = 512 (stage 2, N = 128: 3 rounds of 128-wide tiles; gpurun_out/r4_15).  The
+// forward with BN statistics stays on the 128-row kernel; 1x1 convs the long-reduction kernel (conv1x1_wide.hip)
+// takes are routed there first.
 constexpr int kPPConvMinN = 128;
-constexpr int kPPConvDgradK = 512;
+constexpr int kPPConvDgradK = 512;          // (with the BN epilogue: tuning pp_dgrad_bn_k)
 // 128-row kernel bf16 epilogue: 1 = stores staged through LDS (full rows), 0 = direct fragment stores (tests)
 int g_stage_store = 1;
 int stage_store_mode() { return g_stage_store; }
@@ -981,7 +983,7 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
                              hipStream_t stream) {
     if (res_mask && (st != 1 || C % 8 || !res || res == dx)) return (int)hipErrorInvalidValue;
     ensure_attrs();
-    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= kPPConvMinN && !bn_x && Ko >= kPPConvDgradK) {
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && C >= kPPConvMinN && Ko >= (bn_x ? tune().pp_dgrad_bn_k : kPPConvDgradK)) {
         // 1x1 stride-1: dx[M][C] = dy[M][Ko] . w[Ko][C] (w as a [k][n] matrix) on the ping-pong engine
         GemmArgs a{};
         a.M = Nimg * H * W; a.N = C; a.K = Ko;

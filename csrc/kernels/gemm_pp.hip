@@ -276,9 +276,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             // shape (dev/probes/epi_cost.py, gpurun_out/r4_13).
             // (the 288-wide tile keeps the operand loads per fragment: its prefetch registers spilled to scratch;
             // it runs the GPT-2 qkv GEMM, whose epilogue has only a bias)
+            // The BN-backward epilogue prefetches its BN input t the same way (the 1x1 conv3 data gradients).
             constexpr bool PF = EM == E_BF16 && FX == 0;
-            constexpr bool PFO = PF && C::FN <= 8;
-            const bf16_t* const eop = PFO ? (a.ep_dgelu ? a.ep_dgelu : a.ep_res) : nullptr;   // prefetched operand
+            constexpr bool PFO = (PF || (EM == E_BF16 && FX == FX_BNB)) && C::FN <= 8;
+            const bf16_t* const eop = !PFO ? nullptr : FX == FX_BNB ? a.ep_x : (a.ep_dgelu ? a.ep_dgelu : a.ep_res);
             float4 bia[PF ? C::FN : 1];
             u16x4_t nx[PFO ? C::FN : 1];
             auto load_op = [&](int fm_) {      // PFO only
@@ -295,9 +296,9 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     const int n = min(n0 + bcol + fn * 16 + 4 * lg, a.N - 4);
                     bia[fn] = a.bias ? *reinterpret_cast<const float4*>(a.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
                 }
-                if constexpr (PFO) {
-                    if (eop) load_op(0);
-                }
+            }
+            if constexpr (PFO) {
+                if (eop) load_op(0);
             }
             static_for<0, C::FM>([&](auto FMC) {
                 constexpr int fm = decltype(FMC)::value;
@@ -345,14 +346,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                         }
                         if (a.ep_dgelu && ok) {
                             u16x4_t u;
-                            if constexpr (PFO) u = cu[fn];
+                            if constexpr (PFO && FX == 0) u = cu[fn];
                             else u = *reinterpret_cast<const u16x4_t*>(a.ep_dgelu + off);
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[j] *= gelu_tanh_grad(bf2f(u[j]));
                         }
                         if (a.ep_res && ok) {
                             u16x4_t r;
-                            if constexpr (PFO) r = a.ep_dgelu ? *reinterpret_cast<const u16x4_t*>(a.ep_res + off) : cu[fn];
+                            if constexpr (PFO && FX == 0) r = a.ep_dgelu ? *reinterpret_cast<const u16x4_t*>(a.ep_res + off) : cu[fn];
                             else r = *reinterpret_cast<const u16x4_t*>(a.ep_res + off);
                             const uint32_t mb = a.ep_rmask ? (uint32_t)(a.ep_rmask[off >> 3] >> (off & 4)) : 0xFu;
 #pragma unroll
@@ -364,7 +365,8 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                             // at the flush (per-fragment mean / invstd loads pushed this variant into scratch)
                             u16x4_t tv = {0, 0, 0, 0};
                             float4 ms = {0, 0, 0, 0}, mh = ms;
-                            if (ok) tv = *reinterpret_cast<const u16x4_t*>(a.ep_x + off);
+                            if constexpr (PFO) tv = cu[fn];          // (masked by `ok` below)
+                            else if (ok) tv = *reinterpret_cast<const u16x4_t*>(a.ep_x + off);
                             ms = *reinterpret_cast<const float4*>(ptab + n);
                             mh = *reinterpret_cast<const float4*>(ptab + PP_PRO_MAXK + n);
                             const float msa[4] = {ms.x, ms.y, ms.z, ms.w}, mha[4] = {mh.x, mh.y, mh.z, mh.w};

@@ -15,7 +15,9 @@ namespace pg {
                "the operands allow (tests)")                                                                 \
     X(pp, 1, "ping-pong engine for plain GEMMs (and fp8): 0 off, 1 automatic, 2 whenever the operands allow (tests)") \
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
-    X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")
+    X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
+    X(pp_dgrad_bn_k, 1024, "1x1 data gradients with the BN-backward epilogue on the ping-pong engine from this "   \
+                           "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")
 
 struct Tune {
 #define PDNN_TUNE_FIELD(n, d, doc) int n = d;

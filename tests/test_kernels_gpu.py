@@ -369,7 +369,8 @@ def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
 
 
 @pytest.mark.parametrize("shape", [(16, 28, 28, 128, 512, False), (16, 28, 28, 512, 128, True),
-                                   (4, 14, 14, 1024, 256, True), (3, 10, 10, 256, 128, True)])
+                                   (4, 14, 14, 1024, 256, True), (3, 10, 10, 256, 128, True),
+                                   (8, 14, 14, 256, 1024, False), (5, 7, 7, 512, 2048, False)])
 def test_conv1x1_fused_resnet_shapes(K, shape):
     """1x1 stride-1 convs at bottleneck shapes (the ping-pong engine in auto mode): forward with the
     BN-affine+ReLU prologue and BN statistics; data gradient with residual, and with the BN-backward

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 
 # kernel-side entries -> alternative values
-ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1]}
+ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1], "pp_dgrad_bn_k": [512, 1 << 20]}
 
 
 def rel(a, b):
@@ -23,7 +23,8 @@ def _battery(K):
     x, w = rn(1000, 512), rn(776, 512, sc=0.05)
     assert rel(K.gemm_nt(x, w), x.float() @ w.float().t()) < 1e-2
     for (N, H, C, Ko, R, st, pad) in [(2, 14, 128, 128, 3, 1, 1), (2, 14, 128, 128, 3, 2, 1), (2, 14, 64, 256, 1, 1, 0),
-                                      (2, 8, 256, 512, 1, 1, 0), (2, 14, 128, 512, 1, 1, 0), (2, 8, 512, 128, 1, 1, 0), (3, 7, 512, 512, 3, 1, 1)]:
+                                      (2, 8, 256, 512, 1, 1, 0), (2, 14, 128, 512, 1, 1, 0), (2, 8, 512, 128, 1, 1, 0), (3, 7, 512, 512, 3, 1, 1),
+                                      (4, 14, 256, 1024, 1, 1, 0), (8, 14, 128, 512, 1, 1, 0)]:
         xi = torch.randn(N, C, H, H, device="cuda", generator=g, requires_grad=True)
         wk = rn(Ko, R, R, C, sc=0.05)
         y = F.conv2d(xi, wk.float().permute(0, 3, 1, 2), None, st, pad)
@@ -36,6 +37,18 @@ def _battery(K):
         assert torch.allclose(slab.view(-1, 2, Ko).sum(0)[0], yk.float().reshape(-1, Ko).sum(0), rtol=1e-3,
                               atol=1e-2 * yk.float().abs().max().item())
         assert rel(K.conv_dgrad(dy, wk, (N, H, H, C), st, pad), xi.grad.permute(0, 2, 3, 1)) < 1.5e-2
+        if R == 1 and st == 1:
+            # the BN-backward epilogue form of the data gradient (pp_dgrad_bn_k routes it between engines)
+            t = rn(*xn.shape)
+            mean, inv = torch.randn(C, device="cuda", generator=g) * 0.1, torch.rand(C, device="cuda", generator=g) + 0.5
+            bsc, bsh = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g) * 0.3
+            gm, slab = K.conv_dgrad(dy, wk, (N, H, H, C), 1, 0, bn=(t, mean, inv, bsc, bsh))
+            z = t.float() * bsc + bsh
+            gm_ref = xi.grad.permute(0, 2, 3, 1).to(BF).float() * (z > 0)
+            sure = z.abs() > 1e-4
+            assert rel(gm.float() * sure, gm_ref * sure) < 1.5e-2
+            s0 = slab.view(-1, 2, C).sum(0)[0]
+            assert torch.allclose(s0, gm_ref.reshape(-1, C).sum(0), rtol=1e-2, atol=5e-2 + 1e-3 * gm_ref.abs().sum(dim=(0, 1, 2)).max().item())
         dw = K.conv_wgrad(xn, dy, R, R, st, pad)
         dwr = torch.nn.grad.conv2d_weight(xn.float().permute(0, 3, 1, 2), wk.permute(0, 3, 1, 2).shape,
                                           dy.float().permute(0, 3, 1, 2), st, pad).permute(0, 2, 3, 1)
