@@ -76,49 +76,85 @@ __device__ __forceinline__ int halo_off(int hp, int q) {   // bf16 elements
 }
 
 // ---------------- epilogue: lane holds y[pixel m = wave*64 + fm*16 + (lane&15)][n = fn*16 + 4*(lane>>4) + j]
+// Processed one fragment pair (fn, fn+1) at a time.  The operands a pair reads (residual or BN input t, the
+// residual mask words) are loaded one pair AHEAD, before the current
+// pair's stores, and unconditionally (rows past P read row 0 and are never stored): s_waitcnt vmcnt counts
+// stores too on gfx9, so loads issued after a pair's stores waited for them and serialised one store drain +
+// load latency per pair (the GPT-2 GEMM epilogues lost 13-20 us per call that way, gpurun_out/r4_13-14).
+template <int NB, int EPI>
+struct C3PairOps {
+    static constexpr bool RES = EPI == C3_RES, BNB = EPI == C3_BNB;
+    u16x4_t tv[(RES || BNB) ? 2 : 1][4];
+    uint32_t mw[RES ? 4 : 1];
+};
+
+template <int NB, int EPI>
+__device__ __forceinline__ void c3_load_pair(const C3Args& a, const long (&lrow)[4], int n0, int lg, int fp,
+                                             C3PairOps<NB, EPI>& o) {
+    constexpr bool RES = EPI == C3_RES, BNB = EPI == C3_BNB;
+    if constexpr (RES) {
+        // mask bits of this pair's 32 channels: ONE aligned 32-bit load per pixel (bit c = channel n0 + 32*fp + c),
+        // not a byte load per fragment (that doubled the epilogue's memory instructions: ResNet-50 stage-1 conv1
+        // data gradient 239 -> 341 us with the mask, gpurun_out/r3_18)
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm)
+            o.mw[fm] = a.rmask ? *reinterpret_cast<const uint32_t*>(a.rmask + ((lrow[fm] + n0 + 32 * fp) >> 3))
+                               : 0xFFFFFFFFu;
+    }
+    if constexpr (RES || BNB) {
+        const bf16_t* src = BNB ? a.ep_x : a.res;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int n = n0 + (2 * fp + h) * 16 + 4 * lg;
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) o.tv[h][fm] = *reinterpret_cast<const u16x4_t*>(src + lrow[fm] + n);
+        }
+    }
+}
+
 template <int NB, int EPI>
 __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile, int p0, int n0,
                                             int wave, int lane, const bool (&pv)[4]) {
-    constexpr int FN = NB / 16;
+    constexpr int FN = NB / 16, NP = FN / 2;
+    constexpr bool RES = EPI == C3_RES;
     const int lg = lane >> 4;
-    long orow[4];
+    long orow[4], lrow[4];
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm) orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
-    // processed one fragment pair (fn, fn+1) at a time: only that pair's loads / packed results are live
+    for (int fm = 0; fm < 4; ++fm) {
+        orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
+        lrow[fm] = pv[fm] ? orow[fm] : 0;
+    }
+    C3PairOps<NB, EPI> cur, nxt;
+    if constexpr (NP > 1) c3_load_pair<NB, EPI>(a, lrow, n0, lg, 0, cur);
+    else if constexpr (RES) {
 #pragma unroll
-    for (int fp = 0; fp < FN / 2; ++fp) {
+        for (int fm = 0; fm < 4; ++fm)
+            cur.mw[fm] = a.rmask ? *reinterpret_cast<const uint32_t*>(a.rmask + ((lrow[fm] + n0) >> 3)) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int fp = 0; fp < NP; ++fp) {
+        if (fp + 1 < NP) c3_load_pair<NB, EPI>(a, lrow, n0, lg, fp + 1, nxt);
         uint32_t pk[4][2][2];
-        // C3_RES mask bits of this pair's 32 channels: ONE aligned 32-bit load per pixel (bit c = channel
-        // n0 + 32*fp + c), not a byte load per fragment (that doubled the epilogue's memory instructions:
-        // ResNet-50 stage-1 conv1 data gradient 239 -> 341 us with the mask, gpurun_out/r3_18)
-        constexpr bool RES = EPI == C3_RES;
-        uint32_t mw[4];
-        if constexpr (RES) {
-#pragma unroll
-            for (int fm = 0; fm < 4; ++fm) {
-                const long mo = ((pv[fm] ? orow[fm] : 0) + n0 + 32 * fp) >> 3;
-                mw[fm] = a.rmask ? *reinterpret_cast<const uint32_t*>(a.rmask + mo) : 0xFFFFFFFFu;
-            }
-        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int fn = 2 * fp + h;
             const int n = n0 + fn * 16 + 4 * lg;
-            u16x4_t tv[4];
-            if constexpr (EPI == C3_BNB || RES) {
+            // fused BN backward: q accumulates sum gm * t; sum gm * xhat = invstd * (sum gm t - mean * sum gm) is
+            // formed at the flush, so mean / invstd are not live through the fragment loop
+            float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+            float bms[4], bmh[4];
+            if constexpr (NP == 1 && (RES || EPI == C3_BNB)) {
+                // one pair (the 4 x 32 A-stationary kernels, at the register limit): only this half's operand live
                 const bf16_t* src = EPI == C3_BNB ? a.ep_x : a.res;
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
-                    tv[fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(src + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
+                    cur.tv[h][fm] = pv[fm] ? *reinterpret_cast<const u16x4_t*>(src + orow[fm] + n) : u16x4_t{0, 0, 0, 0};
             }
-            // fused BN backward: q accumulates sum gm * t; sum gm * xhat = invstd * (sum gm t - mean * sum gm) is
-            // formed at the flush, so mean / invstd are not live through the fragment loop (the K = 256
-            // A-stationary variants sit at the 256-VGPR limit there)
-            float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
-            float bms[4], bmh[4];
-            if constexpr (EPI == C3_BNB) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) { bms[j] = a.ep_mscale[n + j]; bmh[j] = a.ep_mshift[n + j]; }
+            if constexpr (EPI == C3_BNB) {     // (per-channel tables: L2-resident, not prefetched -- registers)
+                const float4 m4 = *reinterpret_cast<const float4*>(a.ep_mscale + n);
+                const float4 h4 = *reinterpret_cast<const float4*>(a.ep_mshift + n);
+                bms[0] = m4.x; bms[1] = m4.y; bms[2] = m4.z; bms[3] = m4.w;
+                bmh[0] = h4.x; bmh[1] = h4.y; bmh[2] = h4.z; bmh[3] = h4.w;
             }
 #pragma unroll
             for (int fm = 0; fm < 4; ++fm) {
@@ -127,14 +163,14 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j];
                 if constexpr (RES) {
-                    const uint32_t mb = mw[fm] >> (16 * h + 4 * lg);
+                    const uint32_t mb = cur.mw[fm] >> (16 * h + 4 * lg);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(tv[fm][j]) : 0.f;
+                    for (int j = 0; j < 4; ++j) v[j] += ((mb >> j) & 1) ? bf2f(cur.tv[h][fm][j]) : 0.f;
                 }
                 if constexpr (EPI == C3_BNB) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const float tt = bf2f(tv[fm][j]);
+                        const float tt = bf2f(cur.tv[h][fm][j]);
                         const float gm = (ok && fmaf(tt, bms[j], bmh[j]) > 0.f) ? bf2f(f2bf(v[j])) : 0.f;
                         v[j] = gm;
                         s[j] += gm;
@@ -179,6 +215,7 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
             const int n = n0 + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
             if (pv[fm]) *reinterpret_cast<uint4*>(a.y + orow[fm] + n) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         }
+        if (fp + 1 < NP) cur = nxt;
     }
 }
 
