@@ -23,12 +23,10 @@ constexpr int NT = 256;
 // U=2 everywhere 7530-7556, U=4 7508, U=8 7400 (VGPR pressure costs more occupancy than the extra loads
 // in flight buy); reduce U=1/2/4 and 16 vs 64 rows per thread-row all within noise; apply U=1 7553.
 // The templated reduce kernel itself (mode / second-BN specialisations) was the +2% (7385 -> 7530+).
-// A/B builds override them with -DPDNN_BN_UR=n (backward reduce) / -DPDNN_BN_UA=n (apply kernels).
+// The apply kernels are software-pipelined across rows instead (next row's loads before this row's stores).
+// A/B builds override the reduce unroll with -DPDNN_BN_UR=n.
 #ifndef PDNN_BN_UR
 #define PDNN_BN_UR 2
-#endif
-#ifndef PDNN_BN_UA
-#define PDNN_BN_UA 1
 #endif
 // Minimum rows per thread-row of a statistics reduction (more blocks for the narrow, short late layers:
 // ResNet-50 layer4 has only 12544 rows of 2048 channels at bs256).
@@ -39,7 +37,7 @@ constexpr int NT = 256;
 #ifndef PDNN_BN_WIDE_FIN
 #define PDNN_BN_WIDE_FIN 1
 #endif
-constexpr int BN_UR = PDNN_BN_UR, BN_UA = PDNN_BN_UA, BN_RMIN = PDNN_BN_RMIN;
+constexpr int BN_UR = PDNN_BN_UR, BN_RMIN = PDNN_BN_RMIN;
 
 // Level-1 reduction of a partial-statistics slab [rows][2][C] -> [RB][2][C]: block (cx, ry) sums the
 // rows ry, ry+RB, ... for 64 channels with 4 row lanes (coalesced 256-byte row segments).
@@ -399,44 +397,44 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
         sh[j] = shift[c + j] + (RSC ? rshift[c + j] : 0.f);
         if constexpr (RSC) rs_[j] = rscale[c + j];
     }
+    // Software-pipelined over the rows this thread visits: row r+step's operands are loaded BEFORE row r's
+    // stores (s_waitcnt vmcnt counts stores too on gfx9: loads issued after a store wait for it, so the
+    // load-then-store loop serialised one store drain + load latency per row), unconditionally from a clamped
+    // row (the last row is re-read once, never stored twice).
     const long step = (long)gridDim.x * RPI;
-    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += BN_UA * step) {
-        long rws[BN_UA];
-        u16x8_t xv[BN_UA], rv[RES ? BN_UA : 1];
+    long r = (long)blockIdx.x * RPI + rr;
+    if (r >= L) return;
+    u16x8_t xv = *reinterpret_cast<const u16x8_t*>(x + r * C + c), rv;
+    if constexpr (RES) rv = *reinterpret_cast<const u16x8_t*>(res + r * C + c);
+    for (; r < L; r += step) {
+        const long rn = r + step < L ? r + step : L - 1;
+        const u16x8_t xn = *reinterpret_cast<const u16x8_t*>(x + rn * C + c);
+        u16x8_t rnv;
+        if constexpr (RES) rnv = *reinterpret_cast<const u16x8_t*>(res + rn * C + c);
+        float v[8];
+        unpack8(xv, v);
+        if constexpr (RES) {
+            float rf[8];
+            unpack8(rv, rf);
 #pragma unroll
-        for (int u = 0; u < BN_UA; ++u) {
-            rws[u] = r0 + u * step;
-            if (rws[u] < L) {
-                xv[u] = *reinterpret_cast<const u16x8_t*>(x + rws[u] * C + c);
-                if constexpr (RES) rv[u] = *reinterpret_cast<const u16x8_t*>(res + rws[u] * C + c);
-            }
+            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], fmaf(rf[j], RSC ? rs_[j] : 1.f, sh[j]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
         }
+        if constexpr (RELU) {
 #pragma unroll
-        for (int u = 0; u < BN_UA; ++u) {
-            if (rws[u] >= L) break;
-            float v[8];
-            unpack8(xv[u], v);
-            if constexpr (RES) {
-                float r[8];
-                unpack8(rv[u], r);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], fmaf(r[j], RSC ? rs_[j] : 1.f, sh[j]));
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
-            }
-            if constexpr (RELU) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-            }
-            if constexpr (MASK) {
-                unsigned bits = 0;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) bits |= (v[j] > 0.f ? 1u : 0u) << j;
-                mbits[rws[u] * CG + cg] = (uint8_t)bits;
-            }
-            *reinterpret_cast<u16x8_t*>(y + rws[u] * C + c) = pack8(v);
+            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
         }
+        if constexpr (MASK) {
+            unsigned bits = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bits |= (v[j] > 0.f ? 1u : 0u) << j;
+            mbits[r * CG + cg] = (uint8_t)bits;
+        }
+        *reinterpret_cast<u16x8_t*>(y + r * C + c) = pack8(v);
+        xv = xn;
+        if constexpr (RES) rv = rnv;
     }
 }
 
@@ -555,7 +553,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __rest
 // dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
 // registers; optionally also a second BN's dx2 (shared gm) and/or gm itself.
 // Specialised on the mask mode / second BN / outputs so unused coefficient arrays take no registers
-// (occupancy), and BN_UA rows per thread per iteration so U times the loads are in flight.
+// (occupancy).
 template <int MODE, bool X2, bool DX, bool GMO>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, long L, int C,
@@ -583,56 +581,56 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
         }
         if constexpr (MODE == 2) { ms[j] = mscale[c + j]; mh[j] = mshift[c + j]; }
     }
+    // software-pipelined over rows like bn_apply_kernel: row r+step's loads are issued before row r's stores
     const long step = (long)gridDim.x * RPI;
-    for (long r0 = (long)blockIdx.x * RPI + rr; r0 < L; r0 += BN_UA * step) {
-        u16x8_t gv[BN_UA], xv8[BN_UA], mv[MODE == 1 ? BN_UA : 1], x2v8[X2 ? BN_UA : 1];
-        unsigned mb[MODE == 3 ? BN_UA : 1];
+    long r = (long)blockIdx.x * RPI + rr;
+    if (r >= L) return;
+    struct Ops {
+        u16x8_t g, x, m, x2;
+        unsigned mb;
+    };
+    auto load = [&](long row, Ops& o) {
+        const long off = row * C + c;
+        o.g = *reinterpret_cast<const u16x8_t*>(g + off);
+        o.x = *reinterpret_cast<const u16x8_t*>(x + off);
+        if constexpr (MODE == 1) o.m = *reinterpret_cast<const u16x8_t*>(msrc + off);
+        if constexpr (MODE == 3) o.mb = reinterpret_cast<const uint8_t*>(msrc)[row * CG + cg];
+        if constexpr (X2) o.x2 = *reinterpret_cast<const u16x8_t*>(x2 + off);
+    };
+    Ops cur, nxt;
+    load(r, cur);
+    for (; r < L; r += step) {
+        load(r + step < L ? r + step : L - 1, nxt);
+        const long off = r * C + c;
+        float gm[8], xv[8], o[8];
+        unpack8(cur.g, gm);
+        unpack8(cur.x, xv);
+        if constexpr (MODE == 1) {
+            float m[8];
+            unpack8(cur.m, m);
 #pragma unroll
-        for (int u = 0; u < BN_UA; ++u) {       // issue every load of all U rows first
-            const long r = r0 + u * step;
-            if (r < L) {
-                const long off = r * C + c;
-                gv[u] = *reinterpret_cast<const u16x8_t*>(g + off);
-                xv8[u] = *reinterpret_cast<const u16x8_t*>(x + off);
-                if constexpr (MODE == 1) mv[u] = *reinterpret_cast<const u16x8_t*>(msrc + off);
-                if constexpr (MODE == 3) mb[u] = reinterpret_cast<const uint8_t*>(msrc)[r * CG + cg];
-                if constexpr (X2) x2v8[u] = *reinterpret_cast<const u16x8_t*>(x2 + off);
-            }
+            for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
+        } else if constexpr (MODE == 2) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
+        } else if constexpr (MODE == 3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gm[j] = ((cur.mb >> j) & 1u) ? gm[j] : 0.f;
         }
+        if constexpr (DX) {
 #pragma unroll
-        for (int u = 0; u < BN_UA; ++u) {
-            const long r = r0 + u * step;
-            if (r >= L) break;
-            const long off = r * C + c;
-            float gm[8], xv[8], o[8];
-            unpack8(gv[u], gm);
-            unpack8(xv8[u], xv);
-            if constexpr (MODE == 1) {
-                float m[8];
-                unpack8(mv[u], m);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) gm[j] = m[j] > 0.f ? gm[j] : 0.f;
-            } else if constexpr (MODE == 2) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) gm[j] = fmaf(xv[j], ms[j], mh[j]) > 0.f ? gm[j] : 0.f;
-            } else if constexpr (MODE == 3) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) gm[j] = ((mb[u] >> j) & 1u) ? gm[j] : 0.f;
-            }
-            if constexpr (DX) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gm[j], fmaf(xv[j], A1[j], B1[j]));
-                *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
-            }
-            if constexpr (X2) {
-                float x2v[8];
-                unpack8(x2v8[u], x2v);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = fmaf(k2[j], gm[j], fmaf(x2v[j], A2[j], B2[j]));
-                *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
-            }
-            if constexpr (GMO) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
+            for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gm[j], fmaf(xv[j], A1[j], B1[j]));
+            *reinterpret_cast<u16x8_t*>(dx + off) = pack8(o);
         }
+        if constexpr (X2) {
+            float x2v[8];
+            unpack8(cur.x2, x2v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = fmaf(k2[j], gm[j], fmaf(x2v[j], A2[j], B2[j]));
+            *reinterpret_cast<u16x8_t*>(dx2 + off) = pack8(o);
+        }
+        if constexpr (GMO) *reinterpret_cast<u16x8_t*>(gm_out + off) = pack8(gm);
+        cur = nxt;
     }
 }
 
