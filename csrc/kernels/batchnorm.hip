@@ -19,7 +19,7 @@ namespace {
 constexpr int NT = 256;
 
 // Rows per thread per iteration of the streaming kernels: all U rows' loads are issued before any is
-// consumed.  Measured on the ResNet-50 bs256 step (tools/gpu_runs/gpu_run44.sh, gpu_run45.sh), img/s:
+// consumed.  Measured on the ResNet-50 bs256 step (gpu_run44 / gpu_run45 in dev/gpu_runs/archive_r1_r3.txt), img/s:
 // U=2 everywhere 7530-7556, U=4 7508, U=8 7400 (VGPR pressure costs more occupancy than the extra loads
 // in flight buy); reduce U=1/2/4 and 16 vs 64 rows per thread-row all within noise; apply U=1 7553.
 // The templated reduce kernel itself (mode / second-BN specialisations) was the +2% (7385 -> 7530+).

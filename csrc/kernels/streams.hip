@@ -7,7 +7,7 @@
 // step, against ~1-2 us between plain back-to-back kernels).  Both streams here live on one device, and
 // each kernel's own end-of-dispatch release already makes its results visible device-wide, so the marker
 // needs no system-scope fence: these events are created with hipEventDisableSystemFence (and no timing).
-// Measured (dev/gpu_runs/r3_58.sh, same box): median compute-stream gap 7.3 -> 5.5 us, ResNet-50
+// Measured (dev/gpu_runs/archive_r1_r3.txt "r3_58", same box): median compute-stream gap 7.3 -> 5.5 us, ResNet-50
 // 10,604-10,615 -> 10,687-10,689 img/s.
 #include "common.h"
 

@@ -1,4 +1,4 @@
-"""Per-kernel PMC summary of a rocprofv3 `--pmc` run (dev/gpu_runs/gpu_run61.sh layout).
+"""Per-kernel PMC summary of a rocprofv3 `--pmc` run (dev/gpu_runs/r4_08.sh layout).
 
 python tools/pmc_summary.py DIR [--steps N] [--top T]
 

@@ -1,9 +1,9 @@
 """Per-stream occupancy of one training step from a rocprofv3 --kernel-trace CSV (no PMC: real concurrency).
 
-python tools/stream_timeline.py TRACE.csv [--steps N]
+python tools/stream_timeline.py TRACE.csv [--top N]
 
-Splits the trace into steps at the optimizer kernel (sgd/adam), then per stream reports busy time (union of
-its kernel intervals), the gaps between consecutive kernels, and the largest gaps (what the compute stream
+Takes the last full step of the trace (between the last two optimizer kernels, sgd/adam), then per stream
+reports busy time (sum of its kernel intervals: one stream's kernels do not overlap), the gaps between consecutive kernels, and the largest gaps (what the compute stream
 waits on); finally the top kernels by time on the critical (compute) stream."""
 import argparse
 import csv
