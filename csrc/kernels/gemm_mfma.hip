@@ -154,7 +154,10 @@ struct KLoader {
                 const ConvGeom& g = a.g;
                 int th = hb[i] - (g.r0 + g.st * r), tw = wb[i] - (g.s0 + g.st * s);
                 bool v = vrow[i] && kv && th >= 0 && tw >= 0;
-                if (g.st != 1) {     // exact by construction of the parity class
+                if (g.st == 2) {     // exact by construction of the parity class (negative: invalid anyway);
+                    th >>= 1;        // a shift, not the runtime integer division (a ~40-instruction sequence
+                    tw >>= 1;        // per chunk and K-step in the stride-2 data gradients)
+                } else if (g.st != 1) {
                     th /= g.st;
                     tw /= g.st;
                 }
