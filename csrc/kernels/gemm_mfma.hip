@@ -483,18 +483,24 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 }
         }
         uint32_t pk[4][FN][2];     // packed bf16 results (2 dwords = 4 columns per lane and fragment)
+        // per-column sums of every fragment column, stored after the loop: a statistics store inside it made the
+        // next column's coefficient loads wait for it (s_waitcnt vmcnt counts stores too on gfx9)
+        float ss[FN][4], qs[FN][4];
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
             const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
             const bool nv = n < a.N, n4 = n + 4 <= a.N;
             float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
             float bmu[4], bis[4], bms[4], bmh[4];
-            if (bnb && n4) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    bmu[j] = a.ep_mean[n + j]; bis[j] = a.ep_invstd[n + j];
-                    bms[j] = a.ep_mscale[n + j]; bmh[j] = a.ep_mshift[n + j];
-                }
+            if (bnb && n4) {          // n % 4 == 0: 16-byte coefficient loads
+                const float4 mu4 = *reinterpret_cast<const float4*>(a.ep_mean + n);
+                const float4 is4 = *reinterpret_cast<const float4*>(a.ep_invstd + n);
+                const float4 ms4 = *reinterpret_cast<const float4*>(a.ep_mscale + n);
+                const float4 mh4 = *reinterpret_cast<const float4*>(a.ep_mshift + n);
+                bmu[0] = mu4.x; bmu[1] = mu4.y; bmu[2] = mu4.z; bmu[3] = mu4.w;
+                bis[0] = is4.x; bis[1] = is4.y; bis[2] = is4.z; bis[3] = is4.w;
+                bms[0] = ms4.x; bms[1] = ms4.y; bms[2] = ms4.z; bms[3] = ms4.w;
+                bmh[0] = mh4.x; bmh[1] = mh4.y; bmh[2] = mh4.z; bmh[3] = mh4.w;
             }
 #pragma unroll
             for (int fm = 0; fm < 4; ++fm) {
@@ -564,17 +570,22 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
             if (want_stats) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {      // sum over the 16 rows (lanes l & 15) of the fragment column
-                    s[j] = row16_sum(s[j]);
-                    q[j] = row16_sum(q[j]);
+                    ss[fn][j] = row16_sum(s[j]);
+                    qs[fn][j] = row16_sum(q[j]);
                 }
-                if (lm == 0 && nv) {
-                    const long row = (long)(a.stats_row0 + tm * 2 + wm) * 2;
-                    float* ps = a.stats + row * a.N + n;
-                    float* pq = a.stats + (row + 1) * a.N + n;
+            }
+        }
+        if (want_stats && lm == 0) {
+            const long row = (long)(a.stats_row0 + tm * 2 + wm) * 2;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        if (n + j < a.N) { ps[j] = s[j]; pq[j] = q[j]; }
-                    }
+            for (int fn = 0; fn < FN; ++fn) {
+                const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
+                if (n >= a.N) continue;
+                float* ps = a.stats + row * a.N + n;
+                float* pq = a.stats + (row + 1) * a.N + n;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (n + j < a.N) { ps[j] = ss[fn][j]; pq[j] = qs[fn][j]; }
                 }
             }
         }
