@@ -1006,6 +1006,21 @@ PDNN_API int pdnn_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int 
         a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
         if (pp_supported(a, A_KMAJOR, B_MNMAJOR, E_BF16, 1, 1)) return pp_launch(a, A_KMAJOR, B_MNMAJOR, E_BF16, stream);
     }
+    if (R == 1 && S == 1 && st == 2 && pad == 0 && !bn_x && !res_mask && (res == dx || !res) &&
+        C >= kPPConvMinN && Ko >= kPPConvDgradK) {
+        // 1x1 stride-2 (the ResNet shortcut) accumulated in place: one parity class, whose GEMM rows are dy's
+        // pixels as they are (A plain K-major), scattered to the even pixels of dx by the ping-pong epilogue
+        // (with res == dx the odd pixels keep dx); 180 / 145 / 135 us on the 128-row engine's gather before
+        GemmArgs a{};
+        a.M = Nimg * Ho * Wo; a.N = C; a.K = Ko;
+        a.A = dy; a.lda = Ko; a.B = w; a.ldb = C; a.C = dx; a.ldc = C; a.alpha = 1.f;
+        a.ep_res = res;
+        fill_geom(a.g, Nimg, H, W, C, Ho, Wo, R, S, st, pad, Ko);
+        a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
+        a.scatter = 1;
+        if (res == dx && pp_supported(a, A_KMAJOR, B_MNMAJOR, E_BF16, 1, 1))
+            return pp_launch(a, A_KMAJOR, B_MNMAJOR, E_BF16, stream);
+    }
     DgradClass cl[16];
     bool any_empty;
     const int ncl = dgrad_classes(H, W, R, S, st, pad, cl, &any_empty);

@@ -252,6 +252,16 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     const int lm = lane & 15, lg = lane >> 4;
     float alpha = a.alpha;
     if (a.alpha_ptr) alpha *= *a.alpha_ptr;
+    // output row of GEMM row m: m itself, or with `scatter` the pixel (n, st*y + ph, st*x + pw) of the strided
+    // conv's input grid that row m = (n, y, x) of the parity class maps to (the 1x1 stride-2 data gradient)
+    auto orow_of = [&](int m) -> long {
+        if (!a.scatter) return m;
+        const uint32_t nn = fdiv((uint32_t)m, a.g.dHW);
+        const uint32_t rem = (uint32_t)m - nn * a.g.dHW.d;
+        const uint32_t hc = fdiv(rem, a.g.dW);
+        const uint32_t wc = rem - hc * a.g.dW.d;
+        return ((long)nn * a.g.H + hc * a.g.st + a.g.ph) * a.g.W + wc * a.g.st + a.g.pw;
+    };
 
     int s = 0, cur = 0, rd_off = 0;                      // slice within the current item, item index, read slot
     auto epilogue = [&]() {
@@ -283,7 +293,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             float4 bia[PF ? C::FN : 1];
             u16x4_t nx[PFO ? C::FN : 1];
             auto load_op = [&](int fm_) {      // PFO only
-                const long mm = min(m0 + arow + fm_ * 16 + lm, a.M - 1);
+                const long mm = orow_of(min(m0 + arow + fm_ * 16 + lm, a.M - 1));
 #pragma unroll
                 for (int fn = 0; fn < C::FN; ++fn) {
                     const int n = min(n0 + bcol + fn * 16 + 4 * lg, a.N - 4);
@@ -307,6 +317,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                 if constexpr ((FX & FX_BNB) != 0) __builtin_amdgcn_sched_barrier(0);
                 const int m = m0 + arow + fm * 16 + lm;
                 const bool mv = m < a.M;
+                const long orow = orow_of(mv ? m : 0);
                 if constexpr (EM == E_BF16) {
                     uint32_t pk[C::FN][2];
                     u16x4_t cu[PFO ? C::FN : 1];
@@ -321,7 +332,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     for (int fn = 0; fn < C::FN; ++fn) {
                         const int n = n0 + bcol + fn * 16 + 4 * lg;
                         const bool ok = mv && n + 4 <= a.N;
-                        const long off = (long)m * a.ldc + n;
+                        const long off = orow * a.ldc + n;
                         float v[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
@@ -391,7 +402,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                         pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
                         pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
                     }
-                    bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + (long)m * a.ldc;
+                    bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc;
 #pragma unroll
                     for (int fp = 0; fp < C::FN / 2; ++fp) {   // 16-byte stores: permlane16 swap pairs fragments
                         const auto s0_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
@@ -777,7 +788,8 @@ int& pp_mode_ref() { return tune().pp; }
 bool pp_supported(const GemmArgs& a, int amode, int bmode, int em, int batch, int splits) {
     const int mode = pp_mode_ref();
     if (!mode || batch != 1 || splits != 1 || em == E_ATOMIC) return false;
-    if (a.causal || a.scatter || a.transC || a.stats_row0) return false;
+    if (a.causal || a.transC || a.stats_row0) return false;
+    if (a.scatter && (em != E_BF16 || fx_of(a) != 0)) return false;      // scatter rows: plain bf16 epilogues
     if (a.K % PP_SK || a.M < 16 || a.N < 16 || a.N % 8 || a.lda % 8 || a.ldb % 8) return false;
     if (!((amode == A_KMAJOR && (bmode == B_KMAJOR || bmode == B_MNMAJOR)) ||
           (amode == A_MNMAJOR && bmode == B_MNMAJOR)))

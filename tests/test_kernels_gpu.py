@@ -465,3 +465,23 @@ def test_conv_dgrad_masked_residual(K, shape):
     assert rel(dx, ref) < 1.5e-2
 
 
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 256, 512), (2, 14, 512, 1024), (3, 7, 1024, 2048), (2, 9, 128, 512)])
+def test_conv1x1_stride2_dgrad_in_place(K, shape):
+    """The ResNet shortcut's data gradient: 1x1 / stride 2, accumulated in place into dx (the ping-pong engine with
+    its rows scattered to the even pixels; odd pixels keep dx) against fp32 torch."""
+    N, H, C, Ko = shape
+    Ho = (H - 1) // 2 + 1
+    dy = rnd(N, Ho, Ho, Ko)
+    w = rnd(Ko, 1, 1, C, scale=0.05)
+    dx0 = rnd(N, H, H, C)
+    dx = dx0.clone()
+    out = K.conv_dgrad(dy, w, (N, H, H, C), 2, 0, res=dx, out=dx)
+    assert out.data_ptr() == dx.data_ptr()
+    xi = torch.zeros(N, C, H, H, device="cuda", requires_grad=True)
+    y = F.conv2d(xi, w.float().permute(0, 3, 1, 2), None, 2, 0)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    ref = xi.grad.permute(0, 2, 3, 1) + dx0.float()
+    assert rel(dx, ref) < 1.5e-2
+    assert torch.equal(dx[:, 1::2, :, :], dx0[:, 1::2, :, :]) and torch.equal(dx[:, :, 1::2, :], dx0[:, :, 1::2, :])
