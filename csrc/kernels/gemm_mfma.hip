@@ -70,13 +70,57 @@ __device__ __forceinline__ u16x8_t affine_relu8(u16x8_t v, const float* sc, cons
 // ---- K-major operands: row = tile row (m or n), 8 chunks of 8 k per row ----------------------
 template <int ROWS, int KIND, bool PRO>   // KIND: 0 plain, 1 conv gather, 2 conv-transposed gather
 struct KLoader {
+    // The conv gathers resolve a chunk's source pixel once per TAP (r, s), not once per K-step: within a tap the
+    // K-steps walk the channels of the same pixel, so a load is one add from the tap's pixel pointer.  Per-step
+    // coordinate and 64-bit address math had made the stride-2 data gradients VALU-bound (23 vector instructions
+    // per MFMA; rocprofv3 SQ_INSTS_VALU / SQ_INSTS_MFMA, gpurun_out/r4_29).
     static constexpr int NCH = ROWS / 32;
     const bf16_t* base[NCH];   // plain: row pointer; conv: image base pointer of the row's pixel
+    const bf16_t* tp[NCH];     // conv: the row's source pixel for the current tap (valid when tv)
     int hb[NCH], wb[NCH];      // conv: top-left input coordinate of the row's window
-    bool vrow[NCH];
+    bool vrow[NCH], tv[NCH];
     int ch;                    // chunk column (fixed per thread)
     int r, s, c;               // conv: current (r, s, c) of this thread's chunk column
     int kcur;                  // current k of this thread's chunk
+
+    __device__ __forceinline__ void retap(const GemmArgs& a) {
+        const ConvGeom& g = a.g;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            if constexpr (KIND == 1) {
+                const int hi = hb[i] + r, wi = wb[i] + s;
+                tv[i] = vrow[i] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                tp[i] = base[i] + ((long)(tv[i] ? hi : 0) * g.W + (tv[i] ? wi : 0)) * g.C;
+            } else if constexpr (KIND == 2) {
+                int th = hb[i] - (g.r0 + g.st * r), tw = wb[i] - (g.s0 + g.st * s);
+                bool v = vrow[i] && th >= 0 && tw >= 0;
+                if (g.st == 2) {     // exact by construction of the parity class (negative: invalid anyway)
+                    th >>= 1;
+                    tw >>= 1;
+                } else if (g.st != 1) {
+                    th /= g.st;
+                    tw /= g.st;
+                }
+                v = v && th < g.Ho && tw < g.Wo;
+                tv[i] = v;
+                tp[i] = base[i] + ((long)(v ? th : 0) * g.Wo + (v ? tw : 0)) * g.Ko;
+            }
+        }
+    }
+    __device__ __forceinline__ void derive_tap(const GemmArgs& a) {     // (r, s, c) of kcur
+        const ConvGeom& g = a.g;
+        if constexpr (KIND == 1) {
+            const uint32_t rs = fdiv((uint32_t)kcur, g.dC);
+            c = kcur - rs * g.C;
+            r = fdiv(rs, g.dS);
+            s = rs - r * g.S;
+        } else if constexpr (KIND == 2) {     // r, s = tap indices within the parity class
+            const uint32_t rs = fdiv((uint32_t)kcur, g.dKo);
+            c = kcur - rs * g.Ko;
+            r = fdiv(rs, g.dSc);
+            s = rs - r * g.Sc;
+        }
+    }
 
     __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int rows_total,
                                          int row0, int tid) {
@@ -107,32 +151,16 @@ struct KLoader {
             }
         }
         kcur = ch * 8;
-        if constexpr (KIND == 1) {
-            const ConvGeom& g = a.g;
-            const uint32_t rs = fdiv((uint32_t)kcur, g.dC);
-            c = kcur - rs * g.C;
-            r = fdiv(rs, g.dS);
-            s = rs - r * g.S;
-        } else if constexpr (KIND == 2) {     // r, s = tap indices within the parity class
-            const ConvGeom& g = a.g;
-            const uint32_t rs = fdiv((uint32_t)kcur, g.dKo);
-            c = kcur - rs * g.Ko;
-            r = fdiv(rs, g.dSc);
-            s = rs - r * g.Sc;
+        if constexpr (KIND != 0) {
+            derive_tap(a);
+            retap(a);
         }
     }
     __device__ __forceinline__ void seek(const GemmArgs& a, int k) {   // jump to K offset k (split-K)
         kcur = k + ch * 8;
-        if constexpr (KIND == 1) {
-            const uint32_t rs = fdiv((uint32_t)kcur, a.g.dC);
-            c = kcur - rs * a.g.C;
-            r = fdiv(rs, a.g.dS);
-            s = rs - r * a.g.S;
-        } else if constexpr (KIND == 2) {
-            const uint32_t rs = fdiv((uint32_t)kcur, a.g.dKo);
-            c = kcur - rs * a.g.Ko;
-            r = fdiv(rs, a.g.dSc);
-            s = rs - r * a.g.Sc;
+        if constexpr (KIND != 0) {
+            derive_tap(a);
+            retap(a);
         }
     }
     __device__ __forceinline__ void load(const GemmArgs& a, int Ktot, u16x8_t* reg) {
@@ -141,52 +169,29 @@ struct KLoader {
         for (int i = 0; i < NCH; ++i) {
             if constexpr (KIND == 0) {
                 reg[i] = (vrow[i] && kv) ? ldg16(base[i] + kcur) : zero8();
-            } else if constexpr (KIND == 1) {
-                const ConvGeom& g = a.g;
-                const int hi = hb[i] + r, wi = wb[i] + s;
-                const bool v = vrow[i] && kv && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                u16x8_t x = v ? ldg16(base[i] + ((long)hi * g.W + wi) * g.C + c) : zero8();
-                if constexpr (PRO) {
-                    if (v) x = affine_relu8(x, a.pro_scale + c, a.pro_shift + c);
+            } else {
+                u16x8_t x = (tv[i] && kv) ? ldg16(tp[i] + c) : zero8();
+                if constexpr (KIND == 1 && PRO) {
+                    if (tv[i] && kv) x = affine_relu8(x, a.pro_scale + c, a.pro_shift + c);
                 }
                 reg[i] = x;
-            } else {
-                const ConvGeom& g = a.g;
-                int th = hb[i] - (g.r0 + g.st * r), tw = wb[i] - (g.s0 + g.st * s);
-                bool v = vrow[i] && kv && th >= 0 && tw >= 0;
-                if (g.st == 2) {     // exact by construction of the parity class (negative: invalid anyway);
-                    th >>= 1;        // a shift, not the runtime integer division (a ~40-instruction sequence
-                    tw >>= 1;        // per chunk and K-step in the stride-2 data gradients)
-                } else if (g.st != 1) {
-                    th /= g.st;
-                    tw /= g.st;
-                }
-                v = v && th < g.Ho && tw < g.Wo;
-                reg[i] = v ? ldg16(base[i] + ((long)th * g.Wo + tw) * g.Ko + c) : zero8();
             }
         }
     }
     __device__ __forceinline__ void advance(const GemmArgs& a) {
         kcur += BK;
-        if constexpr (KIND == 1) {
-            if (a.g.C >= BK) {          // C % 64 == 0: at most one wrap per K-step
+        if constexpr (KIND != 0) {
+            const int CC = KIND == 1 ? a.g.C : a.g.Ko;      // channels per tap
+            if (CC >= BK) {          // CC % 64 == 0: at most one wrap (= one new tap) per K-step
                 c += BK;
-                if (c >= a.g.C) { c -= a.g.C; if (++s == a.g.S) { s = 0; ++r; } }
-            } else {                    // few channels (the 7x7 stem, C = 8): re-derive (r, s, c)
-                const uint32_t rs = fdiv((uint32_t)kcur, a.g.dC);
-                c = kcur - rs * a.g.C;
-                r = fdiv(rs, a.g.dS);
-                s = rs - r * a.g.S;
-            }
-        } else if constexpr (KIND == 2) {
-            if (a.g.Ko >= BK) {
-                c += BK;
-                if (c >= a.g.Ko) { c -= a.g.Ko; if (++s == a.g.Sc) { s = 0; ++r; } }
-            } else {
-                const uint32_t rs = fdiv((uint32_t)kcur, a.g.dKo);
-                c = kcur - rs * a.g.Ko;
-                r = fdiv(rs, a.g.dSc);
-                s = rs - r * a.g.Sc;
+                if (c >= CC) {
+                    c -= CC;
+                    if (++s == (KIND == 1 ? a.g.S : a.g.Sc)) { s = 0; ++r; }
+                    retap(a);
+                }
+            } else {                 // few channels (the 7x7 stem, C = 8): re-derive (r, s, c) every step
+                derive_tap(a);
+                retap(a);
             }
         }
     }
@@ -215,6 +220,26 @@ struct MLoader {
     int cr, cs, cc;
     int kbase;
     float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];   // fused-prologue coefficients of this thread's 8 channels
+    // weight gather (KIND 1): each chunk row's (ko, tap) and weight pointer, advanced incrementally (the per-step
+    // two fast divisions and 64-bit address math per chunk were a large part of the VALU-bound stride-2 data
+    // gradients, gpurun_out/r4_29)
+    int wko[KIND == 1 ? NCH : 1], wrs[KIND == 1 ? NCH : 1];
+    const bf16_t* wpt[KIND == 1 ? NCH : 1];
+
+    __device__ __forceinline__ void wt_derive(const GemmArgs& a, int i) {
+        const ConvGeom& g = a.g;
+        const int k = kbase + krow0 + RPP * i;
+        const uint32_t rs = fdiv((uint32_t)k, g.dKo);
+        wko[i] = k - rs * g.Ko;
+        wrs[i] = rs;
+        wt_point(a, i);
+    }
+    __device__ __forceinline__ void wt_point(const GemmArgs& a, int i) {
+        const ConvGeom& g = a.g;
+        const uint32_t ir = fdiv((uint32_t)wrs[i], g.dSc);
+        const int rr = g.r0 + g.st * (int)ir, ss = g.s0 + g.st * (int)(wrs[i] - ir * g.Sc);
+        wpt[i] = ptr + ((long)wko[i] * g.R * g.S + rr * g.S + ss) * g.C + col;
+    }
 
     __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld_, int cols_total,
                                          int col0, int tid) {
@@ -225,6 +250,10 @@ struct MLoader {
         ptr = p;
         ld = ld_;
         kbase = 0;
+        if constexpr (KIND == 1) {
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) wt_derive(a, i);
+        }
         if constexpr (KIND == 2) {
             const ConvGeom& g = a.g;
             const int cl = vcol ? col : 0;
@@ -238,7 +267,13 @@ struct MLoader {
             }
         }
     }
-    __device__ __forceinline__ void seek(const GemmArgs&, int k) { kbase = k; }
+    __device__ __forceinline__ void seek(const GemmArgs& a, int k) {
+        kbase = k;
+        if constexpr (KIND == 1) {
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) wt_derive(a, i);
+        }
+    }
     __device__ __forceinline__ void load(const GemmArgs& a, int Ktot, u16x8_t* reg) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
@@ -247,14 +282,8 @@ struct MLoader {
             if constexpr (KIND == 0) {
                 reg[i] = v ? ldg16(ptr + (long)k * ld + col) : zero8();
             } else if constexpr (KIND == 1) {
-                // reduction index k = (r*S + s)*Ko + ko ; weight W[ko][r][s][c], column = c
-                const ConvGeom& g = a.g;
-                const int kk = v ? k : 0;
-                const uint32_t rs = fdiv((uint32_t)kk, g.dKo);
-                const int ko = kk - rs * g.Ko;
-                const uint32_t ir = fdiv(rs, g.dSc);
-                const int rr = g.r0 + g.st * (int)ir, ss = g.s0 + g.st * (int)(rs - ir * g.Sc);
-                reg[i] = v ? ldg16(ptr + ((long)ko * g.R * g.S + rr * g.S + ss) * g.C + col) : zero8();
+                // reduction index k = (r*S + s)*Ko + ko ; weight W[ko][r][s][c], column = c (pointer kept by advance)
+                reg[i] = v ? ldg16(wpt[i]) : zero8();
             } else {
                 // reduction index k = output pixel (n, yo, xo); column = (r, s, c) of the input window
                 const ConvGeom& g = a.g;
@@ -276,7 +305,27 @@ struct MLoader {
             }
         }
     }
-    __device__ __forceinline__ void advance(const GemmArgs&) { kbase += BK; }
+    __device__ __forceinline__ void advance(const GemmArgs& a) {
+        kbase += BK;
+        if constexpr (KIND == 1) {
+            const ConvGeom& g = a.g;
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) {
+                if (g.Ko >= BK) {         // at most one wrap into the next tap per K-step
+                    wko[i] += BK;
+                    if (wko[i] >= g.Ko) {
+                        wko[i] -= g.Ko;
+                        ++wrs[i];
+                        wt_point(a, i);
+                    } else {
+                        wpt[i] += (long)BK * g.R * g.S * g.C;
+                    }
+                } else {
+                    wt_derive(a, i);
+                }
+            }
+        }
+    }
     __device__ __forceinline__ void store(bf16_t* img, const u16x8_t* reg, int) const {
 #pragma unroll
         for (int i = 0; i < NCH; ++i)
