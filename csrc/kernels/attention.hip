@@ -282,6 +282,9 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
                                                             bf16_t* __restrict__ dqkv, int T, int H, float scale,
                                                             int causal) {
     __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][Q|dO]
+    // the query tile's lse2 / delta ride along with its Q / dO tile through LDS: loaded from global memory in the
+    // compute loop they were waited on behind the next tile's prefetch loads (vmcnt is in order), every tile
+    __shared__ __attribute__((aligned(16))) float lsd[2][2][64];              // [buf][lse2|delta][query]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const int nkb = T / 64;
     const int kb = blockIdx.x;                       // early key tiles have the most work: launched first
@@ -309,11 +312,19 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
 
     const int qb0 = causal ? kb : 0;
     const int nqb = T / 64;
+    // threads 0-15 move the tile's lse2, 16-31 its delta (one float4 each)
+    const float* lsrc = tid < 16 ? L2 + 4 * tid : Dl + 4 * (tid - 16);
+    float4 lrow = {0.f, 0.f, 0.f, 0.f};
     TileLd tq, tdo;
     tq.load(Q + (long)qb0 * 64 * ld, ld, tid);
     tdo.load(dOp + (long)qb0 * 64 * D, D, tid);
+    if (tid < 32) lrow = *reinterpret_cast<const float4*>(lsrc + qb0 * 64);
     tq.store(smem[0][0], tid);
     tdo.store(smem[0][1], tid);
+    if (tid < 32) *reinterpret_cast<float4*>(&lsd[0][tid >> 4][4 * (tid & 15)]) = lrow;
+    // every prologue load (the K / V fragments above included) has landed: no wait for them inside the loop,
+    // where the compiler's in-order vmcnt waits would otherwise also wait out the next tile's prefetch
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     for (int qb = qb0; qb < nqb; ++qb) {
         const int cur = (qb - qb0) & 1;
@@ -321,6 +332,7 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
         if (more) {
             tq.load(Q + (long)(qb + 1) * 64 * ld, ld, tid);
             tdo.load(dOp + (long)(qb + 1) * 64 * D, D, tid);
+            if (tid < 32) lrow = *reinterpret_cast<const float4*>(lsrc + (qb + 1) * 64);
         }
         const int qs = qb * 64;
         if (!causal || qs + 63 >= k0) {
@@ -341,8 +353,8 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
 #pragma unroll
             for (int qi = 0; qi < 4; ++qi) {
                 const int qr = qs + 16 * qi + 4 * g;
-                const float4 lv = *reinterpret_cast<const float4*>(L2 + qr);
-                const float4 dl = *reinterpret_cast<const float4*>(Dl + qr);
+                const float4 lv = *reinterpret_cast<const float4*>(&lsd[cur][0][16 * qi + 4 * g]);
+                const float4 dl = *reinterpret_cast<const float4*>(&lsd[cur][1][16 * qi + 4 * g]);
                 const float la[4] = {lv.x, lv.y, lv.z, lv.w}, da[4] = {dl.x, dl.y, dl.z, dl.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) s[qi][r] = __builtin_amdgcn_exp2f(fmaf(s[qi][r], c, -la[r]));
@@ -358,16 +370,25 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
             for (int kk = 0; kk < 2; ++kk) {
                 const bf16x8_t pb = pack_acc(s[2 * kk], s[2 * kk + 1]);
                 const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+                // all eight transposed fragments of this k-step issued before the MFMAs that use them (one at a
+                // time, every MFMA waited out its own LDS read)
+                bf16x8_t fo[4], fq[4];
 #pragma unroll
                 for (int df = 0; df < 4; ++df) {
-                    dv[df] = mfma(frag_tr_perm(Oi, 16 * df, kk, lane), pb, dv[df]);
-                    dk[df] = mfma(frag_tr_perm(Qi, 16 * df, kk, lane), sb, dk[df]);
+                    fo[df] = frag_tr_perm(Oi, 16 * df, kk, lane);
+                    fq[df] = frag_tr_perm(Qi, 16 * df, kk, lane);
+                }
+#pragma unroll
+                for (int df = 0; df < 4; ++df) {
+                    dv[df] = mfma(fo[df], pb, dv[df]);
+                    dk[df] = mfma(fq[df], sb, dk[df]);
                 }
             }
         }
         if (more) {
             tq.store(smem[cur ^ 1][0], tid);
             tdo.store(smem[cur ^ 1][1], tid);
+            if (tid < 32) *reinterpret_cast<float4*>(&lsd[cur ^ 1][tid >> 4][4 * (tid & 15)]) = lrow;
         }
         __syncthreads();
     }
@@ -463,8 +484,11 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
                 const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+                bf16x8_t fk[4];                  // fragments issued before the MFMAs (as in attn_bwd_dkdv)
 #pragma unroll
-                for (int df = 0; df < 4; ++df) dq[df] = mfma(frag_tr_perm(Ki, 16 * df, kk, lane), sb, dq[df]);
+                for (int df = 0; df < 4; ++df) fk[df] = frag_tr_perm(Ki, 16 * df, kk, lane);
+#pragma unroll
+                for (int df = 0; df < 4; ++df) dq[df] = mfma(fk[df], sb, dq[df]);
             }
         }
         if (more) {
