@@ -113,7 +113,8 @@ def main():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--lr", type=float, default=0.1)
-    ap.add_argument("--fp8", action="store_true", help="forward GEMMs on the fp8 engine (BASELINE config 5)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="BASELINE config 5: ResNet 3x3 convs / GPT-2 forward linears on the fp8 MFMA kernels")
     ap.add_argument("--graph", default="auto", choices=["off", "on", "auto", "collectives"],
                     help="replay each step as one captured hipGraph (auto: single-GPU runs, not the side-stream ResNets)")
     ap.add_argument("--comm-bf16", action="store_true", help="DDP: all-reduce gradients in bf16 on the wire")
@@ -280,7 +281,7 @@ def main():
             "vs_baseline": None,
             "vs_stock_pytorch_rocm": (round(value / (STOCK_PYTORCH_1GPU * world), 4)
                                       if a.model == "resnet50" and B == 256 and not a.fp8 else None),
-            "dtype": "fp8(e4m3) 1x1-conv fwd GEMMs + bf16" if a.fp8 else "bf16",
+            "dtype": "fp8 3x3 convs (e4m3 fwd / e5m2 dgrad) + bf16" if a.fp8 else "bf16",
             "data": f"synthetic (device-resident random {in_chw[1]}x{in_chw[2]}x{in_chw[0]} images, random labels), "
                     "random-init weights",
             "final_loss": round(float(loss.detach()), 4),

@@ -32,7 +32,39 @@
 namespace {
 using namespace pg;
 
-template <int NB, int EPI, bool PRE>
+typedef __attribute__((ext_vector_type(8))) int c3v8i;
+typedef __attribute__((ext_vector_type(4))) int c3v4i;
+constexpr int C3_AMAX_PARTS = 1024;              // fp8.hip FP8_AMAX_PARTS
+
+// 16 floats -> 16 fp8 bytes (FMT 0: e4m3fn, saturating at 448; 1: e5m2, at 57344)
+template <int FMT>
+__device__ __forceinline__ uint4 c3_to_fp8(const float* v) {
+    constexpr float MX = FMT ? 57344.f : 448.f;
+    int w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const float c0 = fminf(fmaxf(v[4 * d], -MX), MX), c1 = fminf(fmaxf(v[4 * d + 1], -MX), MX);
+        const float c2 = fminf(fmaxf(v[4 * d + 2], -MX), MX), c3 = fminf(fmaxf(v[4 * d + 3], -MX), MX);
+        int x = 0;
+        if constexpr (FMT) {
+            x = __builtin_amdgcn_cvt_pk_bf8_f32(c0, c1, x, false);
+            x = __builtin_amdgcn_cvt_pk_bf8_f32(c2, c3, x, true);
+        } else {
+            x = __builtin_amdgcn_cvt_pk_fp8_f32(c0, c1, x, false);
+            x = __builtin_amdgcn_cvt_pk_fp8_f32(c2, c3, x, true);
+        }
+        w[d] = x;
+    }
+    return make_uint4((uint32_t)w[0], (uint32_t)w[1], (uint32_t)w[2], (uint32_t)w[3]);
+}
+
+// F8 = 0: bf16 operands (v_mfma_f32_16x16x32_bf16, 64-channel chunks).
+// F8 = 1 / 2: fp8 (the forward's activations in e4m3 / the data gradient's in e5m2; weights e4m3), 128-channel
+// chunks on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales): the bf16 input is
+// quantised with the tensor's delayed scale WHILE the halo is staged (no separate quantisation pass, no fp8
+// copy in HBM), so a halo pixel is the same 128 bytes and the per-tap work covers twice the channels at the
+// same LDS traffic and MFMA cycles.  The staged values' |max| feeds the next call's scale (f8_amax partials).
+template <int NB, int EPI, bool PRE, int F8 = 0>
 __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
     constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
     constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
@@ -64,6 +96,19 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         hb[f] = (gr - gr0 + 1) * a.W + px[f];
     }
 
+    [[maybe_unused]] uint32_t tmask[4];         // fp8 path: bit tap of f = tap (r, s) of pixel f inside the image
+    if constexpr (F8 != 0) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+                if (pv[f] && (unsigned)(py[f] + dr) < (unsigned)a.H && (unsigned)(px[f] + ds) < (unsigned)a.W) m |= 1u << tap;
+            }
+            tmask[f] = m;
+        }
+    }
     // the zero pixel sits after the largest halo (halo_max): taps outside the image read it
     const int zpx = a.halo_max;
     if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + zpx * 64 + tid * 8) = c3_zero8();
@@ -74,14 +119,19 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    const int nchunks = a.C >> 6;
+    const int nchunks = F8 ? a.C >> 7 : a.C >> 6;
     const long wrow = 9L * a.C;                   // elements per weight row n
     u16x8_t rb[BCH];
+    [[maybe_unused]] const uint8_t* wb8 =
+        reinterpret_cast<const uint8_t*>(a.w) + (long)(n0 + (tid >> 3)) * wrow + (tid & 7) * 16;
     auto load_b = [&](int c0, int tap) {
 #pragma unroll
         for (int i = 0; i < BCH; ++i) {
             const int li = tid + 256 * i, row = li >> 3, q = li & 7;
-            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tap * a.C + c0 + q * 8);
+            if constexpr (F8 != 0)   // rows tid / 8 + 32 i: one base, uniform offsets
+                rb[i] = *reinterpret_cast<const u16x8_t*>(wb8 + (long)(32 * i) * wrow + (long)tap * a.C + c0);
+            else
+                rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tap * a.C + c0 + q * 8);
         }
     };
     auto store_b = [&](int buf) {
@@ -93,11 +143,108 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         }
     };
 
+    [[maybe_unused]] float qs = 0.f, amx = 0.f;
+    if constexpr (F8 != 0) qs = a.f8_scale[0];
+
     for (int ck = 0; ck < nchunks; ++ck) {
-        const int c0 = ck << 6;
+        const int c0 = F8 ? ck << 7 : ck << 6;
         if (ck) __syncthreads();                 // the previous chunk's halo / weights are no longer read
-        // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
         const int nch = hpx * 8;
+        if constexpr (F8 != 0) {
+            // ---- stage the fp8 halo of this 128-channel chunk: 16 channels (32 bf16 bytes -> 16 fp8 bytes) per
+            // 16-byte chunk i & 7 of halo pixel i >> 3
+            constexpr int J = PRE ? 1 : 4;
+            PreCoef pc[PRE ? 2 : 1];
+            if constexpr (PRE) {
+                pre_coef(a, c0 + (tid & 7) * 16, pc[0]);
+                pre_coef(a, c0 + (tid & 7) * 16 + 8, pc[1]);
+            }
+            for (int i0 = 0; i0 < nch; i0 += 256 * J) {
+                u16x8_t v[J][2], tv[PRE ? J : 1][2];
+                bool okj[J];
+                int gpj[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int i = i0 + j * 256 + tid;
+                    const long gp = gp0 + (i >> 3);
+                    okj[j] = i < nch && gp >= 0 && gp < a.P;
+                    const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+                    gpj[j] = (int)gc;
+                    const bf16_t* src = a.x + gc * a.C + c0 + (i & 7) * 16;
+                    v[j][0] = *reinterpret_cast<const u16x8_t*>(src);
+                    v[j][1] = *reinterpret_cast<const u16x8_t*>(src + 8);
+                    if constexpr (PRE) {
+                        const bf16_t* ts = a.pre_t + gc * a.C + c0 + (i & 7) * 16;
+                        tv[j][0] = *reinterpret_cast<const u16x8_t*>(ts);
+                        tv[j][1] = *reinterpret_cast<const u16x8_t*>(ts + 8);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    if constexpr (PRE) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            v[j][h] = pre_apply(pc[h], v[j][h], tv[j][h]);
+                            if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
+                                *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 16 + 8 * h) =
+                                    v[j][h];
+                        }
+                    }
+                    float f[16];
+                    unpack8(v[j][0], f);
+                    unpack8(v[j][1], f + 8);
+                    float m = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        m = fmaxf(m, fabsf(f[e]));
+                        f[e] *= qs;
+                    }
+                    if (okj[j]) amx = fmaxf(amx, m);
+                    const uint4 q8 = c3_to_fp8<F8 - 1>(f);
+                    const int i = i0 + j * 256 + tid;
+                    const int off = i < nch ? halo_off(i >> 3, i & 7) : zpx * 64 + (i & 7) * 8;
+                    *reinterpret_cast<u16x8_t*>(halo + off) = mask16(__builtin_bit_cast(u16x8_t, q8), okj[j]);
+                }
+            }
+            load_b(c0, 0);
+            store_b(0);
+            __syncthreads();
+            const int g = lane >> 4;
+#pragma unroll 1
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dr = tap / 3 - 1, ds = tap - (tap / 3) * 3 - 1;
+                // branch-free tap body (tap 8 re-fetches its own weights into the idle buffer): with a conditional
+                // store the MFMAs were sunk below it, every fragment was live at once and the kernel spilled
+                load_b(c0, tap < 8 ? tap + 1 : 8);
+                const bf16_t* B = bbuf + (tap & 1) * NB * 64;
+                c3v8i bq[FN];
+#pragma unroll
+                for (int f = 0; f < FN; ++f) {
+                    const int row = f * 16 + (lane & 15);
+                    const c3v4i lo = *reinterpret_cast<const c3v4i*>(B + kimg_off(row, 2 * g));
+                    const c3v4i hi = *reinterpret_cast<const c3v4i*>(B + kimg_off(row, 2 * g + 1));
+                    bq[f] = c3v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+                // one pixel fragment at a time against all NB weight columns (the 4 x FN accumulators, the FN weight
+                // fragments and the 9-tap state leave no room for all four pixel fragments at once)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) {
+                    const bool v = (tmask[fm] >> tap) & 1;
+                    const int hp = v ? hb[fm] + dr * a.W + ds : zpx;
+                    const c3v4i lo = *reinterpret_cast<const c3v4i*>(halo + halo_off(hp, 2 * g));
+                    const c3v4i hi = *reinterpret_cast<const c3v4i*>(halo + halo_off(hp, 2 * g + 1));
+                    const c3v8i af = c3v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+                    for (int fn = 0; fn < FN; ++fn)
+                        acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                            bq[fn], af, acc[fm][fn], 0, F8 - 1, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                }
+                store_b((tap + 1) & 1);
+                __syncthreads();
+            }
+            continue;
+        }
+        // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
         constexpr int J = PRE ? (NB == 128 ? 2 : 4) : 8;   // PRE: two operands (and their coefficients) live
         PreCoef pc;
         if constexpr (PRE) pre_coef(a, c0 + (tid & 7) * 8, pc);   // this thread's 8 channels (i & 7 == tid & 7)
@@ -172,6 +319,18 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         }
     }
 
+    if constexpr (F8 != 0) {
+        amx = wave_max(amx);
+        if (lane == 0)
+            atomicMax(reinterpret_cast<unsigned int*>(a.f8_amax + (blockIdx.x & (C3_AMAX_PARTS - 1))), __float_as_uint(amx));
+        const float gs = a.f8_inv[0] * a.f8_winv[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][j][e] *= gs;
+    }
     c3_epilogue<NB, EPI>(a, acc, tile, p0, n0, wave, lane, pv);
 }
 
@@ -466,6 +625,18 @@ int c3_halo_max(int W) {
     return rows * W;
 }
 
+// the e4m3 bytes of W -> W' (same per-tensor scale): the fp8 data gradient's weight
+__global__ void __launch_bounds__(256) conv3x3_flip8_kernel(const uint8_t* __restrict__ w, uint8_t* __restrict__ wt,
+                                                            int K, int C) {
+    const long n = 9L * K * C;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int k = (int)(i % K);              // W'[c][r][s][k]
+        const long r0 = i / K;
+        const int tap = (int)(r0 % 9), c = (int)(r0 / 9);
+        wt[i] = w[((long)k * 9 + (8 - tap)) * C + c];
+    }
+}
+
 template <int NB>
 int c3_smem(int W) { return (c3_halo_max(W) + 1) * 128 + 2 * NB * 128; }
 
@@ -484,16 +655,16 @@ int c3r_launch(const C3Args& a, hipStream_t st) {
     PDNN_LAUNCH_RET;
 }
 
-template <int NB, int EPI, bool PRE>
+template <int NB, int EPI, bool PRE, int F8 = 0>
 int c3_launch(const C3Args& a, hipStream_t st) {
     static int attr_done = 0;
     const int sm = c3_smem<NB>(a.W);
     if (sm > attr_done) {
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  sm);
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI, PRE, F8>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, sm);
         attr_done = sm;
     }
-    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI, PRE, F8>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }
 
@@ -591,6 +762,11 @@ PDNN_API int pdnn_conv3x3_flip(const bf16_t* w, bf16_t* wt, int K, int C, hipStr
     PDNN_LAUNCH_RET;
 }
 
+PDNN_API int pdnn_conv3x3_flip8(const uint8_t* w, uint8_t* wt, int K, int C, hipStream_t st) {
+    hipLaunchKernelGGL(conv3x3_flip8_kernel, dim3(stream_grid(9L * K * C, 256)), dim3(256), 0, st, w, wt, K, C);
+    PDNN_LAUNCH_RET;
+}
+
 // y[P][N] = conv3x3(x, w) with pad 1, stride 1 (w: [N][3][3][C]); epilogue: stats (fwd BN statistics),
 // bn_x (BN-backward mask + sums), res (residual add), else plain.  nb: 0 = automatic, 64 / 128 forced.
 // pre_*: optional BN-backward operand prologue (x = gm; the conv's operand is dt = bn_bwd_apply(gm, pre_t),
@@ -635,6 +811,47 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     a.ntiles = N / nb;
     if (nb == 128) return pre ? c3_dispatch<128, true>(a, epi, st) : c3_dispatch<128, false>(a, epi, st);
     return pre ? c3_dispatch<64, true>(a, epi, st) : c3_dispatch<64, false>(a, epi, st);
+}
+
+// Whether the fp8 halo kernel takes this shape: the bf16 kernel's, with 128-channel chunks and 128-wide column tiles.
+PDNN_API int pdnn_conv3x3_fp8_supported(int Nimg, int H, int W, int C, int N) {
+    return pdnn_conv3x3_supported(Nimg, H, W, C, N) && C % 128 == 0 && N % 128 == 0 &&
+           c3_smem<128>(W) <= 80 * 1024;
+}
+
+// The fp8 halo conv (conv3x3_kernel F8 = 1 + e5m2): x bf16 [P][C] (quantised while staged with scale[0], the
+// staged |max| max-accumulated into amax[FP8_AMAX_PARTS]), wq e4m3 [N][3][3][C] (dequantised by winv[0]), y bf16;
+// epilogues plain / stats / fused BN backward (bn_x), pre_*: the BN-backward operand prologue, as pdnn_conv3x3.
+// e5m2: the operand in e5m2 (data gradients) instead of e4m3.
+PDNN_API int pdnn_conv3x3_fp8(const bf16_t* x, const uint8_t* wq, bf16_t* y, int Nimg, int H, int W, int C, int N,
+                              float* stats, const bf16_t* bn_x, const float* bn_mean, const float* bn_invstd,
+                              const float* bn_mscale, const float* bn_mshift, const bf16_t* pre_t,
+                              const float* pre_mean, const float* pre_invstd, const float* pre_gamma,
+                              const float* pre_dgamma, const float* pre_dbeta, bf16_t* pre_out, const float* scale,
+                              const float* inv, const float* winv, float* amax, int e5m2, hipStream_t st) {
+    if (!pdnn_conv3x3_fp8_supported(Nimg, H, W, C, N) || !scale || !inv || !winv || !amax)
+        return (int)hipErrorInvalidValue;
+    C3Args a{};
+    a.x = x; a.w = reinterpret_cast<const bf16_t*>(wq); a.y = y;
+    a.Nimg = Nimg; a.H = H; a.W = W; a.C = C; a.N = N; a.P = Nimg * H * W;
+    a.dW = make_fdiv_c3(W); a.dH = make_fdiv_c3(H);
+    a.tiles = (int)cdiv(a.P, C3_BM);
+    a.halo_max = c3_halo_max(W);
+    a.stats = stats;
+    if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
+        return (int)hipErrorInvalidValue;
+    a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
+    if (bn_x && !stats) return (int)hipErrorInvalidValue;
+    a.f8_scale = scale; a.f8_inv = inv; a.f8_winv = winv; a.f8_amax = amax;
+    a.ntiles = N / 128;
+    const bool pre = pre_t != nullptr;
+    if (e5m2) {
+        if (bn_x) return pre ? c3_launch<128, C3_BNB, true, 2>(a, st) : c3_launch<128, C3_BNB, false, 2>(a, st);
+        if (stats) return (int)hipErrorInvalidValue;
+        return pre ? c3_launch<128, C3_PLAIN, true, 2>(a, st) : c3_launch<128, C3_PLAIN, false, 2>(a, st);
+    }
+    if (pre || bn_x) return (int)hipErrorInvalidValue;
+    return stats ? c3_launch<128, C3_STATS, false, 1>(a, st) : c3_launch<128, C3_PLAIN, false, 1>(a, st);
 }
 
 // 1x1 / stride-1 conv on the A-stationary kernel: y[P][N] = x[P][K] . w[N][K]^T, K in {64, 128, 256},

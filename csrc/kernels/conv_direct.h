@@ -31,6 +31,11 @@ struct C3Args {
     const bf16_t* pre_t;
     const float *pre_mean, *pre_invstd, *pre_gamma, *pre_dgamma, *pre_dbeta;
     bf16_t* pre_out;
+    // fp8 halo kernel (conv3x3.hip F8 != 0): w is e4m3 bytes; the staged operand is quantised with f8_scale[0]
+    // (delayed scaling), its |max| goes to the FP8_AMAX_PARTS partials f8_amax, acc is dequantised by
+    // f8_inv[0] * f8_winv[0]
+    const float *f8_scale, *f8_inv, *f8_winv;
+    float* f8_amax;
 };
 
 // per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)

@@ -56,7 +56,7 @@ __global__ void fp8_scale_kernel(const float* amax, float* scale, float* inv, in
 // gemm_scale = inv (the inverse scale the tensor was just quantised with) * inv_w; then the next call's
 // scale is derived from the amax recorded by that quantisation, and the amax accumulator is reset.
 __global__ void __launch_bounds__(NT) fp8_scale_step_kernel(float* amax, float* scale, float* inv, const float* inv_w,
-                                                            float* gemm_scale, int margin) {
+                                                            float* gemm_scale, int margin, float fmax) {
     // amax holds FP8_AMAX_PARTS per-block partial maxima of the last quantisation (quant_fp8_kernel)
     float m = 0.f;
     for (int i = threadIdx.x; i < FP8_AMAX_PARTS; i += NT) {
@@ -70,9 +70,9 @@ __global__ void __launch_bounds__(NT) fp8_scale_step_kernel(float* amax, float* 
     if (threadIdx.x == 0) {
         float a = sm[0];
         for (int i = 1; i < NT / 64; ++i) a = fmaxf(a, sm[i]);
-        gemm_scale[0] = inv[0] * (inv_w ? inv_w[0] : 1.f);
+        if (gemm_scale) gemm_scale[0] = inv[0] * (inv_w ? inv_w[0] : 1.f);
         if (a > 0.f) {
-            const float s = ldexpf(FP8_MAX / a, -margin);
+            const float s = ldexpf(fmax / a, -margin);
             scale[0] = s;
             inv[0] = 1.f / s;
         }
@@ -243,7 +243,16 @@ PDNN_API int pdnn_fp8_scale(const float* amax, float* scale, float* inv, int mar
 
 PDNN_API int pdnn_fp8_scale_step(float* amax, float* scale, float* inv, const float* inv_w, float* gemm_scale,
                                  int margin, hipStream_t st) {
-    hipLaunchKernelGGL(fp8_scale_step_kernel, dim3(1), dim3(NT), 0, st, amax, scale, inv, inv_w, gemm_scale, margin);
+    hipLaunchKernelGGL(fp8_scale_step_kernel, dim3(1), dim3(NT), 0, st, amax, scale, inv, inv_w, gemm_scale, margin,
+                       FP8_MAX);
+    PDNN_LAUNCH_RET;
+}
+
+// After a kernel that quantised in-line (the fp8 halo conv): reduce and reset the amax partials and roll the
+// delayed scale forward (scale = fmax / amax * 2^-margin; e4m3 448, e5m2 57344).
+PDNN_API int pdnn_fp8_scale_roll(float* amax, float* scale, float* inv, int e5m2, int margin, hipStream_t st) {
+    hipLaunchKernelGGL(fp8_scale_step_kernel, dim3(1), dim3(NT), 0, st, amax, scale, inv, (const float*)nullptr,
+                       (float*)nullptr, margin, e5m2 ? 57344.f : FP8_MAX);
     PDNN_LAUNCH_RET;
 }
 

@@ -41,8 +41,11 @@ _SIGS = {
     "pdnn_gemm_stats_rows": [I],
     "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
+    "pdnn_conv3x3_fp8_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
+    "pdnn_conv3x3_flip8": [P, P, I, I, P],
+    "pdnn_conv3x3_fp8": [P, P, P, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P] * 4 + [I, P],
     "pdnn_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, P],
     "pdnn_conv3x3_wgrad_supported": [I, I, I, I, I],
     "pdnn_conv3x3_wgrad_ws": [I, I, I, I, I],
@@ -126,6 +129,7 @@ _SIGS = {
     "pdnn_amax_f32": [P, L, P, P],
     "pdnn_fp8_scale": [P, P, P, I, P],
     "pdnn_fp8_scale_step": [P, P, P, P, P, I, P],
+    "pdnn_fp8_scale_roll": [P, P, P, I, I, P],
     "pdnn_quant_fp8": [P, L, P, P, P, P],
     "pdnn_quant_fp8_current": [P, L, P, P, P, I, P],
     "pdnn_quant_fp8_f32": [P, L, P, P, P],

@@ -48,6 +48,71 @@ class Fp8Meta:
         return q, self.gemm_scale
 
 
+class Fp8Act:
+    """Delayed-scaling state of an operand that a kernel quantises in-line (the fp8 halo conv: ``K.conv3x3_fp8``):
+    the kernel reads ``scale``, records its staged |max| into the ``amax`` partials, and ``K.fp8_scale_roll``
+    rolls the scale forward after it.  e5m2 for gradients (range), e4m3 for activations (precision)."""
+
+    def __init__(self, device, e5m2: bool = False, margin: int = 0):
+        self.amax = torch.zeros(Fp8Meta.AMAX_PARTS, device=device, dtype=F32)
+        self.scale = torch.ones(1, device=device, dtype=F32)
+        self.inv = torch.ones(1, device=device, dtype=F32)
+        self.e5m2 = bool(e5m2)
+        self.margin = margin
+        self.primed = False
+
+
+def _wait_prefetch(p):
+    # made on the side stream by prefetch_fp8_weights: the compute stream waits once per prefetch (shared token)
+    tok = p.__dict__.get("_pdnn_fp8_wait")
+    if tok is not None:
+        if not tok[1]:
+            torch.cuda.current_stream(p.device).wait_event(tok[0])
+            tok[1] = True
+        p._pdnn_fp8_wait = None
+
+
+def prefetch_fp8_weights(ps, side):
+    """Make the e4m3 weights (and tap-flipped copies) of ``ps`` whose cache is stale on the ``side`` stream, at
+    the start of a forward: ~17 us of small quantisation / flip kernels per 3x3 conv leave the compute stream
+    (the first fp8 conv waits on one event).  Skipped for parameters still arriving (PS workers: await_param)."""
+    todo = [p for p in ps if "_pdnn_await" not in p.__dict__
+            and (getattr(p, "_pdnn_fp8_flip", None) or (None,))[0] != _weight_version(p)]
+    if not todo:
+        return
+    dev = todo[0].device
+    main = torch.cuda.current_stream(dev)
+    for p in todo:
+        weight_bf16(p, krsc=True)          # the shadows current on the compute stream first
+    K.stream_wait(side, main)
+    with torch.cuda.stream(side):
+        for p in todo:
+            weight_fp8_flip(p)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    tok = [ev, False]
+    for p in todo:
+        p._pdnn_fp8_wait = tok
+        p._pdnn_fp8[1].record_stream(main)
+        p._pdnn_fp8[2].record_stream(main)
+        p._pdnn_fp8_flip[1].record_stream(main)
+
+
+def weight_fp8_flip(p: torch.Tensor):
+    """(e4m3 tap-flipped transposed 3x3 weight [C][3][3][K], inverse scale) for the fp8 data gradient, made from
+    weight_fp8's bytes (same scale) and cached per parameter version alongside it."""
+    wq, inv = weight_fp8(p, krsc=True)
+    _wait_prefetch(p)
+    st = getattr(p, "_pdnn_fp8_flip", None)
+    ver = _weight_version(p)
+    if st is not None and st[0] == ver:
+        return st[1], inv
+    Kc, C = p.shape[0], p.shape[1]
+    wt = K.conv3x3_flip8(wq, Kc, C)
+    p._pdnn_fp8_flip = (ver, wt)
+    return wt, inv
+
+
 def _weight_version(p):
     # flat-arena parameters are updated in place by the fused optimizer (no autograd version bump):
     # key on the arena's update generation as well
@@ -61,6 +126,7 @@ def weight_fp8(p: torch.Tensor, krsc: bool = False):
     that reduces them itself (no fill, no single-thread scale kernel)."""
     from ..optim.flat import await_param
     await_param(p)                     # before the cache check: a PS bucket landing bumps the generation
+    _wait_prefetch(p)
     st = getattr(p, "_pdnn_fp8", None)
     ver = _weight_version(p)
     if st is not None and st[0] == ver:

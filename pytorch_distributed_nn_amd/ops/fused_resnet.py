@@ -186,21 +186,29 @@ def _join_at_backward_end(side):
     torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
-def _conv1x1_bn_fp8(x, w_param, meta, training, bn_params, bufs, mom, eps):
-    """1x1 stride-1 conv as an fp8 GEMM (x and W in e4m3, per-tensor delayed scaling, fused BN stats)."""
+def _conv3x3_bn_fp8(a1, w_param, act, training, bn_params, bufs, mom, eps):
+    """conv2 (3x3, stride 1) forward on the fp8 halo kernel: a1 quantised to e4m3 in the kernel's halo staging
+    (delayed scaling, no separate quantisation pass), e4m3 weight (current scaling, once per weight version),
+    fused BN statistics."""
     from .fp8 import weight_fp8
-    N, H, W, C = x.shape
-    M = N * H * W
     wq, winv = weight_fp8(w_param, krsc=True)
-    xq, gs = meta.quantize(x.view(M, C), winv)
-    Ko = wq.shape[0]
-    slab = torch.empty(2 * K.stats_rows(M), Ko, device=x.device, dtype=F32) if training else None
-    t = K.gemm_fp8(xq, wq, gs, stats=slab).view(N, H, W, Ko)
+    t, slab = K.conv3x3_fp8(a1, wq, winv, act, want_stats=training)
+    M = t.numel() // t.shape[-1]
     if training:
         mean, inv, sc, sh = _bn_train(slab, M, bn_params, bufs, mom, eps)
     else:
         mean, inv, sc, sh = _bn_eval(bn_params, bufs, eps)
     return t, mean, inv, sc, sh
+
+
+class Fp8Conv2:
+    """fp8 state of one Bottleneck's 3x3 conv (BASELINE.json config 5): the forward operand a1 in e4m3, the data
+    gradient's operand dt2 in e5m2, each with its own delayed scale."""
+
+    def __init__(self, device):
+        from .fp8 import Fp8Act
+        self.fwd = Fp8Act(device)
+        self.bwd = Fp8Act(device, e5m2=True)
 
 
 def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
@@ -328,15 +336,17 @@ class BottleneckFn(torch.autograd.Function):
             x.record_stream(side)
             for t in side_down:
                 t.record_stream(main)
-        if fp8_meta is not None:
-            t1, m1, i1, s1, h1 = _conv1x1_bn_fp8(x, w1, fp8_meta, training, (g1, b1), bufs[0:2], mom, eps)
-        else:
-            t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
+        t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
         # a1 = relu(bn1(t1)) is materialised once: the 3x3 conv gathers every element 9 times, so applying
         # the BN affine in its operand loader would cost 9x the VALU work (fwd and wgrad)
         C1 = t1.shape[-1]
         a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)
-        t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
+        fp8 = fp8_meta if (fp8_meta is not None and stride == 1
+                           and K.conv3x3_fp8_ok(*a1.shape, w2.shape[0])) else None
+        if fp8 is not None:
+            t2, m2, i2, s2, h2 = _conv3x3_bn_fp8(a1, w2, fp8.fwd, training, (g2, b2), bufs[2:4], mom, eps)
+        else:
+            t2, m2, i2, s2, h2 = _conv_bn(a1, k2, stride, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
         # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
         # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
         # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs
@@ -368,6 +378,7 @@ class BottleneckFn(torch.autograd.Function):
                               g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2)
         ctx.conf = (stride, training, down)
         ctx.params = params
+        ctx.fp8 = fp8
         return out
 
     @staticmethod
@@ -413,8 +424,14 @@ class BottleneckFn(torch.autograd.Function):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad
             gm2, dg2, db2, (rg2, rb2) = _dgrad_bn_gm(dt3, k3, t2, 1, 0, m2, i2, s2, h2, sink, P[4], P[5], wprep=w3p)
             dt2 = torch.empty_like(t2)
-            gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=(t2, m2, i2, g2, dg2, db2, dt2),
-                                      wprep=w2p)
+            pre2 = (t2, m2, i2, g2, dg2, db2, dt2)
+            if ctx.fp8 is not None:
+                # fp8 data gradient: dt2 (applied in the halo staging) quantised to e5m2 there, tap-flipped e4m3 weight
+                from .fp8 import weight_fp8_flip
+                wt8, winv = weight_fp8_flip(P[3])
+                gm1, slab1 = K.conv3x3_fp8(gm2, wt8, winv, ctx.fp8.bwd, bn=bn1, pre=pre2)
+            else:
+                gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=pre2, wprep=w2p)
             del gm2
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
         else:

@@ -962,6 +962,50 @@ def fp8_scale_step(amax, scale, inv, inv_w, gemm_scale, margin=0):
     call("pdnn_fp8_scale_step", ptr(amax), ptr(scale), ptr(inv), ptr(inv_w), ptr(gemm_scale), int(margin), stream())
 
 
+def fp8_scale_roll(amax, scale, inv, e5m2=False, margin=0):
+    """After an in-line quantisation (conv3x3_fp8): reduce + reset the amax partials, roll the delayed scale."""
+    call("pdnn_fp8_scale_roll", ptr(amax), ptr(scale), ptr(inv), int(bool(e5m2)), int(margin), stream())
+
+
+def conv3x3_fp8_ok(N, H, W, C, Ko):
+    """Whether the fp8 halo kernel takes this 3x3 / stride-1 / pad-1 conv (C, Ko multiples of 128)."""
+    return bool(_C3["mode"]) and lib().pdnn_conv3x3_fp8_supported(N, H, W, C, Ko) == 1
+
+
+def conv3x3_flip8(wq, K, C):
+    """e4m3 [K][3][3][C] -> [C][3][3][K] tap-flipped (same scale): the fp8 data gradient's weight."""
+    wt = torch.empty(C, 3, 3, K, device=wq.device, dtype=U8)
+    call("pdnn_conv3x3_flip8", ptr(wq), ptr(wt), K, C, stream())
+    return wt
+
+
+def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None):
+    """y = conv3x3(x, w) on the fp8 halo kernel: x bf16 NHWC (quantised in the kernel's halo staging with the
+    delayed scale of ``act`` -- an ops.fp8.Fp8Act, e4m3 or e5m2), wq e4m3 [N][3][3][C] with inverse scale ``winv``
+    (device scalar).  Epilogues / ``bn`` / ``pre`` as conv3x3 (bn and pre only with e5m2: data gradients).
+    The first call of an ``act`` runs the kernel once to measure the operand's amax."""
+    _bf16_c(x, "conv3x3_fp8.x")
+    Nimg, H, W, C = x.shape
+    Ko = wq.shape[0]
+    _chk(wq.dtype == U8 and wq.is_contiguous() and wq.numel() == Ko * 9 * C, "conv3x3_fp8: wq e4m3 [N][3][3][C]")
+    y = torch.empty(Nimg, H, W, Ko, device=x.device, dtype=BF16)
+    slab = None
+    t = mean = inv = msc = msh = None
+    if want_stats or bn is not None:
+        slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
+    if bn is not None:
+        t, mean, inv, msc, msh = bn
+    args = (ptr(x), ptr(wq), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh),
+            *_pre_args(pre, x), ptr(act.scale), ptr(act.inv), ptr(winv), ptr(act.amax), int(act.e5m2), stream())
+    if not act.primed:
+        call("pdnn_conv3x3_fp8", *args)
+        fp8_scale_roll(act.amax, act.scale, act.inv, act.e5m2, act.margin)
+        act.primed = True
+    call("pdnn_conv3x3_fp8", *args)
+    fp8_scale_roll(act.amax, act.scale, act.inv, act.e5m2, act.margin)
+    return y, slab
+
+
 _FP8_PARTS = {}
 
 

@@ -175,3 +175,90 @@ def test_bottleneck_fp8_forward_and_resnet_trains():
     # memorising 16 images at batch-16 BatchNorm oscillates (bf16 and fp8 alike: e.g. 7.1 -> 2.2 -> 5.3 -> 2.3,
     # dev/probes/fp8_train_probe.py, gpurun_out/r4_25): the run must reach well below its start, not end there
     assert torch.isfinite(loss) and min(losses) < 0.6 * losses[0], losses
+
+
+# ------------------------------------------------ fp8 halo 3x3 conv (conv3x3.hip F8 = 1 / 2, in-line quantisation)
+E5M2 = torch.float8_e5m2
+C3F8 = [(2, 14, 14, 256, 256), (3, 28, 28, 128, 128), (2, 14, 14, 128, 256), (3, 13, 17, 256, 128),
+        (1, 16, 16, 512, 512)]
+
+
+def _q(x, scale, dt, mx):
+    """torch reference of the kernel's quantise -> dequantise (RNE, saturating)."""
+    return (x.float() * scale).clamp(-mx, mx).to(dt).float() / scale
+
+
+def _conv_ref(x, w):
+    import torch.nn.functional as F
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, 1).permute(0, 2, 3, 1)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("shape", C3F8)
+def test_conv3x3_fp8_fwd_stats(K, shape):
+    """Forward (e4m3 activations quantised in the halo staging, e4m3 weights): equal to the fp32 conv of the
+    same quantised operands, BN statistics consistent with the output, the delayed scale rolled to 448/amax."""
+    from pytorch_distributed_nn_amd.ops.fp8 import Fp8Act
+    N, H, W, C, Ko = shape
+    assert K.conv3x3_fp8_ok(N, H, W, C, Ko)
+    x = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(torch.bfloat16)
+    winv = torch.empty(1, device="cuda")
+    wq = K.quant_fp8_current(w.reshape(Ko, -1).contiguous(), winv)
+    act = Fp8Act(x.device)
+    y, slab = K.conv3x3_fp8(x, wq, winv, act, want_stats=True)
+    sx = 448.0 / x.float().abs().max().item()
+    sw = 1.0 / winv.item()
+    ref = _conv_ref(_q(x, sx, E4M3, 448), _q(w, sw, E4M3, 448))
+    assert _rel(y, ref) < 1e-2
+    assert _rel(y, _conv_ref(x, w)) < 8e-2            # and within fp8 precision of the bf16 conv
+    yf = y.float().reshape(-1, Ko)
+    s = slab.view(-1, 2, Ko).sum(0)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    assert abs(act.scale.item() - sx) < 1e-4 * sx and act.amax.abs().max().item() == 0.0
+    # a second call on a 2x larger input: quantised with the OLD scale (saturating), the next one rolled
+    y2, _ = K.conv3x3_fp8(x * 2, wq, winv, act)
+    assert abs(act.scale.item() - sx / 2) < 1e-4 * sx
+    assert _rel(y2, _conv_ref(_q(x * 2, sx, E4M3, 448), _q(w, sw, E4M3, 448))) < 1e-2
+
+
+@pytest.mark.parametrize("shape", C3F8[:3])
+def test_conv3x3_fp8_dgrad_e5m2_pre_bn(K, shape):
+    """Data gradient on the fp8 kernel: the BN-backward apply of the layer above in the operand loads (dt written
+    bitwise like the bf16 kernel's), the operand quantised to e5m2, the tap-flipped e4m3 weight, the fused BN
+    backward epilogue: matches the bf16 halo kernel within fp8 precision, and the quantised-operand reference."""
+    from pytorch_distributed_nn_amd.ops.fp8 import Fp8Act
+    N, H, W, C, Ko = shape          # dy has Ko channels, dx has C
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(torch.bfloat16)
+    gm = torch.randn(N, H, W, Ko, device="cuda").to(torch.bfloat16)
+    t = torch.randn(N, H, W, Ko, device="cuda").to(torch.bfloat16)
+    mean, inv = torch.randn(Ko, device="cuda") * 0.1, torch.rand(Ko, device="cuda") + 0.5
+    g = torch.rand(Ko, device="cuda") + 0.5
+    dg, db = torch.randn(Ko, device="cuda") * 50, torch.randn(Ko, device="cuda") * 50
+    dt_ref = K.bn_bwd_apply(gm.view(-1, Ko), t.view(-1, Ko), mean, inv, g, dg, db, mode=0)[0].view_as(gm)
+    t1 = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    m1, i1 = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    s1, h1 = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    winv = torch.empty(1, device="cuda")
+    wq = K.quant_fp8_current(w.reshape(Ko, -1).contiguous(), winv)
+    wt = K.conv3x3_flip8(wq, Ko, C)
+    assert torch.equal(wt.view(torch.float8_e4m3fn).float(),
+                       wq.view(torch.float8_e4m3fn).float().view(Ko, 3, 3, C).flip(1, 2).permute(3, 1, 2, 0).contiguous())
+    act = Fp8Act(gm.device, e5m2=True)
+    dt_out = torch.empty_like(gm)
+    g8, sl8 = K.conv3x3_fp8(gm, wt, winv, act, bn=(t1, m1, i1, s1, h1), pre=(t, mean, inv, g, dg, db, dt_out))
+    assert torch.equal(dt_out, dt_ref)
+    g16, sl16 = K.conv_dgrad(dt_ref, w, (N, H, W, C), 1, 1, bn=(t1, m1, i1, s1, h1))
+    assert _rel(g8, g16) < 0.15
+    assert _rel(sl8.view(-1, 2, C).sum(0), sl16.view(-1, 2, C).sum(0)) < 0.1
+    # plain epilogue against the quantised-operand reference
+    sx = act.scale.item()       # rolled to 57344 / amax(dt): the scale of the next call
+    act2 = Fp8Act(gm.device, e5m2=True)
+    y, _ = K.conv3x3_fp8(dt_ref, wt, winv, act2)
+    wflip = w.float().flip(1, 2).permute(3, 1, 2, 0).contiguous()
+    ref = _conv_ref(_q(dt_ref, sx, E5M2, 57344), _q(wflip, 1.0 / winv.item(), E4M3, 448))
+    assert _rel(y, ref) < 1e-2
