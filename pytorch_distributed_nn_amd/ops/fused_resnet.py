@@ -282,10 +282,12 @@ def _prep_dgrad_weights(x, specs):
         if idx in _FWD_FORKED:
             _FWD_FORKED[idx] = SHADOW_EPOCH[0]
     with torch.cuda.stream(side):
-        ws = [K.dgrad_weight(*sp) for sp in specs]
+        ws = [K.dgrad_weight(*sp) if sp is not None else None for sp in specs]
         ev = torch.cuda.Event()
         ev.record(side)
     for sp, w in zip(specs, ws):
+        if sp is None:
+            continue
         sp[1].record_stream(side)
         if w is not None:
             w.record_stream(main)
@@ -370,8 +372,10 @@ class BottleneckFn(torch.autograd.Function):
         out = out.view(t3.shape)
         ctx.wprep = None
         if training:
+            # (an fp8 conv2 takes its flipped e4m3 weight from ops.fp8.weight_fp8_flip instead)
             ctx.wprep = _prep_dgrad_weights(x, [(tuple(t3.shape), k3, tuple(t2.shape), 1, 0),
-                                                (tuple(t2.shape), k2, tuple(t1.shape), stride, 1),
+                                                (tuple(t2.shape), k2, tuple(t1.shape), stride, 1) if fp8 is None
+                                                else None,
                                                 (tuple(t1.shape), k1, tuple(x.shape), 1, 0)])
         # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
         ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
