@@ -35,6 +35,12 @@ using namespace pg;
 typedef __attribute__((ext_vector_type(8))) int c3v8i;
 typedef __attribute__((ext_vector_type(4))) int c3v4i;
 constexpr int C3_AMAX_PARTS = 1024;              // fp8.hip FP8_AMAX_PARTS
+#ifndef C3_PRE_J
+#define C3_PRE_J 3
+#endif
+#ifndef C3_F8_PRE_J
+#define C3_F8_PRE_J 2
+#endif
 
 // 16 floats -> 16 fp8 bytes (FMT 0: e4m3fn, saturating at 448; 1: e5m2, at 57344)
 template <int FMT>
@@ -153,11 +159,12 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         if constexpr (F8 != 0) {
             // ---- stage the fp8 halo of this 128-channel chunk: 16 channels (32 bf16 bytes -> 16 fp8 bytes) per
             // 16-byte chunk i & 7 of halo pixel i >> 3
-            constexpr int J = PRE ? 1 : 4;
-            PreCoef pc[PRE ? 2 : 1];
+            // PRE: the chunk's BN-backward coefficients in LDS (weight buffer 1: idle until tap 0's store)
+            constexpr int J = PRE ? C3_F8_PRE_J : 4;
+            [[maybe_unused]] float* coef = reinterpret_cast<float*>(bbuf + NB * 64);
             if constexpr (PRE) {
-                pre_coef(a, c0 + (tid & 7) * 16, pc[0]);
-                pre_coef(a, c0 + (tid & 7) * 16 + 8, pc[1]);
+                pre_coef_lds<128>(a, c0, coef, tid);
+                __syncthreads();
             }
             for (int i0 = 0; i0 < nch; i0 += 256 * J) {
                 u16x8_t v[J][2], tv[PRE ? J : 1][2];
@@ -184,7 +191,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
                     if constexpr (PRE) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
-                            v[j][h] = pre_apply(pc[h], v[j][h], tv[j][h]);
+                            v[j][h] = pre_apply_lds<128>(coef, (tid & 7) * 16 + 8 * h, v[j][h], tv[j][h]);
                             if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
                                 *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 16 + 8 * h) =
                                     v[j][h];
@@ -245,9 +252,14 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
             continue;
         }
         // ---- stage the halo of this 64-channel chunk: contiguous pixels gp0 .. gp0 + hpx - 1
-        constexpr int J = PRE ? (NB == 128 ? 2 : 4) : 8;   // PRE: two operands (and their coefficients) live
-        PreCoef pc;
-        if constexpr (PRE) pre_coef(a, c0 + (tid & 7) * 8, pc);   // this thread's 8 channels (i & 7 == tid & 7)
+        // PRE: two operands live per load; the chunk's BN-backward coefficients in LDS (weight buffer 1, idle
+        // until tap 0's store), not 24 VGPRs, so more loads stay in flight
+        constexpr int J = PRE ? (NB == 128 ? C3_PRE_J : 4) : 8;
+        [[maybe_unused]] float* coef = reinterpret_cast<float*>(bbuf + NB * 64);
+        if constexpr (PRE) {
+            pre_coef_lds<64>(a, c0, coef, tid);
+            __syncthreads();
+        }
         for (int i0 = 0; i0 < nch; i0 += 256 * J) {
             u16x8_t v[J], tv[PRE ? J : 1];
             bool okj[J];
@@ -267,7 +279,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
 #pragma unroll
             for (int j = 0; j < J; ++j) {
                 if constexpr (PRE) {
-                    v[j] = pre_apply(pc, v[j], tv[j]);
+                    v[j] = pre_apply_lds<64>(coef, (tid & 7) * 8, v[j], tv[j]);
                     // own pixels (each written by exactly one block: column tile 0 of its pixel tile)
                     if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
                         *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 8) = v[j];

@@ -62,6 +62,35 @@ __device__ __forceinline__ u16x8_t pre_apply(const PreCoef& pc, const u16x8_t& g
     return pack8(o);
 }
 
+// The same apply with the coefficients of the chunk's CH channels in LDS (coef: [3][CH] = k, A, B), c = channel
+// index in the chunk: keeps 24 VGPRs per 8 channels free for more operand loads in flight (halo staging)
+template <int CH>
+__device__ __forceinline__ void pre_coef_lds(const C3Args& a, int c0, float* coef, int tid) {
+    const float invL = (float)(1.0 / (double)a.P);
+    for (int c = tid; c < CH; c += 256) {
+        const float is = a.pre_invstd[c0 + c], k = (a.pre_gamma ? a.pre_gamma[c0 + c] : 1.f) * is;
+        const float dg = a.pre_dgamma[c0 + c] * invL, db = a.pre_dbeta[c0 + c] * invL;
+        coef[c] = k;
+        coef[CH + c] = -k * is * dg;
+        coef[2 * CH + c] = k * (a.pre_mean[c0 + c] * is * dg - db);
+    }
+}
+template <int CH>
+__device__ __forceinline__ u16x8_t pre_apply_lds(const float* coef, int c, const u16x8_t& gv, const u16x8_t& tv) {
+    float gm[8], t[8], o[8], k[8], A[8], B[8];
+    unpack8(gv, gm);
+    unpack8(tv, t);
+    *reinterpret_cast<float4*>(k) = *reinterpret_cast<const float4*>(coef + c);
+    *reinterpret_cast<float4*>(k + 4) = *reinterpret_cast<const float4*>(coef + c + 4);
+    *reinterpret_cast<float4*>(A) = *reinterpret_cast<const float4*>(coef + CH + c);
+    *reinterpret_cast<float4*>(A + 4) = *reinterpret_cast<const float4*>(coef + CH + c + 4);
+    *reinterpret_cast<float4*>(B) = *reinterpret_cast<const float4*>(coef + 2 * CH + c);
+    *reinterpret_cast<float4*>(B + 4) = *reinterpret_cast<const float4*>(coef + 2 * CH + c + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(k[j], gm[j], fmaf(t[j], A[j], B[j]));
+    return pack8(o);
+}
+
 // v if ok else 0, as four 32-bit ANDs (a u16x8 AND with a 16-bit mask vector lowers to per-half sdwa/perm ops)
 __device__ __forceinline__ u16x8_t mask16(const u16x8_t& v, bool ok) {
     const uint32_t m = ok ? 0xFFFFFFFFu : 0u;
