@@ -579,6 +579,30 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
 }
 
 // out[m][n] (+)= sum_z slab[z][m][n]  (fp32, ld = ldc, slab stride sz).  float4 per thread.
+// s += slab rows z, z + ST, ... (< splits) for the < 8 rows left after an 8-wide loop: 4 / 2 / 1 loads at a time
+template <int ST>
+__device__ __forceinline__ void pp_sum_tail(const float* __restrict__ slab, long sz, long soff, int z, int splits,
+                                            float4& s) {
+    if (z + 3 * ST < splits) {
+        float4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const float4*>(slab + (z + ST * j) * sz + soff);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
+        z += 4 * ST;
+    }
+    if (z + ST < splits) {
+        const float4 v0 = *reinterpret_cast<const float4*>(slab + z * sz + soff);
+        const float4 v1 = *reinterpret_cast<const float4*>(slab + (z + ST) * sz + soff);
+        s.x += v0.x + v1.x; s.y += v0.y + v1.y; s.z += v0.z + v1.z; s.w += v0.w + v1.w;
+        z += 2 * ST;
+    }
+    if (z < splits) {
+        const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + soff);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+}
+
 __global__ void __launch_bounds__(256) pp_slab_reduce_kernel(const float* __restrict__ slab, long sz, int splits,
                                                              float* __restrict__ out, int M, int N, long ldc,
                                                              int accumulate) {
@@ -596,10 +620,8 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_kernel(const float* __rest
 #pragma unroll
             for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
         }
-        for (; z < splits; ++z) {
-            const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + soff);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-        }
+        // the remaining < 8 splits as 4 / 2 / 1 loads issued together (a 1-load loop serialised their latencies)
+        pp_sum_tail<1>(slab, sz, soff, z, splits, s);
         *reinterpret_cast<float4*>(out + off) = s;
     }
 }
@@ -629,10 +651,7 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_wide_kernel(const float* _
 #pragma unroll
             for (int j = 0; j < 8; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
         }
-        for (; z < splits; z += 8) {
-            const float4 v = *reinterpret_cast<const float4*>(slab + z * sz + soff);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-        }
+        pp_sum_tail<8>(slab, sz, soff, z, splits, s);
     }
     red[zg][o] = s;
     __syncthreads();
