@@ -212,6 +212,215 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
             }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// fp8 variant (BASELINE config 5): the same block structure, the operands quantised while they are staged (dy with
+// the data gradient's e5m2 scale, x with the forward's e4m3 scale: both were just rolled to the exact |max| of these
+// very tensors by the fp8 halo conv that consumed them) and reduced 128 pixels per v_mfma_scale_f32_16x16x128_f8f6f4.
+// Both operands reach MFMA through ds_read_b64_tr_b8 (dev/probes/tr8_probe.hip: lane i of a 16-lane group addresses
+// row i / 2, bytes 8 (i & 1) .. +7, and receives column i of the 8 rows): four reads give a lane its 32 pixels of one
+// channel.  Images: dy [256 px][64 ko] bytes with the 16-byte chunks XOR-swizzled by w8_swz (the 16 pixel rows
+// a 32-lane half reads fall on 16 distinct 4-bank groups); halo pixels of 64 channel bytes + 16 skew (W8_PB).
+constexpr int W8_PB = 80;
+
+__device__ __forceinline__ int w8_swz(int r) { return ((r >> 2) & 1) | (((r >> 5) & 1) << 1); }
+__device__ __forceinline__ int w8_doff(int r, int c16) { return r * 64 + ((c16 ^ w8_swz(r)) << 4); }
+
+// 8 floats -> 8 fp8 bytes (FMT 0: e4m3fn / 448, 1: e5m2 / 57344), saturating
+template <int FMT>
+__device__ __forceinline__ uint2 w8_cvt(const u16x8_t& v, float s) {
+    constexpr float MX = FMT ? 57344.f : 448.f;
+    float f[8];
+    unpack8(v, f);
+    int w[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const float c0 = fminf(fmaxf(f[4 * d] * s, -MX), MX), c1 = fminf(fmaxf(f[4 * d + 1] * s, -MX), MX);
+        const float c2 = fminf(fmaxf(f[4 * d + 2] * s, -MX), MX), c3 = fminf(fmaxf(f[4 * d + 3] * s, -MX), MX);
+        int x = 0;
+        if constexpr (FMT) {
+            x = __builtin_amdgcn_cvt_pk_bf8_f32(c0, c1, x, false);
+            x = __builtin_amdgcn_cvt_pk_bf8_f32(c2, c3, x, true);
+        } else {
+            x = __builtin_amdgcn_cvt_pk_fp8_f32(c0, c1, x, false);
+            x = __builtin_amdgcn_cvt_pk_fp8_f32(c2, c3, x, true);
+        }
+        w[d] = x;
+    }
+    return make_uint2((uint32_t)w[0], (uint32_t)w[1]);
+}
+
+typedef __attribute__((ext_vector_type(2))) int w8v2i;
+typedef __attribute__((ext_vector_type(8))) int w8v8i;
+typedef __attribute__((address_space(3))) w8v2i lds_w8v2i;
+
+struct W8Scale {
+    const float *sx, *sdy;     // quantisation scales of x (e4m3) and dy (e5m2)
+    const float *ix, *idy;     // their inverses (the partials are dequantised by ix * idy)
+};
+
+template <int WT>
+__global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad8_kernel(W3Args a, W8Scale q) {
+    constexpr int PITCH = WT + 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* const dimg = smem;                                      // [256 px][64 ko] e5m2, w8_doff
+    char* const halo = smem + W3_BM * 64;                         // [hrows][PITCH] pixels of W8_PB bytes
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pair = blockIdx.x / a.G, part = blockIdx.x - pair * a.G;
+    const int ko0 = (pair / a.cch) * 64, c0 = (pair % a.cch) * 64;
+    const int t0 = (int)((long)part * a.tiles / a.G), t1 = (int)((long)(part + 1) * a.tiles / a.G);
+    const int hbytes = a.hrows * PITCH * W8_PB;
+    const float sx = q.sx[0], sdy = q.sdy[0];
+
+    const int fn = wave & 3, fmb = (wave >> 2) * 2;
+    f32x4_t acc[2][9];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int DCH = W3_BM * 8 / W3_NT;
+    constexpr int HCH = W3_HMAX * 8 / W3_NT;
+    u16x8_t rd[DCH], rh[HCH];
+    int nch = 0;
+    uint32_t okm = 0;
+    int s_gstart = 0, s_istart = 0;
+
+    auto geo = [&](int t, int& p0, int& plast, int& gstart, int& istart) {
+        p0 = t * W3_BM;
+        plast = min(a.P, p0 + W3_BM) - 1;
+        gstart = (int)fdiv((uint32_t)p0, a.dW) - 1;
+        istart = gstart < 0 ? -1 : (int)fdiv((uint32_t)gstart, a.dH);
+    };
+    auto load_regs = [&](int t) {
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        s_gstart = gstart;
+        s_istart = istart;
+#pragma unroll
+        for (int j = 0; j < DCH; ++j) {
+            const int i = tid + j * W3_NT, row = i >> 3;
+            const int p = p0 + row;
+            const bool ok = p < a.P;
+            rd[j] = *reinterpret_cast<const u16x8_t*>(a.dy + (long)(ok ? p : plast) * a.Ko + ko0 + (i & 7) * 8);
+            okm = ok ? (okm | (1u << j)) : (okm & ~(1u << j));
+        }
+        const int gr1 = (int)fdiv((uint32_t)plast, a.dW);
+        nch = (gr1 + 2 - gstart) * WT * 8;
+        const long gp0 = (long)gstart * WT;
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            const long gp = gp0 + (i >> 3);
+            const bool ok = i < nch && gp >= 0 && gp < a.P;
+            const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+            rh[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+            okm = ok ? (okm | (16u << j)) : (okm & ~(16u << j));
+        }
+    };
+    auto zero_halo = [&]() {
+        for (int o = tid * 16; o < hbytes; o += W3_NT * 16) *reinterpret_cast<u16x8_t*>(halo + o) = c3_zero8();
+    };
+    auto store_lds = [&]() {
+#pragma unroll
+        for (int j = 0; j < DCH; ++j) {
+            const int i = tid + j * W3_NT, row = i >> 3, qq = i & 7;
+            const uint2 v = w8_cvt<1>(rd[j], sdy);
+            const uint32_t m = ((okm >> j) & 1) ? 0xFFFFFFFFu : 0u;
+            *reinterpret_cast<uint2*>(dimg + w8_doff(row, qq >> 1) + 8 * (qq & 1)) = make_uint2(v.x & m, v.y & m);
+        }
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            if (((okm >> (4 + j)) & 1) != 0) {
+                const int gp = s_gstart * WT + (i >> 3);
+                const int gr = (int)fdiv((uint32_t)gp, a.dW);
+                const int xx = gp - gr * WT;
+                const int img = (int)fdiv((uint32_t)gr, a.dH);
+                const int hrow = gr - s_gstart + 2 * (img - s_istart) + 1;
+                *reinterpret_cast<uint2*>(halo + (hrow * PITCH + xx + 1) * W8_PB + (i & 7) * 8) = w8_cvt<0>(rh[j], sx);
+            }
+        }
+    };
+
+    const int g = lane >> 4, li = lane & 15, lr = li >> 1, lh = 8 * (li & 1);
+
+    if (t0 < t1) {
+        load_regs(t0);
+        zero_halo();
+    }
+    __syncthreads();
+    if (t0 < t1) store_lds();
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+        const bool more = t + 1 < t1;
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        if (more) load_regs(t + 1);
+#pragma unroll 1
+        for (int ks = 0; ks < W3_BM / 128; ++ks) {
+            // dy^T fragments: ko column 16 (fmb + f) + li, pixels 128 ks + 32 g + 0..31 (four 8-row transposed reads)
+            w8v8i af[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = ks * 128 + 32 * g + 8 * j + lr;
+                    const w8v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_w8v2i*)(dimg + w8_doff(r, fmb + f) + lh));
+                    af[f][2 * j] = v[0];
+                    af[f][2 * j + 1] = v[1];
+                }
+            // halo byte address of tap (0, 0) for the pixel this lane addresses in each 8-pixel read (past P: real
+            // halo bytes against all-zero dy rows)
+            int base[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p = min(p0 + ks * 128 + 32 * g + 8 * j + lr, plast);
+                const int gr = (int)fdiv((uint32_t)p, a.dW);
+                const int xx = p - gr * WT;
+                const int img = (int)fdiv((uint32_t)gr, a.dH);
+                const int hrow = gr - gstart + 2 * (img - istart) + 1;
+                base[j] = ((hrow - 1) * PITCH + xx) * W8_PB + 16 * fn + lh;
+            }
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int off = ((tap / 3) * PITCH + tap % 3) * W8_PB;
+                w8v8i xf;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const w8v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_w8v2i*)(halo + base[j] + off));
+                    xf[2 * j] = v[0];
+                    xf[2 * j + 1] = v[1];
+                }
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+                    acc[f][tap] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[f], xf, acc[f][tap], 1, 0, 0,
+                                                                                   0x7f7f7f7f, 0, 0x7f7f7f7f);
+            }
+        }
+        __syncthreads();
+        if (more) {
+            zero_halo();
+            __syncthreads();
+            store_lds();
+            __syncthreads();
+        }
+    }
+    const float dq = q.ix[0] * q.idy[0];
+    float* ws = a.ws + (long)blockIdx.x * W3_PS;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ko = (fmb + f) * 16 + 4 * g + j;
+                ws[(ko * 9 + tap) * 64 + fn * 16 + (lane & 15)] = acc[f][tap][j] * dq;
+            }
+}
+
+int w3_hrows(int H, int W);
+int w8_smem(int H, int W);
+
 // dW[ko][tap][c] += sum over the G partials of chunk pair (ko / 64, c / 64).  A block covers OUT = 256 / PG
 // consecutive float4 outputs with PG partial groups (PG ~ G / 8, so every thread sums ~8 partials with all its
 // loads in flight); the groups are combined through LDS.  (One thread per output summing all G partials was a
@@ -268,6 +477,7 @@ int w3_hrows(int H, int W) {
     return R + 2 * imgs + 1;
 }
 int w3_smem(int H, int W) { return W3_BM * 64 * 2 + w3_hrows(H, W) * (W + 2) * W3_PB; }
+int w8_smem(int H, int W) { return W3_BM * 64 + w3_hrows(H, W) * (W + 2) * W8_PB; }
 
 void w3_plan(int P, int C, int Ko, int& tiles, int& cch, int& G) {
     tiles = (P + W3_BM - 1) / W3_BM;
@@ -306,6 +516,48 @@ PDNN_API int pdnn_conv3x3_wgrad_ws(int Nimg, int H, int W, int C, int Ko) {
     int tiles, cch, G;
     w3_plan(Nimg * H * W, C, Ko, tiles, cch, G);
     return (Ko / 64) * cch * G * W3_PS;
+}
+
+// fp8 weight gradient (conv3x3_wgrad8_kernel): x quantised to e4m3 with sx[0], dy to e5m2 with sdy[0], the partials
+// dequantised by ix[0] * idy[0]; same shapes, workspace and reduce as pdnn_conv3x3_wgrad.
+PDNN_API int pdnn_conv3x3_wgrad_fp8(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C, int Ko,
+                                    float* ws, const float* sx, const float* sdy, const float* ix, const float* idy,
+                                    hipStream_t st) {
+    if (!pdnn_conv3x3_wgrad_supported(Nimg, H, W, C, Ko) || !ws || !sx || !sdy || !ix || !idy)
+        return (int)hipErrorInvalidValue;
+    W3Args a{};
+    a.x = x; a.dy = dy; a.ws = ws;
+    a.H = H; a.W = W; a.C = C; a.Ko = Ko; a.P = Nimg * H * W;
+    a.dW = w3_fdiv(W); a.dH = w3_fdiv(H);
+    w3_plan(a.P, C, Ko, a.tiles, a.cch, a.G);
+    a.hrows = w3_hrows(H, W);
+    const W8Scale q{sx, sdy, ix, idy};
+    const int sm = w8_smem(H, W);
+    const int grid = (Ko / 64) * a.cch * a.G;
+    static int attr_done = 0;
+    const bool set = sm > attr_done;
+    if (set) attr_done = sm;
+#define W8_GO(WT)                                                                                                \
+    do {                                                                                                         \
+        if (set) (void)hipFuncSetAttribute((const void*)conv3x3_wgrad8_kernel<WT>,                                \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
+        hipLaunchKernelGGL((conv3x3_wgrad8_kernel<WT>), dim3(grid), dim3(W3_NT), sm, st, a, q);                   \
+    } while (0)
+    if (W == 56) W8_GO(56); else if (W == 28) W8_GO(28); else if (W == 14) W8_GO(14); else W8_GO(7);
+#undef W8_GO
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    const long outs = (long)Ko * 9 * (C / 4);
+#define W3_R(PG) hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel<PG>, dim3((unsigned)cdiv(outs, 256 / PG)), dim3(256), 0, st, \
+                                    (const float*)ws, dw, Ko, C, a.cch, a.G)
+    if (a.G >= 256) W3_R(32);
+    else if (a.G >= 128) W3_R(16);
+    else if (a.G >= 64) W3_R(8);
+    else if (a.G >= 32) W3_R(4);
+    else if (a.G >= 16) W3_R(2);
+    else W3_R(1);
+#undef W3_R
+    PDNN_LAUNCH_RET;
 }
 
 // dw [Ko][3][3][C] fp32 += weight gradient of y = conv3x3(x, w) (stride 1, pad 1) given dy [P][Ko]

@@ -47,6 +47,7 @@ _SIGS = {
     "pdnn_conv3x3_flip8": [P, P, I, I, P],
     "pdnn_conv3x3_fp8": [P, P, P, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P] * 4 + [I, P],
     "pdnn_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, P],
+    "pdnn_conv3x3_wgrad_fp8": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
     "pdnn_conv3x3_wgrad_supported": [I, I, I, I, I],
     "pdnn_conv3x3_wgrad_ws": [I, I, I, I, I],
     "pdnn_set_w3_ablate": [I],

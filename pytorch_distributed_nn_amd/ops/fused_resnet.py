@@ -115,10 +115,10 @@ class _Sink:
         dg, db = K.bn_bwd_finalize(slab, rows, acc=acc)
         return (dg, db), ((None, None) if acc is not None else (dg, db))
 
-    def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None):
+    def wgrad(self, w_p, x, dy, R, S, st, pad, pro=None, fp8=None):
         if self.side is None:
-            return self._wgrad(w_p, x, dy, R, S, st, pad, pro)
-        return self._fork([(w_p, x, dy, R, S, st, pad, pro)])
+            return self._wgrad(w_p, x, dy, R, S, st, pad, pro, fp8)
+        return self._fork([(w_p, x, dy, R, S, st, pad, pro, fp8)])
 
     def _fork(self, jobs):
         # (holding a weight gradient back to share the next fork's marker measured neutral: gpurun_out/r3_60)
@@ -140,8 +140,13 @@ class _Sink:
             self.returned = True
         return g
 
-    def _wgrad(self, w_p, x, dy, R, S, st, pad, pro):
+    def _wgrad(self, w_p, x, dy, R, S, st, pad, pro, fp8=None):
         acc = self.acc(w_p)
+        if fp8 is not None:          # fp8 conv2 (Fp8Conv2): both operands' scales are current for x and dy
+            if acc is not None:
+                K.conv3x3_wgrad_fp8(x, dy, fp8.fwd, fp8.bwd, out=acc[0].permute(0, 2, 3, 1))
+                return None
+            return _krsc_grad(K.conv3x3_wgrad_fp8(x, dy, fp8.fwd, fp8.bwd))
         if acc is not None:
             K.conv_wgrad(x, dy, R, S, st, pad, pro=pro, out=acc[0].permute(0, 2, 3, 1))
             return None
@@ -437,7 +442,7 @@ class BottleneckFn(torch.autograd.Function):
             else:
                 gm1, slab1 = K.conv_dgrad(gm2, k2, t1.shape, stride, 1, bn=bn1, pre=pre2, wprep=w2p)
             del gm2
-            dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)
+            dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1, fp8=ctx.fp8)
         else:
             dt2, rg2, rb2 = _fused_dgrad_bn(dt3, k3, t2, 1, 0, m2, i2, s2, h2, g2, sink, P[4], P[5], wprep=w3p)
             dw2 = sink.wgrad(P[3], a1, dt2, 3, 3, stride, 1)

@@ -979,6 +979,24 @@ def conv3x3_flip8(wq, K, C):
     return wt
 
 
+def conv3x3_wgrad_fp8(x, dy, act_x, act_dy, out=None):
+    """dW [K][3][3][C] fp32 (+= into ``out``) of a 3x3 / stride-1 / pad-1 conv on the fp8 direct weight-gradient
+    kernel: x quantised to e4m3 with ``act_x``'s current scale, dy to e5m2 with ``act_dy``'s (ops.fp8.Fp8Act: the
+    scales the fp8 halo conv just rolled to these tensors' own |max|)."""
+    _bf16_c(x, "conv3x3_wgrad_fp8.x")
+    _bf16_c(dy, "conv3x3_wgrad_fp8.dy")
+    N, H, W, C = x.shape
+    _, Ho, Wo, K = dy.shape
+    _chk((Ho, Wo) == (H, W) and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, K) == 1, "conv3x3_wgrad_fp8: shape")
+    if out is None:
+        out = torch.zeros(K, 3, 3, C, device=x.device, dtype=F32)
+    _chk(out.shape == (K, 3, 3, C) and out.is_contiguous() and out.dtype == F32, "conv3x3_wgrad_fp8: out")
+    ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
+    call("pdnn_conv3x3_wgrad_fp8", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(act_x.scale),
+         ptr(act_dy.scale), ptr(act_x.inv), ptr(act_dy.inv), stream())
+    return out
+
+
 def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None):
     """y = conv3x3(x, w) on the fp8 halo kernel: x bf16 NHWC (quantised in the kernel's halo staging with the
     delayed scale of ``act`` -- an ops.fp8.Fp8Act, e4m3 or e5m2), wq e4m3 [N][3][3][C] with inverse scale ``winv``

@@ -262,3 +262,29 @@ def test_conv3x3_fp8_dgrad_e5m2_pre_bn(K, shape):
     wflip = w.float().flip(1, 2).permute(3, 1, 2, 0).contiguous()
     ref = _conv_ref(_q(dt_ref, sx, E5M2, 57344), _q(wflip, 1.0 / winv.item(), E4M3, 448))
     assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256), (3, 28, 28, 128, 128), (2, 13, 14, 128, 256),
+                                   (1, 56, 56, 64, 64), (3, 7, 7, 128, 128)])
+def test_conv3x3_wgrad_fp8(K, shape):
+    """fp8 direct weight gradient (dy e5m2, x e4m3, ds_read_b64_tr_b8 operands): equal to the fp32 weight gradient of
+    the same quantised operands, and within fp8 precision of the bf16 kernel's."""
+    from pytorch_distributed_nn_amd.ops.fp8 import Fp8Act
+    N, H, W, C, Ko = shape
+    x = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    dy = (torch.randn(N, H, W, Ko, device="cuda") * 1e-3).to(torch.bfloat16)
+    ax, ad = Fp8Act(x.device), Fp8Act(x.device, e5m2=True)
+    sx = 448.0 / x.float().abs().max().item()
+    sd = 57344.0 / dy.float().abs().max().item()
+    ax.scale.fill_(sx); ax.inv.fill_(1.0 / sx)
+    ad.scale.fill_(sd); ad.inv.fill_(1.0 / sd)
+    dw = K.conv3x3_wgrad_fp8(x, dy, ax, ad)
+    xq = _q(x, sx, E4M3, 448).permute(0, 3, 1, 2)
+    dq = _q(dy, sd, E5M2, 57344).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xq, (Ko, C, 3, 3), dq, padding=1).permute(0, 2, 3, 1)
+    assert _rel(dw, ref) < 1e-3
+    d16 = K.conv_wgrad(x, dy, 3, 3, 1, 1)
+    assert _rel(dw, d16) < 0.1
+    # accumulates into out
+    dw2 = K.conv3x3_wgrad_fp8(x, dy, ax, ad, out=dw.clone())
+    assert _rel(dw2, 2 * dw) < 1e-5
