@@ -65,13 +65,43 @@ __global__ void __launch_bounds__(NT) layernorm_bwd_kernel(const bf16_t* __restr
                                                            int D) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int CH = D / 8;
-    float pb[MAXC][8], pg[MAXC][8];
+    float pb[MAXC][8], pg[MAXC][8], gam[MAXC][8];
 #pragma unroll
-    for (int i = 0; i < MAXC; ++i)
+    for (int i = 0; i < MAXC; ++i) {
+        const int c = lane + 64 * i;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[i][j] = pg[i][j] = 0.f;
-    for (int row = blockIdx.x * (NT / 64) + w; row < rows; row += gridDim.x * (NT / 64)) {
-        const float mu = mean[row], rs = rstd[row];
+        for (int j = 0; j < 8; ++j) {
+            pb[i][j] = pg[i][j] = 0.f;
+            gam[i][j] = c < CH ? g[c * 8 + j] : 0.f;          // gamma of this lane's channels, once
+        }
+    }
+    // a wave walks rows row0, row0 + stride, ...: the next row's dy / x / dres / statistics are loaded before this
+    // row's dx is stored (the loads of a row used to start only after the previous row's stores and its own
+    // reductions: 17 us for GPT-2's 8192 x 768, ~2 TB/s)
+    const int stride = gridDim.x * (NT / 64);
+    int row = blockIdx.x * (NT / 64) + w;
+    u16x8_t cdy[MAXC], cx[MAXC], cr[MAXC];
+    float cmu = 0.f, crs = 0.f;
+    auto load = [&](int r, u16x8_t (&dyv)[MAXC], u16x8_t (&xv)[MAXC], u16x8_t (&rv)[MAXC], float& mu, float& rs) {
+        const int rr = r < rows ? r : rows - 1;                // clamped: a past-the-end prefetch reads a valid row
+        mu = mean[rr];
+        rs = rstd[rr];
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = lane + 64 * i;
+            if (c < CH) {
+                dyv[i] = *reinterpret_cast<const u16x8_t*>(dy + (long)rr * D + c * 8);
+                xv[i] = *reinterpret_cast<const u16x8_t*>(x + (long)rr * D + c * 8);
+                if (dres) rv[i] = *reinterpret_cast<const u16x8_t*>(dres + (long)rr * D + c * 8);
+            }
+        }
+    };
+    if (row < rows) load(row, cdy, cx, cr, cmu, crs);
+    for (; row < rows; row += stride) {
+        u16x8_t ndy[MAXC], nx[MAXC], nr[MAXC];
+        float nmu, nrs;
+        load(row + stride, ndy, nx, nr, nmu, nrs);
+        const float mu = cmu, rs = crs;
         float gv[MAXC][8], xh[MAXC][8];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -79,14 +109,14 @@ __global__ void __launch_bounds__(NT) layernorm_bwd_kernel(const bf16_t* __restr
             const int c = lane + 64 * i;
             if (c < CH) {
                 float xv[8];
-                unpack8(*reinterpret_cast<const u16x8_t*>(dy + (long)row * D + c * 8), gv[i]);
-                unpack8(*reinterpret_cast<const u16x8_t*>(x + (long)row * D + c * 8), xv);
+                unpack8(cdy[i], gv[i]);
+                unpack8(cx[i], xv);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     xh[i][j] = (xv[j] - mu) * rs;
                     pb[i][j] += gv[i][j];
                     pg[i][j] += gv[i][j] * xh[i][j];
-                    const float gg = gv[i][j] * g[c * 8 + j];
+                    const float gg = gv[i][j] * gam[i][j];
                     s1 += gg;
                     s2 += gg * xh[i][j];
                 }
@@ -99,13 +129,21 @@ __global__ void __launch_bounds__(NT) layernorm_bwd_kernel(const bf16_t* __restr
             const int c = lane + 64 * i;
             if (c < CH) {
                 float o[8], rr[8];
-                if (dres) unpack8(*reinterpret_cast<const u16x8_t*>(dres + (long)row * D + c * 8), rr);
+                if (dres) unpack8(cr[i], rr);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    o[j] = rs * (gv[i][j] * g[c * 8 + j] - s1 - xh[i][j] * s2) + (dres ? rr[j] : 0.f);
+                    o[j] = rs * (gv[i][j] * gam[i][j] - s1 - xh[i][j] * s2) + (dres ? rr[j] : 0.f);
                 *reinterpret_cast<u16x8_t*>(dx + (long)row * D + c * 8) = pack8(o);
             }
         }
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            cdy[i] = ndy[i];
+            cx[i] = nx[i];
+            cr[i] = nr[i];
+        }
+        cmu = nmu;
+        crs = nrs;
     }
     // block-level combine of the 4 waves' column partials, then one slab row pair per block
     __shared__ float red[2][NT / 64][MAXC * 512];

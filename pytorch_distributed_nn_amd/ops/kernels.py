@@ -722,7 +722,7 @@ def xent_fwd(logits, labels, ignore_index=-100):
     _chk(logits.dtype in (BF16, F32), "xent: bf16/fp32 logits")
     loss = torch.empty(R, device=logits.device, dtype=F32)
     lse = torch.empty(R, device=logits.device, dtype=F32)
-    acc = torch.zeros(2, device=logits.device, dtype=F32)
+    acc = torch.empty(2, device=logits.device, dtype=F32)          # [loss sum, valid-label count], set by the call
     call("pdnn_xent_fwd", ptr(logits), logits.stride(0), R, V, ptr(labels), int(ignore_index), ptr(loss), ptr(lse),
          ptr(acc), ptr(acc[1:]), dt, stream())
     return loss, lse, acc
