@@ -70,7 +70,8 @@ __device__ __forceinline__ uint4 c3_to_fp8(const float* v) {
 // quantised with the tensor's delayed scale WHILE the halo is staged (no separate quantisation pass, no fp8
 // copy in HBM), so a halo pixel is the same 128 bytes and the per-tap work covers twice the channels at the
 // same LDS traffic and MFMA cycles.  The staged values' |max| feeds the next call's scale (f8_amax partials).
-template <int NB, int EPI, bool PRE, int F8 = 0>
+// FP: the forward prologue relu(x * pro_sc + pro_sh) on the staged operand (its coefficients in LDS like PRE's).
+template <int NB, int EPI, bool PRE, int F8 = 0, bool FP = false>
 __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
     constexpr int FN = NB / 16;                  // column fragments per wave (every wave spans all NB)
     constexpr int BCH = NB * 8 / 256;            // 16-byte weight chunks per thread per tap
@@ -165,6 +166,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
             if constexpr (PRE) {
                 pre_coef_lds<128>(a, c0, coef, tid);
                 __syncthreads();
+            } else if constexpr (FP) {
+                fpro_coef_lds<128>(a, c0, coef, tid);
+                __syncthreads();
             }
             for (int i0 = 0; i0 < nch; i0 += 256 * J) {
                 u16x8_t v[J][2], tv[PRE ? J : 1][2];
@@ -196,6 +200,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
                                 *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 16 + 8 * h) =
                                     v[j][h];
                         }
+                    }
+                    if constexpr (FP) {
+                        v[j][0] = fpro_apply_lds<128>(coef, (tid & 7) * 16, v[j][0]);
+                        v[j][1] = fpro_apply_lds<128>(coef, (tid & 7) * 16 + 8, v[j][1]);
                     }
                     float f[16];
                     unpack8(v[j][0], f);
@@ -259,6 +267,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
         if constexpr (PRE) {
             pre_coef_lds<64>(a, c0, coef, tid);
             __syncthreads();
+        } else if constexpr (FP) {
+            fpro_coef_lds<64>(a, c0, coef, tid);
+            __syncthreads();
         }
         for (int i0 = 0; i0 < nch; i0 += 256 * J) {
             u16x8_t v[J], tv[PRE ? J : 1];
@@ -284,6 +295,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(C3Args a) {
                     if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
                         *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 8) = v[j];
                 }
+                if constexpr (FP) v[j] = fpro_apply_lds<64>(coef, (tid & 7) * 8, v[j]);
                 v[j] = mask16(v[j], okj[j]);     // masked, not selected: keeps the load unconditional
             }
 #pragma unroll
@@ -667,16 +679,16 @@ int c3r_launch(const C3Args& a, hipStream_t st) {
     PDNN_LAUNCH_RET;
 }
 
-template <int NB, int EPI, bool PRE, int F8 = 0>
+template <int NB, int EPI, bool PRE, int F8 = 0, bool FP = false>
 int c3_launch(const C3Args& a, hipStream_t st) {
     static int attr_done = 0;
     const int sm = c3_smem<NB>(a.W);
     if (sm > attr_done) {
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI, PRE, F8>,
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<NB, EPI, PRE, F8, FP>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, sm);
         attr_done = sm;
     }
-    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI, PRE, F8>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    hipLaunchKernelGGL((conv3x3_kernel<NB, EPI, PRE, F8, FP>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }
 
@@ -789,7 +801,7 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
                           const float* bn_invstd, const float* bn_mscale, const float* bn_mshift, int nb,
                           const bf16_t* pre_t, const float* pre_mean, const float* pre_invstd,
                           const float* pre_gamma, const float* pre_dgamma, const float* pre_dbeta, bf16_t* pre_out,
-                          hipStream_t st) {
+                          const float* pro_sc, const float* pro_sh, hipStream_t st) {
     if (!pdnn_conv3x3_supported(Nimg, H, W, C, N)) return (int)hipErrorInvalidValue;
     C3Args a{};
     a.x = x; a.w = w; a.y = y;
@@ -805,6 +817,18 @@ PDNN_API int pdnn_conv3x3(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg,
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
     const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
     if (bn_x && !stats) return (int)hipErrorInvalidValue;
+    if (!pro_sc != !pro_sh) return (int)hipErrorInvalidValue;
+    if (pro_sc) {
+        // forward prologue (the BN + ReLU of the layer below): the streaming kernel, statistics or plain epilogue
+        if (pre || (epi != C3_STATS && epi != C3_PLAIN)) return (int)hipErrorInvalidValue;
+        a.pro_sc = pro_sc; a.pro_sh = pro_sh;
+        if (nb <= 1) nb = N % 128 == 0 ? 128 : 64;
+        if (nb == 128 && (N % 128 || c3_smem<128>(W) > 80 * 1024)) nb = 64;
+        a.ntiles = N / nb;
+        if (nb == 128)
+            return epi == C3_STATS ? c3_launch<128, C3_STATS, false, 0, true>(a, st) : c3_launch<128, C3_PLAIN, false, 0, true>(a, st);
+        return epi == C3_STATS ? c3_launch<64, C3_STATS, false, 0, true>(a, st) : c3_launch<64, C3_PLAIN, false, 0, true>(a, st);
+    }
     // 64 -> 64 channels: the weight-resident persistent kernel (nb = 1; measured slower than the streaming
     // kernel at ResNet-50 stage 1, 125 / 173 vs 104 / 142 us fwd / dgrad, gpurun_out/r3_04: one wave per SIMD
     // exposes the LDS latency of the unrolled tap sequence)
@@ -840,7 +864,8 @@ PDNN_API int pdnn_conv3x3_fp8(const bf16_t* x, const uint8_t* wq, bf16_t* y, int
                               const float* bn_mscale, const float* bn_mshift, const bf16_t* pre_t,
                               const float* pre_mean, const float* pre_invstd, const float* pre_gamma,
                               const float* pre_dgamma, const float* pre_dbeta, bf16_t* pre_out, const float* scale,
-                              const float* inv, const float* winv, float* amax, int e5m2, hipStream_t st) {
+                              const float* inv, const float* winv, float* amax, int e5m2, const float* pro_sc,
+                              const float* pro_sh, hipStream_t st) {
     if (!pdnn_conv3x3_fp8_supported(Nimg, H, W, C, N) || !scale || !inv || !winv || !amax)
         return (int)hipErrorInvalidValue;
     C3Args a{};
@@ -863,6 +888,11 @@ PDNN_API int pdnn_conv3x3_fp8(const bf16_t* x, const uint8_t* wq, bf16_t* y, int
         return pre ? c3_launch<128, C3_PLAIN, true, 2>(a, st) : c3_launch<128, C3_PLAIN, false, 2>(a, st);
     }
     if (pre || bn_x) return (int)hipErrorInvalidValue;
+    if (!pro_sc != !pro_sh) return (int)hipErrorInvalidValue;
+    if (pro_sc) {
+        a.pro_sc = pro_sc; a.pro_sh = pro_sh;
+        return stats ? c3_launch<128, C3_STATS, false, 1, true>(a, st) : c3_launch<128, C3_PLAIN, false, 1, true>(a, st);
+    }
     return stats ? c3_launch<128, C3_STATS, false, 1>(a, st) : c3_launch<128, C3_PLAIN, false, 1>(a, st);
 }
 

@@ -39,8 +39,25 @@ struct W3Args {
     int H, W, C, Ko, P;
     FastDiv dW, dH;
     int tiles, cch, G, hrows;
+    const float *psc, *psh;   // optional forward prologue: x' = relu(x * psc[c] + psh[c]) (the BN + ReLU that made
+                              // the conv's input, applied while staging instead of materialised: fused_resnet a1)
 };
-int g_w3_abl = 0;
+
+// this thread's 8 prologue coefficients (channels c .. c+7), and the prologue on a staged chunk (bn_apply's rounding)
+struct W3Pro {
+    float sc[8], sh[8];
+};
+__device__ __forceinline__ void w3_pro_load(const W3Args& a, int c, W3Pro& pr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { pr.sc[j] = a.psc[c + j]; pr.sh[j] = a.psh[c + j]; }
+}
+__device__ __forceinline__ u16x8_t w3_pro(const W3Pro& pr, const u16x8_t& v) {
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], pr.sc[j], pr.sh[j]), 0.f);
+    return pack8(f);
+}
 
 // Halo layout (per tile): the tile's input rows from one above its first to one below its last, each
 // image's rows bracketed by an all-zero row above and below, every row padded by a zero pixel left and
@@ -49,7 +66,7 @@ int g_w3_abl = 0;
 // address (no per-tap validity, select or swizzle arithmetic; that VALU work was 3x the MFMA time).
 //   hrow(gr) = gr - gstart + 2 (img(gr) - img(gstart)) + 1,  gstart = first row - 1 (global row index over
 //   the whole batch; img(-1) = -1).
-template <int WT, int ABL>
+template <int WT, bool FP>
 __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
     constexpr int PITCH = WT + 2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -60,6 +77,8 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
     const int ko0 = (pair / a.cch) * 64, c0 = (pair % a.cch) * 64;
     const int t0 = (int)((long)part * a.tiles / a.G), t1 = (int)((long)(part + 1) * a.tiles / a.G);
     const int hbytes = a.hrows * PITCH * W3_PB;
+    [[maybe_unused]] W3Pro pro;
+    if constexpr (FP) w3_pro_load(a, c0 + (tid & 7) * 8, pro);       // this thread's halo chunks: i & 7 == tid & 7
 
     // wave roles: input channels [16 fn, +16), output-channel fragments fmb, fmb + 1 (32 ko), all 9 taps
     const int fn = wave & 3, fmb = (wave >> 2) * 2;
@@ -128,7 +147,9 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
                 const int xx = gp - gr * WT;
                 const int img = (int)fdiv((uint32_t)gr, a.dH);
                 const int hrow = gr - s_gstart + 2 * (img - s_istart) + 1;
-                *reinterpret_cast<u16x8_t*>(halo + (hrow * PITCH + xx + 1) * W3_PB + (i & 7) * 16) = rh[j];
+                u16x8_t hv = rh[j];
+                if constexpr (FP) hv = w3_pro(pro, hv);
+                *reinterpret_cast<u16x8_t*>(halo + (hrow * PITCH + xx + 1) * W3_PB + (i & 7) * 16) = hv;
             }
         }
     };
@@ -148,7 +169,7 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
         const bool more = t + 1 < t1;
         int p0, plast, gstart, istart;
         geo(t, p0, plast, gstart, istart);
-        if (more && !(ABL & 4)) load_regs(t + 1);               // under this tile's MFMAs
+        if (more) load_regs(t + 1);                             // under this tile's MFMAs
 #pragma unroll 1
         for (int ks = 0; ks < W3_BM / 32; ++ks) {
             bf16x8_t af[2];
@@ -168,31 +189,19 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad_kernel(W3Args a) {
             }
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                constexpr int dummy = 0;
-                (void)dummy;
                 const int off = ((tap / 3) * PITCH + tap % 3) * W3_PB;
-                bf16x8_t xf;
-                if constexpr ((ABL & 2) != 0) {
-                    xf = af[tap & 1];
-                    asm volatile("" ::"v"(base[0]), "v"(base[1]));
-                } else {
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[0] + off));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[1] + off));
-                    typedef __attribute__((ext_vector_type(8))) short s16x8;
-                    const s16x8 xv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    xf = __builtin_bit_cast(bf16x8_t, xv);
-                }
-                if constexpr ((ABL & 1) != 0) {
-                    asm volatile("" ::"v"(xf), "v"(af[0]), "v"(af[1]));
-                } else {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[0] + off));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[1] + off));
+                typedef __attribute__((ext_vector_type(8))) short s16x8;
+                const s16x8 xv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                const bf16x8_t xf = __builtin_bit_cast(bf16x8_t, xv);
 #pragma unroll
-                    for (int f = 0; f < 2; ++f)
-                        acc[f][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], xf, acc[f][tap], 0, 0, 0);
-                }
+                for (int f = 0; f < 2; ++f)
+                    acc[f][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], xf, acc[f][tap], 0, 0, 0);
             }
         }
         __syncthreads();                          // every wave is done reading this tile's images
-        if (more && !(ABL & 4)) {
+        if (more) {
             zero_halo();
             __syncthreads();
             store_lds();
@@ -258,7 +267,7 @@ struct W8Scale {
     const float *ix, *idy;     // their inverses (the partials are dequantised by ix * idy)
 };
 
-template <int WT>
+template <int WT, bool FP>
 __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad8_kernel(W3Args a, W8Scale q) {
     constexpr int PITCH = WT + 2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -270,6 +279,8 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad8_kernel(W3Args a, W8Sc
     const int t0 = (int)((long)part * a.tiles / a.G), t1 = (int)((long)(part + 1) * a.tiles / a.G);
     const int hbytes = a.hrows * PITCH * W8_PB;
     const float sx = q.sx[0], sdy = q.sdy[0];
+    [[maybe_unused]] W3Pro pro;
+    if constexpr (FP) w3_pro_load(a, c0 + (tid & 7) * 8, pro);
 
     const int fn = wave & 3, fmb = (wave >> 2) * 2;
     f32x4_t acc[2][9];
@@ -337,7 +348,9 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad8_kernel(W3Args a, W8Sc
                 const int xx = gp - gr * WT;
                 const int img = (int)fdiv((uint32_t)gr, a.dH);
                 const int hrow = gr - s_gstart + 2 * (img - s_istart) + 1;
-                *reinterpret_cast<uint2*>(halo + (hrow * PITCH + xx + 1) * W8_PB + (i & 7) * 8) = w8_cvt<0>(rh[j], sx);
+                u16x8_t hv = rh[j];
+                if constexpr (FP) hv = w3_pro(pro, hv);
+                *reinterpret_cast<uint2*>(halo + (hrow * PITCH + xx + 1) * W8_PB + (i & 7) * 8) = w8_cvt<0>(hv, sx);
             }
         }
     };
@@ -488,6 +501,20 @@ void w3_plan(int P, int C, int Ko, int& tiles, int& cch, int& G) {
     if (G < 1) G = 1;
 }
 
+// the 160 KB dynamic-LDS opt-in, once per kernel instantiation (whichever variant a call picks)
+void w3_attr(const void* fn) {
+    static const void* done[32] = {};
+    for (int i = 0; i < 32; ++i) {
+        if (done[i] == fn) return;
+        if (!done[i]) {
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            done[i] = fn;
+            return;
+        }
+    }
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 FastDiv w3_fdiv(uint32_t d) {
     FastDiv f;
     f.d = d ? d : 1;
@@ -498,8 +525,6 @@ FastDiv w3_fdiv(uint32_t d) {
     return f;
 }
 }  // namespace
-
-PDNN_API void pdnn_set_w3_ablate(int v) { g_w3_abl = v; }
 
 // Whether the direct kernel takes this 3x3 / stride-1 / pad-1 weight gradient (image widths 7/14/28/56: the
 // ResNet stages; the tap offsets are compile-time immediates).
@@ -522,7 +547,7 @@ PDNN_API int pdnn_conv3x3_wgrad_ws(int Nimg, int H, int W, int C, int Ko) {
 // dequantised by ix[0] * idy[0]; same shapes, workspace and reduce as pdnn_conv3x3_wgrad.
 PDNN_API int pdnn_conv3x3_wgrad_fp8(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C, int Ko,
                                     float* ws, const float* sx, const float* sdy, const float* ix, const float* idy,
-                                    hipStream_t st) {
+                                    const float* pro_sc, const float* pro_sh, hipStream_t st) {
     if (!pdnn_conv3x3_wgrad_supported(Nimg, H, W, C, Ko) || !ws || !sx || !sdy || !ix || !idy)
         return (int)hipErrorInvalidValue;
     W3Args a{};
@@ -531,19 +556,20 @@ PDNN_API int pdnn_conv3x3_wgrad_fp8(const bf16_t* x, const bf16_t* dy, float* dw
     a.dW = w3_fdiv(W); a.dH = w3_fdiv(H);
     w3_plan(a.P, C, Ko, a.tiles, a.cch, a.G);
     a.hrows = w3_hrows(H, W);
+    if (!pro_sc != !pro_sh) return (int)hipErrorInvalidValue;
+    a.psc = pro_sc; a.psh = pro_sh;
+    const bool fp = pro_sc != nullptr;
     const W8Scale q{sx, sdy, ix, idy};
     const int sm = w8_smem(H, W);
     const int grid = (Ko / 64) * a.cch * a.G;
-    static int attr_done = 0;
-    const bool set = sm > attr_done;
-    if (set) attr_done = sm;
-#define W8_GO(WT)                                                                                                \
+#define W8_GO(WT, F)                                                                                             \
     do {                                                                                                         \
-        if (set) (void)hipFuncSetAttribute((const void*)conv3x3_wgrad8_kernel<WT>,                                \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
-        hipLaunchKernelGGL((conv3x3_wgrad8_kernel<WT>), dim3(grid), dim3(W3_NT), sm, st, a, q);                   \
+        w3_attr((const void*)conv3x3_wgrad8_kernel<WT, F>);                                                      \
+        hipLaunchKernelGGL((conv3x3_wgrad8_kernel<WT, F>), dim3(grid), dim3(W3_NT), sm, st, a, q);                \
     } while (0)
-    if (W == 56) W8_GO(56); else if (W == 28) W8_GO(28); else if (W == 14) W8_GO(14); else W8_GO(7);
+#define W8_W(WT) do { if (fp) W8_GO(WT, true); else W8_GO(WT, false); } while (0)
+    if (W == 56) W8_W(56); else if (W == 28) W8_W(28); else if (W == 14) W8_W(14); else W8_W(7);
+#undef W8_W
 #undef W8_GO
     const int e = (int)hipGetLastError();
     if (e) return e;
@@ -561,8 +587,10 @@ PDNN_API int pdnn_conv3x3_wgrad_fp8(const bf16_t* x, const bf16_t* dy, float* dw
 }
 
 // dw [Ko][3][3][C] fp32 += weight gradient of y = conv3x3(x, w) (stride 1, pad 1) given dy [P][Ko]
+// pro_sc / pro_sh (optional, both or neither): x is the pre-activation t of relu(t * pro_sc + pro_sh), applied as the
+// halo is staged
 PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C, int Ko,
-                                float* ws, hipStream_t st) {
+                                float* ws, const float* pro_sc, const float* pro_sh, hipStream_t st) {
     if (!pdnn_conv3x3_wgrad_supported(Nimg, H, W, C, Ko) || !ws) return (int)hipErrorInvalidValue;
     W3Args a{};
     a.x = x; a.dy = dy; a.ws = ws;
@@ -570,25 +598,18 @@ PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, in
     a.dW = w3_fdiv(W); a.dH = w3_fdiv(H);
     w3_plan(a.P, C, Ko, a.tiles, a.cch, a.G);
     a.hrows = w3_hrows(H, W);
-    const int abl = g_w3_abl & 7;
+    if (!pro_sc != !pro_sh) return (int)hipErrorInvalidValue;
+    a.psc = pro_sc; a.psh = pro_sh;
+    const bool fp = pro_sc != nullptr;
     const int sm = w3_smem(H, W);
     const int grid = (Ko / 64) * a.cch * a.G;
-    static int attr_done = 0;
-    const bool set = sm > attr_done;
-    if (set) attr_done = sm;
-#define W3_GO(WT, A)                                                                                             \
+#define W3_GO(WT, F)                                                                                             \
     do {                                                                                                         \
-        if (set) (void)hipFuncSetAttribute((const void*)conv3x3_wgrad_kernel<WT, A>,                              \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
-        hipLaunchKernelGGL((conv3x3_wgrad_kernel<WT, A>), dim3(grid), dim3(W3_NT), sm, st, a);                   \
+        w3_attr((const void*)conv3x3_wgrad_kernel<WT, F>);                                                       \
+        hipLaunchKernelGGL((conv3x3_wgrad_kernel<WT, F>), dim3(grid), dim3(W3_NT), sm, st, a);                   \
     } while (0)
-#define W3_W(WT)                                                                                                 \
-    switch (abl) {                                                                                               \
-        case 1: W3_GO(WT, 1); break; case 2: W3_GO(WT, 2); break; case 3: W3_GO(WT, 3); break;                   \
-        case 4: W3_GO(WT, 4); break; case 5: W3_GO(WT, 5); break; case 6: W3_GO(WT, 6); break;                   \
-        case 7: W3_GO(WT, 7); break; default: W3_GO(WT, 0);                                                      \
-    }
-    if (W == 56) { W3_W(56) } else if (W == 28) { W3_W(28) } else if (W == 14) { W3_W(14) } else { W3_W(7) }
+#define W3_W(WT) do { if (fp) W3_GO(WT, true); else W3_GO(WT, false); } while (0)
+    if (W == 56) W3_W(56); else if (W == 28) W3_W(28); else if (W == 14) W3_W(14); else W3_W(7);
 #undef W3_W
 #undef W3_GO
     const int e = (int)hipGetLastError();

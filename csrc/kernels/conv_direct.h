@@ -36,6 +36,9 @@ struct C3Args {
     // f8_inv[0] * f8_winv[0]
     const float *f8_scale, *f8_inv, *f8_winv;
     float* f8_amax;
+    // forward operand prologue (conv3x3.hip FP): the staged operand is relu(x * pro_sc[c] + pro_sh[c]) -- the BN + ReLU
+    // of the layer that produced x, so its output never has to be materialised (bn_apply's formula and rounding)
+    const float *pro_sc, *pro_sh;
 };
 
 // per-channel coefficients of 8 consecutive channels c .. c+7 (batchnorm.hip bn_bwd_apply_kernel)
@@ -89,6 +92,27 @@ __device__ __forceinline__ u16x8_t pre_apply_lds(const float* coef, int c, const
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(k[j], gm[j], fmaf(t[j], A[j], B[j]));
     return pack8(o);
+}
+
+// forward prologue coefficients of the chunk's CH channels in LDS (coef: [2][CH] = scale, shift) and its apply
+template <int CH>
+__device__ __forceinline__ void fpro_coef_lds(const C3Args& a, int c0, float* coef, int tid) {
+    for (int c = tid; c < CH; c += 256) {
+        coef[c] = a.pro_sc[c0 + c];
+        coef[CH + c] = a.pro_sh[c0 + c];
+    }
+}
+template <int CH>
+__device__ __forceinline__ u16x8_t fpro_apply_lds(const float* coef, int c, const u16x8_t& v) {
+    float x[8], sc[8], sh[8];
+    unpack8(v, x);
+    *reinterpret_cast<float4*>(sc) = *reinterpret_cast<const float4*>(coef + c);
+    *reinterpret_cast<float4*>(sc + 4) = *reinterpret_cast<const float4*>(coef + c + 4);
+    *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(coef + CH + c);
+    *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(coef + CH + c + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = fmaxf(fmaf(x[j], sc[j], sh[j]), 0.f);
+    return pack8(x);
 }
 
 // v if ok else 0, as four 32-bit ANDs (a u16x8 AND with a 16-bit mask vector lowers to per-half sdwa/perm ops)

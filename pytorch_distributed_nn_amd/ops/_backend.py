@@ -39,18 +39,17 @@ _SIGS = {
     "pdnn_conv_dgrad_stats_rows": [I, I, I, I, I, I, I],
     "pdnn_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "pdnn_gemm_stats_rows": [I],
-    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P],
+    "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
     "pdnn_conv3x3_fp8_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
     "pdnn_conv3x3_flip8": [P, P, I, I, P],
-    "pdnn_conv3x3_fp8": [P, P, P, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P] * 4 + [I, P],
-    "pdnn_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, P],
-    "pdnn_conv3x3_wgrad_fp8": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
+    "pdnn_conv3x3_fp8": [P, P, P, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P] * 4 + [I, P, P, P],
+    "pdnn_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, P, P, P],
+    "pdnn_conv3x3_wgrad_fp8": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_wgrad_supported": [I, I, I, I, I],
     "pdnn_conv3x3_wgrad_ws": [I, I, I, I, I],
-    "pdnn_set_w3_ablate": [I],
     "pdnn_conv3x3_force": [I],
     "pdnn_tune_set": [ctypes.c_char_p, I],
     "pdnn_tune_get": [ctypes.c_char_p],

@@ -259,9 +259,10 @@ def conv3x3_flip(w):
     return wt
 
 
-def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, pre=None):
+def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, pre=None, pro=None):
     """y = conv3x3(x, w) (stride 1, pad 1) on the halo kernel, w: bf16 [N][3][3][C].  Epilogues as
-    conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward)."""
+    conv_fwd / conv_dgrad (stats slab, residual add, fused BN backward).  pro = (scale, shift) fp32 [C]: the operand
+    is relu(x * scale + shift), applied while the halo is staged (x is the BN input; plain / stats epilogues)."""
     Nimg, H, W, C = x.shape
     Ko = w.shape[0]
     y = out if out is not None else torch.empty(Nimg, H, W, Ko, device=x.device, dtype=BF16)
@@ -271,8 +272,9 @@ def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, 
         slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
     if bn is not None:
         t, mean, inv, msc, msh = bn
+    psc, psh = pro if pro is not None else (None, None)
     call("pdnn_conv3x3", ptr(x), ptr(w), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), _C3["nb"], *_pre_args(pre, x), stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), _C3["nb"], *_pre_args(pre, x), ptr(psc), ptr(psh), stream())
     return y, slab
 
 
@@ -287,8 +289,8 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     _chk(C2 == C, f"conv_fwd: weight {tuple(w.shape)} must be [K][R][S][C] with C={C}")
     _chk(C % 8 == 0 and K % 8 == 0, f"conv_fwd: channels must be multiples of 8 (C={C}, K={K})")
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
-    if pro is None and _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
-        return conv3x3(x, w, want_stats=want_stats)
+    if _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
+        return conv3x3(x, w, want_stats=want_stats, pro=pro)
     if pro is None and _panel_ok(N * H * W, C, K, R, S, st, pad, fwd=True):
         y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats)
         return y.view(N, H, W, K), slab
@@ -306,6 +308,13 @@ def _panel_dgrad_k(K):
     """Data gradients (dx[P][C] = dy[P][K] . W) on the A-stationary kernel (K in {64, 128, 256}) or the
     long-reduction streaming kernel (K >= 512, conv1x1_wide.hip)."""
     return K in (64, 128, 256) or K >= 512
+
+
+def conv3x3_pro_ok(x_shape, Ko):
+    """Whether a 3x3 / stride-1 conv of this input takes its input's BN + ReLU as an operand prologue in both its
+    forward (halo kernel) and its weight gradient (direct kernel): the activation then need not be materialised."""
+    N, H, W, C = x_shape
+    return _conv3x3_ok(N, H, W, C, Ko, 3, 3, 1, 1) and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, Ko) == 1
 
 
 def dgrad_pre_ok(dy_shape, w_shape, st, pad):
@@ -414,11 +423,11 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     _chk(out.shape == (K, R, S, C) and out.is_contiguous() and out.dtype == F32, "conv_wgrad: out [K][R][S][C] fp32")
     sc, sh = pro if pro is not None else (None, None)
     P = N * H * W
-    if (pro is None and R == 3 and S == 3 and st == 1 and pad == 1
-            and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, K) == 1):
-        # direct kernel: LDS halo + transpose reads, partials per block, then one reduce (conv3x3_wgrad.hip)
+    if R == 3 and S == 3 and st == 1 and pad == 1 and lib().pdnn_conv3x3_wgrad_supported(N, H, W, C, K) == 1:
+        # direct kernel: LDS halo + transpose reads, partials per block, then one reduce (conv3x3_wgrad.hip); the
+        # prologue relu(x * sc + sh) applied as the halo is staged
         ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
-        call("pdnn_conv3x3_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), stream())
+        call("pdnn_conv3x3_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(sc), ptr(sh), stream())
         return out
     if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _WGRAD1X1_PP_PIX
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
@@ -979,7 +988,7 @@ def conv3x3_flip8(wq, K, C):
     return wt
 
 
-def conv3x3_wgrad_fp8(x, dy, act_x, act_dy, out=None):
+def conv3x3_wgrad_fp8(x, dy, act_x, act_dy, out=None, pro=None):
     """dW [K][3][3][C] fp32 (+= into ``out``) of a 3x3 / stride-1 / pad-1 conv on the fp8 direct weight-gradient
     kernel: x quantised to e4m3 with ``act_x``'s current scale, dy to e5m2 with ``act_dy``'s (ops.fp8.Fp8Act: the
     scales the fp8 halo conv just rolled to these tensors' own |max|)."""
@@ -992,12 +1001,13 @@ def conv3x3_wgrad_fp8(x, dy, act_x, act_dy, out=None):
         out = torch.zeros(K, 3, 3, C, device=x.device, dtype=F32)
     _chk(out.shape == (K, 3, 3, C) and out.is_contiguous() and out.dtype == F32, "conv3x3_wgrad_fp8: out")
     ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
+    psc, psh = pro if pro is not None else (None, None)
     call("pdnn_conv3x3_wgrad_fp8", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(act_x.scale),
-         ptr(act_dy.scale), ptr(act_x.inv), ptr(act_dy.inv), stream())
+         ptr(act_dy.scale), ptr(act_x.inv), ptr(act_dy.inv), ptr(psc), ptr(psh), stream())
     return out
 
 
-def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None):
+def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None, pro=None):
     """y = conv3x3(x, w) on the fp8 halo kernel: x bf16 NHWC (quantised in the kernel's halo staging with the
     delayed scale of ``act`` -- an ops.fp8.Fp8Act, e4m3 or e5m2), wq e4m3 [N][3][3][C] with inverse scale ``winv``
     (device scalar).  Epilogues / ``bn`` / ``pre`` as conv3x3 (bn and pre only with e5m2: data gradients).
@@ -1014,7 +1024,8 @@ def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None):
     if bn is not None:
         t, mean, inv, msc, msh = bn
     args = (ptr(x), ptr(wq), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh),
-            *_pre_args(pre, x), ptr(act.scale), ptr(act.inv), ptr(winv), ptr(act.amax), int(act.e5m2), stream())
+            *_pre_args(pre, x), ptr(act.scale), ptr(act.inv), ptr(winv), ptr(act.amax), int(act.e5m2),
+            ptr(pro[0] if pro is not None else None), ptr(pro[1] if pro is not None else None), stream())
     if not act.primed:
         call("pdnn_conv3x3_fp8", *args)
         fp8_scale_roll(act.amax, act.scale, act.inv, act.e5m2, act.margin)

@@ -245,3 +245,26 @@ def test_conv3x3_wgrad_direct(K, shape):
     base = torch.randn(Ko, 3, 3, C, device="cuda")
     out = K.conv_wgrad(x, dy, 3, 3, 1, 1, out=base.clone())          # accumulates into out
     assert rel(out - base, ref) < 5e-3
+
+
+# ------------------------------------------- BN + ReLU of the layer below applied while staging (pro=)
+@pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 256),
+                                   (3, 13, 14, 128, 64)])
+def test_conv3x3_forward_prologue_matches_materialised(K, shape):
+    """The halo forward and the direct weight gradient with the operand relu(t * sc + sh) formed while staging: bitwise
+    equal to running them on bn_apply's materialised activation (same kernels, same tiles, bn_apply's rounding)."""
+    N, H, W, C, Ko = shape
+    t = torch.randn(N, H, W, C, device="cuda").to(BF)
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    a = K.bn_apply(t.view(-1, C), sc, sh, relu=True).view_as(t)
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(BF)
+    y0, s0 = K.conv3x3(a, w, want_stats=True)
+    y1, s1 = K.conv3x3(t, w, want_stats=True, pro=(sc, sh))
+    assert torch.equal(y0, y1) and torch.equal(s0, s1)
+    y2, _ = K.conv_fwd(t, w, 1, 1, pro=(sc, sh))          # routed to the halo kernel with the prologue
+    assert torch.equal(y2, y0)
+    assert K.conv3x3_pro_ok(tuple(t.shape), Ko)
+    dy = torch.randn(N, H, W, Ko, device="cuda").to(BF)
+    d0 = K.conv_wgrad(a, dy, 3, 3, 1, 1)
+    d1 = K.conv_wgrad(t, dy, 3, 3, 1, 1, pro=(sc, sh))
+    assert torch.equal(d0, d1)

@@ -288,3 +288,28 @@ def test_conv3x3_wgrad_fp8(K, shape):
     # accumulates into out
     dw2 = K.conv3x3_wgrad_fp8(x, dy, ax, ad, out=dw.clone())
     assert _rel(dw2, 2 * dw) < 1e-5
+
+
+def test_conv3x3_fp8_forward_prologue(K):
+    """fp8 halo forward and fp8 weight gradient with the BN + ReLU prologue: equal to the same kernels on the
+    materialised activation (the prologue runs before the quantisation, so the delayed scales agree too)."""
+    from pytorch_distributed_nn_amd.ops.fp8 import Fp8Act
+    N, H, W, C, Ko = 2, 14, 14, 256, 256
+    t = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    a = K.bn_apply(t.view(-1, C), sc, sh, relu=True).view_as(t)
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.1).to(torch.bfloat16)
+    winv = torch.empty(1, device="cuda")
+    wq = K.quant_fp8_current(w.reshape(Ko, -1).contiguous(), winv)
+    act0, act1 = Fp8Act(t.device), Fp8Act(t.device)
+    y0, s0 = K.conv3x3_fp8(a, wq, winv, act0, want_stats=True)
+    y1, s1 = K.conv3x3_fp8(t, wq, winv, act1, want_stats=True, pro=(sc, sh))
+    assert torch.equal(y0, y1) and torch.equal(s0, s1)
+    assert torch.equal(act0.scale, act1.scale)
+    dy = (torch.randn(N, H, W, Ko, device="cuda") * 1e-3).to(torch.bfloat16)
+    ad = Fp8Act(t.device, e5m2=True)
+    ad.scale.fill_(57344.0 / dy.float().abs().max().item())
+    ad.inv.fill_(1.0 / ad.scale.item())
+    d0 = K.conv3x3_wgrad_fp8(a, dy, act0, ad)
+    d1 = K.conv3x3_wgrad_fp8(t, dy, act0, ad, pro=(sc, sh))
+    assert torch.equal(d0, d1)
