@@ -181,29 +181,41 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
         mu[j] = mean[c]; is[j] = invstd[c]; ms[j] = mscale[c]; mh[j] = mshift[c];
         s[j] = 0.f; q[j] = 0.f;
     }
-    for (int i = t0; i < total; i += gridDim.x * NT) {
+    // software-pipelined: item i + stride's 12 loads are issued before item i's 4 stores (s_waitcnt vmcnt counts
+    // stores too and retires in order: loads issued after the stores waited for them every iteration)
+    struct Item {
+        uint2 pk[2][2];
+        u16x8_t gv[2][2], tv[2][2];
+    };
+    auto load = [&](int i, Item& it) {
         int r = i / CG;
         const int wo = r % Wo; r /= Wo;
         const int ho = r % Ho;
         const int n = r / Ho;
         const bool wn = wo + 1 < Wo, hn = ho + 1 < Ho;
-        uint2 pk[2][2];
-        u16x8_t gv[2][2], tv[2][2];
 #pragma unroll
         for (int da = 0; da < 2; ++da)
 #pragma unroll
             for (int db = 0; db < 2; ++db) {
-                const long o = ((long)(n * Ho + ho + da) * Wo + wo + db) * C + cg * 8;
                 const bool ok = (da == 0 || hn) && (db == 0 || wn);
-                pk[da][db] = make_uint2(0xffffffffu, 0xffffffffu);    // no window index matches 0xff
-                gv[da][db] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                if (ok) {
-                    pk[da][db] = *reinterpret_cast<const uint2*>(idx + o);
-                    gv[da][db] = *reinterpret_cast<const u16x8_t*>(dy + o);
-                }
-                tv[da][db] = *reinterpret_cast<const u16x8_t*>(
+                // rows / columns past the edge read the item's own output (valid address), then are ignored
+                const long o = ((long)(n * Ho + ho + (ok ? da : 0)) * Wo + wo + (ok ? db : 0)) * C + cg * 8;
+                it.pk[da][db] = *reinterpret_cast<const uint2*>(idx + o);
+                it.gv[da][db] = *reinterpret_cast<const u16x8_t*>(dy + o);
+                if (!ok) it.pk[da][db] = make_uint2(0xffffffffu, 0xffffffffu);    // no window index matches 0xff
+                it.tv[da][db] = *reinterpret_cast<const u16x8_t*>(
                     tin + ((long)(n * 2 * Ho + 2 * ho + da) * W + 2 * wo + db) * C + cg * 8);
             }
+    };
+    const int stride = gridDim.x * NT;
+    Item cur, nxt;
+    if (t0 < total) load(t0, cur);
+    for (int i = t0; i < total; i += stride) {
+        load(i + stride < total ? i + stride : i, nxt);
+        int r = i / CG;
+        const int wo = r % Wo; r /= Wo;
+        const int ho = r % Ho;
+        const int n = r / Ho;
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -217,10 +229,10 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
                     for (int db = 0; db <= b; ++db) {
                         const uint32_t want = (uint32_t)((a + 1 - 2 * da) * 3 + (b + 1 - 2 * db));
                         float g[8];
-                        unpack8(gv[da][db], g);
+                        unpack8(cur.gv[da][db], g);
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
-                            const uint32_t word = j < 4 ? pk[da][db].x : pk[da][db].y;
+                            const uint32_t word = j < 4 ? cur.pk[da][db].x : cur.pk[da][db].y;
                             if (((word >> (8 * (j & 3))) & 0xffu) == want) acc[j] += g[j];
                         }
                     }
@@ -229,7 +241,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
                     packed;
                 float g[8], tv8[8];
                 unpack8(packed, g);                          // the stored (bf16) gradient, as a separate pass reads it
-                unpack8(tv[a][b], tv8);
+                unpack8(cur.tv[a][b], tv8);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float gm = fmaf(tv8[j], ms[j], mh[j]) > 0.f ? g[j] : 0.f;
@@ -237,6 +249,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
                     q[j] += gm * (tv8[j] - mu[j]) * is[j];
                 }
             }
+        cur = nxt;
     }
     const int t = threadIdx.x, RPI = NT / CG;
 #pragma unroll
@@ -330,7 +343,7 @@ PDNN_API int pdnn_maxpool_bwd_bnred_rows(int N, int Ho, int Wo, int C) {
     if ((long)N * 4 * Ho * Wo * C >= (1L << 31)) return 0;
     const long work = (long)N * Ho * Wo * (C / 8);
     long g = (work + NT - 1) / NT;
-    return (int)(g < 1 ? 1 : g > 768 ? 768 : g);         // one wave of blocks: 140 VGPRs = 3 blocks per CU
+    return (int)(g < 1 ? 1 : g > 512 ? 512 : g);         // one wave of blocks: 174 VGPRs = 2 blocks per CU
 }
 
 // dy [N][Ho][Wo][C], idx its window bytes, t [N][2Ho][2Wo][C] (pre-BN) -> dx (pooled gradient, same shape

@@ -332,7 +332,8 @@ PDNN_API int pdnn_bn_relu_maxpool(const bf16_t* t, const float* scale, const flo
                                   int N, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
     if (C % 8 || Ho != (H + 2 - 3) / 2 + 1 || Wo != (W + 2 - 3) / 2 + 1) return (int)hipErrorInvalidValue;
     const long work = (long)N * Ho * Wo * (C / 8);
-    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(stream_grid(work, 256)), dim3(256), 0, st, t, scale, shift, y,
+    // one item per thread (no grid-stride loop: a thread's next item's 9 loads would wait for its 2 stores)
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3((unsigned)cdiv(work, 256)), dim3(256), 0, st, t, scale, shift, y,
                        idx, N, H, W, C, Ho, Wo);
     PDNN_LAUNCH_RET;
 }
