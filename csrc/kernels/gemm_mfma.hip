@@ -801,9 +801,12 @@ template <int BNW>
 int tiles_of(const GemmArgs& a) { return (int)(cdiv(a.M, BMt) * cdiv(a.N, BNW)); }
 
 int pick_splits(const GemmArgs& a, int ktiles, int tiles, int max_splits) {
-    // enough workgroups to cover 256 CUs twice (r2 sweep: 256 / 384 -2% / -1%, 768 equal), but keep >= 4
-    // K-steps per split
-    const int blocks = 512;
+    // about one workgroup per CU, but keep >= 4 K-steps per split.  These are the atomic-epilogue weight
+    // gradients (stride-2 3x3, the largest 1x1s) on the side stream: every split adds its tile into dW with
+    // float atomics, so fewer splits mean fewer L2 atomics competing with the compute stream (ResNet-50 same
+    // box: 256 vs 512 +0.3..+0.7% in 4 pairs, 384 equal, 128 -1.2..-1.8%, 1024 -0.2%; gpurun_out/r4_59-60;
+    // the r2 sweep that chose 512 predates the two-stream schedule)
+    const int blocks = 256;
     int want = (blocks + tiles - 1) / tiles;
     int s = want < max_splits ? want : max_splits;
     int cap = ktiles / 4;
