@@ -496,7 +496,10 @@ void w3_plan(int P, int C, int Ko, int& tiles, int& cch, int& G) {
     tiles = (P + W3_BM - 1) / W3_BM;
     cch = C / 64;
     const int pairs = (Ko / 64) * cch;
-    G = (256 + pairs - 1) / pairs;               // ~one block per CU in total
+    // ~128 blocks in total (half the CUs): the kernel runs on the side stream beside the data-gradient chain, and a
+    // smaller grid leaves more of the chip to it (ResNet-50 same box: 128 vs 256 blocks +0.6..+0.7%, 64 +0.1..+0.3%
+    // more, 512 -1%; gpurun_out/r4_61-62)
+    G = (128 + pairs - 1) / pairs;
     if (G > tiles) G = tiles;
     if (G < 1) G = 1;
 }
