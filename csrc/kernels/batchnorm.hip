@@ -634,6 +634,15 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(
     }
 }
 
+// BN apply / BN-backward apply: 512 blocks (2 per CU), each thread row walking many rows through the
+// software pipeline; the generic 2048-block stream grid ran ResNet-50 2.7% slower, 1024 1.3% slower, 256 2% slower
+// (profiles/resnet50_bn_grid_r4.txt, gpurun_out/r4_65-67)
+inline unsigned bn_stream_grid(long work) {
+    long g = (work + NT - 1) / NT;
+    if (g > 512) g = 512;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
 inline unsigned reduce_grid(long L, int C) {
     const int rpi = NT / (C / 8);
     long g = (L + rpi * BN_RMIN - 1) / (rpi * BN_RMIN);   // >= BN_RMIN rows per thread-row
@@ -701,7 +710,7 @@ PDNN_API int pdnn_bn_stats(const bf16_t* x, long L, int C, float* slab, hipStrea
 PDNN_API int pdnn_bn_apply(const bf16_t* x, long L, int C, const float* scale, const float* shift,
                            const bf16_t* res, const float* rscale, const float* rshift, int relu, bf16_t* y,
                            uint8_t* mbits, hipStream_t st) {
-    const dim3 grid(stream_grid(L * (C / 8), NT));
+    const dim3 grid(bn_stream_grid(L * (C / 8)));
 #define PDNN_BA(RES, RSC, RELU, MASK)                                                                  \
     hipLaunchKernelGGL((bn_apply_kernel<RES, RSC, RELU, MASK>), grid, dim3(NT), 0, st, x, L, C, scale, shift, res, \
                        rscale, rshift, y, mbits)
@@ -770,7 +779,7 @@ PDNN_API int pdnn_bn_bwd_apply(const bf16_t* g, const bf16_t* x, long L, int C, 
                                const float* mshift, bf16_t* dx, const bf16_t* x2, const float* mean2,
                                const float* invstd2, const float* gamma2, const float* dgamma2,
                                const float* dbeta2, bf16_t* dx2, bf16_t* gm_out, hipStream_t st) {
-    const dim3 grid(stream_grid(L * (C / 8), NT));
+    const dim3 grid(bn_stream_grid(L * (C / 8)));
 #define PDNN_BWA(MODE, X2, DX, GMO)                                                                              \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MODE, X2, DX, GMO>), grid, dim3(NT), 0, st, g, x, L, C, mean, invstd, \
                        gamma, dgamma, dbeta, msrc, mscale, mshift, dx, x2, mean2, invstd2, gamma2, dgamma2,      \

@@ -112,6 +112,6 @@ __host__ __device__ constexpr inline long cdiv(long a, long b) { return (a + b -
 inline unsigned stream_grid(long work_items, int per_block) {
     long g = (work_items + per_block - 1) / per_block;
     if (g < 1) g = 1;
-    if (g > 2048) g = 2048;
+    if (g > 512) g = 512;   // 2 blocks per CU walking the grid-stride loop: GPT-2 +0.4%, ResNet-50 flat vs 2048 (r4_68)
     return (unsigned)g;
 }
