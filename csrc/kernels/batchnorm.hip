@@ -29,9 +29,10 @@ constexpr int NT = 256;
 #define PDNN_BN_UR 2
 #endif
 // Minimum rows per thread-row of a statistics reduction (more blocks for the narrow, short late layers:
-// ResNet-50 layer4 has only 12544 rows of 2048 channels at bs256).
+// ResNet-50 layer4 has only 12544 rows of 2048 channels at bs256); 32 with the 512-block cap of reduce_grid:
+// ResNet-50 +1.0% over 64 / 1024 (profiles/resnet50_bn_grid_r4.txt, gpurun_out/r4_70-71)
 #ifndef PDNN_BN_RMIN
-#define PDNN_BN_RMIN 64
+#define PDNN_BN_RMIN 32
 #endif
 // wide-grid slab finalize (bn_slab_level1 + bn_slab_final); 0 = the older slab_reduce + finalize path
 #ifndef PDNN_BN_WIDE_FIN
@@ -646,7 +647,7 @@ inline unsigned bn_stream_grid(long work) {
 inline unsigned reduce_grid(long L, int C) {
     const int rpi = NT / (C / 8);
     long g = (L + rpi * BN_RMIN - 1) / (rpi * BN_RMIN);   // >= BN_RMIN rows per thread-row
-    if (g > 1024) g = 1024;
+    if (g > 512) g = 512;
     if (g < 1) g = 1;
     return (unsigned)g;
 }

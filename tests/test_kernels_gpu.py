@@ -364,8 +364,10 @@ def test_conv_dgrad_fused_bn_backward_and_residual(K, shape):
     assert rel(gm, gm_ref) < 1.5e-2
     sums = slab.view(-1, 2, C).sum(0)
     xh = (t.float() - mean) * inv
-    assert torch.allclose(sums[0], gm_ref.reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
-    assert torch.allclose(sums[1], (gm_ref * xh).reshape(-1, C).sum(0), atol=5e-2, rtol=1e-2)
+    # norm-relative: the reference sums bf16-rounded gm, the kernel its fp32 values, so a channel whose sum
+    # lands near zero can miss any per-element atol (unseeded inputs; r4_71)
+    assert rel(sums[0], gm_ref.reshape(-1, C).sum(0)) < 1e-2
+    assert rel(sums[1], (gm_ref * xh).reshape(-1, C).sum(0)) < 1e-2
 
 
 @pytest.mark.parametrize("shape", [(16, 28, 28, 128, 512, False), (16, 28, 28, 512, 128, True),
