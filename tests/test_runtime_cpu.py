@@ -154,10 +154,19 @@ def test_native_ps_backup_workers_with_evaluator(tmp_path):
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_role, args=("master", srv.port, 0, nprocs, ncollect, iters, out))]
     ps.append(ctx.Process(target=_role, args=("evaluator", srv.port, 1, nprocs, ncollect, iters, out)))
-    ps += [ctx.Process(target=_role, args=("worker", srv.port, r, nprocs, ncollect, iters, out)) for r in range(2, nprocs)]
+    workers = [ctx.Process(target=_role, args=("worker", srv.port, r, nprocs, ncollect, iters, out))
+               for r in range(2, nprocs)]
     try:
         for p in ps:
             p.start()
+        # the evaluator scores the newest model it finds: start the workers only once it is connected (its
+        # output file is open), or under load the whole run can finish first and leave it one row to write
+        deadline = time.time() + 60
+        while not any(f.startswith("time_loss_out_") for f in os.listdir(tmp_path)) and time.time() < deadline:
+            time.sleep(0.05)
+        for p in workers:
+            p.start()
+        ps += workers
         for p in ps:
             p.join(120)
             assert p.exitcode == 0
