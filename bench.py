@@ -126,6 +126,9 @@ def main():
                     help="at --gpus 1, skip the second measurement of the DDP code path")
     ap.add_argument("--diag-steps", type=int, default=5,
                     help="DDP path: extra steps after the timed region with per-bucket communication timing")
+    ap.add_argument("--hang-timeout", type=float, default=90.0,
+                    help="N > 1: hang watchdog (s without a completed step; the process-group timeout is 1.25x): "
+                         "on a hang every rank prints one diagnostic JSON line and exits 75")
     a = ap.parse_args()
 
     from pytorch_distributed_nn_amd.parallel import runtime
@@ -134,9 +137,18 @@ def main():
     from pytorch_distributed_nn_amd.optim import SGD, AdamW, flatten_module
     from pytorch_distributed_nn_amd.ops import functional as OF
 
-    env = runtime.init_process_group()
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    # PDNN_BENCH_BACKEND: tests only (world 2 over gloo on a one-GPU box or on the CPU)
+    backend = os.environ.get("PDNN_BENCH_BACKEND") or None
+    env = runtime.init_process_group(backend=backend, device="cpu" if backend == "gloo" and not torch.cuda.is_available()
+                                      else None, timeout_s=1.25 * a.hang_timeout if multi else 600.0)
     world = runtime.world_size()
     dev = runtime.device()
+    on_gpu = dev.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
     torch.manual_seed(1234 + env.rank)
 
     lm = a.model.lower().startswith("gpt2")
@@ -168,7 +180,8 @@ def main():
     else:
         opt = SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5)
         B, S = a.batch or (128 if small else 256), in_chw[-1]
-        xs = [torch.randn(B, *in_chw, device=dev).to(torch.bfloat16) for _ in range(2)]
+        # bf16 images on the GPU; fp32 on the CPU (the gloo test rehearsal of the N > 1 path: torch's CPU convs)
+        xs = [torch.randn(B, *in_chw, device=dev).to(torch.bfloat16 if on_gpu else torch.float32) for _ in range(2)]
         ys = [torch.randint(0, nc, (B,), device=dev) for _ in range(2)]
 
     # auto: graphed on one GPU, except the ImageNet ResNets, whose weight gradients run on a side stream
@@ -204,6 +217,32 @@ def main():
     # The side-stream ResNets run their compute stream at high priority (the side stream stays at the default,
     # lowest one): the wavefront dispatcher then fills the CUs with the critical-path data-gradient chain first
     # and the weight gradients take the gaps (+0.5% on ResNet-50, gpurun_out/r2_35).
+    watchdog = None
+    if world > 1:
+        # a collective that never completes must not eat the driver's whole run: no step completed for
+        # --hang-timeout seconds -> one JSON line per rank saying where it stood, then exit 75 (no re-exec)
+        from pytorch_distributed_nn_amd.parallel.watchdog import EXIT_HANG, CommWatchdog
+
+        def on_hang(rec):
+            diag = {"metric": "hang", "error": f"no step completed for {rec['idle_s']} s", "rank": env.rank,
+                    "world": world, "last_step_completed": rec["step"], "exit_code": EXIT_HANG,
+                    "abort": rec.get("abort")}
+            if isinstance(net, DistributedDataParallel):
+                diag.update({("ddp_" + k if k == "step" else k): v for k, v in net.progress().items()})
+            print(json.dumps(diag), flush=True)
+        watchdog = CommWatchdog(timeout_s=a.hang_timeout, rank=env.rank, on_hang=on_hang).start()
+    hang_at = int(os.environ.get("PDNN_BENCH_HANG_STEP", "-1"))       # tests: this step of the last rank never ends
+    base_step = step
+
+    def step(i):                                                        # noqa: F811
+        if i == hang_at and env.rank == world - 1:
+            while True:
+                time.sleep(1)
+        loss = base_step(i)
+        if watchdog is not None:
+            watchdog.beat(i)
+        return loss
+
     ctx = contextlib.nullcontext()
     if side_overlap and dev.type == "cuda":
         main_stream = torch.cuda.Stream(device=dev, priority=-1)
@@ -213,12 +252,12 @@ def main():
         for i in range(a.warmup):
             loss = step(i)
         runtime.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            loss = step(i)
+            loss = step(a.warmup + i)
         runtime.barrier()
-        torch.cuda.synchronize()
+        sync()
     dt = time.perf_counter() - t0
     comm = None
     if use_ddp and not use_graph and isinstance(net, DistributedDataParallel) and dev.type == "cuda":
@@ -226,10 +265,15 @@ def main():
         # all-reduce, the exposed tail and the BN-buffer broadcast -- fp32 wire, then bf16 wire
         with ctx:
             comm = comm_diagnostics(net, step, a.diag_steps)
+    if use_ddp and not on_gpu and isinstance(net, DistributedDataParallel):
+        comm = {"bucket_mb": [round(v, 3) for v in net.bucket_sizes_mb()], "world": net.world, "fp32": None,
+                "bf16": None, "note": "per-bucket device timing needs a GPU (CPU rehearsal)"}
     t = torch.tensor([dt], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = t.item()
+    if watchdog is not None:
+        watchdog.stop()
     ms = 1e3 * dt / a.steps
     value = B * world * a.steps / dt
     if getattr(net, "kofn", None) is not None:
@@ -281,7 +325,7 @@ def main():
             "vs_baseline": None,
             "vs_stock_pytorch_rocm": (round(value / (STOCK_PYTORCH_1GPU * world), 4)
                                       if a.model == "resnet50" and B == 256 and not a.fp8 else None),
-            "dtype": "fp8 3x3 convs (e4m3 fwd / e5m2 dgrad) + bf16" if a.fp8 else "bf16",
+            "dtype": "fp8 3x3 convs (e4m3 fwd / e5m2 dgrad) + bf16" if a.fp8 else "bf16" if on_gpu else "fp32 (CPU rehearsal)",
             "data": f"synthetic (device-resident random {in_chw[1]}x{in_chw[2]}x{in_chw[0]} images, random labels), "
                     "random-init weights",
             "final_loss": round(float(loss.detach()), 4),

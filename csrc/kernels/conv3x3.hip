@@ -674,7 +674,7 @@ int c3r_launch(const C3Args& a, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)conv3x3_w64_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
         attr_done = sm;
     }
-    const int grid = a.tiles < 256 ? a.tiles : 256;        // one persistent block per CU
+    const int grid = a.tiles < grid_cus() ? a.tiles : grid_cus();     // one persistent block per CU
     hipLaunchKernelGGL((conv3x3_w64_kernel<EPI>), dim3(grid), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }

@@ -547,16 +547,6 @@ gemm_glds_kernel(GemmArgs a) {
     }   // tile loop
 }
 
-inline int device_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    }
-    return n;
-}
-
 template <int AM, int BMODE, int EM, int BN, int DT = 0>
 int launch_glds_w(const GemmArgs& a, int splits, hipStream_t st, int batch) {
     constexpr int NTH = GWaves<BN>::WM * GWaves<BN>::WN * 64;

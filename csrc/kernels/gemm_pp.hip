@@ -706,15 +706,8 @@ using C8_96 = PPC<96, 2, 3, 1>;
 
 long long* g_pp_trace = nullptr;
 
-int device_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    }
-    return n;
-}
+// CUs a persistent grid fills (all of them unless RCCL channels are reserved: tuning.h comm_cus)
+int device_cus() { return grid_cus(); }
 
 
 template <class C, int FX>

@@ -300,7 +300,8 @@ PDNN_API int pdnn_stem_conv(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nim
         (void)hipFuncSetAttribute((const void*)stem7_kernel<C3_PLAIN>, hipFuncAttributeMaxDynamicSharedMemorySize, sm);
         attr = true;
     }
-    int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
+    const int cap = 2 * grid_cus();                    // two persistent blocks per CU
+    int grid = a.tiles < cap ? a.tiles : cap;
     grid = (grid + 7) / 8 * 8;
     if (stats) hipLaunchKernelGGL(stem7_kernel<C3_STATS>, dim3(grid), dim3(256), sm, st, a, g);
     else hipLaunchKernelGGL(stem7_kernel<C3_PLAIN>, dim3(grid), dim3(256), sm, st, a, g);
@@ -321,7 +322,8 @@ PDNN_API int pdnn_stem_conv_nchw(const bf16_t* x, const bf16_t* w, bf16_t* y, in
     a.stats = stats;
     StemGeo g{H, W, Ho, Wo, make_fdiv_stem(Wo), make_fdiv_stem(Ho)};
     const int sm = STEM_R * 64 * 32 * 2;              // 28 KB
-    int grid = a.tiles < 512 ? a.tiles : 512;          // two persistent blocks per CU
+    const int cap = 2 * grid_cus();                    // two persistent blocks per CU
+    int grid = a.tiles < cap ? a.tiles : cap;
     grid = (grid + 7) / 8 * 8;
     if (stats) hipLaunchKernelGGL(stem7n_kernel<C3_STATS>, dim3(grid), dim3(256), sm, st, a, g);
     else hipLaunchKernelGGL(stem7n_kernel<C3_PLAIN>, dim3(grid), dim3(256), sm, st, a, g);

@@ -17,7 +17,11 @@ namespace pg {
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
     X(pp_dgrad_bn_k, 1024, "1x1 data gradients with the BN-backward epilogue on the ping-pong engine from this "   \
-                           "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")
+                           "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")                 \
+    X(comm_cus, 16, "CUs the persistent grids (ping-pong GEMMs, stem) leave free for RCCL's channel blocks while " \
+                    "a multi-rank process group is live (set_comm_world > 1; 0 = fill the chip). A persistent block " \
+                    "holds its CU for the whole kernel, so a bucket all-reduce issued beside it would wait for the " \
+                    "GEMM to drain; 16 = 2 per XCD (unmeasured at N > 1: no multi-GPU box this round)")
 
 struct Tune {
 #define PDNN_TUNE_FIELD(n, d, doc) int n = d;
@@ -26,5 +30,10 @@ struct Tune {
 };
 
 Tune& tune();     // the process-wide table (PDNN_TUNE applied on first use)
+
+// CUs a persistent grid may fill: the device's CU count, minus tune().comm_cus while the process is one rank of
+// a multi-rank job (pdnn_set_comm_world), rounded down to whole XCDs (8 on gfx950) so the blockIdx -> XCD
+// round-robin stays balanced
+int grid_cus();
 
 }  // namespace pg

@@ -50,6 +50,23 @@ Tune& tune() {
     return t;
 }
 
+namespace {
+int g_comm_world = 1;
+}
+
+int grid_cus() {
+    static int hw = 0;
+    if (!hw) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&hw, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || hw <= 0) hw = 256;
+    }
+    int n = hw;
+    if (g_comm_world > 1 && tune().comm_cus > 0) n -= tune().comm_cus;
+    n = (n / 8) * 8;
+    return n < 8 ? 8 : n;
+}
+
 }  // namespace pg
 
 // old value, or INT32_MIN for an unknown name
@@ -60,6 +77,16 @@ PDNN_API int pdnn_tune_set(const char* name, int value) {
     *f = value;
     return old;
 }
+
+// world size of the process group the caller's collectives run on (1 = no concurrent RCCL kernels to make room
+// for); returns the previous value
+PDNN_API int pdnn_set_comm_world(int world) {
+    const int old = pg::g_comm_world;
+    pg::g_comm_world = world < 1 ? 1 : world;
+    return old;
+}
+
+PDNN_API int pdnn_grid_cus() { return pg::grid_cus(); }
 
 PDNN_API int pdnn_tune_get(const char* name) {
     int* f = pg::field(pg::tune(), name);

@@ -56,6 +56,8 @@ _SIGS = {
     "pdnn_tune_list": [ctypes.c_char_p, I],
     "pdnn_tune_error": [],
     "pdnn_tune_unknown": [],
+    "pdnn_set_comm_world": [I],
+    "pdnn_grid_cus": [],
     "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],

@@ -166,6 +166,17 @@ def tune_get(key: str) -> int:
     return v
 
 
+def set_comm_world(world: int) -> int:
+    """Tell the kernels how many ranks this process's collectives span: above 1, the persistent grids leave
+    ``tune_get("comm_cus")`` CUs to RCCL's channel blocks (csrc/kernels/tuning.h).  Returns the previous value."""
+    return lib().pdnn_set_comm_world(int(world))
+
+
+def grid_cus() -> int:
+    """CUs a persistent grid fills under the current comm world and dispatch table."""
+    return lib().pdnn_grid_cus()
+
+
 def tune_table():
     """[(key, value, default, doc)] of the kernel-side dispatch table."""
     import ctypes

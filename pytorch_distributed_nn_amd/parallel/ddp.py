@@ -201,6 +201,13 @@ def warm_abort_path(exc_type=None):
         h.remove()
 
 
+def _work_done(w):
+    try:
+        return bool(w.is_completed())
+    except Exception:
+        return False
+
+
 def _is_nccl(pg):
     try:
         return dist.get_backend(pg) == "nccl"
@@ -247,8 +254,15 @@ class DistributedDataParallel(nn.Module):
         self.grad_scale_dev = None
         self._buffers_list = [b for b in module.buffers() if b is not None and b.numel() > 0]
         self._bn_views = False
+        self._bn_work = None             # buffer broadcast issued at the end of the last backward (see forward)
         if self._comm and self.broadcast_buffers:
             self._flatten_bn_buffers()
+        if self._comm and self.world > 1 and self.flat.data.is_cuda:
+            # RCCL's channel blocks run beside the backward: the persistent GEMM grids leave them CUs
+            # (csrc/kernels/tuning.h comm_cus)
+            from ..ops import _backend, kernels as K
+            if _backend.available():
+                K.set_comm_world(self.world)
         self._broadcast_init()
         self._build_buckets(bucket_cap_mb, first_bucket_cap_mb)
         self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
@@ -413,7 +427,9 @@ class DistributedDataParallel(nn.Module):
     def _op(self):
         if self.straggler_mode or not self.average:
             return dist.ReduceOp.SUM
-        return dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
+        # one rank: the average IS the sum, and RCCL runs an in-place one-rank SUM as a no-op, where AVG launched
+        # a scale-by-1 pass over every bucket (0.42 ms of HBM traffic per ResNet-50 step, BENCH_r04 comm block)
+        return dist.ReduceOp.AVG if self.nccl and self.world > 1 else dist.ReduceOp.SUM
 
     def _launch(self, b, zero=False):
         # Fused ResNet blocks write weight gradients on a side stream and do not join it back before announcing
@@ -507,6 +523,7 @@ class DistributedDataParallel(nn.Module):
             cnt = torch.tensor(self._contrib, dtype=torch.float32, pin_memory=fp.grad.is_cuda)
             cnt = cnt.to(fp.grad.device, non_blocking=True)
             self._works.append((-1, dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
+        self._issue_buffer_broadcast()
         for b, w in self._works:
             w.wait()
         if ev_bwd is not None and self._ev_start:
@@ -551,13 +568,46 @@ class DistributedDataParallel(nn.Module):
         if self.kofn is not None:
             self.kofn.stop()
 
+    def _buffer_sync_due(self):
+        return (self.broadcast_buffers and self._comm and self.module.training
+                and self._fwd_count % self.buffer_sync_interval == 0)
+
+    @torch.no_grad()
+    def _issue_buffer_broadcast(self):
+        """End of a backward: broadcast rank 0's BatchNorm buffers for the NEXT training forward now, behind the
+        last gradient bucket on the communicator's stream.  Only the forward changes the buffers, so their
+        values here equal those at the next forward's start (where the reference broadcasts them,
+        data_parallel_dist.py:133-138); issued here, the collective overlaps the optimizer step instead of
+        being a cross-rank sync point in front of the forward's first kernel, and forward() only makes its
+        stream wait for it (a device-side wait on RCCL).  The int64 step counters and any non-BN buffers keep
+        the forward-time path."""
+        self._bn_work = None
+        if not (self._bn_views and self._buffer_sync_due()) or self._buffers_list:
+            return
+        works = [dist.broadcast(flat, 0, group=self.pg, async_op=True)
+                 for key, flat in self._buf_flat.items() if isinstance(key, tuple) and key[0] == "bn"]
+        self._bn_work = (works, self._fwd_count)
+
     def forward(self, *args, **kwargs):
         """Raises :class:`StepAborted` when k-of-n closed this step during the forward (after the step's
         collectives have completed with a zero contribution from this rank): skip the loss and backward and
         go on to the optimizer step, as after ``backward(loss)`` returned True."""
         if self.broadcast_buffers and self._comm and self.module.training:
             if self._fwd_count % self.buffer_sync_interval == 0:
-                if self.comm_timing and self.flat.grad.is_cuda:
+                pre = self._bn_work
+                self._bn_work = None
+                if pre is not None and pre[1] == self._fwd_count:
+                    # issued after the last backward: the stream waits, the host does not.  Timed: the compute
+                    # stream's stall on it (0 when it finished during the optimizer step)
+                    timed = self.comm_timing and self.flat.grad.is_cuda
+                    if timed:
+                        self._ev_bn = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                        self._ev_bn[0].record()
+                    for w in pre[0]:
+                        w.wait()
+                    if timed:
+                        self._ev_bn[1].record()
+                elif self.comm_timing and self.flat.grad.is_cuda:
                     self._ev_bn = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     self._ev_bn[0].record()
                     self._broadcast_buffers()
@@ -580,6 +630,17 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._in_fwd = False
 
+    def progress(self):
+        """Where this rank's gradient communication stands, without blocking (a hang watchdog reads it from its
+        own thread): the step being reduced, the buckets launched so far in it, and the last bucket whose
+        collective has completed (``Work.is_completed`` is a query, not a wait)."""
+        works = list(self._works)
+        done = [b for b, w in works if b >= 0 and _work_done(w)]
+        return {"step": self.step, "in_backward": self._armed, "buckets": len(self.buckets),
+                "last_bucket_launched": self.launch_order[-1] if self.launch_order else None,
+                "last_bucket_completed": max(done) if done else None,
+                "buckets_in_flight": [b for b, w in works if b >= 0 and b not in done]}
+
     def sync_buffers(self):
         """Broadcast rank 0's buffers now (e.g. before evaluation or a checkpoint: the last training forward
         updated every rank's BN running statistics with its own batch)."""
@@ -595,7 +656,9 @@ class DistributedDataParallel(nn.Module):
         """Per logged step (``comm_timing=True``): ``bucket_ms`` (per bucket, ready -> all-reduced),
         ``bucket_ready_ms`` / ``bucket_done_ms`` (from the first gradient hook), ``bwd_end_ms`` (last backward
         kernel, both streams), ``tail_ms`` (last bucket done minus the backward's end: the exposed
-        communication) and ``bn_bcast_ms`` (the forward's BatchNorm-buffer broadcast).  Synchronises."""
+        communication) and ``bn_bcast_ms`` (what the BatchNorm-buffer broadcast cost the forward's stream: the
+        whole collective when issued at the forward, the stall on it when it was issued after the previous
+        backward).  Synchronises."""
         out = []
         for r in self._ev_log:
             arm = r["arm"]

@@ -77,16 +77,30 @@ class StepAborted(RuntimeError):
 
 
 class _StagedRecv:
-    """irecv of a CUDA tensor over gloo through a host buffer (gloo's p2p moves host memory only)."""
+    """irecv of a CUDA tensor over gloo through a host buffer (gloo's p2p moves host memory only).
+
+    A reused host buffer (``host`` = a ``[buffer, event]`` pair owned by the caller) is not received into again
+    until the asynchronous H2D copy of its previous contents has finished: the pair's event is recorded after
+    that copy and waited on before the next irecv is posted."""
 
     def __init__(self, dst, src, host=None):
         self.dst = dst
-        self.buf = host if host is not None else torch.empty(dst.shape, dtype=dst.dtype, pin_memory=True)
+        self.slot = host
+        if host is not None:
+            if host[1] is not None:
+                host[1].synchronize()
+            self.buf = host[0]
+        else:
+            self.buf = torch.empty(dst.shape, dtype=dst.dtype, pin_memory=True)
         self.work = dist.irecv(self.buf, src)
 
     def wait(self):
         self.work.wait()
         self.dst.copy_(self.buf, non_blocking=True)
+        if self.slot is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.slot[1] = ev
 
 
 class _StagedSend:
@@ -123,7 +137,7 @@ class PSConfig:
     decay_steps: int = 0              # 0 = constant lr
     max_steps: int = 100
     out_dir: str = "outfiles"
-    store_port: int = 0               # 0 = MASTER_PORT + 1
+    store_port: int = 0               # 0 = an ephemeral port chosen by the master's store and published to all ranks
     bucket_cap_mb: float = 4.0        # gradient streaming granularity
     first_bucket_mb: float = 0.25
     compute_times: bool = False       # workers write compute_times_rank<r>.jsonl (TF-04 side channel)
@@ -154,8 +168,24 @@ def staircase_lr(cfg: PSConfig, step: int) -> float:
     return cfg.lr * cfg.lr_decay_factor ** ((step - 1) // cfg.decay_steps)
 
 
-def _store_port(cfg: PSConfig) -> int:
-    return cfg.store_port or int(os.environ.get("MASTER_PORT", "29500")) + 1
+def _start_control_plane(cfg: PSConfig):
+    """Rank 0 starts the native control-plane store and every rank learns its port -> (server or None, port).
+
+    The store binds ``cfg.store_port`` (0: the kernel picks a free port at bind time, so nothing can hold it
+    already) and the real port travels to the other ranks over the process group that is already up.  The
+    reference needs no port at all: its ranks find each other through MPI_COMM_WORLD
+    (MPI_code/src/distributed_nn.cpp:16-24); a fixed ``MASTER_PORT + 1`` raced with gloo's own listeners."""
+    server, err = None, ""
+    if dist.get_rank() == 0:
+        try:
+            server = StoreServer(cfg.store_port)
+        except OSError as e:          # still broadcast, so no rank is left waiting for the port
+            err = str(e)
+    box = [server.port if server is not None else -1, err]
+    dist.broadcast_object_list(box, src=0)
+    if box[0] < 0:
+        raise OSError(f"parameter-server control plane did not start on rank 0: {box[1]}")
+    return server, int(box[0])
 
 
 class _Base:
@@ -173,12 +203,9 @@ class _Base:
         self.n_workers = len(self.workers)
         self.scheme = (f"PS{cfg.comm_type}_k{cfg.num_aggregate}_collect{cfg.n_to_collect or self.n_workers}"
                        f"_of{self.n_workers}{'_shortcircuit' if cfg.shortcircuit else ''}")
-        self._server = None
-        if self.rank == 0:
-            self._server = StoreServer(_store_port(cfg))
-        dist.barrier()
+        self._server, self.store_port = _start_control_plane(cfg)
         self.host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-        self.store = Store(self.host, _store_port(cfg))
+        self.store = Store(self.host, self.store_port)
         self._pending, self._land = {}, {}
 
     # point-to-point transfers: direct on RCCL (and for host tensors); staged through host memory when CUDA
@@ -257,7 +284,9 @@ class PSMaster(_Base):
         self.coord = PSCoordinator(self.n_workers, self.nb, cfg.n_to_collect, cfg.num_aggregate)
         self.opt = make_optimizer(self.flat.params, cfg)
         # one staging slot per (worker, bucket), allocated on first use and reused every step: a receive is
-        # posted the moment its arrival is announced, so the transfers of all workers overlap (the reference
+        # posted the moment its arrival is announced, so the transfers of all workers overlap.  Memory: one fp32
+        # copy of the model per worker on the master's device (plus a pinned host copy when CUDA tensors travel
+        # over gloo) -- ~0.8 GB for ResNet-50 at 8 workers, well inside one MI355X's 288 GB (the reference
         # pre-posts P x (N-1) Irecv(ANY_SOURCE) and Waitany's over them, sync_replicas_master_nn.py:143-150,
         # 275-284; the C++ master 100 per layer, sync_replicas_master_nn.h:163-186)
         self._slots = {}
@@ -283,7 +312,7 @@ class PSMaster(_Base):
         if slot is None:
             s, e, _ = self.buckets[b]
             dev = torch.zeros(e - s, dtype=torch.float32, device=self.flat.grad.device)
-            host = torch.empty(e - s, dtype=torch.float32, pin_memory=True) if self._staged(dev) else None
+            host = [torch.empty(e - s, dtype=torch.float32, pin_memory=True), None] if self._staged(dev) else None
             slot = self._slots[(r, b)] = (dev, host)
         return slot[0], self._irecv(slot[0], r, slot[1])
 
@@ -417,7 +446,7 @@ class PSWorker(_Base):
         self.compute_records = []
         self.sent = []                      # (step, bucket) in send order (tests / timeline)
         self._stop = False
-        self.wstore = Store(self.host, _store_port(cfg))    # the watcher's own connection
+        self.wstore = Store(self.host, self.store_port)     # the watcher's own connection
         from .ddp import warm_abort_path
         warm_abort_path(StepAborted)        # the first exception through autograd costs ~0.3 s once
         self._watcher = threading.Thread(target=self._watch, daemon=True)

@@ -8,11 +8,23 @@ import torch.multiprocessing as mp
 
 
 def free_port():
+    """A port that was free a moment ago (bind-and-close).  Only for launchers that must be given a port up
+    front (torchrun's rendezvous endpoint); :func:`run_world` hosts its store itself instead."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def host_store():
+    """The rendezvous TCPStore, hosted by the test process on a port the kernel assigns at bind time (nothing
+    can already hold it), the way torchrun's agent hosts it for its workers
+    (``TORCHELASTIC_USE_AGENT_STORE=True``: every rank, rank 0 included, connects as a client)."""
+    import datetime
+    import torch.distributed as dist
+    return dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                         timeout=datetime.timedelta(seconds=300))
 
 
 def _to_np(obj):
@@ -39,7 +51,7 @@ def _from_np(obj):
 
 def _entry(rank, world, port, fn, args, q, device="cpu", backend="gloo", env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), **(env or {}))
+                      LOCAL_RANK=str(rank), TORCHELASTIC_USE_AGENT_STORE="True", **(env or {}))
     try:
         import torch
         torch.set_num_threads(1)
@@ -63,7 +75,8 @@ def run_world(fn, world=2, args=(), timeout=180, device="cpu", backend="gloo", e
     and env={"PDNN_FORCE_PG": "1", ...} runs the RCCL path on a one-GPU box."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
+    store = host_store()          # kept alive (and its port held) until every rank has finished
+    port = store.port
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device, backend, env)) for r in range(world)]
     for p in procs:
         p.start()
@@ -79,6 +92,7 @@ def run_world(fn, world=2, args=(), timeout=180, device="cpu", backend="gloo", e
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        del store
     return [out[r] for r in range(world)]
 
 

@@ -360,3 +360,44 @@ def test_kofn_rank_killed_in_forward_stops_before_next_layer():
     for aborted, phase, counts, err, n_entered, n_layers in out[1]:
         assert aborted == "forward" and phase == "forward" and n_entered <= 2 < n_layers, out[1]
     assert all(a is False for a, *_ in out[0])
+
+
+def _bn_buffers_at_forward(rank, world):
+    """Buffers seen by every training forward, recorded by a pre-hook on the wrapped module (after DDP.forward has
+    made them rank 0's): identical on all ranks at every step, although each rank's own forward moves them with its
+    own batch.  From the second forward on they come from the broadcast issued at the end of the previous backward."""
+    import torch.distributed as dist
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    torch.manual_seed(rank)
+    m = build_model("resnet18", 10)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_cap_mb=0.25)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9)
+    seen, pre_issued = [], []
+    m.register_forward_pre_hook(lambda mod, inp: seen.append(torch.cat([b.float().reshape(-1) for b in mod.buffers()])))
+    for step in range(4):
+        g = torch.Generator().manual_seed(100 * step + rank)
+        x, y = torch.randn(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)
+        pre_issued.append(ddp._bn_work is not None)
+        opt.zero_grad()
+        OF.cross_entropy(ddp(x), y).backward()
+        opt.step()
+    same = []
+    for v in seen:
+        allv = [torch.empty_like(v) for _ in range(world)]
+        dist.all_gather(allv, v)
+        same.append(all(torch.equal(a, allv[0]) for a in allv))
+    moved = not torch.equal(seen[0], seen[-1])
+    return same, pre_issued, moved
+
+
+def test_bn_buffer_broadcast_issued_after_backward_keeps_every_forward_semantics():
+    """the BN-buffer broadcast leaves the start of the step (issued behind the last bucket of
+    the previous backward) but every training forward still starts from rank 0's buffers
+    (data_parallel_dist.py:133-138)."""
+    out = run_world(_bn_buffers_at_forward, 2)
+    for same, pre, moved in out:
+        assert all(same) and moved
+        assert pre == [False, True, True, True]

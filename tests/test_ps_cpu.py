@@ -102,6 +102,35 @@ def test_ps_backup_workers_drop_stragglers():
         assert torch.equal(r[1], res[0][1])                         # consistent final weights
 
 
+def _ps_job_port_taken(rank, world, out_dir, steps):
+    """Every rank holds a listening socket on MASTER_PORT + 1 (and + 2) for the whole job: the port the control
+    plane used to take blind.  The job must still run."""
+    import socket
+    held = []
+    for off in (1, 2):
+        s = socket.socket()
+        try:
+            s.bind(("0.0.0.0", int(os.environ["MASTER_PORT"]) + off))
+            s.listen(1)
+            held.append(s)
+        except OSError:       # another rank (or process) holds it already: occupied either way
+            s.close()
+    try:
+        return _ps_job_cfg(rank, world, {"comm_type": "Async"}, out_dir, steps)
+    finally:
+        for s in held:
+            s.close()
+
+
+def test_ps_control_plane_survives_occupied_master_port_plus_one():
+    """the PS store binds an ephemeral port and publishes it over the process group, so a busy
+    MASTER_PORT + 1 cannot stop the job."""
+    out = tempfile.mkdtemp()
+    res = run_world(_ps_job_port_taken, 3, (out, 4))
+    assert len(res[0][0]) == 4 and all(r["count"] == 2 for r in res[0][0])
+    assert torch.equal(res[1][1], res[0][1]) and torch.equal(res[2][1], res[0][1])
+
+
 def test_ps_interval_mode_closes_steps_on_timer():
     """PAR-DP-INTERVAL (TF TimeoutReplicasOptimizer): a step closes interval_ms after its first gradient
     with whatever arrived; a worker slower than the interval is left out."""

@@ -9,7 +9,8 @@ pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
 
 # kernel-side entries -> alternative values
-ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1], "pp_dgrad_bn_k": [512, 1 << 20]}
+ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1], "pp_dgrad_bn_k": [512, 1 << 20],
+       "comm_cus": [0, 64]}
 
 
 def rel(a, b):
@@ -72,10 +73,34 @@ def test_table_lists_every_entry(K):
 @pytest.mark.parametrize("key,value", [(k, v) for k, vs in ALT.items() for v in vs])
 def test_kernel_entry_alternatives(K, key, value):
     old = K.tune_set(key, value)
+    old_world = K.set_comm_world(4) if key == "comm_cus" else None      # the entry acts only at world > 1
     try:
         _battery(K)
     finally:
         K.tune_set(key, old)
+        if old_world is not None:
+            K.set_comm_world(old_world)
+
+
+def test_comm_world_reserves_cus_for_rccl(K):
+    """VERDICT r4 #3b: while a multi-rank process group is live the persistent grids leave comm_cus CUs (whole
+    XCDs' worth, multiple of 8) to RCCL's channel blocks; at world 1 they fill the chip.  The persistent GEMMs and
+    convs must stay exact under the smaller grids (a persistent grid that assumed one block per CU would skip
+    tiles)."""
+    hw = torch.cuda.get_device_properties(0).multi_processor_count
+    assert K.grid_cus() == hw // 8 * 8
+    old = K.set_comm_world(8)
+    try:
+        assert K.grid_cus() == (hw - K.tune_get("comm_cus")) // 8 * 8
+        prev = K.tune_set("comm_cus", 21)
+        try:
+            assert K.grid_cus() == (hw - 21) // 8 * 8
+            _battery(K)
+        finally:
+            K.tune_set("comm_cus", prev)
+    finally:
+        K.set_comm_world(old)
+    assert K.grid_cus() == hw // 8 * 8
 
 
 def _resnet_grads(arch="resnet50"):

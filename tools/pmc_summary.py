@@ -36,6 +36,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--steps", type=int, default=3, help="training steps in the profiled program")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--ledger", action="store_true", help="also print read / written GB per step by kernel family")
     a = ap.parse_args()
     q1 = load(os.path.join(a.dir, "q1_counters.csv"))
     trace = os.path.join(a.dir, "q1_trace.csv")
@@ -71,6 +72,39 @@ def main():
         conf = k["SQ_LDS_BANK_CONFLICT"] / k["SQ_LDS_IDX_ACTIVE"] if k["SQ_LDS_IDX_ACTIVE"] else 0.0
         print(f"{k['t'] / 1e6 / a.steps:8.3f} {k['n'] / a.steps:6.1f} {fl / t / 1e3:8.1f} "
               f"{100 * fl / t * 1e9 / PEAK_BF16:6.1f} {conf:7.3f} {k['rd'] / t:8.0f} {k['wr'] / t:8.0f}  {name[:90]}")
+    if a.ledger:
+        fam = defaultdict(lambda: defaultdict(float))
+        for name, k in by_name.items():
+            f = family(name, k)
+            for c in ("t", "rd", "wr"):
+                fam[f][c] += k[c]
+        print(f"\nbyte ledger per step (rd = 2 x FETCH_SIZE: an upper estimate; wr = WRITE_SIZE)")
+        print(f"{'family':28} {'ms':>7} {'rd GB':>7} {'wr GB':>7} {'GB/s':>6}")
+        tot = defaultdict(float)
+        for f, k in sorted(fam.items(), key=lambda kv: -(kv[1]["rd"] + kv[1]["wr"])):
+            for c in ("t", "rd", "wr"):
+                tot[c] += k[c]
+            print(f"{f:28} {k['t'] / 1e6 / a.steps:7.3f} {k['rd'] / 1e9 / a.steps:7.2f} {k['wr'] / 1e9 / a.steps:7.2f} "
+                  f"{(k['rd'] + k['wr']) / max(k['t'], 1):6.0f}")
+        print(f"{'total':28} {tot['t'] / 1e6 / a.steps:7.3f} {tot['rd'] / 1e9 / a.steps:7.2f} {tot['wr'] / 1e9 / a.steps:7.2f} "
+              f"{(tot['rd'] + tot['wr']) / max(tot['t'], 1):6.0f}")
+
+
+FAMILIES = (("bn_bwd_apply", "BN backward apply"), ("bn_bwd_reduce", "BN backward reduce"),
+            ("bn_apply", "BN apply (fwd)"), ("bn_slab_fused", "BN finalize"), ("bn_stats", "BN statistics"),
+            ("maxpool_bwd_bnred", "stem pool/BN"), ("bn_relu_maxpool", "stem pool/BN"),
+            ("slab_reduce", "split-K / slab reduces"), ("sgd", "optimizer"), ("adam", "optimizer"),
+            ("xent", "loss"), ("copyBuffer", "copies / fills"), ("fill", "copies / fills"),
+            ("avgpool", "pooling"), ("maxpool", "pooling"))
+
+
+def family(name, k):
+    for key, f in FAMILIES:
+        if key in name:
+            return f
+    if k["SQ_INSTS_VALU_MFMA_MOPS_BF16"] > 0 or any(s in name for s in ("gemm", "conv", "stem")):
+        return "MFMA GEMM / conv"
+    return "other"
 
 
 if __name__ == "__main__":
