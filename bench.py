@@ -9,7 +9,10 @@ One process per GPU (RCCL over xGMI for N > 1).  Model: ResNet-50, ImageNet layo
 (NHWC activations, fp32 accumulation, fp32 master weights / BN statistics / gradients), optimizer:
 fused SGD with momentum 0.9 + weight decay, full step timed (forward, backward, bucketed all-reduce,
 optimizer).  Per-GPU batch is fixed as N grows (weak scaling).  Rank 0 prints one JSON line with the
-WHOLE-JOB samples/sec (max step time over ranks).
+WHOLE-JOB samples/sec (max step time over ranks).  Every N runs the DDP code path: at N = 1 the wrapper's
+bucket hooks all-reduce every bucket over a one-rank RCCL process group (BASELINE config 2, "DDP
+world_size=1"), and the plain single-GPU step is measured in a second process and reported beside it
+(``plain_step_1gpu``).
 
 ``--model gpt2_small`` benchmarks BASELINE.json config 4 instead: GPT-2 small (124M, T=1024, vocab
 50304), per-GPU batch 8 sequences, fused AdamW, metric tokens/sec (whole node).
@@ -40,27 +43,22 @@ def native_loaded():
         return []
 
 
-def _ddp_rehearsal(a):
-    """Re-run this benchmark in a child process through the DDP path at world size 1 (PDNN_FORCE_PG +
-    PDNN_DDP_FORCE_COMM: RCCL process group of one rank); returns {value, ms_per_step} or an error note."""
-    import socket
+def _plain_run(a):
+    """Re-run this benchmark in a child process as the plain single-GPU step (no process group, no DDP wrapper);
+    returns {value, ms_per_step} or an error note."""
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    env = dict(os.environ, PDNN_FORCE_PG="1", PDNN_DDP_FORCE_COMM="1", MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    env = {k: v for k, v in os.environ.items() if k not in ("PDNN_FORCE_PG", "PDNN_DDP_FORCE_COMM", "WORLD_SIZE",
+                                                             "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     argv = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.steps), "--warmup",
             str(a.warmup), "--model", a.model, "--bucket-mb", str(a.bucket_mb), "--graph", a.graph,
-            "--ddp-rehearsal"] + (["--batch", str(a.batch)] if a.batch else []) + (["--fp8"] if a.fp8 else [])
+            "--plain"] + (["--batch", str(a.batch)] if a.batch else []) + (["--fp8"] if a.fp8 else [])
     try:
         r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         rec = json.loads(line)
-        return {"value": rec["value"], "ms_per_step": rec["ms_per_step"], "comm": rec.get("comm"),
-                "note": "same step through DDP: bucket hooks + RCCL all-reduce over a 1-rank process group"}
-    except Exception as e:       # never lose the headline line over the rehearsal
+        return {"value": rec["value"], "ms_per_step": rec["ms_per_step"], "hipgraph": rec["config"]["hipgraph"],
+                "note": "same model and step without the DDP wrapper / process group (no bucket hooks, no RCCL)"}
+    except Exception as e:       # never lose the headline line over the second run
         return {"error": f"{type(e).__name__}: {e}"[:200]}
 
 
@@ -120,10 +118,10 @@ def main():
     ap.add_argument("--comm-bf16", action="store_true", help="DDP: all-reduce gradients in bf16 on the wire")
     ap.add_argument("--num-aggregate", type=int, default=0,
                     help="DDP k-of-n straggler mode with this k (control plane + host throttle on every step)")
-    ap.add_argument("--ddp-rehearsal", action="store_true",
-                    help="(internal) the 1-GPU DDP-path run: RCCL process group of one rank, every bucket all-reduced")
-    ap.add_argument("--no-ddp-rehearsal", action="store_true",
-                    help="at --gpus 1, skip the second measurement of the DDP code path")
+    ap.add_argument("--plain", action="store_true",
+                    help="one GPU without the DDP wrapper and process group (the second run of a --gpus 1 bench)")
+    ap.add_argument("--no-ddp-rehearsal", "--no-plain-run", dest="no_plain_run", action="store_true",
+                    help="at --gpus 1, skip the second measurement (the plain step)")
     ap.add_argument("--diag-steps", type=int, default=5,
                     help="DDP path: extra steps after the timed region with per-bucket communication timing")
     ap.add_argument("--hang-timeout", type=float, default=90.0,
@@ -138,6 +136,11 @@ def main():
     from pytorch_distributed_nn_amd.ops import functional as OF
 
     multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if not multi and not a.plain:
+        # BASELINE config 2 is "ResNet-50 bf16 DDP world_size=1": one GPU runs the same DDP code path as eight --
+        # bucket hooks and an RCCL all-reduce of every bucket over a one-rank process group
+        os.environ.setdefault("PDNN_FORCE_PG", "1")
+        os.environ.setdefault("PDNN_DDP_FORCE_COMM", "1")
     # PDNN_BENCH_BACKEND: tests only (world 2 over gloo on a one-GPU box or on the CPU)
     backend = os.environ.get("PDNN_BENCH_BACKEND") or None
     env = runtime.init_process_group(backend=backend, device="cpu" if backend == "gloo" and not torch.cuda.is_available()
@@ -190,7 +193,7 @@ def main():
     # (8,160-8,196 img/s; gpurun_out/r2_32)
     from pytorch_distributed_nn_amd import tuning
     side_overlap = not lm and not small and tuning.get("side_wgrad") == 1
-    use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and world == 1
+    use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and not use_ddp
                                                                    and not side_overlap)
     if use_graph:
         # whole step (fwd + bwd + optimizer [+ RCCL buckets if 'collectives']) replayed as one hipGraph
@@ -282,9 +285,9 @@ def main():
     # configuration); the same step through the DDP code path (bucket hooks, RCCL all-reduce of every bucket
     # over a one-rank process group) is measured in a child process and reported alongside, so a scaling
     # efficiency can be read against either.
-    ddp_rehearsal = None
-    if world == 1 and not use_ddp and not a.no_ddp_rehearsal and not a.ddp_rehearsal and env.rank == 0:
-        ddp_rehearsal = _ddp_rehearsal(a)
+    plain = None
+    if world == 1 and use_ddp and not a.no_plain_run and env.rank == 0:
+        plain = _plain_run(a)
     if lm and env.rank == 0:
         tok = value * S
         print(json.dumps({
@@ -302,8 +305,9 @@ def main():
             "data": "synthetic (device-resident random token ids), random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "native_loaded": native_loaded(),
-            "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
-            "ddp_path_1gpu": ddp_rehearsal,
+            "n1_point": "plain single-GPU step" if not use_ddp else
+                        ("DDP path (1-rank process group: RCCL on a GPU)" if world == 1 else "DDP path"),
+            "plain_step_1gpu": plain,
             "comm": comm,
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
@@ -330,8 +334,9 @@ def main():
                     "random-init weights",
             "final_loss": round(float(loss.detach()), 4),
             "native_loaded": native_loaded(),
-            "n1_point": "plain single-GPU step" if world == 1 and not use_ddp else "DDP path",
-            "ddp_path_1gpu": ddp_rehearsal,
+            "n1_point": "plain single-GPU step" if not use_ddp else
+                        ("DDP path (1-rank process group: RCCL on a GPU)" if world == 1 else "DDP path"),
+            "plain_step_1gpu": plain,
             "comm": comm,
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,

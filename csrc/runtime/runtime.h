@@ -25,6 +25,7 @@ RT_API int pdnn_store_set(void* h, const char* key, const void* val, uint64_t n)
 RT_API int pdnn_store_get(void* h, const char* key, int64_t timeout_ms);
 RT_API int pdnn_store_wait(void* h, const char* key, int64_t timeout_ms);
 RT_API int64_t pdnn_store_add(void* h, const char* key, int64_t delta);
+RT_API int64_t pdnn_store_push(void* h, const char* queue, const void* val, uint64_t n);
 RT_API int pdnn_store_check(void* h, const char* key);
 RT_API int pdnn_store_del(void* h, const char* key);
 RT_API int pdnn_store_keys(void* h, const char* prefix);

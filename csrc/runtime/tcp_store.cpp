@@ -9,7 +9,9 @@
 // Protocol (little endian): request  = u8 op | u32 klen | key | u64 vlen | value
 //                           response = u8 status | u64 len | data
 // ops: SET, GET (blocking up to timeout_ms carried in value), ADD (int64 delta -> new value),
-//      CHECK (exists?), DEL, WAIT (block until key exists), KEYS (newline-joined keys with prefix)
+//      CHECK (exists?), DEL, WAIT (block until key exists), KEYS (newline-joined keys with prefix),
+//      PUSH (append to a queue in ONE round trip: n = ++<key>_n, <key>/<n> = value -> n; the arrival queue of
+//      the parameter server, whose workers used to pay an ADD and a SET per gradient bucket)
 // One server thread per connection; waits are condition-variable based (no polling).
 #include "runtime.h"
 
@@ -37,7 +39,7 @@ constexpr uint64_t kMaxValue = 1ull << 30;        // 1 GiB values (the native ML
 
 namespace {
 
-enum Op : uint8_t { SET = 1, GET = 2, ADD = 3, CHECK = 4, DEL = 5, WAIT = 6, KEYS = 7, PING = 8 };
+enum Op : uint8_t { SET = 1, GET = 2, ADD = 3, CHECK = 4, DEL = 5, WAIT = 6, KEYS = 7, PING = 8, PUSH = 9 };
 enum Status : uint8_t { OK = 0, TIMEOUT = 1, MISSING = 2, ERR = 3 };
 
 bool send_all(int fd, const void* p, size_t n) {
@@ -154,6 +156,20 @@ struct Server {
                     }
                 }
                 reply(fd, OK, out.data(), out.size());
+            } else if (op == PUSH) {
+                int64_t nv;
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    auto& c = kv[key + "_n"];
+                    int64_t cur = 0;
+                    if (c.size() == 8) memcpy(&cur, c.data(), 8);
+                    nv = cur + 1;
+                    c.resize(8);
+                    memcpy(c.data(), &nv, 8);
+                    kv[key + "/" + std::to_string(nv)] = std::move(val);
+                }
+                cv.notify_all();
+                reply(fd, OK, &nv, 8);
             } else if (op == PING) {
                 reply(fd, OK, nullptr, 0);
             } else {
@@ -303,6 +319,14 @@ RT_API int64_t pdnn_store_add(void* h, const char* key, int64_t delta) {
     auto* c = static_cast<Client*>(h);
     std::vector<char> r;
     if (c->rpc(ADD, key, &delta, 8, &r) != 0 || r.size() != 8) return INT64_MIN;
+    int64_t v;
+    memcpy(&v, r.data(), 8);
+    return v;
+}
+RT_API int64_t pdnn_store_push(void* h, const char* queue, const void* val, uint64_t n) {
+    auto* c = static_cast<Client*>(h);
+    std::vector<char> r;
+    if (c->rpc(PUSH, queue, val, n, &r) != 0 || r.size() != 8) return INT64_MIN;
     int64_t v;
     memcpy(&v, r.data(), 8);
     return v;

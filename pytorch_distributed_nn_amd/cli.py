@@ -210,7 +210,7 @@ def main(argv=None):
         return out
 
     net = model
-    if mode == "ddp" and world > 1:
+    if mode == "ddp" and (world > 1 or os.environ.get("PDNN_DDP_FORCE_COMM") == "1"):
         # --straggler-mode: k-of-n kill (--num-aggregate k) or backup workers (--n-to-collect k) and/or a step
         # deadline (--interval-ms) in collective form (parallel/ddp.py)
         kofn = (args.n_to_collect or args.num_aggregate) if args.straggler_mode else 0
@@ -233,8 +233,13 @@ def main(argv=None):
         for p in model.parameters():
             p.register_post_accumulate_grad_hook(lambda _p, d=strag[rank] / 1e3: _t.sleep(d))
 
-    loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world, num_workers=args.num_workers,
-                        seed=args.seed)
+    if args.synthetic and dev.type == "cuda":
+        # synthetic data lives in HBM like bench.py's: the input pipeline is not what is being measured
+        from .data.datasets import DeviceDataLoader
+        loader = DeviceDataLoader(train_ds, args.batch_size, dev, rank=rank, world=world, seed=args.seed, dtype=xdt)
+    else:
+        loader = DataLoader(train_ds, args.batch_size, "cpu", rank=rank, world=world, num_workers=args.num_workers,
+                            seed=args.seed)
 
     hang_at = None
     if args.inject_hang and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0":
@@ -254,6 +259,9 @@ def main(argv=None):
 
         def __len__(self):
             return len(loader)
+
+        def skip(self, n):              # a resume fast-forward: the sampler only (Trainer.train)
+            loader.skip(n)
 
     graph = {"off": False, "on": world == 1, "collectives": "collectives"}[args.graph]
     if strag:                      # per-step host sleeps in grad hooks cannot be replayed from a graph
@@ -275,8 +283,21 @@ def main(argv=None):
         ck = tr.resume(args.resume)
         if ck is not None and rank == 0:
             print(f"resumed from step {tr.step_no} (epoch {tr.epoch})")
-    hist = tr.train(_DevLoader(), epochs=args.epochs, max_steps=args.max_steps, batch_size=args.batch_size,
-                    dataset_size=len(train_ds))
+    import contextlib
+    ctx = contextlib.nullcontext()
+    from . import tuning
+    if dev.type == "cuda" and tuning.get("side_wgrad") == 1:
+        # as bench.py: the fused ResNets' data-gradient chain runs on a high-priority stream, their weight
+        # gradients on the default-priority side stream (ops/fused_resnet.py), so the dispatcher fills the CUs
+        # with the critical path first
+        main_stream = torch.cuda.Stream(device=dev, priority=-1)
+        main_stream.wait_stream(torch.cuda.current_stream(dev))
+        ctx = torch.cuda.stream(main_stream)
+    with ctx:
+        hist = tr.train(_DevLoader(), epochs=args.epochs, max_steps=args.max_steps, batch_size=args.batch_size,
+                        dataset_size=len(train_ds))
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     test_loader = DataLoader(test_ds, min(args.test_batch_size, len(test_ds)), "cpu")
 
     class _TestLoader:

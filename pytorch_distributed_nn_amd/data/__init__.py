@@ -11,8 +11,12 @@
   benchmarks and tests use synthetic data of the real shapes).
 * :class:`DataLoader` — batches from any of the above with a background prefetch thread, pinned host
   memory and async host->device copies (the reference's custom multiprocess loader, PT-11
-  my_data_loader.py:137-319, incl. ``next_batch``).
+  my_data_loader.py:137-319, incl. ``next_batch``); ``skip(n)`` fast-forwards a resumed run without
+  building the skipped batches.
+* :class:`DeviceDataLoader` — the whole dataset in HBM, batches gathered on the device (synthetic data and
+  small datasets; the CLI's ``--synthetic`` path on a GPU).
 * :class:`MNISTDataset` / :class:`Cifar10Dataset` — torch ``Dataset`` wrappers (PT-12).
 """
-from .datasets import (Cifar10Dataset, DataLoader, DataSet, MNISTDataset, SyntheticDataset,  # noqa: F401
+from .datasets import (Cifar10Dataset, DataLoader, DataSet, DeviceDataLoader, MNISTDataset,  # noqa: F401
+                       SyntheticDataset,
                        SyntheticTokens, augment_crop_flip, read_cifar10, read_mnist, write_mnist_like)

@@ -125,6 +125,13 @@ class GPT2(nn.Module):
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, 0.0, 0.02)
 
+    def awaits_params(self, idx, *args, **kwargs):
+        """The fused GPU forward fetches every block's weight shadows through await_param (OF.weight_bf16), so a
+        k-of-n DistributedDataParallel forward is checked before every block without the per-op ParamUseMode
+        dispatch (a PS worker still uses ParamUseMode: its LayerNorm / bias parameters must have
+        ARRIVED before use, which only the per-op hook guarantees)."""
+        return bool(getattr(idx, "is_cuda", False))
+
     def num_params(self, non_embedding=True):
         n = sum(p.numel() for p in self.parameters())
         return n - self.transformer.wpe.weight.numel() if non_embedding else n

@@ -75,8 +75,9 @@ def _wait_prefetch(p):
 def prefetch_fp8_weights(ps, side):
     """Make the e4m3 weights (and tap-flipped copies) of ``ps`` whose cache is stale on the ``side`` stream, at
     the start of a forward: ~17 us of small quantisation / flip kernels per 3x3 conv leave the compute stream
-    (the first fp8 conv waits on one event).  Skipped for parameters still arriving (PS workers: await_param)."""
-    todo = [p for p in ps if "_pdnn_await" not in p.__dict__
+    (the first fp8 conv waits on one event).  Skipped for parameters still arriving (PS workers mark them
+    ``_pdnn_weight_pending``; a k-of-n DDP forward check, which also hooks ``_pdnn_await``, does not)."""
+    todo = [p for p in ps if "_pdnn_weight_pending" not in p.__dict__
             and (getattr(p, "_pdnn_fp8_flip", None) or (None,))[0] != _weight_version(p)]
     if not todo:
         return

@@ -68,6 +68,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
+from ..ops.fused_resnet import side_stream_if_active
 from ..optim.flat import ParamUseMode, flatten_module, register_grad_ready_hook, reverse_buckets
 from ..utils.native import PSCoordinator, Store, StoreServer, StoreTimeout
 
@@ -432,6 +433,8 @@ class PSWorker(_Base):
         super().__init__(model, cfg, device)
         self.loss_fn = loss_fn
         self.delay = cfg.inject_straggler.get(self.rank, 0) / 1e3
+        self._killable = bool(cfg.num_aggregate or cfg.interval_ms
+                              or (cfg.n_to_collect and cfg.n_to_collect < self.n_workers))
         self.cur = 0
         self.abort_step = -1
         self.done_step = 0
@@ -468,6 +471,7 @@ class PSWorker(_Base):
             return []
         for p in self.flat.params:
             p._pdnn_await = self._before_param
+            p._pdnn_weight_pending = True     # weights arrive during the forward: no early fp8 re-quantisation
         return list(self.flat.params)
 
     def _check_armed(self):
@@ -518,16 +522,27 @@ class PSWorker(_Base):
     def _send(self, b):
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
-        if view.is_cuda:
-            # keep the host at most two buckets ahead of the GPU so a kill stops real GPU work
+        if view.is_cuda and self._killable:
+            # keep the host at most two buckets ahead of the GPU so a kill stops real GPU work.  Only where a
+            # kill can happen (k-of-n, backup workers, interval close): under full sync no worker is ever cut
+            # short, and the wait would only hold the host back.  The event is on the compute stream, as in
+            # DistributedDataParallel._launch (the side stream lags by design).
             if len(self._events) >= 2:
                 self._events[-2].synchronize()
             ev = torch.cuda.Event()
             ev.record()
             self._events.append(ev)
-        n = self.store.add("q_n", 1)
-        self.store.set(f"q/{n}", f"{self.rank},{self.cur},{b}")
-        self._works.append(self._isend(view, 0))
+        self.store.push("q", f"{self.rank},{self.cur},{b}")        # one round trip (arrival queue)
+        side = side_stream_if_active(view)
+        if side is None:
+            self._works.append(self._isend(view, 0))
+        else:
+            # fused ResNet blocks leave their weight gradients on the side stream (the hook is side-aware, so
+            # the block does not join it before announcing them): the send is ordered after both streams
+            from ..ops import kernels as K
+            K.stream_wait(side, torch.cuda.current_stream(side.device))
+            with torch.cuda.stream(side):
+                self._works.append(self._isend(view, 0))
         self.sent.append((self.cur, b))
 
     def train(self, batches):
@@ -569,8 +584,7 @@ class PSWorker(_Base):
                                          "compute_ms": 1e3 * (time.perf_counter() - t_deq)})
             # end-of-step marker: the master drains this worker's sends up to it (late ones are dropped); it
             # carries the dequeue -> finish compute time, the master's live per-step ELAPSED TIMES
-            n = self.store.add("q_n", 1)
-            self.store.set(f"q/{n}", f"{self.rank},{s},-1,{self.compute_records[-1]['compute_ms']:.4f}")
+            self.store.push("q", f"{self.rank},{s},-1,{self.compute_records[-1]['compute_ms']:.4f}")
             for w in self._works:
                 w.wait()
         self._stop = True
@@ -636,3 +650,6 @@ def run_ps(model, cfg: PSConfig, device, loss_fn=None, batches=None, eval_fn=Non
         out = role.train(batches)
     role.close()
     return out
+
+
+PSWorker._param_done._pdnn_side_aware = True      # _send orders each bucket after the weight-gradient stream

@@ -65,8 +65,9 @@ def init_process_group(backend: str | None = None, device: str | None = None, ti
     # multi-GPU code path (DDP hooks + RCCL kernels on their stream) that the 8-GPU node runs
     force = os.environ.get("PDNN_FORCE_PG") == "1"
     if (env.world_size > 1 or force) and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", env.master_addr)
-        os.environ.setdefault("MASTER_PORT", str(env.master_port))
+        if env.world_size > 1:
+            os.environ.setdefault("MASTER_ADDR", env.master_addr)
+            os.environ.setdefault("MASTER_PORT", str(env.master_port))
         # dmabuf IPC is the only mode the box's driver supports (see task environment notes)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         be = backend or ("nccl" if use_gpu else "gloo")
@@ -75,7 +76,10 @@ def init_process_group(backend: str | None = None, device: str | None = None, ti
         if be == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
-        if restart not in (None, "", "0"):
+        if env.world_size == 1 and "MASTER_PORT" not in os.environ:
+            # a one-rank group (PDNN_FORCE_PG) needs no rendezvous: an in-process store, no port
+            kw["store"] = dist.HashStore()
+        elif restart not in (None, "", "0"):
             # a restarted worker group (parallel/watchdog.py) may share the launcher's store with the failed
             # attempt: namespace this attempt's keys so no rank reads a dead peer's address
             store, _, _ = next(dist.rendezvous("env://", env.rank, env.world_size,

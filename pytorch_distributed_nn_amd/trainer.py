@@ -56,9 +56,26 @@ class Trainer:
                                           allow_collectives=graph == "collectives")
 
     # ----------------------------------------------------------------------------------------- step
-    def _sync(self):
+    def _mark(self):
+        """A phase boundary: a timing event on the current stream (GPU: read lazily, the host never waits for
+        it) or the host clock (CPU: the ops ran synchronously)."""
         if self.timing:
-            torch.cuda.synchronize(self.device)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    @staticmethod
+    def _phases(marks):
+        """Phase durations (s) between consecutive marks; GPU events are waited for (only the last one)."""
+        if isinstance(marks[0], float):
+            return tuple(b - a for a, b in zip(marks, marks[1:]))
+        marks[-1].synchronize()
+        return tuple(a.elapsed_time(b) / 1e3 for a, b in zip(marks, marks[1:]))
+
+    @staticmethod
+    def _done(marks):
+        return isinstance(marks[-1], float) or marks[-1].query()
 
     def _span(self, name):
         if self.tracer is None:
@@ -67,17 +84,22 @@ class Trainer:
         return self.tracer.span(name)
 
     def step(self, x, y):
-        """One training iteration; returns (loss tensor, logits, phase timings in seconds)."""
-        t0 = time.perf_counter()
+        """One training iteration; returns (loss tensor, logits, phase marks).
+
+        The marks are 4 phase boundaries (start, forward end, backward+all-reduce end, optimizer end): HIP
+        events on a GPU, resolved into durations by :meth:`_phases` only when a record is written, so the host
+        never synchronises inside the step and keeps running ahead of the device (the reference's per-phase
+        Forward / Backward / Step fields, nn_ops/__init__.py:46-85; on a GPU they are device times)."""
         if self.lr_schedule is not None:
             for g in self.opt.param_groups:
                 g["lr"] = self.lr_schedule(self.step_no)
+        m0 = self._mark()
         if self.graph_step is not None:       # whole step is one graph: no per-phase split
             with self._span("graph_step"):
                 loss = self.graph_step(x, y)
-            self._sync()
+            m1 = self._mark()
             self.step_no += 1
-            return loss, self.graph_step.output, (0.0, time.perf_counter() - t0, 0.0)
+            return loss, self.graph_step.output, (m0, m0, m1, m1)
         self.opt.zero_grad()
         kofn = getattr(self.model, "kofn", None) is not None
         with self._span("forward"):
@@ -90,8 +112,7 @@ class Trainer:
                 if not kofn:
                     raise
                 out = loss = None
-        self._sync()
-        t1 = time.perf_counter()
+        m1 = self._mark()
         with self._span("backward+allreduce"):
             if loss is None:
                 pass
@@ -99,31 +120,52 @@ class Trainer:
                 self.model.backward(loss)        # k-of-n DDP: a killed rank skips the rest of its backward
             else:
                 loss.backward()
-        self._sync()
-        t2 = time.perf_counter()
+        m2 = self._mark()
         if self.grad_clip:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip)
         with self._span("optimizer"):
             self.opt.step()
-        self._sync()
-        t3 = time.perf_counter()
+        m3 = self._mark()
         self.step_no += 1
-        return loss, out, (t1 - t0, t2 - t1, t3 - t2)
+        return loss, out, (m0, m1, m2, m3)
 
     # ----------------------------------------------------------------------------------------- loops
+    def _finish(self, pend):
+        """Write the per-step record of a step whose phase marks have resolved."""
+        rec, marks, fetch, t_deq, bs = pend
+        tfw, tbw, topt = self._phases(marks)
+        total = fetch + tfw + tbw + topt
+        rec.update(fetch_ms=1e3 * fetch, forward_ms=1e3 * tfw, backward_ms=1e3 * tbw, opt_ms=1e3 * topt,
+                   samples_per_s=bs * self.world / max(total, 1e-9))
+        self.metrics.log(**rec)
+        self.history.append(rec)
+        if self.compute_log is not None:
+            self.compute_log.log(rank=self.rank, step=rec["step"], t_dequeue=t_deq, t_finish=t_deq + total,
+                                 compute_ms=1e3 * (tfw + tbw + topt))
+        return total
+
     def train(self, loader, epochs: int = 1, max_steps: int | None = None, steps_per_epoch: int | None = None,
               batch_size: int | None = None, dataset_size: int | None = None, skip_consumed: bool = True):
+        from collections import deque
         n_per_epoch = steps_per_epoch or (len(loader) if hasattr(loader, "__len__") else 100)
-        it = iter(loader)
         done = False
         # a resumed run continues at its checkpoint: `epoch` is the epoch in progress (epoch-end checkpoints
         # store the NEXT epoch), and a mid-epoch checkpoint resumes after the steps that epoch already ran
         first_i = max(0, self.step_no - self.epoch * n_per_epoch)
         # the loader is ONE stream across epochs (per-epoch reshuffles included) and a fresh loader restarts it
-        # at its first batch: consume every batch the checkpointed run trained on -- all earlier epochs too, not
-        # only this epoch's -- so the resumed run sees exactly the uninterrupted run's batches
-        for _ in range(self.step_no if skip_consumed else 0):
+        # at its first batch: skip every batch the checkpointed run trained on -- all earlier epochs too, not
+        # only this epoch's (ADVICE r3).  Loaders with skip() move only their sampler (no gather, no copy;
+        # ADVICE r4), and the watchdog is fed meanwhile, so a long fast-forward is not taken for a hang.
+        n_skip = self.step_no if skip_consumed else 0
+        if n_skip and hasattr(loader, "skip"):
+            loader.skip(n_skip)
+            n_skip = 0
+        it = iter(loader)
+        for k in range(n_skip):
             next(it)
+            if self.watchdog is not None and k % 64 == 0:
+                self.watchdog.beat(self.step_no)
+        pending = deque()          # steps whose phase events have not resolved yet (GPU), in step order
         for ep in range(self.epoch, epochs):
             self.epoch = ep
             start, first_i = (first_i if first_i < n_per_epoch else 0), 0
@@ -133,30 +175,32 @@ class Trainer:
                 if x.device != self.device:
                     x, y = x.to(self.device, non_blocking=True), y.to(self.device, non_blocking=True)
                 fetch = time.perf_counter() - tf
-                loss, out, (tfw, tbw, topt) = self.step(x, y)
-                total = fetch + tfw + tbw + topt
+                loss, out, marks = self.step(x, y)
                 bs = x.shape[0]
-                rec = {"step": self.step_no, "epoch": ep, "loss": None, "fetch_ms": 1e3 * fetch,
-                       "forward_ms": 1e3 * tfw, "backward_ms": 1e3 * tbw, "opt_ms": 1e3 * topt,
-                       "samples_per_s": bs * self.world / max(total, 1e-9)}
-                if loss is not None and (self.step_no % self.log_interval == 0 or
-                                         (max_steps and self.step_no >= max_steps)):
+                rec = {"step": self.step_no, "epoch": ep, "loss": None}
+                pending.append((rec, marks, fetch, tf, bs))
+                log_now = loss is not None and (self.step_no % self.log_interval == 0 or
+                                                 (max_steps and self.step_no >= max_steps))
+                if log_now:
                     lv = float(loss.detach())
                     if lv != lv or lv in (float("inf"), float("-inf")):      # TF trainer's NaN assert
                         raise FloatingPointError(f"Model diverged with loss = {lv} at step {self.step_no}")
                     p1 = float(accuracy(out.detach(), y, (1,))[0]) if out.dim() == 2 else float("nan")
                     rec["loss"], rec["prec1"] = lv, p1
+                if log_now:          # once this step has completed on the device: a wall-clock point of the run
+                    if not isinstance(marks[-1], float):
+                        marks[-1].synchronize()
+                    rec["wall_s"] = time.perf_counter()
+                while pending and (log_now or self._done(pending[0][1])):
+                    total = self._finish(pending.popleft())
+                if log_now:
                     seen = (i + 1) * bs
                     tot = dataset_size or n_per_epoch * bs
                     self.print(f"Worker: {self.rank}, Train Epoch: {ep} [{seen}/{tot} ({100.0 * seen / tot:.0f}%)], "
                                f"Train Loss: {lv:.4f}, Time Cost: {total:.4f}, FetchData: {fetch:.4f}, "
-                               f"Forward: {tfw:.4f}, Backward: {tbw:.4f}, Step: {topt:.4f}, "
-                               f"Samples/s: {rec['samples_per_s']:.1f}, Prec@1: {p1:.2f}")
-                self.metrics.log(**rec)
-                self.history.append(rec)
-                if self.compute_log is not None:
-                    self.compute_log.log(rank=self.rank, step=self.step_no, t_dequeue=tf, t_finish=time.perf_counter(),
-                                         compute_ms=1e3 * (tfw + tbw + topt))
+                               f"Forward: {rec['forward_ms'] / 1e3:.4f}, Backward: {rec['backward_ms'] / 1e3:.4f}, "
+                               f"Step: {rec['opt_ms'] / 1e3:.4f}, Samples/s: {rec['samples_per_s']:.1f}, "
+                               f"Prec@1: {p1:.2f}")
                 if self.watchdog is not None:
                     self.watchdog.beat(self.step_no)
                 if (self.checkpoint_dir and self.checkpoint_interval and self.rank == 0
@@ -172,6 +216,8 @@ class Trainer:
                 break
         else:
             self.epoch = max(self.epoch, epochs)
+        while pending:
+            self._finish(pending.popleft())
         if self.tracer is not None:
             self.tracer.save()
         return self.history

@@ -31,6 +31,7 @@ _SIGS = {
     "pdnn_store_get": (_I, [_P, _CP, _L]),
     "pdnn_store_wait": (_I, [_P, _CP, _L]),
     "pdnn_store_add": (_L, [_P, _CP, _L]),
+    "pdnn_store_push": (_L, [_P, _CP, _P, _U64]),
     "pdnn_store_check": (_I, [_P, _CP]),
     "pdnn_store_del": (_I, [_P, _CP]),
     "pdnn_store_keys": (_I, [_P, _CP]),
@@ -159,6 +160,15 @@ class Store:
 
     def add(self, key: str, delta: int = 1) -> int:
         return lib().pdnn_store_add(self.h, key.encode(), delta)
+
+    def push(self, queue: str, value) -> int:
+        """Append to a queue in one round trip: n = ++``<queue>_n``, ``<queue>/<n>`` = value; returns n."""
+        b = value.encode() if isinstance(value, str) else bytes(value)
+        buf = ctypes.create_string_buffer(b, len(b))
+        n = lib().pdnn_store_push(self.h, queue.encode(), buf, len(b))
+        if n == -2 ** 63:
+            raise ConnectionError("store push failed")
+        return n
 
     def check(self, key: str) -> bool:
         return lib().pdnn_store_check(self.h, key.encode()) == 1

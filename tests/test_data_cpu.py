@@ -80,3 +80,29 @@ def test_augmentation_helpers():
     assert len(tx) == 4 and set(ty.tolist()) == {6, 8} and len(vx) == 3
     ax, ay = A.aug_data_set(x, labels, times_expand=3, aug_type="noise", rng=rng)
     assert ax.shape[0] == 18 and len(ay) == 18
+
+
+def _mk_ds():
+    import numpy as np
+    from pytorch_distributed_nn_amd.data.datasets import DataSet
+    x = np.arange(100 * 3, dtype=np.float32).reshape(100, 3)
+    return DataSet(x, np.arange(100), seed=5)
+
+
+@pytest.mark.parametrize("nw", [0, 2])
+@pytest.mark.parametrize("world,rank", [(1, 0), (2, 1)])
+def test_loader_skip_matches_consuming_batches(nw, world, rank):
+    """a resume fast-forwards with DataLoader.skip(n) -- no gather, no pin, no copy -- and must land on
+    exactly the batch the uninterrupted stream would deliver next (epoch reshuffles included: 100 rows, batch 8)."""
+    import time
+    from pytorch_distributed_nn_amd.data.datasets import DataLoader
+    for n in (0, 1, 3, 7, 40):
+        a = DataLoader(_mk_ds(), 8, rank=rank, world=world, num_workers=nw, seed=3)
+        ref = [a.next_batch()[1].tolist() for _ in range(n + 5)][n:]
+        a.close()
+        b = DataLoader(_mk_ds(), 8, rank=rank, world=world, num_workers=nw, seed=3)
+        time.sleep(0.05)                         # let the producers prefetch (skip must drop those)
+        b.skip(n)
+        got = [b.next_batch()[1].tolist() for _ in range(5)]
+        b.close()
+        assert got == ref, (n, got, ref)

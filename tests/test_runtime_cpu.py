@@ -38,6 +38,9 @@ def test_store_basic_and_blocking_get():
         assert sorted(b.keys("kill/3/")) == ["kill/3/1", "kill/3/2"]
         a.delete("k")
         assert not b.check("k")
+        # PUSH: queue append in one round trip, numbered like add("q_n") + set("q/<n>")
+        assert a.push("q", "0,1,2") == 1 and b.push("q", b"3,4,5") == 2
+        assert a.get("q/1") == b"0,1,2" and a.get("q/2") == b"3,4,5" and a.get_int("q_n") == 2
         big = np.random.rand(1 << 18).astype(np.float32)
         a.set("big", big)
         assert np.array_equal(np.frombuffer(b.get("big"), np.float32), big)

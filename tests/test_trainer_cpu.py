@@ -84,3 +84,34 @@ def test_resume_in_later_epoch_sees_the_uninterrupted_batches(tmp_path):
     t2.train(_EpochLoader(), epochs=3)
     assert t2.step_no == 9
     assert torch.equal(t2.model.weight, ref)
+
+
+def test_resume_at_large_step_fast_forwards_without_building_batches(tmp_path):
+    """resuming at step 20,000 must not decode / transform / copy 20,000 batches (the loader skips its
+    sampler), and a short hang watchdog started before train() must not fire during the fast-forward."""
+    import time
+
+    import numpy as np
+
+    from pytorch_distributed_nn_amd.data.datasets import DataLoader, DataSet
+    from pytorch_distributed_nn_amd.parallel.watchdog import CommWatchdog
+    built = []
+
+    def slow_transform(x):          # ~2 ms per built batch: 20,000 of them would take 40 s
+        built.append(1)
+        time.sleep(0.002)
+        return x
+
+    rng = np.random.RandomState(0)
+    ds = DataSet(rng.randn(64, 8).astype(np.float32), rng.randint(0, 4, 64))
+    loader = DataLoader(ds, 4, transform=slow_transform)
+    fired = []
+    wd = CommWatchdog(timeout_s=1.0, rank=0, exit_on_hang=False, on_hang=fired.append, poll_s=0.05).start()
+    t = _trainer(tmp_path, watchdog=wd)
+    t.step_no = 20000
+    t0 = time.perf_counter()
+    t.train(loader, epochs=10 ** 6, steps_per_epoch=16, max_steps=20003)
+    wd.stop()
+    loader.close()
+    assert t.step_no == 20003 and not fired
+    assert time.perf_counter() - t0 < 5.0 and len(built) < 50
