@@ -128,6 +128,14 @@ def main():
                     help="N > 1: hang watchdog (s without a completed step; the process-group timeout is 1.25x): "
                          "on a hang every rank prints one diagnostic JSON line and exits 75")
     a = ap.parse_args()
+    # stdout carries exactly the result line: libraries that print banners to fd 1 from C (RCCL's version block at
+    # communicator init) are sent to stderr with everything else; the JSON lines go to the saved descriptor
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(rec):
+        os.write(out_fd, (json.dumps(rec) + "\n").encode())
 
     from pytorch_distributed_nn_amd.parallel import runtime
     from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
@@ -232,7 +240,7 @@ def main():
                     "abort": rec.get("abort")}
             if isinstance(net, DistributedDataParallel):
                 diag.update({("ddp_" + k if k == "step" else k): v for k, v in net.progress().items()})
-            print(json.dumps(diag), flush=True)
+            emit(diag)
         watchdog = CommWatchdog(timeout_s=a.hang_timeout, rank=env.rank, on_hang=on_hang).start()
     hang_at = int(os.environ.get("PDNN_BENCH_HANG_STEP", "-1"))       # tests: this step of the last rank never ends
     base_step = step
@@ -290,7 +298,7 @@ def main():
         plain = _plain_run(a)
     if lm and env.rank == 0:
         tok = value * S
-        print(json.dumps({
+        emit({
             "metric": "tokens/sec (whole node) GPT-2-small DDP",
             "value": round(tok, 1),
             "unit": "tokens/s",
@@ -313,9 +321,9 @@ def main():
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
                        "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
-        }), flush=True)
+        })
     elif env.rank == 0:
-        print(json.dumps({
+        emit({
             "metric": "samples/sec (whole node) ResNet-50 DDP" if a.model == "resnet50"
                       else f"samples/sec (whole node) {a.model} DDP",
             "value": round(value, 2),
@@ -342,7 +350,7 @@ def main():
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
                        "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
-        }), flush=True)
+        })
     runtime.destroy()
 
 

@@ -8,8 +8,10 @@
 // kernel in a ResNet block is `pdnn_bn_apply` at the block output, which also fuses the residual
 // branch (identity, or the downsample conv's own BN) and the final ReLU.
 //
-// Slab layout shared by every partial-statistics producer: [rows][2][C] fp32 — for partial row i,
-// slab[(2i)*C + c] = sum, slab[(2i+1)*C + c] = sum of squares (or, in backward, sum(g) / sum(g*xhat)).
+// Slab layout shared by every partial-statistics producer: STAT_BINS bins [64][2][C] fp32 (common.h) that the
+// producers ADD their partial rows into (partial row i -> bin i % 64): slab[(2b)*C + c] += sum,
+// slab[(2b+1)*C + c] += sum of squares (or, in backward, sum(g) / sum(g*xhat)).  The finalize reads the 64
+// bins and leaves them zeroed for the next producer.
 //
 // Memory layout: x is [L][C] with L = N*H*W, channel fastest.  Each thread owns 8 consecutive channels
 // (16-byte loads, Guideline 13); C must be a multiple of 8 and C/8 <= 256.
@@ -34,81 +36,7 @@ constexpr int NT = 256;
 #ifndef PDNN_BN_RMIN
 #define PDNN_BN_RMIN 32
 #endif
-// wide-grid slab finalize (bn_slab_level1 + bn_slab_final); 0 = the older slab_reduce + finalize path
-#ifndef PDNN_BN_WIDE_FIN
-#define PDNN_BN_WIDE_FIN 1
-#endif
 constexpr int BN_UR = PDNN_BN_UR, BN_RMIN = PDNN_BN_RMIN;
-
-// Level-1 reduction of a partial-statistics slab [rows][2][C] -> [RB][2][C]: block (cx, ry) sums the
-// rows ry, ry+RB, ... for 64 channels with 4 row lanes (coalesced 256-byte row segments).
-__global__ void __launch_bounds__(NT) slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                          float* __restrict__ out) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
-    const int RB = gridDim.y;
-    __shared__ float red[2][4][64];
-    float s = 0.f, q = 0.f;
-    if (c < C) {
-        for (int r = blockIdx.y + RB * lr; r < rows; r += RB * 4) {
-            s += slab[(long)(2 * r) * C + c];
-            q += slab[(long)(2 * r + 1) * C + c];
-        }
-    }
-    red[0][lr][threadIdx.x & 63] = s;
-    red[1][lr][threadIdx.x & 63] = q;
-    __syncthreads();
-    if (lr == 0 && c < C) {
-        const int l = threadIdx.x;
-        out[(long)(2 * blockIdx.y) * C + c] = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
-        out[(long)(2 * blockIdx.y + 1) * C + c] = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
-    }
-}
-
-// finalize (few) partial rows -> mean, invstd, scale/shift (+ running-stat update), fp64 accumulation.
-// Block = 64 channels x 4 row-lanes (rows strided by 4, combined through LDS).
-__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ slab, int rows, int C, double L,
-                                                         float eps, float momentum, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* run_mean,
-                                                         float* run_var, float* mean_out, float* invstd_out,
-                                                         float* scale_out, float* shift_out) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
-    __shared__ double red[2][4][64];
-    double s = 0.0, q = 0.0;
-    if (c < C)
-        for (int r = lr; r < rows; r += 4) {
-            s += slab[(long)(2 * r) * C + c];
-            q += slab[(long)(2 * r + 1) * C + c];
-        }
-    red[0][lr][threadIdx.x & 63] = s;
-    red[1][lr][threadIdx.x & 63] = q;
-    __syncthreads();
-    if (lr != 0 || c >= C) return;
-    const int l = threadIdx.x;
-    s = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
-    q = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
-    const double mean = s / L;
-    double var = q / L - mean * mean;
-    if (var < 0) var = 0;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    if (run_mean) {
-        const double unb = L > 1 ? var * L / (L - 1) : var;
-        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
-        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
-    }
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    if (mean_out) mean_out[c] = (float)mean;
-    if (invstd_out) invstd_out[c] = inv;
-    scale_out[c] = g * inv;
-    shift_out[c] = b - (float)mean * g * inv;
-}
-
-// Statistics finalize of a slab [rows][2][C] in two launches: a level-1 pass over a wide grid (float4
-// loads, 16 channel groups x 16 row lanes per block, RB blocks per 64-channel column) into `work`
-// [RB][2][C], then one block per column sums the RB rows in fp64 and runs the epilogue.  The old level-1
-// had only C/64 x 64 blocks of scalar loads (20 us for ResNet-50's 12544-row layer1 slabs).  A one-launch
-// variant (last-arriving block finalizes) measured 3-8x slower per call: the agent-scope release fence
-// every block needs writes back the XCD's whole L2 (buffer_wbl2) right after a conv epilogue filled it.
-constexpr int FIN_RB_MAX = 256;       // level-1 rows per column (work holds FIN_RB_MAX * 2 * C floats)
 
 struct FinFwd {
     double L; float eps, momentum;
@@ -140,60 +68,35 @@ struct FinBwd {
     }
 };
 
-__global__ void __launch_bounds__(NT) bn_slab_level1_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             float* __restrict__ work) {
-    const int col = blockIdx.x, RB = gridDim.y, y = blockIdx.y;
-    const int ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
-    const int c0 = col * 64 + ch * 4;
-    const bool on = c0 < C;
-    __shared__ float4 red[2][16][16];
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
-    if (on) {
-        const int stride = RB * 16;
-        int r = y * 16 + lane;
-        for (; r + stride < rows; r += 2 * stride) {       // two rows' loads in flight
-            const float4 a0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r) * C + c0);
-            const float4 b0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r + 1) * C + c0);
-            const float4 a1 = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + stride)) * C + c0);
-            const float4 b1 = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + stride) + 1) * C + c0);
-            s.x += a0.x + a1.x; s.y += a0.y + a1.y; s.z += a0.z + a1.z; s.w += a0.w + a1.w;
-            q.x += b0.x + b1.x; q.y += b0.y + b1.y; q.z += b0.z + b1.z; q.w += b0.w + b1.w;
-        }
-        if (r < rows) {
-            const float4 a0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r) * C + c0);
-            const float4 b0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r + 1) * C + c0);
-            s.x += a0.x; s.y += a0.y; s.z += a0.z; s.w += a0.w;
-            q.x += b0.x; q.y += b0.y; q.z += b0.z; q.w += b0.w;
-        }
-    }
-    red[0][lane][ch] = s;
-    red[1][lane][ch] = q;
-    __syncthreads();
-    if (lane == 0 && on) {
-        float4 a = red[0][0][ch], b = red[1][0][ch];
-        for (int k = 1; k < 16; ++k) {
-            const float4 u = red[0][k][ch], v = red[1][k][ch];
-            a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-            b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
-        }
-        *reinterpret_cast<float4*>(work + (long)(2 * y) * C + c0) = a;
-        *reinterpret_cast<float4*>(work + (long)(2 * y + 1) * C + c0) = b;
-    }
-}
-
-// level 2: block = one 64-channel column, 16 float4 channel groups x 16 row lanes, fp64 sums.
+// Finalize of the STAT_BINS bins: block = one 64-channel column, 16 float4 channel groups x 16 bin lanes (4 bins
+// each, all loads in flight together), fp64 sums; every element read is zeroed again by the thread that read it
+// (the next producer adds into zeros; a bin buffer is reused only in stream order after this kernel).  Replaces a
+// level-1 + last-arriver pass over one row pair per producer tile (up to 12544 rows: 7.7-20 us per call,
+// gpurun_out/r5_01).
 template <class Epi>
-__global__ void __launch_bounds__(NT) bn_slab_final_kernel(const float* __restrict__ part, int rows, int C, Epi epi) {
+__global__ void __launch_bounds__(NT) bn_bins_final_kernel(float* __restrict__ bins, int C, Epi epi) {
     const int col = blockIdx.x, ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
     const int c0 = col * 64 + ch * 4;
+    constexpr int PER = STAT_BINS / 16;
     double sd[4] = {0, 0, 0, 0}, qd[4] = {0, 0, 0, 0};
-    if (c0 < C)
-        for (int r = lane; r < rows; r += 16) {
-            const float4 a = *reinterpret_cast<const float4*>(part + (long)(2 * r) * C + c0);
-            const float4 b = *reinterpret_cast<const float4*>(part + (long)(2 * r + 1) * C + c0);
-            sd[0] += a.x; sd[1] += a.y; sd[2] += a.z; sd[3] += a.w;
-            qd[0] += b.x; qd[1] += b.y; qd[2] += b.z; qd[3] += b.w;
+    if (c0 < C) {
+        float4 a[PER], b[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int r = lane + 16 * j;
+            a[j] = *reinterpret_cast<const float4*>(bins + (long)(2 * r) * C + c0);
+            b[j] = *reinterpret_cast<const float4*>(bins + (long)(2 * r + 1) * C + c0);
         }
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int r = lane + 16 * j;
+            sd[0] += a[j].x; sd[1] += a[j].y; sd[2] += a[j].z; sd[3] += a[j].w;
+            qd[0] += b[j].x; qd[1] += b[j].y; qd[2] += b[j].z; qd[3] += b[j].w;
+            *reinterpret_cast<float4*>(bins + (long)(2 * r) * C + c0) = z;
+            *reinterpret_cast<float4*>(bins + (long)(2 * r + 1) * C + c0) = z;
+        }
+    }
     __shared__ double redd[2][16][64];
 #pragma unroll
     for (int j = 0; j < 4; ++j) { redd[0][lane][ch * 4 + j] = sd[j]; redd[1][lane][ch * 4 + j] = qd[j]; }
@@ -205,136 +108,6 @@ __global__ void __launch_bounds__(NT) bn_slab_final_kernel(const float* __restri
         for (int k = 0; k < 16; ++k) { a += redd[0][k][threadIdx.x]; b += redd[1][k][threadIdx.x]; }
         if (c < C) epi(c, a, b);
     }
-}
-
-// One-launch finalize: the level-1 blocks of a column hand their partial rows to the column's LAST-arriving
-// block, which sums them and runs the epilogue (cdna_hip_programming.md §6 Guideline 16, counter form): the
-// partial rows are stored write-through (sc1, so no release fence and no L2 write-back of the conv output
-// that just filled it -- the cost that sank a __threadfence() version), the storing wave drains them
-// (vmcnt(0)) before one lane draws a ticket with an agent-scope atomic, and the last arriver acquires once
-// and reads the rows with sc1 loads.  `cnt` holds one zeroed counter per column; the last arriver puts it
-// back to zero, so a pool of counters is reused across calls without a memset launch.
-typedef __attribute__((address_space(1))) unsigned int gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-__device__ __forceinline__ void st_sc1(float* p, float4 v) {     // 16 bytes as two 8-byte sc1 stores
-    gu64* g = (gu64*)p;
-    __hip_atomic_store(g, (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 1, (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float4 ld_sc1(const float* p) {
-    const gu64* g = (const gu64*)p;
-    const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_float4(__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
-                       __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32)));
-}
-
-template <class Epi>
-__global__ void __launch_bounds__(NT) bn_slab_fused_kernel(const float* __restrict__ slab, int rows, int C,
-                                                           float* work, unsigned* cnt, Epi epi) {
-    const int col = blockIdx.x, RB = gridDim.y, y = blockIdx.y;
-    const int ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
-    const int c0 = col * 64 + ch * 4;
-    const bool on = c0 < C;
-    __shared__ double redd[2][16][64];
-    float4* red = reinterpret_cast<float4*>(&redd[0][0][0]);    // level-1 view: [2][16][16] float4
-    __shared__ int last;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
-    if (on) {
-        const int stride = RB * 16;
-        int r = y * 16 + lane;
-        for (; r + 3 * stride < rows; r += 4 * stride) {
-            float4 a[4], b[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                a[j] = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + j * stride)) * C + c0);
-                b[j] = *reinterpret_cast<const float4*>(slab + (long)(2 * (r + j * stride) + 1) * C + c0);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                s.x += a[j].x; s.y += a[j].y; s.z += a[j].z; s.w += a[j].w;
-                q.x += b[j].x; q.y += b[j].y; q.z += b[j].z; q.w += b[j].w;
-            }
-        }
-        for (; r < rows; r += stride) {
-            const float4 a0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r) * C + c0);
-            const float4 b0 = *reinterpret_cast<const float4*>(slab + (long)(2 * r + 1) * C + c0);
-            s.x += a0.x; s.y += a0.y; s.z += a0.z; s.w += a0.w;
-            q.x += b0.x; q.y += b0.y; q.z += b0.z; q.w += b0.w;
-        }
-    }
-    red[lane * 16 + ch] = s;
-    red[256 + lane * 16 + ch] = q;
-    __syncthreads();
-    if (threadIdx.x < 64) {                  // wave 0: lanes 0..15 publish this block's row, lane 0 draws the ticket
-        if (lane == 0 && on) {
-            float4 a = red[ch], b = red[256 + ch];
-            for (int k = 1; k < 16; ++k) {
-                const float4 u = red[k * 16 + ch], v = red[256 + k * 16 + ch];
-                a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-                b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
-            }
-            st_sc1(work + (long)(2 * y) * C + c0, a);
-            st_sc1(work + (long)(2 * y + 1) * C + c0, b);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the storing wave drains its sc1 stores
-        if (threadIdx.x == 0) {
-            const unsigned t = __hip_atomic_fetch_add((gu32*)(cnt + col), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = t == (unsigned)(RB - 1);
-        }
-    }
-    __syncthreads();                          // also: every wave is done with the level-1 LDS view
-    if (!last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    double sd[4] = {0, 0, 0, 0}, qd[4] = {0, 0, 0, 0};
-    if (on) {
-        int r = lane;
-        for (; r + 48 < RB; r += 64) {
-            float4 a[4], b[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                a[j] = ld_sc1(work + (long)(2 * (r + 16 * j)) * C + c0);
-                b[j] = ld_sc1(work + (long)(2 * (r + 16 * j) + 1) * C + c0);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sd[0] += a[j].x; sd[1] += a[j].y; sd[2] += a[j].z; sd[3] += a[j].w;
-                qd[0] += b[j].x; qd[1] += b[j].y; qd[2] += b[j].z; qd[3] += b[j].w;
-            }
-        }
-        for (; r < RB; r += 16) {
-            const float4 a = ld_sc1(work + (long)(2 * r) * C + c0);
-            const float4 b = ld_sc1(work + (long)(2 * r + 1) * C + c0);
-            sd[0] += a.x; sd[1] += a.y; sd[2] += a.z; sd[3] += a.w;
-            qd[0] += b.x; qd[1] += b.y; qd[2] += b.z; qd[3] += b.w;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { redd[0][lane][ch * 4 + j] = sd[j]; redd[1][lane][ch * 4 + j] = qd[j]; }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const int c = col * 64 + threadIdx.x;
-        double a = 0.0, b = 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) { a += redd[0][k][threadIdx.x]; b += redd[1][k][threadIdx.x]; }
-        if (c < C) epi(c, a, b);
-        if (threadIdx.x == 0) __hip_atomic_store((gu32*)(cnt + col), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-inline unsigned fin_rows(int rows) {       // level-1 blocks per column: >= 4 slab rows per thread
-    int rb = rows / (16 * 4);
-    if (rows <= 64) return 0;                // few rows: level 2 reads the slab directly
-    if (rb > FIN_RB_MAX) rb = FIN_RB_MAX;
-    if (rb < 1) rb = 1;
-    return (unsigned)rb;
 }
 
 // eval-mode scale/shift from running statistics
@@ -371,8 +144,9 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
         const int g = c >> 3, j = c & 7;
         float a = 0.f, b = 0.f;
         for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + g) * 8 + j]; b += red[1][(k * CG + g) * 8 + j]; }
-        slab[(long)(2 * blockIdx.x) * C + c] = a;
-        slab[(long)(2 * blockIdx.x + 1) * C + c] = b;
+        float* row = stat_row(slab, blockIdx.x, C);
+        stat_add(row + c, a);
+        stat_add(row + C + c, b);
     }
 }
 
@@ -520,35 +294,12 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(
             const int gg = cc >> 3, j = cc & 7;
             float a = 0.f, b = 0.f;
             for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + gg) * 8 + j]; b += red[1][(k * CG + gg) * 8 + j]; }
-            out[(long)(2 * blockIdx.x) * C + cc] = a;
-            out[(long)(2 * blockIdx.x + 1) * C + cc] = b;
+            float* row = stat_row(out, blockIdx.x, C);
+            stat_add(row + cc, a);
+            stat_add(row + C + cc, b);
         }
         __syncthreads();
     }
-}
-
-// sum partial rows -> dbeta (= sum gm), dgamma (= sum gm*xhat).  Optionally accumulate (+=).
-__global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             float* dgamma, float* dbeta, int accumulate,
-                                                             float* gacc, float* bacc) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), lr = threadIdx.x >> 6;
-    __shared__ double red[2][4][64];
-    double s = 0.0, q = 0.0;
-    if (c < C)
-        for (int r = lr; r < rows; r += 4) {
-            s += slab[(long)(2 * r) * C + c];
-            q += slab[(long)(2 * r + 1) * C + c];
-        }
-    red[0][lr][threadIdx.x & 63] = s;
-    red[1][lr][threadIdx.x & 63] = q;
-    __syncthreads();
-    if (lr != 0 || c >= C) return;
-    const int l = threadIdx.x;
-    s = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
-    q = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
-    if (accumulate) { dbeta[c] += (float)s; dgamma[c] += (float)q; }
-    else { dbeta[c] = (float)s; dgamma[c] = (float)q; }
-    if (gacc) { gacc[c] += (float)q; bacc[c] += (float)s; }     // direct accumulation into param grads
 }
 
 // dx = gamma*invstd*(gm - dbeta/L - xhat*dgamma/L) = k*gm + x*A + B with per-channel k, A, B held in
@@ -655,43 +406,13 @@ inline unsigned reduce_grid(long L, int C) {
 
 PDNN_API int pdnn_bn_reduce_rows(long L, int C) { return (int)reduce_grid(L, C); }
 
-// floats of `work` the finalize calls need for a slab of `rows` partial rows
-PDNN_API int pdnn_bn_fin_work(int rows, int C) {
-#if PDNN_BN_WIDE_FIN
-    return 2 * (int)fin_rows(rows) * C;
-#else
-    return rows > 64 ? 2 * 64 * C : 0;
-#endif
-}
-
-// work: >= pdnn_bn_fin_work(rows, C) floats of scratch for the level-1 reduction; cnt (optional): C/64 zeroed
-// counters -> one launch (bn_slab_fused_kernel), left zeroed
-PDNN_API int pdnn_bn_finalize(const float* slab, int rows, int C, double L, float eps, float momentum,
+// slab = STAT_BINS bins [64][2][C] (common.h), left zeroed.  rows: kept in the signature (= STAT_BINS)
+PDNN_API int pdnn_bn_finalize(float* slab, int rows, int C, double L, float eps, float momentum,
                               const float* gamma, const float* beta, float* run_mean, float* run_var,
-                              float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
-                              float* work, unsigned* cnt, hipStream_t st) {
-#if PDNN_BN_WIDE_FIN
+                              float* mean_out, float* invstd_out, float* scale_out, float* shift_out, hipStream_t st) {
+    if (rows != STAT_BINS) return (int)hipErrorInvalidValue;
     const FinFwd epi{L, eps, momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out};
-    const unsigned rb = fin_rows(rows);
-    if (rb && cnt) {
-        hipLaunchKernelGGL(bn_slab_fused_kernel<FinFwd>, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work,
-                           cnt, epi);
-        PDNN_LAUNCH_RET;
-    }
-    if (rb) hipLaunchKernelGGL(bn_slab_level1_kernel, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work);
-    hipLaunchKernelGGL(bn_slab_final_kernel<FinFwd>, dim3((C + 63) / 64), dim3(NT), 0, st, rb ? work : slab,
-                       rb ? (int)rb : rows, C, epi);
-#else
-    const float* src = slab;
-    int r = rows;
-    if (rows > 64) {
-        hipLaunchKernelGGL(slab_reduce_kernel, dim3((C + 63) / 64, 64), dim3(NT), 0, st, slab, rows, C, work);
-        src = work;
-        r = 64;
-    }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, st, src, r, C, L, eps,
-                       momentum, gamma, beta, run_mean, run_var, mean_out, invstd_out, scale_out, shift_out);
-#endif
+    hipLaunchKernelGGL(bn_bins_final_kernel<FinFwd>, dim3((C + 63) / 64), dim3(NT), 0, st, slab, C, epi);
     PDNN_LAUNCH_RET;
 }
 
@@ -745,32 +466,12 @@ PDNN_API int pdnn_bn_bwd_reduce(const bf16_t* g, const bf16_t* x, long L, int C,
 }
 
 // dgamma/dbeta of this backward (consumed by bn_bwd_apply); gacc/bacc (optional): also added into the
-// parameters' gradient accumulators.
-PDNN_API int pdnn_bn_bwd_finalize(const float* slab, int rows, int C, float* dgamma, float* dbeta,
-                                  int accumulate, float* work, float* gacc, float* bacc, unsigned* cnt,
-                                  hipStream_t st) {
-#if PDNN_BN_WIDE_FIN
+// parameters' gradient accumulators.  slab = STAT_BINS bins, left zeroed.
+PDNN_API int pdnn_bn_bwd_finalize(float* slab, int rows, int C, float* dgamma, float* dbeta, int accumulate,
+                                  float* gacc, float* bacc, hipStream_t st) {
+    if (rows != STAT_BINS) return (int)hipErrorInvalidValue;
     const FinBwd epi{dgamma, dbeta, accumulate, gacc, bacc};
-    const unsigned rb = fin_rows(rows);
-    if (rb && cnt) {
-        hipLaunchKernelGGL(bn_slab_fused_kernel<FinBwd>, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work,
-                           cnt, epi);
-        PDNN_LAUNCH_RET;
-    }
-    if (rb) hipLaunchKernelGGL(bn_slab_level1_kernel, dim3((C + 63) / 64, rb), dim3(NT), 0, st, slab, rows, C, work);
-    hipLaunchKernelGGL(bn_slab_final_kernel<FinBwd>, dim3((C + 63) / 64), dim3(NT), 0, st, rb ? work : slab,
-                       rb ? (int)rb : rows, C, epi);
-#else
-    const float* src = slab;
-    int r = rows;
-    if (rows > 64) {
-        hipLaunchKernelGGL(slab_reduce_kernel, dim3((C + 63) / 64, 64), dim3(NT), 0, st, slab, rows, C, work);
-        src = work;
-        r = 64;
-    }
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, st, src, r, C, dgamma,
-                       dbeta, accumulate, gacc, bacc);
-#endif
+    hipLaunchKernelGGL(bn_bins_final_kernel<FinBwd>, dim3((C + 63) / 64), dim3(NT), 0, st, slab, C, epi);
     PDNN_LAUNCH_RET;
 }
 

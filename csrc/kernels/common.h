@@ -27,6 +27,17 @@ typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
 
 constexpr int kWave = 64;
 
+// BatchNorm statistics "slabs" are STAT_BINS row pairs [bin][sum | second][C] that producers ADD into with
+// fp32 atomics (no-return global_atomic_add_f32; partial row r goes to bin r % STAT_BINS), not one stored row
+// pair per tile: the finalize then reads 64 rows instead of up to 12544 (ResNet-50 stage 1) and zeroes them
+// again for the next producer (batchnorm.hip bn_slab_final_kernel).  Summation order varies run to run in the
+// last fp32 bits.
+constexpr int STAT_BINS = 64;
+__device__ __forceinline__ float* stat_row(float* slab, long row, int C) {
+    return slab + (long)(2 * (row & (STAT_BINS - 1))) * C;
+}
+__device__ __forceinline__ void stat_add(float* p, float v) { atomicAdd(p, v); }
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
     return __uint_as_float(((uint32_t)v) << 16);
 }

@@ -486,8 +486,10 @@ __global__ void __launch_bounds__(256, 1) conv3x3_w64_kernel(C3Args a) {
 // one B fragment per 4 MFMAs, the panel kernel's A-from-LDS reads and its 64 KB+ A panel are gone, and
 // K = 256 fits (ResNet-50 stage-3 conv3 forward / conv1 data gradient: 50176 x 256 -> 1024).
 // PRE: the BatchNorm-backward apply runs on the fragments as they are loaded (once per pixel tile).
+// FP: the forward prologue relu(x * pro_sc + pro_sh) likewise (the BN + ReLU of the layer that produced x, e.g. a
+// Bottleneck's conv3 reading t2: a2 = relu(bn2(t2)) is never written), bn_apply's formula and rounding.
 // ---------------------------------------------------------------------------------------------------
-template <int KC, int NB, int EPI, bool PRE>
+template <int KC, int NB, int EPI, bool PRE, bool FP = false>
 __global__ void __launch_bounds__(256, 2) conv1x1_areg_kernel(C3Args a) {
     constexpr int FN = NB / 16, NKS = 2 * KC, K = 64 * KC;
     constexpr int BPT = NB * KC * 8 / 256;               // 16-byte weight pieces per thread per step
@@ -532,13 +534,23 @@ __global__ void __launch_bounds__(256, 2) conv1x1_areg_kernel(C3Args a) {
     }
     bf16x8_t af[NKS][4];
     if constexpr (!PRE) {
+        [[maybe_unused]] float* coef = reinterpret_cast<float*>(bbuf + 2 * KC * NB * 64);      // FP: [2][K]
+        if constexpr (FP) {
+            for (int c = tid; c < K; c += 256) {
+                coef[c] = a.pro_sc[c];
+                coef[K + c] = a.pro_sh[c];
+            }
+            __syncthreads();
+        }
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
+            for (int fm = 0; fm < 4; ++fm) {
                 // rows past P hold row P-1's values: their outputs are neither stored nor counted in the statistics
-                af[ks][fm] = __builtin_bit_cast(
-                    bf16x8_t, *reinterpret_cast<const u16x8_t*>(a.x + prow[fm] + ks * 32 + (lane >> 4) * 8));
+                u16x8_t v = *reinterpret_cast<const u16x8_t*>(a.x + prow[fm] + ks * 32 + (lane >> 4) * 8);
+                if constexpr (FP) v = fpro_apply_lds<K>(coef, ks * 32 + (lane >> 4) * 8, v);
+                af[ks][fm] = __builtin_bit_cast(bf16x8_t, v);
+            }
     } else {
         // BN-backward coefficients of all K channels computed once per block into LDS (after the weight
         // buffers), then the fragments are loaded GB k-steps at a time (gm and t of all of them in flight
@@ -706,15 +718,22 @@ int c3_dispatch(const C3Args& a, int epi, hipStream_t st) {
 
 
 
-template <int KC, int NB, int EPI, bool PRE>
+template <int KC, int NB, int EPI, bool PRE, bool FP = false>
 int areg_launch(const C3Args& a, hipStream_t st) {
-    constexpr int sm = 2 * KC * NB * 128 + (PRE ? 3 * 64 * KC * 4 : 0);
-    hipLaunchKernelGGL((conv1x1_areg_kernel<KC, NB, EPI, PRE>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
+    constexpr int sm = 2 * KC * NB * 128 + (PRE ? 3 * 64 * KC * 4 : (FP ? 2 * 64 * KC * 4 : 0));
+    hipLaunchKernelGGL((conv1x1_areg_kernel<KC, NB, EPI, PRE, FP>), dim3(a.tiles * a.ntiles), dim3(256), sm, st, a);
     PDNN_LAUNCH_RET;
 }
 
 template <int KC, int NB, bool PRE>
 int areg_dispatch(const C3Args& a, int epi, hipStream_t st) {
+    if constexpr (!PRE) {
+        if (a.pro_sc) {         // forward prologue: the forward epilogues only
+            if (epi == C3_STATS) return areg_launch<KC, NB, C3_STATS, false, true>(a, st);
+            if (epi == C3_PLAIN) return areg_launch<KC, NB, C3_PLAIN, false, true>(a, st);
+            return (int)hipErrorInvalidValue;
+        }
+    }
     switch (epi) {
         case C3_BNB: return areg_launch<KC, NB, C3_BNB, PRE>(a, st);
         case C3_STATS: return areg_launch<KC, NB, C3_STATS, PRE>(a, st);
@@ -909,8 +928,9 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
                                 const float* bn_invstd, const float* bn_mscale, const float* bn_mshift,
                                 const bf16_t* pre_t, const float* pre_mean, const float* pre_invstd,
                                 const float* pre_gamma, const float* pre_dgamma, const float* pre_dbeta,
-                                bf16_t* pre_out, hipStream_t st) {
-    if (!pdnn_conv1x1_panel_supported(P, K, N) || (bn_x && !stats) || (res_mask && !res))
+                                bf16_t* pre_out, const float* pro_sc, const float* pro_sh, hipStream_t st) {
+    if (!pdnn_conv1x1_panel_supported(P, K, N) || (bn_x && !stats) || (res_mask && !res) || (!pro_sc != !pro_sh) ||
+        (pro_sc && (pre_t || bn_x || res)))
         return (int)hipErrorInvalidValue;
     C3Args a{};
     a.x = x; a.w = w; a.y = y; a.C = K; a.N = N; a.P = (int)P;
@@ -919,6 +939,7 @@ PDNN_API int pdnn_conv1x1_panel(const bf16_t* x, const bf16_t* w, bf16_t* y, lon
     a.ep_x = bn_x; a.ep_mean = bn_mean; a.ep_invstd = bn_invstd; a.ep_mscale = bn_mscale; a.ep_mshift = bn_mshift;
     if (!set_pre(a, pre_t, pre_mean, pre_invstd, pre_gamma, pre_dgamma, pre_dbeta, pre_out))
         return (int)hipErrorInvalidValue;
+    a.pro_sc = pro_sc; a.pro_sh = pro_sh;
     const int epi = bn_x ? C3_BNB : (stats ? C3_STATS : (res ? C3_RES : C3_PLAIN));
     return pre_t ? areg_run<true>(a, K, epi, st) : areg_run<false>(a, K, epi, st);
 }

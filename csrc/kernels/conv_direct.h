@@ -254,14 +254,14 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
                     q[j] = row16_sum(q[j]);
                 }
                 if ((lane & 15) == 0) {
-                    float* ps = a.stats + (long)(tile * 4 + wave) * 2 * a.N + n;
+                    float* ps = stat_row(a.stats, (long)tile * 4 + wave, a.N) + n;
                     float* pq = ps + a.N;
                     if constexpr (EPI == C3_BNB) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) q[j] = (q[j] - a.ep_mean[n + j] * s[j]) * a.ep_invstd[n + j];
                     }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) { ps[j] = s[j]; pq[j] = q[j]; }
+                    for (int j = 0; j < 4; ++j) { stat_add(ps + j, s[j]); stat_add(pq + j, q[j]); }
                 }
             }
         }

@@ -529,11 +529,11 @@ gemm_glds_kernel(GemmArgs a) {
 #pragma unroll
                         for (int fn = 0; fn < FN; ++fn) {
                             const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
-                            float* ps = a.stats + (long)(2 * slab_row) * a.N + n;
+                            float* ps = stat_row(a.stats, slab_row, a.N) + n;
                             float* pq = ps + a.N;
 #pragma unroll
                             for (int j = 0; j < 4; ++j)
-                                if (n + j < a.N) { ps[j] = s_[fn][j]; pq[j] = q_[fn][j]; }
+                                if (n + j < a.N) { stat_add(ps + j, s_[fn][j]); stat_add(pq + j, q_[fn][j]); }
                         }
                     }
 #pragma unroll

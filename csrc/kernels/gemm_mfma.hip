@@ -630,11 +630,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
             for (int fn = 0; fn < FN; ++fn) {
                 const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
                 if (n >= a.N) continue;
-                float* ps = a.stats + row * a.N + n;
-                float* pq = a.stats + (row + 1) * a.N + n;
+                float* ps = stat_row(a.stats, row / 2, a.N) + n;
+                float* pq = ps + a.N;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    if (n + j < a.N) { ps[j] = ss[fn][j]; pq[j] = qs[fn][j]; }
+                    if (n + j < a.N) { stat_add(ps + j, ss[fn][j]); stat_add(pq + j, qs[fn][j]); }
                 }
             }
         }

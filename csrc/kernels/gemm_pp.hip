@@ -445,9 +445,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                                             q_[fn][2] = is.z * (q_[fn][2] - mu.z * s_[fn][2]);
                                             q_[fn][3] = is.w * (q_[fn][3] - mu.w * s_[fn][3]);
                                         }
-                                        float* ps = a.stats + (long)(2 * (g64 / 64)) * a.N + n;
-                                        *reinterpret_cast<float4*>(ps) = make_float4(s_[fn][0], s_[fn][1], s_[fn][2], s_[fn][3]);
-                                        *reinterpret_cast<float4*>(ps + a.N) = make_float4(q_[fn][0], q_[fn][1], q_[fn][2], q_[fn][3]);
+                                        float* ps = stat_row(a.stats, g64 / 64, a.N) + n;
+#pragma unroll
+                                        for (int j = 0; j < 4; ++j) {
+                                            stat_add(ps + j, s_[fn][j]);
+                                            stat_add(ps + a.N + j, q_[fn][j]);
+                                        }
                                     }
                                 }
                             }

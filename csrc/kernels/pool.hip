@@ -259,8 +259,9 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_bnred_kernel(
         const int gg = cc >> 3, j = cc & 7;
         float a = 0.f, b = 0.f;
         for (int k = 0; k < RPI; ++k) { a += red[0][(k * CG + gg) * 8 + j]; b += red[1][(k * CG + gg) * 8 + j]; }
-        slab[(long)(2 * blockIdx.x) * C + cc] = a;
-        slab[(long)(2 * blockIdx.x + 1) * C + cc] = b;
+        float* row = stat_row(slab, blockIdx.x, C);
+        stat_add(row + cc, a);
+        stat_add(row + C + cc, b);
     }
 }
 

@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(NT) layernorm_fwd_kernel(const bf16_t* __restr
 }
 
 // dx = rstd * (gg - mean(gg) - xhat * mean(gg * xhat)) (+ dres, the residual branch), gg = dy * gamma; per-block partial dgamma/dbeta
-// into slab [gridDim.x][2][D] (row 2i = sum dy, 2i+1 = sum dy * xhat) -> pdnn_bn_bwd_finalize.
+// into the STAT_BINS statistics bins (common.h: row pair i adds into bin i % 64) -> pdnn_bn_bwd_finalize.
 template <int MAXC>
 __global__ void __launch_bounds__(NT) layernorm_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                            const float* __restrict__ g, const float* __restrict__ mean,
@@ -158,8 +158,9 @@ __global__ void __launch_bounds__(NT) layernorm_bwd_kernel(const bf16_t* __restr
     for (int d = threadIdx.x; d < D; d += NT) {
         float a = 0.f, bb = 0.f;
         for (int k = 0; k < NT / 64; ++k) { a += red[0][k][d]; bb += red[1][k][d]; }
-        slab[(long)(2 * blockIdx.x) * D + d] = a;
-        slab[(long)(2 * blockIdx.x + 1) * D + d] = bb;
+        float* row = stat_row(slab, blockIdx.x, D);          // STAT_BINS bins (common.h), finalized like BN's
+        stat_add(row + d, a);
+        stat_add(row + D + d, bb);
     }
 }
 

@@ -58,7 +58,7 @@ _SIGS = {
     "pdnn_tune_unknown": [],
     "pdnn_set_comm_world": [I],
     "pdnn_grid_cus": [],
-    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_conv1x1_panel": [P, P, P, L, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv1x1_panel_supported": [L, I, I],
     "pdnn_conv1x1_panel_stats_rows": [L],
     "pdnn_conv1x1_wide": [P, P, P, L, I, I] + [P] * 16,
@@ -82,13 +82,12 @@ _SIGS = {
     "pdnn_transpose_bf16": [P, L, P, L, I, I, P],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
-    "pdnn_bn_fin_work": [I, I],
-    "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P, P, P],
+    "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P],
     "pdnn_bn_eval_coeff": [I, F, P, P, P, P, P, P, P],
     "pdnn_bn_stats": [P, L, I, P, P],
     "pdnn_bn_apply": [P, L, I, P, P, P, P, P, I, P, P, P],
     "pdnn_bn_bwd_reduce": [P, P, L, I, P, P, I, P, P, P, P, P, P, P, P, P],
-    "pdnn_bn_bwd_finalize": [P, I, I, P, P, I, P, P, P, P, P],
+    "pdnn_bn_bwd_finalize": [P, I, I, P, P, I, P, P, P],
     "pdnn_bn_bwd_apply": [P, P, L, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdnn_maxpool_fwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],
     "pdnn_maxpool_bwd": [P, P, P, I, I, I, I, I, I, I, I, I, P],

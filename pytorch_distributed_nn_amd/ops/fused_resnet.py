@@ -360,13 +360,20 @@ class BottleneckFn(torch.autograd.Function):
             t2, m2, i2, s2, h2 = _conv3x3_bn_fp8(src1, w2, fp8.fwd, training, (g2, b2), bufs[2:4], mom, eps, pro=pro1)
         else:
             t2, m2, i2, s2, h2 = _conv_bn(src1, k2, stride, 1, pro1, training, (g2, b2), bufs[2:4], mom, eps)
-        # a2 = relu(bn2(t2)) written once: conv3 (and its weight gradient) then read a plain operand.  The
-        # BN2+ReLU operand prologue re-ran the affine for every 64-column output tile and held the 1x1 GEMM
-        # 1.5-2x over its memory floor (tools/bench_conv1x1.py, gpurun_out/r3_03: 2.82 ms/step fused vs
-        # 0.29 + 1.87 materialised)
+        # a2 = relu(bn2(t2)): on the A-stationary 1x1 kernel conv3 applies BN2 + ReLU to its activation fragments
+        # once per pixel tile as they are loaded (and its weight gradient in the implicit-GEMM engine's operand
+        # prologue), so a2 is never written (tuning a2_fold); elsewhere it is written once -- the 128-row engine's
+        # prologue re-ran the affine for every 64-column output tile (gpurun_out/r3_03: 2.82 ms/step vs 0.29 +
+        # 1.87 materialised)
         C2 = t2.shape[-1]
-        a2 = K.bn_apply(t2.view(-1, C2), s2, h2, relu=True).view(t2.shape)
-        t3, m3, i3, s3, h3 = _conv_bn(a2, k3, 1, 0, None, training, (g3, b3), bufs[4:6], mom, eps)
+        fold = tuning.get("a2_fold")
+        P2 = t2.numel() // C2
+        if fold and K.conv1x1_pro_ok(tuple(t2.shape), k3.shape[0]) and (fold == 2 or P2 > K.WGRAD1X1_PP_PIX):
+            a2, pro2, src2 = None, (s2, h2), t2
+        else:
+            a2 = K.bn_apply(t2.view(-1, C2), s2, h2, relu=True).view(t2.shape)
+            pro2, src2 = None, a2
+        t3, m3, i3, s3, h3 = _conv_bn(src2, k3, 1, 0, pro2, training, (g3, b3), bufs[4:6], mom, eps)
         C3 = t3.shape[-1]
         if down:
             if side_down is not None:
@@ -433,7 +440,8 @@ class BottleneckFn(torch.autograd.Function):
         else:
             dt3, _, gres = K.bn_bwd_apply(g2d, t3_2d, m3, i3, g3, dg3, db3, mode=3, msrc=mb, want_gm=True)
         dt3 = dt3.view(t3.shape)
-        dw3 = sink.wgrad(P[6], a2, dt3, 1, 1, 1, 0)       # conv3 (input a2 = relu(bn2(t2)))
+        # conv3 (input a2 = relu(bn2(t2)), or t2 with BN2 + ReLU as the operand prologue when a2 was folded)
+        dw3 = sink.wgrad(P[6], a2 if a2 is not None else t2, dt3, 1, 1, 1, 0, pro=None if a2 is not None else (s2, h2))
         bn1 = (t1, m1, i1, s1, h1)
         if _pre_ok(t2, k2, stride, 1):
             # BN2's apply runs in conv2's data-gradient operand loads, which also write dt2 for the wgrad

@@ -144,7 +144,8 @@ def conv_out_hw(H, W, R, S, st, pad):
 
 
 def stats_rows(M: int) -> int:
-    return lib().pdnn_gemm_stats_rows(M)
+    """Row pairs of a BatchNorm statistics slab (every producer adds into STAT_BINS bins)."""
+    return STAT_BINS
 
 
 # 3x3 / stride-1 / pad-1 convs run on the LDS-halo kernel (csrc/kernels/conv3x3.hip): 1 = whenever the
@@ -241,24 +242,27 @@ def _pre_args(pre, x):
     return tuple(ptr(v) for v in (t, mean, inv, gamma, dg, db, dt_out))
 
 
-def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None):
+def conv1x1_panel(x2d, w2d, want_stats=False, res=None, bn=None, res_mask=None, out=None, pre=None, pro=None):
     """y[P][N] = x[P][K] . w[N][K]^T on the panel / A-stationary kernels (K <= 256) or the long-reduction kernel
-    (K >= 512); epilogues as conv3x3 / conv_dgrad; pre: the BN-backward operand prologue (_pre_args)."""
+    (K >= 512); epilogues as conv3x3 / conv_dgrad; pre: the BN-backward operand prologue (_pre_args); pro =
+    (scale, shift): the forward operand prologue relu(x * scale + shift) (A-stationary kernel, K <= 256)."""
     P, Kc = x2d.shape
     N = w2d.shape[0]
     y = out if out is not None else torch.empty(P, N, device=x2d.device, dtype=BF16)
     slab = None
     t = mean = inv = msc = msh = None
     if want_stats or bn is not None:
-        slab = torch.empty(2 * lib().pdnn_conv1x1_panel_stats_rows(P), N, device=x2d.device, dtype=F32)
+        slab = stat_bins(N, x2d.device)
     if bn is not None:
         t, mean, inv, msc, msh = bn
     if Kc >= 512:
+        _chk(pro is None, "conv1x1_panel: the forward prologue needs K <= 256")
         call("pdnn_conv1x1_wide", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
              ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
         return y, slab
+    psc, psh = pro if pro is not None else (None, None)
     call("pdnn_conv1x1_panel", ptr(x2d), ptr(w2d), ptr(y), P, Kc, N, ptr(slab), ptr(res), ptr(res_mask), ptr(t),
-         ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), stream())
+         ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x2d), ptr(psc), ptr(psh), stream())
     return y, slab
 
 
@@ -280,7 +284,7 @@ def conv3x3(x, w, want_stats=False, res=None, bn=None, out=None, res_mask=None, 
     slab = None
     t = mean = inv = msc = msh = None
     if want_stats or bn is not None:
-        slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
+        slab = stat_bins(Ko, x.device)
     if bn is not None:
         t, mean, inv, msc, msh = bn
     psc, psh = pro if pro is not None else (None, None)
@@ -302,13 +306,13 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
     if _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
         return conv3x3(x, w, want_stats=want_stats, pro=pro)
-    if pro is None and _panel_ok(N * H * W, C, K, R, S, st, pad, fwd=True):
-        y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats)
+    if (pro is None or C <= 256) and _panel_ok(N * H * W, C, K, R, S, st, pad, fwd=True):
+        y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats, pro=pro)
         return y.view(N, H, W, K), slab
     y = torch.empty(N, Ho, Wo, K, device=x.device, dtype=BF16)
     stats = None
     if want_stats:
-        stats = torch.empty(2 * stats_rows(N * Ho * Wo), K, device=x.device, dtype=F32)
+        stats = stat_bins(K, x.device)
     sc, sh = pro if pro is not None else (None, None)
     call("pdnn_conv_fwd", ptr(x), ptr(w), ptr(y), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
          ptr(stats), stream())
@@ -319,6 +323,13 @@ def _panel_dgrad_k(K):
     """Data gradients (dx[P][C] = dy[P][K] . W) on the A-stationary kernel (K in {64, 128, 256}) or the
     long-reduction streaming kernel (K >= 512, conv1x1_wide.hip)."""
     return K in (64, 128, 256) or K >= 512
+
+
+def conv1x1_pro_ok(x_shape, Ko):
+    """Whether a 1x1 / stride-1 conv of this input runs with its input's BN + ReLU as an operand prologue on the
+    A-stationary kernel (forward; its weight gradient then takes the same prologue on the implicit-GEMM engine)."""
+    N, H, W, C = x_shape
+    return bool(_P1["mode"]) and C in (64, 128, 256) and lib().pdnn_conv1x1_panel_supported(N * H * W, C, Ko) == 1
 
 
 def conv3x3_pro_ok(x_shape, Ko):
@@ -408,8 +419,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
     t = mean = inv = msc = msh = None
     if bn is not None:
         t, mean, inv, msc, msh = bn
-        rows = lib().pdnn_conv_dgrad_stats_rows(N, H, W, R, S, st, pad)
-        slab = torch.empty(2 * rows, C, device=dy.device, dtype=F32)
+        slab = stat_bins(C, dy.device)
     if res is not None:
         _bf16_c(res, "conv_dgrad.res")
         _chk(tuple(res.shape) == (N, H, W, C), "conv_dgrad: res shape")
@@ -420,7 +430,7 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
 
 # 1x1 / stride-1 weight gradients with at most this many pixels run on the ping-pong engine (ResNet-50 stages
 # 2-4 at bs 256; stage 1 loses there: tools/bench_wgrad1x1.py, gpurun_out/r3_38-40, stage 3/4 67/64 -> 57/48 us)
-_WGRAD1X1_PP_PIX = 200704
+_WGRAD1X1_PP_PIX = WGRAD1X1_PP_PIX = 200704
 
 
 def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
@@ -452,32 +462,33 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
 
 
 # ----------------------------------------------------------------------------------- BatchNorm
-def _fin_work(rows, C, device):
-    n = lib().pdnn_bn_fin_work(rows, C)
-    return torch.empty(n, device=device, dtype=F32) if n > 0 else None
+# BatchNorm statistics slabs are STAT_BINS bin-row pairs [64][2][C] fp32 that the producing kernels ADD into
+# (common.h stat_add) and the finalize kernels read and zero again.  A slab therefore has to start zeroed: they
+# come from a free list per (device, stream, C), refilled by bn_finalize / bn_bwd_finalize after they launch the
+# zeroing finalize on that stream (a later producer on the same stream runs after it).  A slab read some other
+# way (tests) is simply not returned; new ones are allocated zeroed.
+STAT_BINS = 64
+_BINS = {}
 
 
-# Zeroed counters for the one-launch BN finalize (batchnorm.hip bn_slab_fused_kernel): each call takes the
-# next C/64 slots of a per-device ring; the kernel's last-arriving block puts its counters back to zero, so
-# no memset is needed per call.  A slot comes round again only after _CNT_SLOTS / (C/64) calls (thousands of
-# launches, several training steps), long after the kernel that last used it finished on its stream.
-_CNT_SLOTS = 1 << 16
-_CNT = {}
+def _bins_key(device, C):
+    return (device.index, torch.cuda.current_stream(device).cuda_stream, C)
 
 
-def _fin_counters(C, device, n=None):
-    """n (optional): that many counters instead of one per 64-channel column."""
-    key = device.index
-    ent = _CNT.get(key)
-    if ent is None:
-        ent = _CNT[key] = [torch.zeros(_CNT_SLOTS, device=device, dtype=torch.int32), 0]
-    buf, pos = ent
-    if n is None:
-        n = (C + 63) // 64
-    if pos + n > _CNT_SLOTS:
-        pos = 0
-    ent[1] = pos + n
-    return buf[pos:pos + n]
+def stat_bins(C, device):
+    """A zeroed [2 * STAT_BINS][C] fp32 statistics slab for a producer launched on the current stream."""
+    free = _BINS.get(_bins_key(device, C))
+    slab = free.pop() if free else torch.zeros(2 * STAT_BINS, C, device=device, dtype=F32)
+    slab._pdnn_bins = "taken"
+    return slab
+
+
+def _release_bins(slab):
+    # only slabs handed out by stat_bins, and each once (a slab finalized twice must not enter the list twice)
+    if getattr(slab, "_pdnn_bins", None) != "taken":
+        return
+    slab._pdnn_bins = "free"
+    _BINS.setdefault(_bins_key(slab.device, slab.shape[1]), []).append(slab)
 
 
 def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
@@ -486,10 +497,10 @@ def bn_finalize(slab, rows, L, eps, momentum, gamma, beta, run_mean, run_var):
     invstd = torch.empty_like(mean)
     scale = torch.empty_like(mean)
     shift = torch.empty_like(mean)
-    work = _fin_work(rows, C, slab.device)
-    cnt = _fin_counters(C, slab.device) if work is not None else None
+    _chk(rows == STAT_BINS and slab.shape[0] == 2 * STAT_BINS, "bn_finalize: a stat_bins() slab")
     call("pdnn_bn_finalize", ptr(slab), rows, C, float(L), float(eps), float(momentum), ptr(gamma), ptr(beta),
-         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(work), ptr(cnt), stream())
+         ptr(run_mean), ptr(run_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
+    _release_bins(slab)
     return mean, invstd, scale, shift
 
 
@@ -505,10 +516,9 @@ def bn_eval_coeff(eps, gamma, beta, rm, rv):
 def bn_stats(x2d):
     L, C = x2d.shape
     _chk(C % 8 == 0 and C <= 2048, f"bn_stats: C={C}")
-    rows = lib().pdnn_bn_reduce_rows(L, C)
-    slab = torch.empty(2 * rows, C, device=x2d.device, dtype=F32)
+    slab = stat_bins(C, x2d.device)
     call("pdnn_bn_stats", ptr(x2d), L, C, ptr(slab), stream())
-    return slab, rows
+    return slab, STAT_BINS
 
 
 def bn_apply(x2d, scale, shift, res=None, rscale=None, rshift=None, relu=True, out=None, want_mask=None):
@@ -530,12 +540,11 @@ def bn_apply(x2d, scale, shift, res=None, rscale=None, rshift=None, relu=True, o
 def bn_bwd_reduce(g, x, mean, invstd, mode=0, msrc=None, mscale=None, mshift=None, x2=None, mean2=None,
                   invstd2=None):
     L, C = x.shape
-    rows = lib().pdnn_bn_reduce_rows(L, C)
-    slab = torch.empty(2 * rows, C, device=x.device, dtype=F32)
-    slab2 = torch.empty_like(slab) if x2 is not None else None
+    slab = stat_bins(C, x.device)
+    slab2 = stat_bins(C, x.device) if x2 is not None else None
     call("pdnn_bn_bwd_reduce", ptr(g), ptr(x), L, C, ptr(mean), ptr(invstd), int(mode), ptr(msrc), ptr(mscale),
          ptr(mshift), ptr(slab), ptr(x2), ptr(mean2), ptr(invstd2), ptr(slab2), stream())
-    return slab, slab2, rows
+    return slab, slab2, STAT_BINS
 
 
 def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=None):
@@ -544,11 +553,11 @@ def bn_bwd_finalize(slab, rows, dgamma=None, dbeta=None, accumulate=False, acc=N
     if dgamma is None:
         dgamma = torch.empty(C, device=slab.device, dtype=F32)
         dbeta = torch.empty_like(dgamma)
-    work = _fin_work(rows, C, slab.device)
-    cnt = _fin_counters(C, slab.device) if work is not None else None
     ga, ba = acc if acc is not None else (None, None)
-    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(work), ptr(ga),
-         ptr(ba), ptr(cnt), stream())
+    _chk(rows == STAT_BINS and slab.shape[0] == 2 * STAT_BINS, "bn_bwd_finalize: a stat_bins() slab")
+    call("pdnn_bn_bwd_finalize", ptr(slab), rows, C, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(ga), ptr(ba),
+         stream())
+    _release_bins(slab)
     return dgamma, dbeta
 
 
@@ -593,7 +602,7 @@ def stem_conv(x, w, want_stats=True):
     y = torch.empty(N, Ho, Wo, 64, device=x.device, dtype=BF16)
     slab = None
     if want_stats:
-        slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
+        slab = stat_bins(64, x.device)
     call("pdnn_stem_conv", ptr(x), ptr(w), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
     return y, slab
 
@@ -614,7 +623,7 @@ def stem_conv_nchw(x, w32, want_stats=True):
     y = torch.empty(N, Ho, Wo, 64, device=x.device, dtype=BF16)
     slab = None
     if want_stats:
-        slab = torch.empty(2 * lib().pdnn_stem_stats_rows(N * Ho * Wo), 64, device=x.device, dtype=F32)
+        slab = stat_bins(64, x.device)
     call("pdnn_stem_conv_nchw", ptr(x), ptr(w32), ptr(y), N, H, W, Ho, Wo, ptr(slab), stream())
     return y, slab
 
@@ -712,10 +721,10 @@ def maxpool_bwd_bnred(dy, idx, t, mean, invstd, mscale, mshift):
     if rows <= 0:
         return None
     ga = torch.empty(N, H, W, C, device=dy.device, dtype=BF16)
-    slab = torch.empty(2 * rows, C, device=dy.device, dtype=F32)
+    slab = stat_bins(C, dy.device)
     call("pdnn_maxpool_bwd_bnred", ptr(dy.contiguous()), ptr(idx), ptr(ga), ptr(t), ptr(mean), ptr(invstd),
          ptr(mscale), ptr(mshift), ptr(slab), N, Ho, Wo, C, stream())
-    return ga, slab, rows
+    return ga, slab, STAT_BINS
 
 
 def avgpool_fwd(x):
@@ -896,14 +905,14 @@ def layernorm_bwd(dy, x, g, mean, rstd, dres=None, acc=None):
     dy = dy.contiguous()
     _chk(dy.shape == x.shape and (dres is None or dres.shape == x.shape), "layernorm_bwd: shapes")
     nb = lib().pdnn_layernorm_bwd_blocks(R)
-    slab = torch.empty(2 * nb, D, device=x.device, dtype=F32)
+    slab = stat_bins(D, x.device)
     dx = torch.empty_like(x)
     call("pdnn_layernorm_bwd", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(slab), R, D,
          nb, stream())
     if acc is not None:
-        bn_bwd_finalize(slab, nb, dgamma=acc[0], dbeta=acc[1], accumulate=True)
+        bn_bwd_finalize(slab, STAT_BINS, dgamma=acc[0], dbeta=acc[1], accumulate=True)
         return dx, None, None
-    dg, db = bn_bwd_finalize(slab, nb)
+    dg, db = bn_bwd_finalize(slab, STAT_BINS)
     return dx, dg, db
 
 
@@ -1031,17 +1040,19 @@ def conv3x3_fp8(x, wq, winv, act, want_stats=False, bn=None, pre=None, pro=None)
     slab = None
     t = mean = inv = msc = msh = None
     if want_stats or bn is not None:
-        slab = torch.empty(2 * lib().pdnn_conv3x3_stats_rows(Nimg, H, W), Ko, device=x.device, dtype=F32)
+        slab = stat_bins(Ko, x.device)
     if bn is not None:
         t, mean, inv, msc, msh = bn
-    args = (ptr(x), ptr(wq), ptr(y), Nimg, H, W, C, Ko, ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh),
-            *_pre_args(pre, x), ptr(act.scale), ptr(act.inv), ptr(winv), ptr(act.amax), int(act.e5m2),
-            ptr(pro[0] if pro is not None else None), ptr(pro[1] if pro is not None else None), stream())
+    def args(sl):
+        return (ptr(x), ptr(wq), ptr(y), Nimg, H, W, C, Ko, ptr(sl), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh),
+                *_pre_args(pre, x), ptr(act.scale), ptr(act.inv), ptr(winv), ptr(act.amax), int(act.e5m2),
+                ptr(pro[0] if pro is not None else None), ptr(pro[1] if pro is not None else None), stream())
     if not act.primed:
-        call("pdnn_conv3x3_fp8", *args)
+        # the priming run's statistics go to a throwaway slab (the bins are added into, not overwritten)
+        call("pdnn_conv3x3_fp8", *args(stat_bins(Ko, x.device) if slab is not None else None))
         fp8_scale_roll(act.amax, act.scale, act.inv, act.e5m2, act.margin)
         act.primed = True
-    call("pdnn_conv3x3_fp8", *args)
+    call("pdnn_conv3x3_fp8", *args(slab))
     fp8_scale_roll(act.amax, act.scale, act.inv, act.e5m2, act.margin)
     return y, slab
 

@@ -10,6 +10,10 @@ side_wgrad         1        conv weight gradients on a second HIP stream beside 
                             (ResNet-50 +8.3%, profiles/resnet50_bs256_side_stream_r2.txt); 0 = one stream
 wide1x1_dgrad      1        1x1 / stride-1 data gradients with K >= 512 and >= 1024 outputs (ResNet-50 stage-4 conv1) on
                             the long-reduction streaming kernel (conv1x1_wide.hip): 81 vs 102 us per layer (r4_02)
+a2_fold            1        Bottleneck conv3 reads relu(bn2(t2)) through the A-stationary kernel's operand prologue
+                            instead of a materialised a2: 0 never, 1 where its weight gradient already runs on the
+                            implicit-GEMM engine (more than 200,704 pixels: ResNet-50 stage 1 at bs 256), 2 wherever
+                            the kernel takes the shape (the weight gradient then leaves the ping-pong engine)
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there
@@ -19,7 +23,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1}
 
 _VALUES = dict(DEFAULTS)
 

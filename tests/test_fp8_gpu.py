@@ -92,7 +92,7 @@ def _gemm_fp8_case(K, M, N, Kd):
     assert ((y.float() - (ref + b)).norm() / (ref + b).norm()) < 1e-2
     y32 = K.gemm_fp8(xq, wq, scale, out_f32=True)
     assert ((y32 - ref).norm() / ref.norm()) < 1e-4
-    slab = torch.empty(2 * K.stats_rows(M), N, device="cuda")
+    slab = K.stat_bins(N, torch.device("cuda"))             # zeroed bins: the epilogue adds into them
     ys = K.gemm_fp8(xq, wq, scale, stats=slab)
     yf = ys.float()
     sums = slab.view(-1, 2, N).sum(0)
@@ -304,7 +304,9 @@ def test_conv3x3_fp8_forward_prologue(K):
     act0, act1 = Fp8Act(t.device), Fp8Act(t.device)
     y0, s0 = K.conv3x3_fp8(a, wq, winv, act0, want_stats=True)
     y1, s1 = K.conv3x3_fp8(t, wq, winv, act1, want_stats=True, pro=(sc, sh))
-    assert torch.equal(y0, y1) and torch.equal(s0, s1)
+    assert torch.equal(y0, y1)
+    s0, s1 = s0.view(-1, 2, Ko).double().sum(0), s1.view(-1, 2, Ko).double().sum(0)      # fp32 atomic bins
+    assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-5 * s0.abs().max().item())
     assert torch.equal(act0.scale, act1.scale)
     dy = (torch.randn(N, H, W, Ko, device="cuda") * 1e-3).to(torch.bfloat16)
     ad = Fp8Act(t.device, e5m2=True)

@@ -120,7 +120,8 @@ def _resnet_grads(arch="resnet50"):
 
 
 @pytest.mark.parametrize("key,arch", [("side_wgrad", "resnet50"), ("wide1x1_dgrad", "resnet50"),
-                                      ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("side_wgrad", "resnet18")])
+                                      ("conv3x3", "resnet50"), ("panel1x1", "resnet50"), ("side_wgrad", "resnet18"),
+                                      ("a2_fold", "resnet50")])
 # (the stem entry is compared at the StemFn level in tests/test_stem_gpu.py: a 1-ulp flip in the stem output
 # -- the NCHW kernel's different summation order -- is amplified by this 4-image net's tiny BatchNorm batches
 # into O(1) gradient differences; modes 0 and 1 are bitwise equal, gpurun_out/r3_23)
@@ -129,6 +130,11 @@ def test_python_entry_alternatives(K, key, arch):
     from pytorch_distributed_nn_amd import tuning
     base = _resnet_grads(arch)
     # conv3x3 / panel1x1: the routers' own switches (set_conv3x3_mode / set_panel_mode), not table entries
+    # a2_fold: the 64x64 test images are below the default's pixel threshold, so compare off (0) against everywhere (2)
+    if key == "a2_fold":
+        tuning.set(key, 2)
+        base = _resnet_grads(arch)
+        tuning.set(key, tuning.DEFAULTS[key])
     old = tuning.set(key, 0) if key in tuning.DEFAULTS else None
     if key == "conv3x3":
         K.set_conv3x3_mode(0)
