@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import torch
 
-from ._backend import call, lib, ptr, stream
+from ._backend import _CUR_DEV, call, lib, ptr, stream
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -472,7 +472,9 @@ _BINS = {}
 
 
 def _bins_key(device, C):
-    return (device.index, torch.cuda.current_stream(device).cuda_stream, C)
+    # the raw stream handle (no torch.cuda.Stream object: ~100 of these per step sit on the host's critical path
+    # in the forward, which the GPU can outrun)
+    return (device.index, stream() if device.index == _CUR_DEV() else torch.cuda.current_stream(device).cuda_stream, C)
 
 
 def stat_bins(C, device):
