@@ -24,8 +24,30 @@
 //   delta[q] = sum_d dO[q][d] O[q][d] comes from attn_bwd_delta.
 #include "common.h"
 
+// Block order over (query or key tile, head, sequence): 0 = 3-D grid, heavy tiles first inside each (head, sequence);
+// 1 = 1-D grid, heavy tiles first over the WHOLE grid (the dispatcher hands out blocks in index order, so the last
+// blocks to start are the lightest ones and the causal triangle's tail is short)
+#ifndef PDNN_ATTN_ORDER
+#define PDNN_ATTN_ORDER 1
+#endif
+
 namespace {
 constexpr int HD = 64;          // head dim
+
+// (tile, head, sequence) of this block; heavy = tile index giving the most work first
+__device__ __forceinline__ void attn_block(int ntile, int H, bool heavy_is_last, int& tile, int& h, int& b) {
+#if PDNN_ATTN_ORDER == 1
+    const int t = blockIdx.x, HB = gridDim.x / ntile;      // 1-D grid of ntile x H x B blocks
+    const int r = t / HB, hb = t - r * HB;
+    tile = heavy_is_last ? ntile - 1 - r : r;
+    h = hb % H;
+    b = hb / H;
+#else
+    tile = heavy_is_last ? ntile - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    h = blockIdx.y;
+    b = blockIdx.z;
+#endif
+}
 constexpr int NTA = 256;
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -112,8 +134,9 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
     __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const int nqb = T / 128;
-    const int qb = nqb - 1 - blockIdx.x;             // heavy (late) query tiles first
-    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    int qb, h, b;
+    attn_block(nqb, H, true, qb, h, b);              // heavy (late) query tiles first
+    const int D = H * HD;
     const long ld = 3L * D;
     const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
     const bf16_t* Kp = Q + D;
@@ -287,8 +310,9 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
     __shared__ __attribute__((aligned(16))) float lsd[2][2][64];              // [buf][lse2|delta][query]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const int nkb = T / 64;
-    const int kb = blockIdx.x;                       // early key tiles have the most work: launched first
-    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    int kb, h, b;
+    attn_block(nkb, H, false, kb, h, b);             // early key tiles have the most work: launched first
+    const int D = H * HD;
     const long ld = 3L * D;
     const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
     const bf16_t* Kp = Q + D;
@@ -416,8 +440,9 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
     __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const int nqb = T / 64;
-    const int qb = nqb - 1 - blockIdx.x;
-    const int h = blockIdx.y, b = blockIdx.z, D = H * HD;
+    int qb, h, b;
+    attn_block(nqb, H, true, qb, h, b);
+    const int D = H * HD;
     const long ld = 3L * D;
     const bf16_t* Q = qkv + (long)b * T * ld + h * HD;
     const bf16_t* Kp = Q + D;
@@ -508,11 +533,19 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
 }
 }  // namespace
 
+static dim3 attn_grid(int ntile, int H, int B) {
+#if PDNN_ATTN_ORDER == 1
+    return dim3(ntile * H * B);
+#else
+    return dim3(ntile, H, B);
+#endif
+}
+
 // qkv [B*T][3*H*64] bf16 -> out [B*T][H*64] bf16, lse2 [B][H][T] fp32.  T % 128 == 0.
 PDNN_API int pdnn_flash_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse2, int B, int T, int H, float scale,
                                  int causal, hipStream_t st) {
     if (T % 128) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3(T / 128, H, B), dim3(NTA), 0, st, qkv, out, lse2, T, H, scale, causal);
+    hipLaunchKernelGGL(attn_fwd_kernel, attn_grid(T / 128, H, B), dim3(NTA), 0, st, qkv, out, lse2, T, H, scale, causal);
     PDNN_LAUNCH_RET;
 }
 
@@ -524,9 +557,9 @@ PDNN_API int pdnn_flash_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf1
     const long n = (long)B * T * H;
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n + NTA - 1) / NTA)), dim3(NTA), 0, st, out, dO, delta,
                        B * T, T, H);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
                        scale, causal);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
                        scale, causal);
     PDNN_LAUNCH_RET;
 }
