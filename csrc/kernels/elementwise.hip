@@ -112,6 +112,9 @@ __global__ void __launch_bounds__(NT) colsum_kernel(const bf16_t* __restrict__ x
 // level 2 sums the partial rows (deterministic, no atomics).  Sized so level 1 fills the chip (>= ~256
 // blocks even for 768 columns: up to 128 row splits of >= 64 rows) and level 2 is a short unrolled
 // reduction spread over 64-column blocks (bias gradients of a GPT-2 step are 60+ of these calls).
+// ATOMIC: the block's sums are added straight into the output (no partial rows, no level-2 launch): for an
+// accumulating destination (a bias gradient in the zero-initialised flat arena); fp32 add order varies.
+template <bool ATOMIC>
 __global__ void __launch_bounds__(NT) colsum_partial_kernel(const bf16_t* __restrict__ x, long rows, int cols,
                                                             float* __restrict__ part) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -140,7 +143,11 @@ __global__ void __launch_bounds__(NT) colsum_partial_kernel(const bf16_t* __rest
     __syncthreads();
     for (int i = threadIdx.x; i < 512; i += NT) {
         const int cc = blockIdx.x * 512 + i;
-        if (cc < cols) part[(long)blockIdx.y * cols + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+        if (cc < cols) {
+            const float t = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+            if (ATOMIC) atomicAdd(part + cc, t);
+            else part[(long)blockIdx.y * cols + cc] = t;
+        }
     }
 }
 
@@ -202,12 +209,16 @@ PDNN_API int pdnn_nhwc_to_nchw_f32(const bf16_t* x, float* y, int N, int C, int 
                        HW, Cp);
     PDNN_LAUNCH_RET;
 }
-// work: pdnn_colsum_splits(rows) * cols floats (required when cols % 8 == 0 and rows > 256)
+// work: pdnn_colsum_splits(rows) * cols floats for the two-level deterministic form (cols % 8 == 0, rows > 256);
+// accumulate with no work: the one-launch atomic form for those shapes
 PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int accumulate, float* work,
                          hipStream_t st) {
-    if (work && cols % 8 == 0 && rows > 256) {
+    if (accumulate && !work && cols % 8 == 0 && rows > 256) {
+        hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3((cols + 511) / 512, pdnn_colsum_splits(rows)), dim3(NT), 0,
+                           st, x, rows, cols, out);
+    } else if (work && cols % 8 == 0 && rows > 256) {
         const int sp = pdnn_colsum_splits(rows);
-        hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 511) / 512, sp), dim3(NT), 0, st, x, rows, cols, work);
+        hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3((cols + 511) / 512, sp), dim3(NT), 0, st, x, rows, cols, work);
         hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, work, sp, cols, out,
                            accumulate);
     } else {
@@ -222,10 +233,8 @@ PDNN_API int pdnn_colsum(const bf16_t* x, long rows, int cols, float* out, int a
 // so the column reads of the transposed pass hit distinct banks.  Used for the reduction-major copies of
 // the transformer weights (ops/functional.weight_bf16_t): the data-gradient GEMM then reads K-major B.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src, long lds, bf16_t* __restrict__ dst,
-                                                             long ldd, int R, int C) {
-    __shared__ bf16_t t[64][66];
-    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+__device__ __forceinline__ void transpose_tile(const bf16_t* __restrict__ src, long lds, bf16_t* __restrict__ dst,
+                                               long ldd, int R, int C, int r0, int c0, bf16_t (*t)[66]) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {                     // 64 rows x 8 chunks = 512 loads
@@ -251,7 +260,59 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __res
     }
 }
 
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src, long lds, bf16_t* __restrict__ dst,
+                                                             long ldd, int R, int C) {
+    __shared__ bf16_t t[64][66];
+    transpose_tile(src, lds, dst, ldd, R, C, blockIdx.y * 64, blockIdx.x * 64, t);
+}
+
+// Many contiguous matrices in one launch (the transposed weight copies of a whole transformer, refreshed
+// once per optimizer step instead of one ~5 us launch per weight inside the backward).  The table rides in
+// the kernel arguments; block b belongs to the last entry with tile0 <= b (binary search, scalar loads).
+constexpr int TMULTI = 64;
+struct TDesc {
+    const bf16_t* src;
+    bf16_t* dst;
+    int R, C, tiles_c, tile0;
+};
+struct TBatch {
+    TDesc d[TMULTI];
+    int n;
+};
+__global__ void __launch_bounds__(256) transpose_bf16_multi_kernel(const TBatch b) {
+    __shared__ bf16_t t[64][66];
+    const int blk = blockIdx.x;
+    int lo = 0, hi = b.n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (b.d[mid].tile0 <= blk) lo = mid;
+        else hi = mid - 1;
+    }
+    const TDesc& e = b.d[lo];
+    const int k = blk - e.tile0, tr = k / e.tiles_c, tc = k - tr * e.tiles_c;
+    transpose_tile(e.src, e.C, e.dst, e.R, e.R, e.C, tr * 64, tc * 64, t);
+}
+
 PDNN_API int pdnn_transpose_bf16(const bf16_t* src, long lds, bf16_t* dst, long ldd, int R, int C, hipStream_t st) {
     hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, st, src, lds, dst, ldd, R, C);
     PDNN_LAUNCH_RET;
+}
+// srcs[i] [R[i]][C[i]] (contiguous) -> dsts[i] [C[i]][R[i]]; any count (launches of TMULTI matrices each)
+PDNN_API int pdnn_transpose_bf16_multi(const bf16_t* const* srcs, bf16_t* const* dsts, const int* R, const int* C,
+                                       int n, hipStream_t st) {
+    for (int base = 0; base < n; base += TMULTI) {
+        TBatch b;
+        b.n = n - base < TMULTI ? n - base : TMULTI;
+        int tiles = 0;
+        for (int i = 0; i < b.n; ++i) {
+            const int q = base + i;
+            if (R[q] <= 0 || C[q] <= 0) return 1;        // hipErrorInvalidValue
+            b.d[i] = TDesc{srcs[q], dsts[q], R[q], C[q], (C[q] + 63) / 64, tiles};
+            tiles += ((R[q] + 63) / 64) * ((C[q] + 63) / 64);
+        }
+        hipLaunchKernelGGL(transpose_bf16_multi_kernel, dim3(tiles), dim3(256), 0, st, b);
+        const int e = (int)hipGetLastError();
+        if (e) return e;
+    }
+    return 0;
 }

@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import tuning
 from ..ops import functional as OF
 from ..ops import transformer as TX
 from ..optim.flat import direct_grad
@@ -142,6 +143,15 @@ class GPT2(nn.Module):
         T = T or c.block_size
         return 6 * self.num_params() + 12 * c.n_layer * c.n_embd * T
 
+    def _t_weights(self):
+        ws = self.__dict__.get("_pdnn_t_ws")
+        if ws is None:
+            ws = [self.transformer.wte.weight]
+            for blk in self.transformer.h:
+                ws += [blk.attn.c_attn.weight, blk.attn.c_proj.weight, blk.mlp.c_fc.weight, blk.mlp.c_proj.weight]
+            self.__dict__["_pdnn_t_ws"] = ws
+        return ws
+
     def forward(self, idx, targets=None):
         B, T = idx.shape
         c = self.config
@@ -150,6 +160,12 @@ class GPT2(nn.Module):
             return self._forward_reference(idx, targets)
         tr = self.transformer
         wte, wpe = tr.wte.weight, tr.wpe.weight
+        pf = tuning.get("wt_prefetch")
+        if pf and targets is not None and torch.is_grad_enabled():
+            # the data-gradient GEMMs' transposed weight copies, refreshed in one launch at forward start
+            # (instead of ~50 small transposes inside the backward)
+            from ..ops.fused_resnet import _side_stream
+            OF.prefetch_weight_t(self._t_weights(), _side_stream(idx.device) if pf == 2 else None)
         wte_k, wpe_k = OF.weight_bf16(wte), OF.weight_bf16(wpe)
         # tied wte: with targets the fused LM head and the embedding both accumulate into its arena gradient
         hd = targets is not None and direct_grad(wte) is not None

@@ -80,6 +80,7 @@ _SIGS = {
     "pdnn_pp_gemm_nt_splitk": [P, L, P, L, P, L, I, I, I, P, I, P],
     "pdnn_pp_splitk_splits": [I, I, I],
     "pdnn_transpose_bf16": [P, L, P, L, I, I, P],
+    "pdnn_transpose_bf16_multi": [P, P, P, P, I, P],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
     "pdnn_bn_finalize": [P, I, I, D, F, F, P, P, P, P, P, P, P, P, P],

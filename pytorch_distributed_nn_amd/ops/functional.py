@@ -47,10 +47,15 @@ def weight_bf16_t(p: torch.Tensor) -> torch.Tensor:
     """bf16 transposed copy W^T [K][N] of a 2-D weight W [N][K] (the data-gradient GEMM's K-major B operand),
     cached per parameter version / flat-arena update generation, rebuilt by the in-tree transpose kernel."""
     await_param(p)                     # before the cache check: a PS bucket landing bumps the generation
-    fp = getattr(p, "_pdnn_flat", None)
-    ver = (p._version, fp.generation if fp is not None else 0)
+    ver = _t_version(p)
     st = getattr(p, "_pdnn_shadow_t", None)
     if st is not None and st[0] == ver:
+        tok = p.__dict__.get("_pdnn_t_wait")
+        if tok is not None:            # made on the side stream by prefetch_weight_t
+            if not tok[1]:
+                torch.cuda.current_stream(p.device).wait_event(tok[0])
+                tok[1] = True
+            p._pdnn_t_wait = None
         return st[1]
     wb = weight_bf16(p)
     if wb.is_cuda:
@@ -60,6 +65,54 @@ def weight_bf16_t(p: torch.Tensor) -> torch.Tensor:
         wt = wb.t().contiguous()
     p._pdnn_shadow_t = (ver, wt)
     return wt
+
+
+def _t_version(p):
+    fp = getattr(p, "_pdnn_flat", None)
+    return (p._version, fp.generation if fp is not None else 0)
+
+
+def prefetch_weight_t(ps, side=None):
+    """Refresh the transposed copies (:func:`weight_bf16_t`) of every stale 2-D weight of ``ps`` in ONE
+    batched launch (``kernels.transpose_bf16_multi``) at the start of a forward, on the ``side`` stream when
+    given (ordered after the compute stream's optimizer step; the first backward use waits on one event), so
+    the ~50 per-weight ~5 us transposes of a GPT-2 step leave the backward.  Parameters still arriving (PS
+    workers mark them ``_pdnn_weight_pending``) keep the lazy per-use path."""
+    todo = []
+    for p in ps:
+        if not p.is_cuda or p.dim() != 2 or "_pdnn_weight_pending" in p.__dict__:
+            continue
+        ver = _t_version(p)
+        st = getattr(p, "_pdnn_shadow_t", None)
+        if st is not None and st[0] == ver:
+            continue
+        wb = weight_bf16(p)
+        if not wb.is_contiguous():
+            continue
+        out = st[1] if st is not None and st[1].shape == (wb.shape[1], wb.shape[0]) else None
+        if out is None:
+            out = torch.empty(wb.shape[1], wb.shape[0], device=wb.device, dtype=BF16)
+        todo.append((p, ver, wb, out))
+    if not todo:
+        return
+    pairs = [(wb, out) for _, _, wb, out in todo]
+    if side is None:
+        K.transpose_bf16_multi(pairs)
+        tok = None
+    else:
+        main = torch.cuda.current_stream(todo[0][0].device)
+        K.stream_wait(side, main)
+        with torch.cuda.stream(side):
+            K.transpose_bf16_multi(pairs)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        tok = [ev, False]
+        for _, _, wb, out in todo:
+            out.record_stream(side)
+            wb.record_stream(side)
+    for p, ver, _, out in todo:
+        p._pdnn_shadow_t = (ver, out)
+        p._pdnn_t_wait = tok
 
 
 def _pad_last(t, mult=8):

@@ -7,6 +7,8 @@ allocator, and launches on torch's current stream.  Activations are NHWC bf16 te
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from ._backend import _CUR_DEV, call, lib, ptr, stream
@@ -98,6 +100,21 @@ def transpose_bf16(x, out=None):
         out = torch.empty(C, R, device=x.device, dtype=BF16)
     call("pdnn_transpose_bf16", ptr(x), x.stride(0), ptr(out), out.stride(0), R, C, stream())
     return out
+
+
+def transpose_bf16_multi(pairs):
+    """dst[C][R] = src[R][C] for every (src, dst) of ``pairs`` (contiguous bf16 2-D), in one launch per 64."""
+    n = len(pairs)
+    if n == 0:
+        return
+    for s_, d_ in pairs:
+        _chk(s_.dtype == BF16 and d_.dtype == BF16 and s_.dim() == 2 and s_.is_contiguous() and d_.is_contiguous()
+             and d_.shape == (s_.shape[1], s_.shape[0]), "transpose_bf16_multi: contiguous bf16 [R][C] -> [C][R]")
+    srcs = (ctypes.c_void_p * n)(*[s_.data_ptr() for s_, _ in pairs])
+    dsts = (ctypes.c_void_p * n)(*[d_.data_ptr() for _, d_ in pairs])
+    rs = (ctypes.c_int * n)(*[s_.shape[0] for s_, _ in pairs])
+    cs = (ctypes.c_int * n)(*[s_.shape[1] for s_, _ in pairs])
+    call("pdnn_transpose_bf16_multi", srcs, dsts, rs, cs, n, stream())
 
 
 def gemm_nt(x, w, bias=None, relu=False, out_f32=False, alpha=1.0, out=None):
@@ -811,12 +828,15 @@ def nhwc_to_nchw_f32(x, C):
     return y
 
 
-def colsum(x2d, out=None, accumulate=False):
+def colsum(x2d, out=None, accumulate=False, deterministic=False):
+    """out[C] (fp32) = (or +=) column sums of a bf16 [R][C] matrix.  Accumulating into ``out`` takes the
+    one-launch atomic form (no partial rows / level-2 kernel; add order varies) unless ``deterministic``."""
     R, C = x2d.shape
+    x2d = x2d.contiguous()
     if out is None:
         out = torch.empty(C, device=x2d.device, dtype=F32)
     work = None
-    if C % 8 == 0 and R > 256 and x2d.is_contiguous():
+    if C % 8 == 0 and R > 256 and (deterministic or not accumulate):
         work = torch.empty(lib().pdnn_colsum_splits(R) * C, device=x2d.device, dtype=F32)
     call("pdnn_colsum", ptr(x2d), R, C, ptr(out), int(accumulate), ptr(work), stream())
     return out

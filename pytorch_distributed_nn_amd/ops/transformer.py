@@ -33,6 +33,7 @@ import torch.nn.functional as F
 from ..optim.flat import direct_grad, grad_ready
 from . import linear as BL
 from . import kernels as K
+from .. import tuning as _tuning
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -196,7 +197,7 @@ class _Sink:
         if p_b is not None:
             tb = self._tgt(p_b)
             if tb is not None:
-                K.colsum(g, out=tb, accumulate=True)
+                K.colsum(g, out=tb, accumulate=True, deterministic=not _tuning.get("colsum_atomic"))
             else:
                 rb = K.colsum(g)
         return rw, rb

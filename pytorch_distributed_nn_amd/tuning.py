@@ -14,6 +14,12 @@ a2_fold            1        Bottleneck conv3 reads relu(bn2(t2)) through the A-s
                             instead of a materialised a2: 0 never, 1 where its weight gradient already runs on the
                             implicit-GEMM engine (more than 200,704 pixels: ResNet-50 stage 1 at bs 256), 2 wherever
                             the kernel takes the shape (the weight gradient then leaves the ping-pong engine)
+wt_prefetch        0        GPT-2 data-gradient GEMMs' transposed weight copies: 0 one transpose launch per weight at
+                            its first backward use, 1 all of them in one launch at forward start (compute stream),
+                            2 that launch on the side stream beside the forward (544.7k / 542.3k / 537.0k tok/s,
+                            gpurun_out/r5_10: the eager backward has launch gaps the small transposes fill)
+colsum_atomic      1        accumulating bias-gradient column sums in one launch with fp32 atomics (0: two-level
+                            deterministic partial rows + level-2 launch; GPT-2 542.3k vs 538.0k tok/s, r5_10)
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there
@@ -23,7 +29,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "colsum_atomic": 1}
 
 _VALUES = dict(DEFAULTS)
 

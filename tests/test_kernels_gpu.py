@@ -425,8 +425,21 @@ def test_colsum(K, R, C):
     out = K.colsum(x)
     ref = x.float().sum(0)
     assert rel(out, ref) < 1e-4
-    K.colsum(x, out=out, accumulate=True)
+    K.colsum(x, out=out, accumulate=True)                       # tall shapes: one-launch atomic form
     assert rel(out, 2 * ref) < 1e-4
+    K.colsum(x, out=out, accumulate=True, deterministic=True)   # two-level form
+    assert rel(out, 3 * ref) < 1e-4
+
+
+def test_transpose_bf16_multi(K):
+    """One launch over many matrices (ragged edges, > 64 entries so the host splits the table)."""
+    shapes = [(768, 2304), (3072, 768), (100, 37), (8, 8), (50257, 768)] + [(64 + i, 72 + 3 * i) for i in range(70)]
+    srcs = [rnd(r, c) for r, c in shapes]
+    dsts = [torch.empty(c, r, device="cuda", dtype=torch.bfloat16) for r, c in shapes]
+    K.transpose_bf16_multi(list(zip(srcs, dsts)))
+    torch.cuda.synchronize()
+    for s_, d_ in zip(srcs, dsts):
+        assert torch.equal(d_, s_.t())
 
 
 @pytest.mark.parametrize("M,N,Kd", [(1000, 776, 1024), (2048, 2048, 64), (4104, 1032, 768), (8192, 3072, 768)])

@@ -214,6 +214,28 @@ def test_gpt2_flat_arena_grads_match_autograd_path():
         assert rel2(pf.grad, p.grad) < 1e-3, n
 
 
+def test_gpt2_prefetched_transposes_track_optimizer_steps():
+    """The forward refreshes every transposed weight copy in one side-stream launch (prefetch_weight_t);
+    after each optimizer step the copies must be current (version key) and equal W^T of the new shadow."""
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
+    m = _tiny(seed=5).cuda()
+    flatten_module(m)
+    opt = AdamW(m.parameters(), lr=1e-3)
+    idx = torch.randint(0, m.config.vocab_size, (2, 128), device="cuda")
+    tgt = torch.randint(0, m.config.vocab_size, (2, 128), device="cuda")
+    for _ in range(3):
+        opt.zero_grad()
+        loss = m(idx, tgt)
+        torch.cuda.synchronize()
+        for p in m._t_weights():
+            ver, wt = p._pdnn_shadow_t
+            assert ver == OF._t_version(p)
+            assert torch.equal(wt, OF.weight_bf16(p).t())
+        loss.backward()
+        opt.step()
+
+
 def test_gpt2_tiny_trains():
     from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
     m = _tiny(seed=1).cuda()
