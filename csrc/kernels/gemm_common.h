@@ -44,6 +44,7 @@ struct GemmArgs {
     int relu;                 // epilogue activation: 0 none, 1 ReLU, 2 GELU (tanh form)
     float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
     int ktiles_per_split;     // split-K (grid.z)
+    int ksl_rem;              // pp engine: the first ksl_rem K-splits take one slice more (uneven splits)
     int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
     int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
     int transC;               // E_ATOMIC: accumulate C^T (C[n * ldc + m])

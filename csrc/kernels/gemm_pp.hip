@@ -189,11 +189,15 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     const int tiles_m = (a.M + PP_BM - 1) / PP_BM, tiles_n = (a.N + C::BN - 1) / C::BN;
     const int ntiles = tiles_m * tiles_n;
     const int splits = a.nb2 > 0 ? a.nb2 : 1;                  // K-splits (slab epilogue when > 1)
-    const int nsl = a.ktiles_per_split;                          // slices per work item (divides K / 32)
+    // slices of K-split z: nsl, one more for the first `rem` splits (split z starts at z nsl + min(z, rem))
+    const int nsl = a.ktiles_per_split, rem = a.ksl_rem;
     const int G = gridDim.x, b = blockIdx.x;
     const int nitems = (ntiles * splits - b + G - 1) / G;
     if (nitems <= 0 || nsl <= 0) return;                         // uniform over the block
-    const int Q = nitems * nsl;                                  // slices this block consumes
+    auto item_nsl = [&](int i) { return nsl + ((b + i * G) / ntiles < rem ? 1 : 0); };
+    int Q = nitems * nsl;                                        // slices this block consumes
+    if (rem)
+        for (int i = 0; i < nitems; ++i) Q += item_nsl(i) - nsl;
 
     // work item i of this block -> (m0, n0, first slice, split)
     auto item = [&](int i, int& m0, int& n0, int& z) {
@@ -209,21 +213,23 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     LA la;
     LB lb;
     // issue cursor (slices run ahead of the compute cursor by up to D): loaders point at the next slice
-    int iss_item = 0, iss_s = 0, wr_off = 0;
+    int iss_item = 0, iss_s = 0, iss_n = nsl, wr_off = 0;
     auto load_item = [&](int i) {
         int m0, n0, z;
         item(i, m0, n0, z);
         la.init(a.A, a.lda, a.M, m0, wave, lane);
         lb.init(a.B, a.ldb, a.N, n0, wave, lane);
-        la.skip(z * nsl);
-        lb.skip(z * nsl);
+        const int k0 = z * nsl + min(z, rem);
+        la.skip(k0);
+        lb.skip(k0);
+        iss_n = item_nsl(i);
     };
     auto issue_next = [&]() {                                    // copy the next stream slice into its slot
         bf16_t* img = sb + wr_off;
         la.issue_next(img);
         lb.issue_next(img + C::IMA);
         wr_off = wr_off + C::SLOT == NB * C::SLOT ? 0 : wr_off + C::SLOT;
-        if (++iss_s == nsl) {
+        if (++iss_s == iss_n) {
             iss_s = 0;
             if (++iss_item < nitems) load_item(iss_item);
         }
@@ -264,12 +270,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     };
 
     int s = 0, cur = 0, rd_off = 0;                      // slice within the current item, item index, read slot
+    int cur_n = item_nsl(0);                             // slices of item `cur`
     auto epilogue = [&]() {
             // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
             if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
             s = 0;
             int m0, n0, z;
             item(cur++, m0, n0, z);
+            cur_n = item_nsl(cur);
             constexpr bool SUMS = (FX & (FX_STATS | FX_BNB)) != 0;
             float s_[SUMS ? C::FN : 1][4], q_[SUMS ? C::FN : 1][4];   // per-column partial sums over 64 rows
             if constexpr (SUMS) {
@@ -574,7 +582,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
-            if (++s < nsl) continue;
+            if (++s < cur_n) continue;
             epilogue();
         }
         if (grp == 0) __builtin_amdgcn_s_barrier();      // balance the stagger
@@ -909,8 +917,9 @@ PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb,
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.alpha = alpha;
     const int nsl = K / PP_SK;
-    while (nsl % splits) --splits;                 // work items have equal slice counts
-    a.ktiles_per_split = nsl / splits;
+    if (splits > nsl) splits = nsl;
+    a.ktiles_per_split = nsl / splits;             // the first nsl % splits splits take one slice more
+    a.ksl_rem = nsl % splits;
     const int bn = pick_bn(a, false);
     if (splits == 1) {
         a.C = out; a.ldc = ldc; a.acc_c = 1;
@@ -970,7 +979,7 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
 
 PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
     using namespace pg;
-    // K-splits (equal slice counts, >= 16 slices each) minimising  rounds x (slices per item + ~10 slices of
+    // K-splits (>= 16 slices each, the first nsl % s one slice longer) minimising  rounds x (longest item + ~10 slices of
     // per-item prologue/epilogue), with a 4% per-split surcharge for the fp32 slab traffic and reduction:
     // a split count that spills a few items into a second round of the persistent grid costs as much as
     // halving it (GPT-2 fc / fc2: 4 -> 2 splits, tools/pp_check.py wg_* rows)
@@ -983,8 +992,8 @@ PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
     int best = 1;
     double bt = 1e300;
     for (int s = 1; s <= 32; ++s) {
-        if (nsl % s || (s > 1 && nsl / s < 16)) continue;
-        const double t = (double)cdiv(tiles * s, cus) * (nsl / s + 10) * (1.0 + 0.04 * (s - 1));
+        if (s > 1 && nsl / s < 16) continue;
+        const double t = (double)cdiv(tiles * s, cus) * (cdiv(nsl, s) + 10) * (1.0 + 0.04 * (s - 1));
         if (t < bt) { bt = t; best = s; }
     }
     return best;

@@ -431,6 +431,18 @@ def test_colsum(K, R, C):
     assert rel(out, 3 * ref) < 1e-4
 
 
+@pytest.mark.parametrize("Kd,M,N,splits", [(8192, 3072, 768, None), (8192, 768, 3072, 3), (8192, 768, 768, 14),
+                                           (1024, 768, 768, 5), (96, 520, 264, 2), (8192, 2304, 768, 1)])
+def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
+    """out += x^T y on the ping-pong engine; split counts that do not divide the K slices give the first
+    splits one slice more (every slice summed exactly once)."""
+    x, y = rnd(Kd, M), rnd(Kd, N)
+    out = torch.randn(M, N, device="cuda")
+    ref = out + x.float().t() @ y.float()
+    K.pp_wgrad(x, y, out, splits=splits)
+    assert rel(out, ref) < 2e-5
+
+
 def test_transpose_bf16_multi(K):
     """One launch over many matrices (ragged edges, > 64 entries so the host splits the table)."""
     shapes = [(768, 2304), (3072, 768), (100, 37), (8, 8), (50257, 768)] + [(64 + i, 72 + 3 * i) for i in range(70)]

@@ -214,9 +214,20 @@ def test_gpt2_flat_arena_grads_match_autograd_path():
         assert rel2(pf.grad, p.grad) < 1e-3, n
 
 
-def test_gpt2_prefetched_transposes_track_optimizer_steps():
-    """The forward refreshes every transposed weight copy in one side-stream launch (prefetch_weight_t);
-    after each optimizer step the copies must be current (version key) and equal W^T of the new shadow."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpt2_prefetched_transposes_track_optimizer_steps(mode):
+    """tuning wt_prefetch 1 / 2: the forward refreshes every transposed weight copy in one launch
+    (prefetch_weight_t) on the compute / side stream; after each optimizer step the copies must be current
+    (version key) and equal W^T of the new shadow."""
+    from pytorch_distributed_nn_amd import tuning
+    old = tuning.set("wt_prefetch", mode)
+    try:
+        _prefetch_run()
+    finally:
+        tuning.set("wt_prefetch", old)
+
+
+def _prefetch_run():
     from pytorch_distributed_nn_amd.ops import functional as OF
     from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
     m = _tiny(seed=5).cuda()
