@@ -5,11 +5,14 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from pytorch_distributed_nn_amd.ops import kernels as K  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "both"
-for name, M, N, Kd in [("fc2", 8192, 768, 3072), ("qkv_dgrad", 8192, 768, 2304), ("proj", 8192, 768, 768)]:
+shapes = [("fc2", 8192, 768, 3072), ("qkv_dgrad", 8192, 768, 2304), ("proj", 8192, 768, 768)]
+if len(sys.argv) > 2:
+    shapes = [s_ for s_ in shapes if s_[0] == sys.argv[2]]
+for name, M, N, Kd in shapes:
     x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
     w = (torch.randn(N, Kd, device="cuda") * 0.05).to(torch.bfloat16)
     for _ in range(20):

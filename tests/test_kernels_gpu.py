@@ -443,6 +443,35 @@ def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
     assert rel(out, ref) < 2e-5
 
 
+@pytest.mark.parametrize("w4", [1, 0])
+@pytest.mark.parametrize("M,N,Kd", [(8192, 768, 3072), (1000, 776, 160), (2048, 200, 64), (777, 96, 2304)])
+def test_pp_96_wide_forms_with_epilogues(K, w4, M, N, Kd):
+    """96-wide ping-pong tiles on the 4-wave form (64 x 96 wave tiles) and the 8-wave form, with every bf16
+    epilogue the GPT-2 linears use, against the fp32 reference (ragged M / N edges included)."""
+    old_bn, old_w4 = K.tune_set("pp_bn", 96), K.tune_set("pp_w4", w4)
+    old_pp = K.tune_set("pp", 2)
+    try:
+        x, w = rnd(M, Kd), rnd(N, Kd, scale=0.05)
+        ref = x.float() @ w.float().t()
+        assert rel(K.gemm_nt_ex(x, w), ref) < 1e-2
+        bias, res = torch.randn(N, device="cuda"), rnd(M, N)
+        assert rel(K.gemm_nt_ex(x, w, bias=bias, res=res), ref + bias + res.float()) < 1e-2
+        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        y = K.gemm_nt_ex(x, w, bias=bias, act=2, aux=aux)
+        u = ref + bias
+        assert rel(aux, u) < 1e-2
+        assert rel(y, F.gelu(aux.float(), approximate="tanh")) < 2e-2
+        dg = rnd(M, N)
+        g = dg.float()
+        t = torch.tanh(0.7978845608 * (g + 0.044715 * g ** 3))
+        dgelu = 0.5 * (1 + t) + 0.5 * g * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * g * g)
+        assert rel(K.gemm_nt_ex(x, w, dgelu=dg), ref * dgelu) < 2e-2
+    finally:
+        K.tune_set("pp_bn", old_bn)
+        K.tune_set("pp_w4", old_w4)
+        K.tune_set("pp", old_pp)
+
+
 def test_transpose_bf16_multi(K):
     """One launch over many matrices (ragged edges, > 64 entries so the host splits the table)."""
     shapes = [(768, 2304), (3072, 768), (100, 37), (8, 8), (50257, 768)] + [(64 + i, 72 + 3 * i) for i in range(70)]
