@@ -50,6 +50,8 @@ constexpr int FX_STATS = 2;    // per-column (sum, sum of squares) of the bf16 o
 constexpr int FX_BNB = 4;      // output gm = v * [ep_x*mscale + mshift > 0]; slab gets sum gm, sum gm*xhat
 constexpr int PP_PRO_MAXK = 1024;
 
+// DT = 2: bf16 with 64-deep slices (128-byte rows: one 128-byte L2 request per row and slice where 32-deep slices
+// issue two 64-byte ones; the N = 768 GEMMs issued 2.1x hipBLASLt's TCP->TCC read requests, gpurun_out/r5_17).
 // DT = 1: fp8 (OCP e4m3) operands, both K-major, every K / ld in units of 2 fp8 (the loaders move bytes);
 // a slice is then 64 units = 128 fp8 per row, consumed by one block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
 // per fragment pair (unit block scales; the per-tensor scales come in through alpha_ptr).
@@ -572,8 +574,17 @@ __global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(Gemm
             const bf16_t* B_ = A_ + C::IMA;
             rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
             bf16x8_t af[C::DT ? 1 : C::FM], bfr[C::DT ? 1 : C::FN];
-            v8i_t aq[C::DT ? C::FM : 1], bq[C::DT ? C::FN : 1];   // fp8: 32 k-bytes per lane and fragment
-            if constexpr (C::DT == 1) {
+            v8i_t aq[C::DT == 1 ? C::FM : 1], bq[C::DT == 1 ? C::FN : 1];   // fp8: 32 k-bytes per lane and fragment
+            bf16x8_t a2[C::DT == 2 ? 2 : 1][C::DT == 2 ? C::FM : 1], b2[C::DT == 2 ? 2 : 1][C::DT == 2 ? C::FN : 1];
+            if constexpr (C::DT == 2) {      // bf16, 64-deep slices: two 32-deep k-steps per 128-byte row
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+                    for (int f = 0; f < C::FN; ++f) b2[ks][f] = frag_kmajor(B_, bcol + f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+                    for (int f = 0; f < C::FM; ++f) a2[ks][f] = frag_kmajor(A_, arow + f * 16 + (lane & 15), ks, lane);
+                }
+            } else if constexpr (C::DT == 1) {
 #pragma unroll
                 for (int f = 0; f < C::FN; ++f) bq[f] = frag8(B_, bcol + f * 16 + (lane & 15), lane);
 #pragma unroll
@@ -614,7 +625,15 @@ __global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(Gemm
             __builtin_amdgcn_s_barrier();
             // ---------------- compute segment ----------------
             __builtin_amdgcn_s_setprio(1);
-            if constexpr (C::DT == 1) {
+            if constexpr (C::DT == 2) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int fm = 0; fm < C::FM; ++fm)
+#pragma unroll
+                        for (int fn = 0; fn < C::FN; ++fn)
+                            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[ks][fn], a2[ks][fm], acc[fm][fn], 0, 0, 0);
+            } else if constexpr (C::DT == 1) {
 #pragma unroll
                 for (int fm = 0; fm < C::FM; ++fm)
 #pragma unroll
@@ -757,6 +776,8 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_bf16_kernel(const float* _
 // ------------------------------------------------------------------------------------------------
 using C96 = PPC<96, 2, 7>;
 using C96w = PPC<96, 4, 7, 0, 4>;    // 4 waves x (64 x 96)
+using C96k = PPC<96, 2, 3, 2>;       // 64-deep bf16 slices: 45 KiB slots, 3 in the ring
+using C128k = PPC<128, 2, 3, 2>;     // 48 KiB slots
 using C128 = PPC<128, 2, 5>;
 using C192 = PPC<192, 2, 5>;
 using C256 = PPC<256, 1, 4>;
@@ -793,6 +814,10 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     GemmArgs b = a;
     b.nb2 = splits;
     b.dbg = g_pp_trace;
+    if constexpr (C::DT == 2) {            // 64-deep slices (callers: K % 64 == 0, no split-K)
+        b.ktiles_per_split = a.K / 64;
+        b.ksl_rem = 0;
+    }
     constexpr int SM = pp_smem<C, FX>();
     set_attr<C, AM, BMODE, EM, FX>();
     hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, FX>), dim3(grid), dim3(C::NT), SM, st, b);
@@ -803,8 +828,13 @@ template <int AM, int BMODE, int EM, int FX = 0>
 int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
     if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && FX == 0) {
         switch (bn) {
-            case 96: return tune().pp_w4 && splits == 1 ? launch_cfg<C96w, AM, BMODE, EM>(a, splits, st)
-                                                        : launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
+            case 96:
+                if (tune().pp_sk64 && splits == 1 && a.K % 64 == 0) return launch_cfg<C96k, AM, BMODE, EM>(a, splits, st);
+                return tune().pp_w4 && splits == 1 ? launch_cfg<C96w, AM, BMODE, EM>(a, splits, st)
+                                                   : launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
+            case 128:
+                if (tune().pp_sk64 && splits == 1 && a.K % 64 == 0) return launch_cfg<C128k, AM, BMODE, EM>(a, splits, st);
+                break;
             case 192: return launch_cfg<C192, AM, BMODE, EM>(a, splits, st);
             case 288: return launch_cfg<C288, AM, BMODE, EM>(a, splits, st);
             case 257: return launch_cfg<C256b, AM, BMODE, EM>(a, splits, st);
@@ -939,7 +969,8 @@ int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) 
 // a kernel template in an anonymous namespace: instantiate every specialisation used explicitly.
 #define PP_I(CFG, AM, BM_, EM) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::AM, pg::BM_, pg::EM, 0>(pg::GemmArgs);
 #define PP_I2(CFG, AM, BM_) PP_I(CFG, AM, BM_, E_BF16) PP_I(CFG, AM, BM_, E_F32)
-PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C96w, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR) PP_I2(C288, A_KMAJOR, B_KMAJOR)
+PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C96w, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR)
+PP_I2(C96k, A_KMAJOR, B_KMAJOR) PP_I2(C128k, A_KMAJOR, B_KMAJOR) PP_I2(C288, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_KMAJOR) PP_I2(C256, A_KMAJOR, B_KMAJOR) PP_I2(C256b, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_MNMAJOR) PP_I2(C256, A_KMAJOR, B_MNMAJOR)
 PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)

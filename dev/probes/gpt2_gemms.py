@@ -57,9 +57,13 @@ def main():
             old = K.tune_set("pp_bn", bn)
             out[f"bn{bn}"] = timeit(fn)
             K.tune_set("pp_bn", old)
-        old = K.tune_set("pp_w4", 0)
-        out["auto_w4off"] = timeit(fn)
-        K.tune_set("pp_w4", old)
+        old = K.tune_set("pp_sk64", 0)
+        out["auto_sk32"] = timeit(fn)
+        for bn in (96, 128):
+            ob = K.tune_set("pp_bn", bn)
+            out[f"bn{bn}_sk32"] = timeit(fn)
+            K.tune_set("pp_bn", ob)
+        K.tune_set("pp_sk64", old)
         out["torch"] = timeit(lambda: x @ w.t())
         if bias is not None:
             out["torch_addmm"] = timeit(lambda: torch.addmm(bias.to(BF), x, w.t()))

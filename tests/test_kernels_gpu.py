@@ -443,13 +443,15 @@ def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
     assert rel(out, ref) < 2e-5
 
 
-@pytest.mark.parametrize("w4", [1, 0])
+@pytest.mark.parametrize("bn,form", [(96, "sk64"), (96, "w4"), (96, "sk32"), (128, "sk64"), (128, "sk32")])
 @pytest.mark.parametrize("M,N,Kd", [(8192, 768, 3072), (1000, 776, 160), (2048, 200, 64), (777, 96, 2304)])
-def test_pp_96_wide_forms_with_epilogues(K, w4, M, N, Kd):
-    """96-wide ping-pong tiles on the 4-wave form (64 x 96 wave tiles) and the 8-wave form, with every bf16
-    epilogue the GPT-2 linears use, against the fp32 reference (ragged M / N edges included)."""
-    old_bn, old_w4 = K.tune_set("pp_bn", 96), K.tune_set("pp_w4", w4)
-    old_pp = K.tune_set("pp", 2)
+def test_pp_narrow_tile_forms_with_epilogues(K, bn, form, M, N, Kd):
+    """96 / 128-wide ping-pong tiles streaming 64-deep slices (sk64, K % 64 == 0; else the 32-deep form), the
+    4-wave form (64 x 96 wave tiles) and the 32-deep 8-wave form, with every bf16 epilogue the GPT-2 linears
+    use, against the fp32 reference (ragged M / N edges included)."""
+    old_bn, old_pp = K.tune_set("pp_bn", bn), K.tune_set("pp", 2)
+    old_w4 = K.tune_set("pp_w4", int(form == "w4"))
+    old_sk = K.tune_set("pp_sk64", int(form == "sk64"))
     try:
         x, w = rnd(M, Kd), rnd(N, Kd, scale=0.05)
         ref = x.float() @ w.float().t()
@@ -469,6 +471,7 @@ def test_pp_96_wide_forms_with_epilogues(K, w4, M, N, Kd):
     finally:
         K.tune_set("pp_bn", old_bn)
         K.tune_set("pp_w4", old_w4)
+        K.tune_set("pp_sk64", old_sk)
         K.tune_set("pp", old_pp)
 
 
