@@ -55,22 +55,15 @@ constexpr int PP_PRO_MAXK = 1024;
 // DT = 1: fp8 (OCP e4m3) operands, both K-major, every K / ld in units of 2 fp8 (the loaders move bytes);
 // a slice is then 64 units = 128 fp8 per row, consumed by one block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
 // per fragment pair (unit block scales; the per-tensor scales come in through alpha_ptr).
-// NW_ = 4: one wave per SIMD, no ping-pong partner: the four waves own 64-row slabs of the whole 256-row tile
-// (wave tile 64 x BN) and overlap their next slice's LDS reads with the current slice's MFMAs through
-// double-buffered fragment registers (one barrier per slice).  For narrow outputs (GPT-2 N = 768: 256 x 96
-// tiles fill the 256 CUs in one round) the 64 x 96 wave tile reads 10 fragments per 24 MFMAs where the
-// ping-pong's 64 x 48 reads 7 per 12.
-template <int BN_, int WR_, int NB_, int DT_ = 0, int NW_ = 8>
+template <int BN_, int WR_, int NB_, int DT_ = 0>
 struct PPC {
-    static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_, DT = DT_, NW = NW_, NT = 64 * NW_;
+    static constexpr int BN = BN_, WR = WR_, WC = 4 / WR_, NB = NB_, DT = DT_;
     static constexpr int SK = DT ? 64 : PP_SK;            // slice depth in bf16 units
-    static constexpr int GROWS = NW == 8 ? 128 : PP_BM;   // output rows of a wave group
-    static constexpr int WTM = GROWS / WR, WTN = BN / WC;
+    static constexpr int WTM = 128 / WR, WTN = BN / WC;
     static constexpr int FM = WTM / 16, FN = WTN / 16;
     static constexpr int IMA = PP_BM * SK, IMB = BN * SK, SLOT = IMA + IMB;
     static constexpr int SMEM = NB * SLOT * 2;
     static_assert(WTN % 16 == 0 && WTM % 16 == 0, "wave tile");
-    static_assert(NW == 8 || (NW == 4 && DT == 0), "4-wave form: bf16");
     static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
@@ -92,13 +85,13 @@ __device__ __forceinline__ v8i_t frag8(const bf16_t* img, int row, int lane) {
 // (NI each; instructions past NR duplicate the last one: identical bytes to identical LDS addresses).
 //   K-major  [rows][K]: instruction j covers rows 16 j .. 16 j + 15 (lane: row 16 j + lane / 4, chunk lane & 3)
 //   MN-major [K][cols]: instruction j covers k-rows RPI j .. RPI j + RPI - 1, RPI = 512 / ROWS
-template <int ROWS, bool KMAJ, int SK = PP_SK, int NW = 8>
+template <int ROWS, bool KMAJ, int SK = PP_SK>
 struct PPLoader {
     static_assert(SK == PP_SK || KMAJ, "128-byte slices: K-major operands only");
     // SK = 64 (fp8): 128-byte rows, instruction j covers rows 8 j .. 8 j + 7 (lane: row 8 j + lane / 8,
     // 16-byte chunk (lane & 7) ^ ((row >> 1) & 7): the kimg_off image read by the fp8 fragments)
     static constexpr int NR = SK == PP_SK ? ROWS / 16 : ROWS / 8;
-    static constexpr int NI = (NR + NW - 1) / NW;
+    static constexpr int NI = (NR + 7) / 8;
     const bf16_t* src[NI];
     int dst[NI];
     long step;
@@ -169,14 +162,13 @@ __device__ __forceinline__ void pp_retire(int keep) {
 // FX (fusions, FX_* bits): A-operand BN-affine+ReLU prologue, BN partial statistics of the output,
 // BN-backward masking + statistics (the conv/1x1 paths of the ResNet blocks).
 template <class C, int AM, int BMODE, int EM, int FX = 0>
-__global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(GemmArgs a) {
+__global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
     static_assert(!(FX & FX_PRO) || AK, "prologue: K-major A only");
     constexpr int NB = C::NB, D = NB - 1;
     static_assert(!C::DT || (AK && BKm && !(FX & FX_PRO)), "fp8: K-major operands, no prologue");
-    using LA = PPLoader<PP_BM, AK, C::SK, C::NW>;
-    using LB = PPLoader<C::BN, BKm, C::SK, C::NW>;
-    static_assert(C::NW == 8 || (AK && BKm && FX == 0), "4-wave form: K-major operands, no fusions");
+    using LA = PPLoader<PP_BM, AK, C::SK>;
+    using LB = PPLoader<C::BN, BKm, C::SK>;
     constexpr int NIT = LA::NI + LB::NI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* const sb = reinterpret_cast<bf16_t*>(smem);
@@ -184,18 +176,18 @@ __global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(Gemm
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if constexpr ((FX & FX_PRO) != 0) {
-        for (int i = tid; i < a.K; i += C::NT) {
+        for (int i = tid; i < a.K; i += 512) {
             ptab[i] = a.pro_scale[i];
             ptab[PP_PRO_MAXK + i] = a.pro_shift[i];
         }
     }
     if constexpr ((FX & FX_BNB) != 0) {     // the BN-output ReLU mask coefficients of every column
-        for (int i = tid; i < a.N; i += C::NT) {
+        for (int i = tid; i < a.N; i += 512) {
             ptab[i] = a.ep_mscale[i];
             ptab[PP_PRO_MAXK + i] = a.ep_mshift[i];
         }
     }
-    const int grp = C::NW == 8 ? wave >> 2 : 0, wr = (wave & 3) / C::WC, wc = (wave & 3) % C::WC;
+    const int grp = wave >> 2, wr = (wave & 3) / C::WC, wc = (wave & 3) % C::WC;
     const int tiles_m = (a.M + PP_BM - 1) / PP_BM, tiles_n = (a.N + C::BN - 1) / C::BN;
     const int ntiles = tiles_m * tiles_n;
     const int splits = a.nb2 > 0 ? a.nb2 : 1;                  // K-splits (slab epilogue when > 1)
@@ -261,10 +253,10 @@ __global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(Gemm
     if (dbg) dbg[1] = wall_clock64();
     if constexpr ((FX & (FX_PRO | FX_BNB)) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // table written
     __builtin_amdgcn_s_barrier();
-    if (C::NW == 8 && grp == 1) __builtin_amdgcn_s_barrier();          // stagger: group 1 runs one barrier behind
+    if (grp == 1) __builtin_amdgcn_s_barrier();          // stagger: group 1 runs one barrier behind
 
     const int koffl = pp_koff(lane & 15, lane >> 4);     // K-major fragment offset (row & 15 == lane & 15)
-    const int arow = grp * C::GROWS + wr * C::WTM, bcol = wc * C::WTN;
+    const int arow = grp * 128 + wr * C::WTM, bcol = wc * C::WTN;
     const int lm = lane & 15, lg = lane >> 4;
     float alpha = a.alpha;
     if (a.alpha_ptr) alpha *= *a.alpha_ptr;
@@ -523,48 +515,7 @@ __global__ void __launch_bounds__(C::NT, C::NW == 8 ? 2 : 1) gemm_pp_kernel(Gemm
                 for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     };
-    if constexpr (C::NW == 4) {
-        // one barrier per slice: [lgkmcnt(0): slice q's fragments in registers and every read of slot q-1 done]
-        // [retire slice q+1] barrier [refill slot q-1 with slice q+D] [read slice q+1 into the other buffer]
-        // [MFMAs of slice q] [epilogue at an item end]
-        bf16x8_t a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
-        auto read_frags = [&](bf16x8_t* af_, bf16x8_t* bf_) {
-            const bf16_t* A_ = sb + rd_off;
-            const bf16_t* B_ = A_ + C::IMA;
-            rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
-#pragma unroll
-            for (int f = 0; f < C::FN; ++f)
-                bf_[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(B_ + (bcol + f * 16) * PP_SK + koffl));
-#pragma unroll
-            for (int f = 0; f < C::FM; ++f)
-                af_[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(A_ + (arow + f * 16) * PP_SK + koffl));
-        };
-        auto step = [&](int q, bf16x8_t* ca, bf16x8_t* cb, bf16x8_t* na, bf16x8_t* nb) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const bool next = q + 1 < Q;
-            if (next) {
-                if (q + D < Q) pp_vmwait<(D - 2) * NIT>();
-                else pp_retire<NIT, D>(Q - q - 2);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            if (q + D < Q) issue_next();
-            if (next) read_frags(na, nb);
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int fm = 0; fm < C::FM; ++fm)
-#pragma unroll
-                for (int fn = 0; fn < C::FN; ++fn)
-                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[fn], ca[fm], acc[fm][fn], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            if (++s == cur_n) epilogue();
-        };
-        read_frags(a0, b0);
-        for (int q = 0; q < Q; q += 2) {
-            step(q, a0, b0, a1, b1);
-            if (q + 1 < Q) step(q + 1, a1, b1, a0, b0);
-        }
-    } else {
+    {
         for (int q = 0; q < Q; ++q) {
             // ---------------- load segment ----------------
             const bool more = q + D < Q;
@@ -775,7 +726,6 @@ __global__ void __launch_bounds__(256) pp_slab_reduce_bf16_kernel(const float* _
 // host side
 // ------------------------------------------------------------------------------------------------
 using C96 = PPC<96, 2, 7>;
-using C96w = PPC<96, 4, 7, 0, 4>;    // 4 waves x (64 x 96)
 using C96k = PPC<96, 2, 3, 2>;       // 64-deep bf16 slices: 45 KiB slots, 3 in the ring
 using C128k = PPC<128, 2, 3, 2>;     // 48 KiB slots
 using C128 = PPC<128, 2, 5>;
@@ -820,7 +770,7 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     }
     constexpr int SM = pp_smem<C, FX>();
     set_attr<C, AM, BMODE, EM, FX>();
-    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, FX>), dim3(grid), dim3(C::NT), SM, st, b);
+    hipLaunchKernelGGL((gemm_pp_kernel<C, AM, BMODE, EM, FX>), dim3(grid), dim3(512), SM, st, b);
     PDNN_LAUNCH_RET;
 }
 
@@ -830,8 +780,7 @@ int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
         switch (bn) {
             case 96:
                 if (tune().pp_sk64 && splits == 1 && a.K % 64 == 0) return launch_cfg<C96k, AM, BMODE, EM>(a, splits, st);
-                return tune().pp_w4 && splits == 1 ? launch_cfg<C96w, AM, BMODE, EM>(a, splits, st)
-                                                   : launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
+                return launch_cfg<C96, AM, BMODE, EM>(a, splits, st);
             case 128:
                 if (tune().pp_sk64 && splits == 1 && a.K % 64 == 0) return launch_cfg<C128k, AM, BMODE, EM>(a, splits, st);
                 break;
@@ -969,7 +918,7 @@ int pp_launch(const GemmArgs& a0, int amode, int bmode, int em, hipStream_t st) 
 // a kernel template in an anonymous namespace: instantiate every specialisation used explicitly.
 #define PP_I(CFG, AM, BM_, EM) template __global__ void pg::gemm_pp_kernel<pg::CFG, pg::AM, pg::BM_, pg::EM, 0>(pg::GemmArgs);
 #define PP_I2(CFG, AM, BM_) PP_I(CFG, AM, BM_, E_BF16) PP_I(CFG, AM, BM_, E_F32)
-PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C96w, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR)
+PP_I2(C96, A_KMAJOR, B_KMAJOR) PP_I2(C192, A_KMAJOR, B_KMAJOR)
 PP_I2(C96k, A_KMAJOR, B_KMAJOR) PP_I2(C128k, A_KMAJOR, B_KMAJOR) PP_I2(C288, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_KMAJOR) PP_I2(C256, A_KMAJOR, B_KMAJOR) PP_I2(C256b, A_KMAJOR, B_KMAJOR)
 PP_I2(C128, A_KMAJOR, B_MNMAJOR) PP_I2(C256, A_KMAJOR, B_MNMAJOR)

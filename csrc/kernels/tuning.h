@@ -15,8 +15,6 @@ namespace pg {
                "the operands allow (tests)")                                                                 \
     X(pp, 1, "ping-pong engine for plain GEMMs (and fp8): 0 off, 1 automatic, 2 whenever the operands allow (tests)") \
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
-    X(pp_w4, 0, "96-wide ping-pong tiles (GPT-2 N = 768) on the 4-wave form (64 x 96 wave tiles, one wave per " \
-                "SIMD); 0 = the 8-wave ping-pong (64 x 48 wave tiles). fc2 57 -> 76 us with it (gpurun_out/r5_16)") \
     X(pp_sk64, 1, "96 / 128-wide ping-pong tiles with K-major operands and K % 64 == 0 (no split-K) stream 64-deep "  \
                   "slices (128-byte rows) instead of 32-deep; 0 = 32-deep")                                    \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \

@@ -443,14 +443,13 @@ def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
     assert rel(out, ref) < 2e-5
 
 
-@pytest.mark.parametrize("bn,form", [(96, "sk64"), (96, "w4"), (96, "sk32"), (128, "sk64"), (128, "sk32")])
+@pytest.mark.parametrize("bn,form", [(96, "sk64"), (96, "sk32"), (128, "sk64"), (128, "sk32")])
 @pytest.mark.parametrize("M,N,Kd", [(8192, 768, 3072), (1000, 776, 160), (2048, 200, 64), (777, 96, 2304)])
 def test_pp_narrow_tile_forms_with_epilogues(K, bn, form, M, N, Kd):
-    """96 / 128-wide ping-pong tiles streaming 64-deep slices (sk64, K % 64 == 0; else the 32-deep form), the
-    4-wave form (64 x 96 wave tiles) and the 32-deep 8-wave form, with every bf16 epilogue the GPT-2 linears
-    use, against the fp32 reference (ragged M / N edges included)."""
+    """96 / 128-wide ping-pong tiles streaming 64-deep slices (sk64, K % 64 == 0; else the 32-deep form) and
+    32-deep slices, with every bf16 epilogue the GPT-2 linears use, against the fp32 reference (ragged M / N
+    edges included)."""
     old_bn, old_pp = K.tune_set("pp_bn", bn), K.tune_set("pp", 2)
-    old_w4 = K.tune_set("pp_w4", int(form == "w4"))
     old_sk = K.tune_set("pp_sk64", int(form == "sk64"))
     try:
         x, w = rnd(M, Kd), rnd(N, Kd, scale=0.05)
@@ -470,7 +469,6 @@ def test_pp_narrow_tile_forms_with_epilogues(K, bn, form, M, N, Kd):
         assert rel(K.gemm_nt_ex(x, w, dgelu=dg), ref * dgelu) < 2e-2
     finally:
         K.tune_set("pp_bn", old_bn)
-        K.tune_set("pp_w4", old_w4)
         K.tune_set("pp_sk64", old_sk)
         K.tune_set("pp", old_pp)
 
