@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     constexpr bool AK = AM == A_KMAJOR, BKm = BMODE == B_KMAJOR;
     static_assert(!(FX & FX_PRO) || AK, "prologue: K-major A only");
     constexpr int NB = C::NB, D = NB - 1;
-    static_assert(!C::DT || (AK && BKm && !(FX & FX_PRO)), "fp8: K-major operands, no prologue");
+    static_assert(!C::DT || (AK && BKm && (C::DT == 2 || !(FX & FX_PRO))), "fp8 / 64-deep: K-major operands");
     using LA = PPLoader<PP_BM, AK, C::SK>;
     using LB = PPLoader<C::BN, BKm, C::SK>;
     constexpr int NIT = LA::NI + LB::NI;
@@ -555,7 +555,25 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             }
             }
             if (more) issue_next();
-            if constexpr ((FX & FX_PRO) != 0) {
+            if constexpr ((FX & FX_PRO) != 0 && C::DT == 2) {
+                // 64-deep slice: k-step ks of this lane covers k = 64 s + 32 ks + 8 lg .. +7
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const float* ps = ptab + s * 64 + ks * 32 + 8 * (lane >> 4);
+                    const float4 c0 = *reinterpret_cast<const float4*>(ps), c1 = *reinterpret_cast<const float4*>(ps + 4);
+                    const float4 h0 = *reinterpret_cast<const float4*>(ps + PP_PRO_MAXK);
+                    const float4 h1 = *reinterpret_cast<const float4*>(ps + PP_PRO_MAXK + 4);
+                    const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+                    for (int f = 0; f < C::FM; ++f) {
+                        u16x8_t v = __builtin_bit_cast(u16x8_t, a2[ks][f]);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) v[j] = f2bf(fmaxf(fmaf(bf2f(v[j]), sc[j], sh[j]), 0.f));
+                        a2[ks][f] = __builtin_bit_cast(bf16x8_t, v);
+                    }
+                }
+            } else if constexpr ((FX & FX_PRO) != 0) {
                 // this lane's 8 reduction indices of the slice: k = 32 s + 8 lg .. +7 (no split-K with FX_PRO)
                 const float* ps = ptab + s * PP_SK + 8 * (lane >> 4);
                 const float4 c0 = *reinterpret_cast<const float4*>(ps), c1 = *reinterpret_cast<const float4*>(ps + 4);
@@ -790,6 +808,9 @@ int launch_bn(const GemmArgs& a, int bn, int splits, hipStream_t st) {
             default: break;
         }
     }
+    if constexpr (AM == A_KMAJOR && BMODE == B_KMAJOR && EM == E_BF16 && FX != 0) {
+        if (bn == 128 && tune().pp_sk64 && splits == 1 && a.K % 64 == 0) return launch_cfg<C128k, AM, BMODE, EM, FX>(a, splits, st);
+    }
     if (bn == 128) return launch_cfg<C128, AM, BMODE, EM, FX>(a, splits, st);
     if constexpr ((FX & (FX_BNB | FX_PRO)) == 0) return launch_cfg<C256, AM, BMODE, EM, FX>(a, splits, st);
     return (int)hipErrorInvalidValue;
@@ -933,6 +954,7 @@ PP_I2(C128, A_MNMAJOR, B_MNMAJOR) PP_I2(C256, A_MNMAJOR, B_MNMAJOR)
 PP_8(C8_128) PP_8(C8_96)
 #undef PP_8
 PP_F5(B_KMAJOR) PP_F5(B_MNMAJOR)
+PP_F(C128k, B_KMAJOR, 1) PP_F(C128k, B_KMAJOR, 2) PP_F(C128k, B_KMAJOR, 3) PP_F(C128k, B_KMAJOR, 4)
 #undef PP_F5
 #undef PP_F2
 #undef PP_F
