@@ -45,6 +45,7 @@ struct GemmArgs {
     float* stats;             // [gridM*2 rows][2][N] per-wave-row partial (sum, sumsq), or null
     int ktiles_per_split;     // split-K (grid.z)
     int ksl_rem;              // pp engine: the first ksl_rem K-splits take one slice more (uneven splits)
+    float* rowsum;            // pp engine E_F32: += alpha * sum_k A[m][k] per output row m (fused bias gradient)
     int scatter;              // epilogue rows are parity-class pixels of dIn (A_CONVT with stride > 1)
     int stats_row0;           // first slab row of this launch (parity-class launches share one slab)
     int transC;               // E_ATOMIC: accumulate C^T (C[n * ldc + m])

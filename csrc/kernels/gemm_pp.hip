@@ -242,6 +242,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // fused row sums of A (E_F32 with a.rowsum: the bias gradient beside a weight gradient): the waves of the
+    // first column block of each n0 == 0 item add one MFMA per A fragment against a ones fragment
+    constexpr bool RS = EM == E_F32 && FX == 0 && C::DT == 0;
+    f32x4_t accr[RS ? C::FM : 1];
+#pragma unroll
+    for (int i = 0; i < (RS ? C::FM : 1); ++i) accr[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     // optional phase trace: [block][wave 0 / 4][0 start, 1 prologue done, 2 + 2i item i computed, 3 + 2i stored]
     long long* const dbg = (a.dbg && lane == 0 && (wave & 3) == 0) ? a.dbg + ((long)b * 2 + grp) * 64 : nullptr;
@@ -273,13 +279,23 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
 
     int s = 0, cur = 0, rd_off = 0;                      // slice within the current item, item index, read slot
     int cur_n = item_nsl(0);                             // slices of item `cur`
+    // row sums this item: a.rowsum set, the item's first column tile, this wave's first column block
+    auto rs_on = [&](int i) {
+        if constexpr (!RS) return false;
+        int m0_, n0_, z_;
+        item(i, m0_, n0_, z_);
+        return a.rowsum != nullptr && n0_ == 0 && wc == 0;
+    };
+    bool cur_rs = rs_on(0);
     auto epilogue = [&]() {
             // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
             if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
             s = 0;
             int m0, n0, z;
+            const bool rs_here = cur_rs;
             item(cur++, m0, n0, z);
             cur_n = item_nsl(cur);
+            cur_rs = cur < nitems && rs_on(cur);
             constexpr bool SUMS = (FX & (FX_STATS | FX_BNB)) != 0;
             float s_[SUMS ? C::FN : 1][4], q_[SUMS ? C::FN : 1][4];   // per-column partial sums over 64 rows
             if constexpr (SUMS) {
@@ -471,6 +487,11 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                         }
                     }
                 } else {
+                    if constexpr (RS) {
+                        // lane (lm, lg): every column of accr[fm] holds row m's sum; lanes of column group 0 add it
+                        if (rs_here && lg == 0 && mv) atomicAdd(a.rowsum + m, accr[fm][0] * alpha);
+                        accr[fm] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                    }
                     // fp32: K-split items write partial slabs at C + z * sC1 (pp_slab_reduce_kernel sums them),
                     // otherwise store / accumulate (acc_c) into C
                     const bool slab = splits > 1;
@@ -615,6 +636,15 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
                 for (int fn = 0; fn < C::FN; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+            if constexpr (RS) {
+                if (cur_rs) {
+                    const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, u16x8_t{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                                              0x3F80, 0x3F80, 0x3F80});
+#pragma unroll
+                    for (int fm = 0; fm < C::FM; ++fm)
+                        accr[fm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[fm], accr[fm], 0, 0, 0);
+                }
+            }
             }
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -963,12 +993,15 @@ PP_F(C128k, B_KMAJOR, 1) PP_F(C128k, B_KMAJOR, 2) PP_F(C128k, B_KMAJOR, 3) PP_F(
 // pp_wgrad: out[M][N] (fp32) += alpha * A[K][M]^T . B[K][N] with split-K partial slabs in `ws`
 // (>= pdnn_pp_wgrad_ws(M, N, splits) floats) reduced by a second kernel; splits == 1 accumulates in place.
 PDNN_API long pdnn_pp_wgrad_ws(int M, int N, int splits) { return splits > 1 ? (long)splits * ((long)M * N + 64) : 0; }
+// rowsum (optional, fp32 [M]): += alpha * sum_k A[k][m], fused (the bias gradient of a linear layer beside its
+// weight gradient: one extra MFMA per A fragment in the first column tile's items, atomically added per split)
 PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* out, long ldc, int M, int N,
-                           int K, float alpha, float* ws, int splits, hipStream_t st) {
+                           int K, float alpha, float* ws, int splits, float* rowsum, hipStream_t st) {
     using namespace pg;
     if (K % PP_SK || M % 8 || N % 8 || splits < 1) return (int)hipErrorInvalidValue;
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.alpha = alpha;
+    a.rowsum = rowsum;
     const int nsl = K / PP_SK;
     if (splits > nsl) splits = nsl;
     a.ktiles_per_split = nsl / splits;             // the first nsl % splits splits take one slice more

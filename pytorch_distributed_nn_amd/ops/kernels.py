@@ -56,10 +56,11 @@ def set_pp_bn(bn: int) -> int:
     return lib().pdnn_set_pp_bn(int(bn))
 
 
-def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None):
+def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None, rowsum=None):
     """out[M][N] (fp32) += alpha * x[K][M]^T @ y[K][N] on the ping-pong engine: split-K partial slabs in a
     workspace (``ws``, allocated when not given) reduced by a second kernel, or in place when one split
-    covers the CUs."""
+    covers the CUs.  ``rowsum`` (fp32 [M], optional) += alpha * x.sum(0), fused: the bias gradient of a
+    linear layer beside its weight gradient."""
     K_, M = x.shape
     K2, N = y.shape
     _chk(K_ == K2 and K_ % 32 == 0 and M % 8 == 0 and N % 8 == 0, f"pp_wgrad: bad shapes {x.shape} {y.shape}")
@@ -69,8 +70,10 @@ def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None):
     if splits > 1 and ws is None:
         ws = torch.empty(splits * (M * N + 64), device=x.device, dtype=F32)     # pdnn_pp_wgrad_ws
     _chk(splits <= 1 or ws.numel() >= splits * (M * N + 64), "pp_wgrad: workspace of splits * (M*N + 64) floats")
+    _chk(rowsum is None or (rowsum.dtype == F32 and rowsum.is_contiguous() and rowsum.numel() == M),
+         "pp_wgrad: rowsum fp32 [M]")
     call("pdnn_pp_wgrad", ptr(x), x.stride(0), ptr(y), y.stride(0), ptr(out), out.stride(0), M, N, K_,
-         float(alpha), ptr(ws), int(splits), stream())
+         float(alpha), ptr(ws), int(splits), ptr(rowsum), stream())
     return out
 
 

@@ -9,7 +9,9 @@ Every call lands in ``csrc/kernels``:
   128-row register-staged kernel;
 * the weight gradient ``dW += g^T x`` (fp32, in place in the flat gradient arena) runs the ping-pong
   engine with both operands reduction-major and split-K partial slabs reduced by a second kernel
-  (``kernels.pp_wgrad``), or the glds engine's split-K atomics for shapes it does not take.
+  (``kernels.pp_wgrad``), or the glds engine's split-K atomics for shapes it does not take; the bias gradient
+  (column sums of g) rides along as row sums of the same MFMA operand (one extra MFMA per fragment against a
+  ones fragment) instead of a separate column-sum pass over g.
 
 Reference GEMM sites this replaces: MPI_code/src/util/util.h:35-81 (cblas_dgemm),
 MPI_code/src/nn/nn_layer.h:111-175 (forward, dgrad, wgrad of the bias-folded dense layer).
@@ -46,10 +48,14 @@ def linear_dgrad(g, wk, dgelu=None, p=None):
     return K.gemm_nt_ex(g, wt, dgelu=dgelu)
 
 
-def wgrad_acc(g, x, out):
-    """out[N][K] (fp32) += g[M][N]^T @ x[M][K]."""
+def wgrad_acc(g, x, out, bias=None):
+    """out[N][K] (fp32) += g[M][N]^T @ x[M][K]; with ``bias`` (fp32 [N]) also bias += column sums of g when the
+    ping-pong engine runs the product (fused: one extra MFMA per g fragment).  Returns whether ``bias`` was
+    accumulated (the caller sums it otherwise)."""
     M, N = g.shape
     Kd = x.shape[1]
     if M % 32 == 0 and N % 8 == 0 and Kd % 8 == 0 and out.is_contiguous() and M * N * Kd >= (1 << 24):
-        return K.pp_wgrad(g, x, out)
-    return K.gemm_tn_acc(g, x, out)
+        K.pp_wgrad(g, x, out, rowsum=bias)
+        return bias is not None
+    K.gemm_tn_acc(g, x, out)
+    return False

@@ -188,14 +188,16 @@ class _Sink:
 
     def linear(self, p_w, p_b, g, x):
         tw = self._tgt(p_w)
+        tb = self._tgt(p_b) if p_b is not None else None
+        bias_done = False
         if tw is not None:
-            BL.wgrad_acc(g, x, tw)
+            # the bias gradient fused into the weight-gradient GEMM when both land in the arena
+            bias_done = BL.wgrad_acc(g, x, tw, bias=tb if _tuning.get("bias_in_wgrad") else None)
             rw = None
         else:
             rw = _wgrad(g, x, p_w.shape)
         rb = None
-        if p_b is not None:
-            tb = self._tgt(p_b)
+        if p_b is not None and not bias_done:
             if tb is not None:
                 K.colsum(g, out=tb, accumulate=True, deterministic=not _tuning.get("colsum_atomic"))
             else:

@@ -20,6 +20,8 @@ wt_prefetch        0        GPT-2 data-gradient GEMMs' transposed weight copies:
                             gpurun_out/r5_10: the eager backward has launch gaps the small transposes fill)
 colsum_atomic      1        accumulating bias-gradient column sums in one launch with fp32 atomics (0: two-level
                             deterministic partial rows + level-2 launch; GPT-2 542.3k vs 538.0k tok/s, r5_10)
+bias_in_wgrad      1        GPT-2 linear bias gradients as fused row sums inside the weight-gradient GEMM (0: a
+                            column-sum pass over the output gradient)
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there
@@ -29,7 +31,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "colsum_atomic": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "colsum_atomic": 1, "bias_in_wgrad": 1}
 
 _VALUES = dict(DEFAULTS)
 

@@ -441,6 +441,13 @@ def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
     ref = out + x.float().t() @ y.float()
     K.pp_wgrad(x, y, out, splits=splits)
     assert rel(out, ref) < 2e-5
+    # the fused row sums (a linear layer's bias gradient beside its weight gradient), accumulated
+    rs = torch.randn(M, device="cuda")
+    rs_ref = rs + x.float().sum(0)
+    out2 = torch.zeros(M, N, device="cuda")
+    K.pp_wgrad(x, y, out2, splits=splits, rowsum=rs)
+    assert rel(out2, x.float().t() @ y.float()) < 2e-5
+    assert rel(rs, rs_ref) < 2e-5
 
 
 @pytest.mark.parametrize("bn,form", [(96, "sk64"), (96, "sk32"), (128, "sk64"), (128, "sk32")])
