@@ -1,5 +1,6 @@
 """Helpers to run a function in `world` CPU processes over gloo (the modern "mpirun -n N on one host",
 SURVEY.md §4)."""
+import faulthandler
 import os
 import socket
 import traceback
@@ -49,9 +50,12 @@ def _from_np(obj):
     return obj
 
 
-def _entry(rank, world, port, fn, args, q, device="cpu", backend="gloo", env=None):
+def _entry(rank, world, port, fn, args, q, device="cpu", backend="gloo", env=None, timeout=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), TORCHELASTIC_USE_AGENT_STORE="True", **(env or {}))
+    if timeout:
+        # a rank stuck past the parent's deadline prints every thread's Python stack to stderr and exits
+        faulthandler.dump_traceback_later(max(5.0, timeout - 10.0), exit=True)
     try:
         import torch
         torch.set_num_threads(1)
@@ -77,7 +81,8 @@ def run_world(fn, world=2, args=(), timeout=180, device="cpu", backend="gloo", e
     q = ctx.Queue()
     store = host_store()          # kept alive (and its port held) until every rank has finished
     port = store.port
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device, backend, env)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, device, backend, env, timeout))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = {}

@@ -204,7 +204,7 @@ def _rccl_graph_job(rank, world):
 
 
 def test_graphed_step_captures_rccl_collectives():
-    res, replays = run_world(_rccl_graph_job, 1, (), timeout=600, device=None, backend="nccl",
+    res, replays = run_world(_rccl_graph_job, 1, (), timeout=150, device=None, backend="nccl",
                              env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
     assert replays >= 4
     for i, err, noise, le, lg in res:

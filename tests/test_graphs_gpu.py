@@ -15,12 +15,12 @@ def _delta_rel(pg, pe, p0):
     return ((pg - pe).norm() / (pe - p0).norm().clamp_min(1e-12)).item()
 
 
-def _pair(name, opt_name, lr):
+def _pair(name, opt_name, lr, n=2):
     from pytorch_distributed_nn_amd.models import build_model
     from pytorch_distributed_nn_amd.optim import SGD, AdamW, flatten_module
     torch.manual_seed(0)
     m0 = build_model(name, 10) if not name.startswith("gpt2") else build_model(name)
-    ms = [copy.deepcopy(m0).cuda() for _ in range(2)]
+    ms = [copy.deepcopy(m0).cuda() for _ in range(n)]
     opts = []
     for m in ms:
         flatten_module(m)
@@ -29,8 +29,9 @@ def _pair(name, opt_name, lr):
     return ms, opts
 
 
-# ResNet-18 at batch 16: even two EAGER runs drift apart (split-K fp32 atomics reorder sums and 16 BN layers
-# amplify it), so its bounds are looser and its learning rate smaller
+# ResNet-18 at batch 16: even two EAGER runs drift apart (split-K and BN-statistics fp32 atomics reorder sums and
+# 16 BN layers amplify it), so its bounds are looser, its learning rate smaller, and the parameter bound also
+# admits 3x the drift of a second eager run over the same batches
 @pytest.mark.parametrize("name,opt_name,shape,lr,tol", [("LeNet", "sgd", (32, 1, 28, 28), 0.05, 2e-2),
                                                         ("ResNet18", "sgd", (16, 3, 32, 32), 0.005, 1e-1),
                                                         ("gpt2_tiny", "adamw", (2, 64), 1e-3, 2e-2)])
@@ -38,7 +39,7 @@ def test_graph_step_matches_eager(name, opt_name, shape, lr, tol):
     from pytorch_distributed_nn_amd.ops import functional as OF
     from pytorch_distributed_nn_amd.utils.graphs import GraphedStep
     lm = name.startswith("gpt2")
-    (me, mg), (oe, og) = _pair(name, opt_name, lr)
+    (me, mg, mt), (oe, og, ot) = _pair(name, opt_name, lr, n=3)
     p0 = me._pdnn_flat.data.clone()
     g = torch.Generator().manual_seed(1)
     if lm:
@@ -54,12 +55,13 @@ def test_graph_step_matches_eager(name, opt_name, shape, lr, tol):
     gs = GraphedStep(mg, og, forward=fwd, warmup=2)
     losses_e, losses_g = [], []
     for i, (x, y) in enumerate(batches):
-        for o in (oe, og):
+        for o in (oe, og, ot):
             o.param_groups[0]["lr"] = base * sched[i]
-        oe.zero_grad()
-        le = fwd(me, x, y)
-        le.backward()
-        oe.step()
+        for m, o in ((me, oe), (mt, ot)):
+            o.zero_grad()
+            le = fwd(m, x, y)
+            le.backward()
+            o.step()
         losses_e.append(float(le.detach()))
         losses_g.append(float(gs(x, y)))
     torch.cuda.synchronize()
@@ -67,7 +69,8 @@ def test_graph_step_matches_eager(name, opt_name, shape, lr, tol):
     for a, b in zip(losses_e, losses_g):
         assert abs(a - b) < tol * max(1.0, abs(a)), (losses_e, losses_g)
     d = _delta_rel(mg._pdnn_flat.data, me._pdnn_flat.data, p0)
-    assert d < 2.5 * tol, d
+    d_eager = _delta_rel(mt._pdnn_flat.data, me._pdnn_flat.data, p0)      # run-to-run drift of the eager path
+    assert d < max(2.5 * tol, 3.0 * d_eager), (d, d_eager)
     # bf16 shadow refreshed by the replayed optimizer kernel
     fp = mg._pdnn_flat
     assert ((fp.shadow.float() - fp.data).norm() / fp.data.norm()).item() < 5e-3
