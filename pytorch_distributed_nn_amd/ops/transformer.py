@@ -264,6 +264,10 @@ class GPT2BlockFn(torch.autograd.Function):
         ctx.params = None
         sink = _Sink()
         g = g.contiguous()
+        if g.is_cuda and _tuning.get("wt_layer_batch"):
+            # the four data-gradient GEMMs' transposed weights of this block in one launch, just before use
+            from .functional import prefetch_weight_t
+            prefetch_weight_t((Pm[10], Pm[8], Pm[4], Pm[2]))
         # MLP
         du = BL.linear_dgrad(g, wfc2, dgelu=u, p=Pm[10])                       # (g . Wfc2) * gelu'(u)
         dfc2_w, dfc2_b = sink.linear(Pm[10], Pm[11], g, h)

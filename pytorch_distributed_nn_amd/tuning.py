@@ -18,6 +18,8 @@ wt_prefetch        0        GPT-2 data-gradient GEMMs' transposed weight copies:
                             its first backward use, 1 all of them in one launch at forward start (compute stream),
                             2 that launch on the side stream beside the forward (544.7k / 542.3k / 537.0k tok/s,
                             gpurun_out/r5_10: the eager backward has launch gaps the small transposes fill)
+wt_layer_batch     1        those transposes (wt_prefetch 0) batched per transformer block: the four weights of a block
+                            in one launch at the start of its backward (592.8k vs 590.1k tok/s, r5_28)
 colsum_atomic      1        accumulating bias-gradient column sums in one launch with fp32 atomics (0: two-level
                             deterministic partial rows + level-2 launch; GPT-2 542.3k vs 538.0k tok/s, r5_10)
 bias_in_wgrad      1        GPT-2 linear bias gradients as fused row sums inside the weight-gradient GEMM (0: a
@@ -31,7 +33,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "colsum_atomic": 1, "bias_in_wgrad": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1}
 
 _VALUES = dict(DEFAULTS)
 
