@@ -122,6 +122,8 @@ def main():
                     help="one GPU without the DDP wrapper and process group (the second run of a --gpus 1 bench)")
     ap.add_argument("--no-ddp-rehearsal", "--no-plain-run", dest="no_plain_run", action="store_true",
                     help="at --gpus 1, skip the second measurement (the plain step)")
+    ap.add_argument("--opt-overlap", action="store_true",
+                    help="DDP path: apply the optimizer per bucket during the backward instead of after it")
     ap.add_argument("--diag-steps", type=int, default=5,
                     help="DDP path: extra steps after the timed region with per-bucket communication timing")
     ap.add_argument("--hang-timeout", type=float, default=90.0,
@@ -194,6 +196,14 @@ def main():
         # bf16 images on the GPU; fp32 on the CPU (the gloo test rehearsal of the N > 1 path: torch's CPU convs)
         xs = [torch.randn(B, *in_chw, device=dev).to(torch.bfloat16 if on_gpu else torch.float32) for _ in range(2)]
         ys = [torch.randint(0, nc, (B,), device=dev) for _ in range(2)]
+
+    # --opt-overlap: the DDP path applies each bucket's optimizer update as soon as the bucket is all-reduced,
+    # beside the rest of the backward (DistributedDataParallel.overlap_optimizer).  Off by default: at N = 1 the
+    # concurrent update slows the backward more than it hides (GPT-2 587k vs 593k tok/s, ResNet-50 11,575 vs
+    # 11,616 img/s, gpurun_out/r5_29)
+    opt_overlap = False
+    if use_ddp and on_gpu and a.opt_overlap and isinstance(net, DistributedDataParallel):
+        opt_overlap = net.overlap_optimizer(opt) is not None
 
     # auto: graphed on one GPU, except the ImageNet ResNets, whose weight gradients run on a side stream
     # concurrently with the data-gradient chain (ops/fused_resnet.py): eager launches overlap the two
@@ -320,7 +330,8 @@ def main():
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
-                       "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
+                       "optimizer": "fused AdamW lr=6e-4 wd=0.1", "bucket_mb": a.bucket_mb, "hipgraph": use_graph,
+                       "opt_overlap": opt_overlap},
         })
     elif env.rank == 0:
         emit({
@@ -349,7 +360,8 @@ def main():
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
-                       "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb, "hipgraph": use_graph},
+                       "optimizer": "fused SGD momentum=0.9 wd=5e-5", "bucket_mb": a.bucket_mb, "hipgraph": use_graph,
+                       "opt_overlap": opt_overlap},
         })
     runtime.destroy()
 

@@ -91,6 +91,47 @@ class _FusedBase(torch.optim.Optimizer):
             if gi in self._hyper:
                 self._fill_hyper(gi, group)
 
+    # ------------------------------------------------------------------ overlapped step (DDP per bucket)
+    # DistributedDataParallel.overlap_optimizer(opt): the update of each gradient bucket is applied on an
+    # optimizer stream as soon as the bucket's all-reduce has completed, while the backward of the earlier layers
+    # still runs; the step() that follows the backward then has nothing left to do.  One param group on the flat
+    # arena, eager (not graph) mode.
+    def _overlap_ok(self):
+        if self._graph or len(self.param_groups) != 1:
+            return None
+        fp, rng = self._group_flat(0, self.param_groups[0])
+        if fp is None or not fp.data.is_cuda:
+            return None
+        return fp, rng
+
+    @torch.no_grad()
+    def _overlap_begin(self):
+        """Host side, once per step before the first range: advance the step state (and create it)."""
+        self._ovl_state = self._begin_ranges(0, self.param_groups[0])
+        self._ovl_done = False
+
+    @torch.no_grad()
+    def _overlap_range(self, a, b):
+        """Update flat-arena elements [a, b) (a bucket) with the state _overlap_begin prepared (current stream)."""
+        self._apply_range(0, self.param_groups[0], a, b, self._ovl_state)
+
+    def _overlap_end(self):
+        fp, _ = self._group_flat(0, self.param_groups[0])
+        fp.generation += 1
+        self._ovl_done = True          # the next step() finds the update applied
+
+    def _begin_ranges(self, gi, group):
+        raise NotImplementedError
+
+    def _apply_range(self, gi, group, a, b, state):
+        raise NotImplementedError
+
+    def _consume_overlap(self):
+        if getattr(self, "_ovl_done", False):
+            self._ovl_done = False
+            return True
+        return False
+
     def zero_grad(self, set_to_none: bool = False):
         done = set()
         for group in self.param_groups:
@@ -120,12 +161,31 @@ class SGD(_FusedBase):
         if self.param_groups[gi]["momentum"] != 0 and "momentum_buffer" not in self.state.get(f"flat{gi}", {}):
             raise RuntimeError("SGD graph mode: run one eager step before capture (momentum buffer init)")
 
+    def _begin_ranges(self, gi, group):
+        fp, (s, e) = self._group_flat(gi, group)
+        st = self.state.setdefault(f"flat{gi}", {})
+        first = "momentum_buffer" not in st
+        if group["momentum"] != 0 and first:
+            st["momentum_buffer"] = torch.zeros(e - s, device=fp.data.device)
+        return first
+
+    def _apply_range(self, gi, group, a, b, first):
+        from ..ops import kernels as K
+        fp, (s, _) = self._group_flat(gi, group)
+        buf = self.state[f"flat{gi}"].get("momentum_buffer")
+        K.sgd_step(fp.data[a:b], fp.grad[a:b], None if buf is None else buf[a - s:b - s],
+                   fp.shadow[a:b] if fp.shadow is not None else None, group["lr"], group["momentum"],
+                   group["dampening"], group["weight_decay"], group["nesterov"], self.grad_scale_dev,
+                   self.grad_scale, first)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._consume_overlap():
+            return loss
         for gi, group in enumerate(self.param_groups):
             lr, mom, damp, wd, nest = (group["lr"], group["momentum"], group["dampening"], group["weight_decay"],
                                        group["nesterov"])
@@ -181,12 +241,34 @@ class Adam(_FusedBase):
         b1, b2 = group["betas"]
         return [group["lr"], 1 - b1 ** t, 1 - b2 ** t]
 
+    def _begin_ranges(self, gi, group):
+        fp, (s, e) = self._group_flat(gi, group)
+        st = self.state.setdefault(f"flat{gi}", {})
+        if "step" not in st:
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros(e - s, device=fp.data.device)
+            st["exp_avg_sq"] = torch.zeros(e - s, device=fp.data.device)
+        st["step"] += 1
+        return max(st["step"], 1)
+
+    def _apply_range(self, gi, group, a, b, t):
+        from ..ops import kernels as K
+        fp, (s, _) = self._group_flat(gi, group)
+        st = self.state[f"flat{gi}"]
+        (b1, b2) = group["betas"]
+        K.adam_step(fp.data[a:b], fp.grad[a:b], st["exp_avg"][a - s:b - s], st["exp_avg_sq"][a - s:b - s],
+                    fp.shadow[a:b] if fp.shadow is not None else None, group["lr"], b1, b2, group["eps"],
+                    group["weight_decay"], self.decoupled, 1 - b1 ** t, 1 - b2 ** t, self.grad_scale_dev,
+                    self.grad_scale)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._consume_overlap():
+            return loss
         for gi, group in enumerate(self.param_groups):
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             fp, rng = self._group_flat(gi, group)

@@ -269,6 +269,8 @@ class DistributedDataParallel(nn.Module):
         self.step = 0
         self.last_counts = None          # per-bucket contributor counts of the last step (k-of-n)
         self.aborted_steps = 0
+        self._ovl_opt = None           # overlap_optimizer(): per-bucket updates on _ovl_stream
+        self._ovl_stream = None
         self._reset()
         self.step_comm_log = []
         self._in_fwd = False
@@ -394,6 +396,7 @@ class DistributedDataParallel(nn.Module):
         self._events = []
         self.launch_order = []
         self._ev_start, self._ev_done = {}, {}
+        self._ovl_step = False          # this step's buckets are being applied by the overlapped optimizer
 
     def _arm(self):
         self.abort_phase = None
@@ -494,7 +497,43 @@ class DistributedDataParallel(nn.Module):
             self._ev_start[b], self._ev_done[b] = ev0, ev1
             self._works.append((b, work))
             return
-        self._works.append((b, dist.all_reduce(t, op=op, group=self.pg, async_op=True)))
+        work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
+        self._works.append((b, work))
+        if self._ovl_active():
+            # the bucket's optimizer update on the optimizer stream, as soon as its all-reduce is done, beside
+            # the backward of the earlier layers (whose weights it does not touch)
+            opt = self._ovl_opt
+            if not self._ovl_step:
+                opt._overlap_begin()           # host side: step counter / state, before the first range
+                self._ovl_step = True
+            os_ = self._ovl_stream
+            with torch.cuda.stream(os_):
+                work.wait()                    # the optimizer stream waits for RCCL's
+                opt._overlap_range(s, e)
+
+    def _ovl_active(self):
+        return (self._ovl_opt is not None and self.comm_dtype is None and not self.straggler_mode
+                and self.kofn is None and not self.comm_timing and not self._aborted and self.flat.grad.is_cuda
+                and not self._ovl_opt._graph)
+
+    def overlap_optimizer(self, opt):
+        """Apply ``opt``'s update bucket by bucket during the backward: each bucket's range of the flat arena is
+        updated on an optimizer stream right after its all-reduce, while the compute stream runs the backward of
+        the earlier layers; ``opt.step()`` after the backward then has nothing left to do (it still works as usual
+        for a step without buckets, e.g. under ``no_sync``).  ``opt`` must be a fused flat optimizer whose single
+        param group spans exactly this wrapper's buckets.  Returns ``opt``; None (no overlap) when it does not
+        qualify."""
+        ok = opt._overlap_ok() if hasattr(opt, "_overlap_ok") else None
+        if ok is None or ok[0] is not self.flat:
+            return None
+        s, e = ok[1]
+        ranges = sorted((bs, be) for bs, be, _ in self.buckets)
+        if not ranges or ranges[0][0] != s or ranges[-1][1] != e or any(ranges[i][1] != ranges[i + 1][0]
+                                                                         for i in range(len(ranges) - 1)):
+            return None
+        self._ovl_opt = opt
+        self._ovl_stream = torch.cuda.Stream(device=self.flat.grad.device)
+        return opt
 
     def _finish(self):
         if not self._armed:
@@ -526,6 +565,11 @@ class DistributedDataParallel(nn.Module):
         self._issue_buffer_broadcast()
         for b, w in self._works:
             w.wait()
+        if self._ovl_step:
+            # every bucket's update was queued on the optimizer stream: the compute stream (the next zero_grad /
+            # forward) waits for them, and the optimizer's step() finds them applied
+            torch.cuda.current_stream(fp.grad.device).wait_stream(self._ovl_stream)
+            self._ovl_opt._overlap_end()
         if ev_bwd is not None and self._ev_start:
             self._ev_log.append({"arm": self._ev_arm, "bwd": ev_bwd, "bn": self._ev_bn,
                                  "buckets": [(b, self._ev_start[b], self._ev_done[b]) for b in sorted(self._ev_start)]})

@@ -142,6 +142,57 @@ def test_ddp_rccl_kofn_single_rank():
         assert not aborted and rel < 1e-5 and all(c == 1.0 for c in counts), res
 
 
+def _rccl_overlap_job(rank, world, opt_name):
+    """overlap_optimizer: every bucket's update applied on the optimizer stream right after its all-reduce, during
+    the backward.  Lockstep against the update after the backward: before each step the overlapped net is re-synced
+    to the reference (weights, buffers, optimizer state); the updated weights must agree to the gradients' own
+    run-to-run noise (fp32 atomics), and step() after an overlapped backward must not update a second time."""
+    import torch.distributed as dist
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.ops import functional as OF
+    from pytorch_distributed_nn_amd.optim import SGD, AdamW
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    assert dist.get_backend() == "nccl"
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m0 = build_model("resnet18", 10).to(dev)
+    nets = [DistributedDataParallel(copy.deepcopy(m0), bucket_cap_mb=4.0, first_bucket_cap_mb=0.5) for _ in range(3)]
+    mk = (lambda m: SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)) if opt_name == "sgd" else \
+        (lambda m: AdamW(m.parameters(), lr=1e-3, weight_decay=0.1))
+    opts = [mk(n.module) for n in nets]
+    (nr, nt, no), (orf, ot, oo) = nets, opts
+    assert no.overlap_optimizer(oo) is oo
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for i in range(4):
+        x = torch.randn(16, 3, 32, 32, generator=g).to(dev)
+        y = torch.randint(0, 10, (16,), generator=g).to(dev)
+        if i >= 1:
+            _sync_state(nt, ot, nr, orf)
+            _sync_state(no, oo, nr, orf)
+        before = nr.flat.data.clone()
+        for n, o in ((nr, orf), (nt, ot), (no, oo)) if i >= 1 else ((nr, orf), (no, oo)):
+            o.zero_grad()
+            OF.cross_entropy(n(x), y).backward()
+            o.step()
+        torch.cuda.synchronize()
+        if i >= 1:
+            d_ref = (nr.flat.data - before).norm().item()
+            noise = (nt.flat.data - nr.flat.data).norm().item()
+            err = (no.flat.data - nr.flat.data).norm().item()
+            out.append((err, noise, d_ref))
+    return out
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adamw"])
+def test_ddp_overlapped_optimizer_matches_step_after_backward(opt_name):
+    res = run_world(_rccl_overlap_job, 1, (opt_name,), timeout=150, device=None, backend="nccl",
+                    env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})[0]
+    for err, noise, moved in res:
+        assert moved > 0
+        assert err < 3 * noise + 1e-3 * moved, res
+
+
 def _sync_state(dst_net, dst_opt, src_net, src_opt):
     """dst := src (flat weights + bf16 shadow, BN buffers, momentum)."""
     dst_net.flat.data.copy_(src_net.flat.data)
