@@ -628,8 +628,17 @@ class DistributedDataParallel(nn.Module):
         self._bn_work = None
         if not (self._bn_views and self._buffer_sync_due()) or self._buffers_list:
             return
-        works = [dist.broadcast(flat, 0, group=self.pg, async_op=True)
-                 for key, flat in self._buf_flat.items() if isinstance(key, tuple) and key[0] == "bn"]
+        flats = [flat for key, flat in self._buf_flat.items() if isinstance(key, tuple) and key[0] == "bn"]
+        side = side_stream_if_active(self.flat.grad)
+        if side is not None:
+            # issued from the weight-gradient side stream after a fence-free wait, like the bucket collectives
+            # (_launch), so the collective's event record lands off the compute stream
+            from ..ops import kernels as K
+            K.stream_wait(side, torch.cuda.current_stream(side.device))
+            with torch.cuda.stream(side):
+                works = [dist.broadcast(flat, 0, group=self.pg, async_op=True) for flat in flats]
+        else:
+            works = [dist.broadcast(flat, 0, group=self.pg, async_op=True) for flat in flats]
         self._bn_work = (works, self._fwd_count)
 
     def forward(self, *args, **kwargs):
