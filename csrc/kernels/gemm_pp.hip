@@ -856,8 +856,11 @@ double bn_eff(int bn) {
     }
 }
 
-// kk: both operands K-major (every tile width); otherwise / with fusions only 128 and 256
-int pick_bn(const GemmArgs& a, bool kk) {
+// kk: both operands K-major (every tile width); otherwise / with fusions only 128 and 256.
+// amn: A (and B) MN-major, the weight-gradient form: both operands are read with ds_read_b64_tr_b16, where the
+// 128-wide tile reaches only ~0.65 of the 256-wide one's per-CU rate (GPT-2 LM-head weight gradient
+// 50304 x 768 x 8192: 3.1 vs 4.8 TF/s per CU, 934 vs 744 us; gpurun_out/r5_31)
+int pick_bn(const GemmArgs& a, bool kk, bool amn = false) {
     const int g_pp_force_bn = tune().pp_bn;
     const int cus = device_cus();
     static const int kk_opts[] = {256, 288, 192, 128, 96};
@@ -875,7 +878,7 @@ int pick_bn(const GemmArgs& a, bool kk) {
         const int bn = opts[i];
         const long tiles = cdiv(a.M, PP_BM) * cdiv(a.N, bn);
         const long rounds = cdiv(tiles, cus);
-        const double t = (double)rounds * bn / bn_eff(bn);
+        const double t = (double)rounds * bn / (amn && bn == 128 ? 0.65 : bn_eff(bn));
         if (t < bt * 0.999) { bt = t; best = bn; }
     }
     return best;
@@ -911,7 +914,8 @@ template <int FX>
 int pp_launch_fx(const GemmArgs& a, int amode, int bmode, int em, hipStream_t st) {
     // the BN-backward epilogue and the operand prologue fit the 256-wide tile's registers only with scratch
     // spills: 128 wide
-    const int bn = (FX & (FX_BNB | FX_PRO)) ? 128 : pick_bn(a, FX == 0 && amode == A_KMAJOR && bmode == B_KMAJOR);
+    const int bn = (FX & (FX_BNB | FX_PRO)) ? 128
+                 : pick_bn(a, FX == 0 && amode == A_KMAJOR && bmode == B_KMAJOR, amode == A_MNMAJOR);
     const int key = amode * 100 + bmode * 10 + em;
     if constexpr (FX != 0) {      // fusions: bf16 output, A K-major
         switch (key) {
@@ -1006,7 +1010,7 @@ PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb,
     if (splits > nsl) splits = nsl;
     a.ktiles_per_split = nsl / splits;             // the first nsl % splits splits take one slice more
     a.ksl_rem = nsl % splits;
-    const int bn = pick_bn(a, false);
+    const int bn = pick_bn(a, false, true);
     if (splits == 1) {
         a.C = out; a.ldc = ldc; a.acc_c = 1;
         return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
@@ -1071,7 +1075,7 @@ PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
     // halving it (GPT-2 fc / fc2: 4 -> 2 splits, tools/pp_check.py wg_* rows)
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K;
-    const int bn = pick_bn(a, false);
+    const int bn = pick_bn(a, false, true);
     const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
     const int cus = device_cus();
     const int nsl = K / PP_SK;
@@ -1093,7 +1097,7 @@ PDNN_API int pdnn_pp_wgrad_splits_long(int M, int N, int K) {
     using namespace pg;
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K;
-    const int bn = pick_bn(a, false);
+    const int bn = pick_bn(a, false, true);
     const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
     const int cus = device_cus();
     const int nsl = K / PP_SK;
