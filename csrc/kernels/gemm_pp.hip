@@ -999,8 +999,9 @@ PP_F(C128k, B_KMAJOR, 1) PP_F(C128k, B_KMAJOR, 2) PP_F(C128k, B_KMAJOR, 3) PP_F(
 PDNN_API long pdnn_pp_wgrad_ws(int M, int N, int splits) { return splits > 1 ? (long)splits * ((long)M * N + 64) : 0; }
 // rowsum (optional, fp32 [M]): += alpha * sum_k A[k][m], fused (the bias gradient of a linear layer beside its
 // weight gradient: one extra MFMA per A fragment in the first column tile's items, atomically added per split)
+// bn: tile width 128 / 256 (pdnn_pp_wgrad_plan), 0 = pick_bn's choice
 PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* out, long ldc, int M, int N,
-                           int K, float alpha, float* ws, int splits, float* rowsum, hipStream_t st) {
+                           int K, float alpha, float* ws, int splits, float* rowsum, int bn, hipStream_t st) {
     using namespace pg;
     if (K % PP_SK || M % 8 || N % 8 || splits < 1) return (int)hipErrorInvalidValue;
     GemmArgs a{};
@@ -1010,7 +1011,7 @@ PDNN_API int pdnn_pp_wgrad(const bf16_t* A, long lda, const bf16_t* B, long ldb,
     if (splits > nsl) splits = nsl;
     a.ktiles_per_split = nsl / splits;             // the first nsl % splits splits take one slice more
     a.ksl_rem = nsl % splits;
-    const int bn = pick_bn(a, false, true);
+    if (tune().pp_bn > 0 || (bn != 128 && bn != 256)) bn = pick_bn(a, false, true);
     if (splits == 1) {
         a.C = out; a.ldc = ldc; a.acc_c = 1;
         return launch_bn<A_MNMAJOR, B_MNMAJOR, E_F32>(a, bn, 1, st);
@@ -1065,6 +1066,32 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
         if (t < bt) { bt = t; best = s; }
     }
     return best;
+}
+
+// Joint (tile width, K-splits) plan of a linear layer's weight gradient, returned as bn * 1000 + splits: minimises
+//   rounds x (slices per item + 10) x u(bn)  +  fp32 traffic of the slabs (split-K) or of the in-place accumulate
+// with u = 0.60 / 0.805 us per 32-deep slice per item round for the 128 / 256-wide MN-major tiles and ~5.5 TB/s for
+// the slabs, fitted to the GPT-2 shapes (dev/probes/wgrad_sweep.py, gpurun_out/r5_33: e.g. fc 3072 x 768 x 8192
+// 256 wide x 6 splits 62.9 us vs 128 x 3 68.6 us).  A forced width (tuning pp_bn) is kept.
+PDNN_API int pdnn_pp_wgrad_plan(int M, int N, int K) {
+    using namespace pg;
+    const int cus = device_cus();
+    const int nsl = K / PP_SK;
+    const int force = tune().pp_bn;
+    int best_bn = 128, best_s = 1;
+    double bt = 1e300;
+    for (int bn : {128, 256}) {
+        if ((force == 128 || force == 256) && bn != force) continue;
+        const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
+        const double u = bn == 128 ? 0.60 : 0.805;
+        for (int s = 1; s <= 32; ++s) {
+            if (s > 1 && nsl / s < 16) continue;
+            const double fp32 = (s > 1 ? (double)s : 1.0) * M * N * 8 / 5.5e6;
+            const double t = (double)cdiv(tiles * s, cus) * (cdiv(nsl, s) + 10) * u + fp32;
+            if (t < bt * 0.999) { bt = t; best_bn = bn; best_s = s; }
+        }
+    }
+    return best_bn * 1000 + best_s;
 }
 
 PDNN_API int pdnn_pp_wgrad_splits(int M, int N, int K) {
