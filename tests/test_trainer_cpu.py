@@ -106,7 +106,9 @@ def test_resume_at_large_step_fast_forwards_without_building_batches(tmp_path):
     ds = DataSet(rng.randn(64, 8).astype(np.float32), rng.randint(0, 4, 64))
     loader = DataLoader(ds, 4, transform=slow_transform)
     fired = []
-    wd = CommWatchdog(timeout_s=1.0, rank=0, exit_on_hang=False, on_hang=fired.append, poll_s=0.05).start()
+    # 3 s: a cold first import inside train() can take over a second on a loaded host; building the 20,000
+    # skipped batches would take ~40 s
+    wd = CommWatchdog(timeout_s=3.0, rank=0, exit_on_hang=False, on_hang=fired.append, poll_s=0.05).start()
     t = _trainer(tmp_path, watchdog=wd)
     t.step_no = 20000
     t0 = time.perf_counter()
