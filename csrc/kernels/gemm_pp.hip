@@ -1084,7 +1084,7 @@ PDNN_API int pdnn_pp_wgrad_plan(int M, int N, int K) {
         if ((force == 128 || force == 256) && bn != force) continue;
         const long tiles = cdiv(M, PP_BM) * cdiv(N, bn);
         const double u = bn == 128 ? 0.60 : 0.805;
-        for (int s = 1; s <= 32; ++s) {
+        for (int s = 1; s <= 256; ++s) {
             if (s > 1 && nsl / s < 16) continue;
             const double fp32 = (s > 1 ? (double)s : 1.0) * M * N * 8 / 5.5e6;
             const double t = (double)cdiv(tiles * s, cus) * (cdiv(nsl, s) + 10) * u + fp32;

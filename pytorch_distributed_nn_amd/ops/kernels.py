@@ -474,7 +474,9 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
     if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _WGRAD1X1_PP_PIX
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
         # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs, split count from
-        # the long-reduction model): ResNet stages 2-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33, r3_38)
+        # the long-reduction model): ResNet stages 2-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33, r3_38).  The joint
+        # width/split plan (pdnn_pp_wgrad_plan) is faster per call in isolation (stage-2 conv1 83 -> 68 us,
+        # dev/probes/wgrad1x1_sweep.py) but 1% slower end to end beside the data-gradient chain (r5_36-37)
         pp_wgrad(dy.view(P, K), x.view(P, C), out.view(K, C), splits=lib().pdnn_pp_wgrad_splits_long(K, C, P))
         return out
     call("pdnn_conv_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, R, S, st, pad, Ho, Wo, ptr(sc), ptr(sh),
