@@ -109,7 +109,10 @@ def main():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="DDP gradient bucket cap (default 32 MB; GPT-2 128 MB: every bucket's collective costs the "
+                         "compute stream a ~21 us stream-sync event, so its 27 MB-per-block buckets cost 2%% at N = 1, "
+                         "gpurun_out/r5_44)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config 5: ResNet 3x3 convs / GPT-2 forward linears on the fp8 MFMA kernels")
@@ -130,6 +133,8 @@ def main():
                     help="N > 1: hang watchdog (s without a completed step; the process-group timeout is 1.25x): "
                          "on a hang every rank prints one diagnostic JSON line and exits 75")
     a = ap.parse_args()
+    if a.bucket_mb is None:
+        a.bucket_mb = 128.0 if a.model.lower().startswith("gpt2") else 32.0
     # stdout carries exactly the result line: libraries that print banners to fd 1 from C (RCCL's version block at
     # communicator init) are sent to stderr with everything else; the JSON lines go to the saved descriptor
     sys.stdout.flush()
