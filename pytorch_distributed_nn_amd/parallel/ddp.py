@@ -18,7 +18,7 @@ What it does, and how it differs from the reference's design:
   (data_parallel_dist.py:211-267).
 * **Averaging** uses RCCL's native AVG reduction (one pass, no extra scale kernel); on gloo (CPU) it is
   SUM followed by a scale.
-* **Bucket sizing for xGMI** (defaults 1 MiB first bucket, 32 MiB afterwards).  A ring all-reduce of S bytes
+* **Bucket sizing for xGMI** (default 32 MiB, the first bucket too: ``first_bucket_cap_mb`` may make it smaller).  A ring all-reduce of S bytes
   over N ranks costs T(S) ~= a + 2(N-1)/N * S / B, with a the per-collective latency and B the per-rank bus
   bandwidth.  Measured here (profiles/rccl_world1_r4.txt, device events, RCCL AVG): a ~= 12-18 us (the
   64 KiB-4 MiB sizes all take 13-18 us), and the world-1 reduction kernel itself runs at ~700 GB/s fp32, so it
@@ -31,8 +31,10 @@ What it does, and how it differs from the reference's design:
   exposed is the LAST bucket (stem + stage-1 parameters, 12.3 MiB, ready only when the backward ends): ~120 us
   at N = 8 by the model above.  Smaller buckets would not shrink it (those parameters' gradients all arrive in
   the backward's last ~1 ms) and would multiply the latency term; larger ones would delay the earlier buckets
-  past the point where they overlap.  The 1 MiB first bucket only starts the pipeline (it holds fc.bias: the
-  8 MB fc.weight does not fit).  Re-derive with ``tools/bench_allreduce.py`` at the real N.
+  past the point where they overlap.  A small first bucket (PyTorch's 1 MiB) would hold only fc.bias here (the
+  8 MB fc.weight does not fit) and start nothing useful early, while every collective also costs its issuing
+  stream ~21 us (ProcessGroupNCCL's stream-sync event, gpurun_out/r5_40-44): the first bucket takes the full cap.
+  Re-derive with ``tools/bench_allreduce.py`` at the real N.
 * **k-of-n straggler kill / backup workers in collective form** (PAR-DP-KILL / PAR-DP-BACKUP, SURVEY.md
   §5.3; reference: pytorch_code/sync_replicas_master_nn.py:172-186 kill on the k-th arrival,
   pytorch_code/model_ops/lenet.py:168-178 worker poll, MPI_code/src/distributed/worker_nn.h:59-84
@@ -217,7 +219,7 @@ def _is_nccl(pg):
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
-                 first_bucket_cap_mb: float = 1.0, broadcast_buffers: bool = True, comm_dtype=None,
+                 first_bucket_cap_mb: float | None = None, broadcast_buffers: bool = True, comm_dtype=None,
                  average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
                  num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True,
                  buffer_sync_interval: int = 1, comm_timing: bool = False):
@@ -264,7 +266,7 @@ class DistributedDataParallel(nn.Module):
             if _backend.available():
                 K.set_comm_world(self.world)
         self._broadcast_init()
-        self._build_buckets(bucket_cap_mb, first_bucket_cap_mb)
+        self._build_buckets(bucket_cap_mb, bucket_cap_mb if first_bucket_cap_mb is None else first_bucket_cap_mb)
         self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
         self.step = 0
         self.last_counts = None          # per-bucket contributor counts of the last step (k-of-n)
