@@ -222,7 +222,7 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_cap_mb: float | None = None, broadcast_buffers: bool = True, comm_dtype=None,
                  average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
                  num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True,
-                 buffer_sync_interval: int = 1, comm_timing: bool = False):
+                 buffer_sync_interval: int = 1, comm_timing: bool = False, native_comm: bool | None = None):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -266,6 +266,14 @@ class DistributedDataParallel(nn.Module):
             if _backend.available():
                 K.set_comm_world(self.world)
         self._broadcast_init()
+        # native_comm (opt-in, PDNN_DDP_NATIVE_COMM=1): bucket all-reduces issued through RCCL directly, ordered by
+        # fence-free events instead of ProcessGroupNCCL's per-collective stream-sync event (parallel/rccl_native.py)
+        if native_comm is None:
+            native_comm = os.environ.get("PDNN_DDP_NATIVE_COMM") == "1"
+        self._native = None
+        if native_comm and self._comm and self.nccl and self.flat.grad.is_cuda:
+            from .rccl_native import NativeComm
+            self._native = NativeComm(self.pg, self.flat.grad.device)
         self._build_buckets(bucket_cap_mb, bucket_cap_mb if first_bucket_cap_mb is None else first_bucket_cap_mb)
         self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
         self.step = 0
@@ -499,7 +507,10 @@ class DistributedDataParallel(nn.Module):
             self._ev_start[b], self._ev_done[b] = ev0, ev1
             self._works.append((b, work))
             return
-        work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
+        if self._native is not None:
+            work = self._native.all_reduce(t, avg=op == dist.ReduceOp.AVG)
+        else:
+            work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
         self._works.append((b, work))
         if self._ovl_active():
             # the bucket's optimizer update on the optimizer stream, as soon as its all-reduce is done, beside
