@@ -15,8 +15,9 @@ Opt-in (``DistributedDataParallel(native_comm=True)`` or ``PDNN_DDP_NATIVE_COMM=
 not been run on this project's one-GPU boxes; the torch process group still carries the BN-buffer broadcasts and
 the straggler counts.  Measured at world 1 (gpurun_out/r5_48, same box): GPT-2 with 13 bucket collectives 608.8k
 vs 606.7k tok/s (ProcessGroupNCCL), with 128 MB buckets 612.5k vs 616.9k; ResNet-50, whose collectives are
-issued from the weight-gradient side stream, 8,184 vs 11,598 img/s -- a 9 ms/step loss not understood yet
-(next step: a kernel trace of that run).  Hence off by default.
+issued from the weight-gradient side stream, 8,184 vs 11,598 img/s -- not understood yet: the kernel trace
+(gpurun_out/r5_49) shows no RCCL kernel at world 1, but the step's own kernels run slower (39.8 vs 34.2 ms of
+kernel time over the two streams, span 29.4 vs 22.4 ms).  Hence off by default.
 """
 from __future__ import annotations
 
