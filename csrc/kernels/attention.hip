@@ -23,6 +23,7 @@
 //       S^T = K Q^T, P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T
 //   delta[q] = sum_d dO[q][d] O[q][d] comes from attn_bwd_delta.
 #include "common.h"
+#include "tuning.h"
 
 // Block order over (query or key tile, head, sequence): 0 = 3-D grid, heavy tiles first inside each (head, sequence);
 // 1 = 1-D grid, heavy tiles first over the WHOLE grid (the dispatcher hands out blocks in index order, so the last
@@ -433,8 +434,12 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
 }
 
 // dQ for 64 queries per block (wave w: queries q0 + 16 w .. +15); loop over 64-key tiles
+// DELTA: the block also forms delta = rowsum(dO . O) of its queries (the four 16-lane groups of a query row take
+// 16 dims each) and writes it for attn_bwd_dkdv_kernel, which then runs after it: no separate delta launch
+template <bool DELTA>
 __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
-                                                          const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                          const float* __restrict__ lse2, float* __restrict__ delta,
+                                                          const bf16_t* __restrict__ o,
                                                           bf16_t* __restrict__ dqkv, int T, int H, float scale,
                                                           int causal) {
     __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
@@ -452,7 +457,25 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
     const int ql = q0 + (lane & 15);
     const float c = scale * LOG2E;
     const float lq = lse2[((long)b * H + h) * T + ql];
-    const float dq_ = delta[((long)b * H + h) * T + ql];
+    float dq_;
+    if constexpr (DELTA) {
+        const long ro = ((long)b * T + ql) * D + h * HD + 16 * g;
+        float sd = 0.f;
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+            float x[8], y[8];
+            unpack8(*reinterpret_cast<const u16x8_t*>(o + ro + 8 * c2), x);
+            unpack8(*reinterpret_cast<const u16x8_t*>(dO + ro + 8 * c2), y);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sd += x[j] * y[j];
+        }
+        sd += __shfl_xor(sd, 16, 64);
+        sd += __shfl_xor(sd, 32, 64);
+        dq_ = sd;
+        if (g == 0) delta[((long)b * H + h) * T + ql] = sd;
+    } else {
+        dq_ = delta[((long)b * H + h) * T + ql];
+    }
 
     bf16x8_t qf[2], of[2];
 #pragma unroll
@@ -554,12 +577,19 @@ PDNN_API int pdnn_flash_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf1
                                  float* delta, bf16_t* dqkv, int B, int T, int H, float scale, int causal,
                                  hipStream_t st) {
     if (T % 128) return (int)hipErrorInvalidValue;
+    if (pg::tune().attn_delta_in_dq) {       // dQ first (it writes delta), then dK / dV
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                           out, dqkv, T, H, scale, causal);
+        hipLaunchKernelGGL(attn_bwd_dkdv_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv,
+                           T, H, scale, causal);
+        PDNN_LAUNCH_RET;
+    }
     const long n = (long)B * T * H;
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n + NTA - 1) / NTA)), dim3(NTA), 0, st, out, dO, delta,
                        B * T, T, H);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
                        scale, causal);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
-                       scale, causal);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                       out, dqkv, T, H, scale, causal);
     PDNN_LAUNCH_RET;
 }

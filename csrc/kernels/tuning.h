@@ -17,6 +17,8 @@ namespace pg {
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
     X(pp_sk64, 1, "96 / 128-wide ping-pong tiles with K-major operands and K % 64 == 0 (no split-K) stream 64-deep "  \
                   "slices (128-byte rows) instead of 32-deep; 0 = 32-deep")                                    \
+    X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
+                           "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
     X(pp_dgrad_bn_k, 1024, "1x1 data gradients with the BN-backward epilogue on the ping-pong engine from this "   \
                            "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")                 \
