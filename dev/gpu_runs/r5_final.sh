@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 end state: full GPU suite, smoke, bench (ResNet-50 DDP path + plain, GPT-2), ResNet-152 bf16 / fp8 pair
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/r5_final2
+O=$GRAFT_REPO_ROOT/gpurun_out/r5_final3
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
