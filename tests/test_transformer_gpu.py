@@ -121,11 +121,11 @@ def test_embedding(K):
     pos = torch.arange(T, device="cuda").repeat(B)
     assert rel(out, wte.float()[idx] + wpe.float()[pos]) < 1e-2
     g = rnd(B * T, D)
-    dwte = torch.zeros(V, D, device="cuda")
-    dwpe = torch.zeros(Tm, D, device="cuda")
+    dwte = torch.ones(V, D, device="cuda")            # accumulates into existing gradients
+    dwpe = torch.ones(Tm, D, device="cuda")
     K.embedding_bwd(idx, g, dwte, dwpe, T)
-    rte = torch.zeros(V, D, device="cuda").index_add_(0, idx, g.float())
-    rpe = torch.zeros(Tm, D, device="cuda").index_add_(0, pos, g.float())
+    rte = torch.ones(V, D, device="cuda").index_add_(0, idx, g.float())
+    rpe = torch.ones(Tm, D, device="cuda").index_add_(0, pos, g.float())
     assert rel(dwte, rte) < 1e-4 and rel(dwpe, rpe) < 1e-4
 
 
