@@ -17,7 +17,9 @@ the straggler counts.  Measured at world 1 (gpurun_out/r5_48, same box): GPT-2 w
 vs 606.7k tok/s (ProcessGroupNCCL), with 128 MB buckets 612.5k vs 616.9k; ResNet-50, whose collectives are
 issued from the weight-gradient side stream, 8,184 vs 11,598 img/s -- not understood yet: the kernel trace
 (gpurun_out/r5_49) shows no RCCL kernel at world 1, but the step's own kernels run slower (39.8 vs 34.2 ms of
-kernel time over the two streams, span 29.4 vs 22.4 ms).  Hence off by default.
+kernel time over the two streams, span 29.4 vs 22.4 ms), and with the weight gradients on the compute stream
+(tuning side_wgrad=0) the native path matches ProcessGroupNCCL (10,031 vs 10,095 img/s, r5_53): the loss comes
+from its interplay with the two-stream schedule.  Hence off by default.
 """
 from __future__ import annotations
 
