@@ -62,6 +62,46 @@ def _plain_run(a):
         return {"error": f"{type(e).__name__}: {e}"[:200]}
 
 
+EXTRA_CONFIGS = (   # BASELINE.json configs 4 and 5, measured by the driver's one --gpus 1 command
+    ("gpt2_small", ["--model", "gpt2_small"]),
+    ("resnet152_bf16", ["--model", "resnet152"]),
+    ("resnet152_fp8", ["--model", "resnet152", "--fp8"]),
+)
+
+
+def _child_run(a, extra, timeout=300):
+    """This benchmark in a child process with ``extra`` arguments (the DDP code path at N = 1, no second plain run,
+    no diagnostics); returns the child's headline fields or an error note."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    argv = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.steps), "--warmup",
+            str(a.warmup), "--no-plain-run", "--no-extra-configs", "--diag-steps", "0"] + extra
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=timeout)
+        rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        return {k: rec.get(k) for k in ("metric", "value", "unit", "ms_per_step", "dtype", "n1_point", "final_loss")} | {
+            "config": {k: rec["config"].get(k) for k in ("model", "global_batch", "seq_len", "image_size", "bucket_mb")},
+            "wall_s": round(time.perf_counter() - t0, 1)}
+    except Exception as e:       # never lose the headline line over a secondary config
+        return {"error": f"{type(e).__name__}: {e}"[:200], "wall_s": round(time.perf_counter() - t0, 1)}
+
+
+def allreduce_probe(dev, world, sizes_mb=(32, 128), iters=10, warmup=3):
+    """N > 1, after the timed region: bus bandwidth of back-to-back RCCL all-reduces (AVG, the DDP op) at the bucket
+    sizes, fp32 and bf16 wire -- with 7 xGMI links per MI355X a ring is one link per hop, so busbw near one link's
+    ~153 GB/s means RCCL is not spreading its channels over the links (tools/bench_allreduce.py, same method)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    from bench_allreduce import _one
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    out = []
+    for dt in (torch.float32, torch.bfloat16):
+        for mb in sizes_mb:
+            r = _one("all_reduce", int(mb * 2 ** 20), dt, dev, world, iters, warmup, sync)
+            out.append({"dtype": r["dtype"], "mib": mb, "us": r["us"], "busbw_GBps": r["busbw_GBps"]})
+    return out
+
+
 def comm_diagnostics(net, step, n):
     """{"bucket_mb", "fp32": {...}, "bf16": {...}}: per wire dtype, over ``n`` steps, the median per-bucket
     all-reduce device time (gradients ready -> reduced), when each bucket was ready / done relative to the first
@@ -110,9 +150,12 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=None,
-                    help="DDP gradient bucket cap (default 32 MB; GPT-2 128 MB: every bucket's collective costs the "
-                         "compute stream a ~21 us stream-sync event, so its 27 MB-per-block buckets cost 2%% at N = 1, "
-                         "gpurun_out/r5_44)")
+                    help="DDP gradient bucket cap (default 32 MB; GPT-2 at N = 1 128 MB: there the all-reduce is a "
+                         "no-op and every bucket collective only costs the compute stream a ~21 us stream-sync event, "
+                         "gpurun_out/r5_44; at N > 1 the ddp.py cost model's 32 MB keeps every bucket but the last "
+                         "under the backward)")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="at --gpus 1 (ResNet-50 headline), skip the child runs of BASELINE configs 4 and 5")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config 5: ResNet 3x3 convs / GPT-2 forward linears on the fp8 MFMA kernels")
@@ -134,7 +177,8 @@ def main():
                          "on a hang every rank prints one diagnostic JSON line and exits 75")
     a = ap.parse_args()
     if a.bucket_mb is None:
-        a.bucket_mb = 128.0 if a.model.lower().startswith("gpt2") else 32.0
+        n_world = int(os.environ.get("WORLD_SIZE", "1"))
+        a.bucket_mb = 128.0 if a.model.lower().startswith("gpt2") and n_world == 1 else 32.0
     # stdout carries exactly the result line: libraries that print banners to fd 1 from C (RCCL's version block at
     # communicator init) are sent to stderr with everything else; the JSON lines go to the saved descriptor
     sys.stdout.flush()
@@ -181,6 +225,11 @@ def main():
             model.config.fp8 = True
         else:
             model.enable_fp8()
+    if on_gpu and os.environ.get("PDNN_BENCH_COMM_WORLD"):
+        # pricing runs only: make the kernels behave as one rank of a job this wide (the comm_cus reservation of the
+        # persistent grids, csrc/kernels/tuning.h) while the process still runs a 1-rank group
+        from pytorch_distributed_nn_amd.ops import kernels as _K
+        _K.set_comm_world(int(os.environ["PDNN_BENCH_COMM_WORLD"]))
     use_ddp = world > 1 or os.environ.get("PDNN_DDP_FORCE_COMM") == "1"     # 1-GPU rehearsal of the DDP path
     if use_ddp:
         net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb, num_aggregate=a.num_aggregate,
@@ -192,7 +241,7 @@ def main():
         opt = AdamW(model.parameters(), lr=6e-4, betas=(0.9, 0.95), weight_decay=0.1)
         B, S = a.batch or 8, a.seq_len
         V = model.config.vocab_size
-        toks = [torch.randint(0, 50257, (B, S + 1), device=dev) for _ in range(2)]
+        toks = [torch.randint(0, min(50257, V), (B, S + 1), device=dev) for _ in range(2)]
         xs = [t[:, :-1].contiguous() for t in toks]
         ys = [t[:, 1:].contiguous() for t in toks]
     else:
@@ -294,6 +343,13 @@ def main():
     if use_ddp and not on_gpu and isinstance(net, DistributedDataParallel):
         comm = {"bucket_mb": [round(v, 3) for v in net.bucket_sizes_mb()], "world": net.world, "fp32": None,
                 "bf16": None, "note": "per-bucket device timing needs a GPU (CPU rehearsal)"}
+    if world > 1 and isinstance(comm, dict):
+        # bus bandwidth of the bucket-size collectives on this node (after the timed region)
+        comm["allreduce_busbw"] = allreduce_probe(dev, world, iters=3 if not on_gpu else 10,
+                                                  warmup=1 if not on_gpu else 3,
+                                                  sizes_mb=(1, 4) if not on_gpu else (32, 128))
+    if isinstance(comm, dict) and isinstance(net, DistributedDataParallel):
+        comm["split_tied_embedding"] = net._tail is not None
     t = torch.tensor([dt], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -311,6 +367,10 @@ def main():
     plain = None
     if world == 1 and use_ddp and not a.no_plain_run and env.rank == 0:
         plain = _plain_run(a)
+    extra = None
+    if (world == 1 and on_gpu and not a.plain and not a.no_extra_configs and a.model == "resnet50" and not a.fp8
+            and env.rank == 0):
+        extra = {name: _child_run(a, args) for name, args in EXTRA_CONFIGS}
     if lm and env.rank == 0:
         tok = value * S
         emit({
@@ -361,6 +421,7 @@ def main():
             "n1_point": "plain single-GPU step" if not use_ddp else
                         ("DDP path (1-rank process group: RCCL on a GPU)" if world == 1 else "DDP path"),
             "plain_step_1gpu": plain,
+            "extra_configs": extra,
             "comm": comm,
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,

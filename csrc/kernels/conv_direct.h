@@ -170,18 +170,17 @@ __device__ __forceinline__ void c3_load_pair(const C3Args& a, const long (&lrow)
     }
 }
 
+// orow[fm]: element offset of this lane's output row in y (and in the epilogue operands laid out like y)
 template <int NB, int EPI>
-__device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile, int p0, int n0,
-                                            int wave, int lane, const bool (&pv)[4]) {
+__device__ __forceinline__ void c3_epilogue_rows(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile,
+                                                 const long (&orow)[4], int n0, int wave, int lane,
+                                                 const bool (&pv)[4]) {
     constexpr int FN = NB / 16, NP = FN / 2;
     constexpr bool RES = EPI == C3_RES;
     const int lg = lane >> 4;
-    long orow[4], lrow[4];
+    long lrow[4];
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm) {
-        orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
-        lrow[fm] = pv[fm] ? orow[fm] : 0;
-    }
+    for (int fm = 0; fm < 4; ++fm) lrow[fm] = pv[fm] ? orow[fm] : 0;
     C3PairOps<NB, EPI> cur, nxt;
     if constexpr (NP > 1) c3_load_pair<NB, EPI>(a, lrow, n0, lg, 0, cur);
     else if constexpr (RES) {
@@ -275,6 +274,16 @@ __device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][N
         }
         if (fp + 1 < NP) cur = nxt;
     }
+}
+
+// output rows = the tile's pixels in order (row length a.N)
+template <int NB, int EPI>
+__device__ __forceinline__ void c3_epilogue(const C3Args& a, f32x4_t (&acc)[4][NB / 16], int tile, int p0, int n0,
+                                            int wave, int lane, const bool (&pv)[4]) {
+    long orow[4];
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) orow[fm] = (long)(p0 + wave * 64 + fm * 16 + (lane & 15)) * a.N;
+    c3_epilogue_rows<NB, EPI>(a, acc, tile, orow, n0, wave, lane, pv);
 }
 
 }  // namespace

@@ -175,6 +175,25 @@ __global__ void __launch_bounds__(NT) colsum_final_kernel(const float* __restric
         out[c] = accumulate ? out[c] + t : t;
     }
 }
+// y[n][i][j][:] = x[n][st*i][st*j][:] (NHWC bf16, C % 8 == 0): the pixels a 1x1 / stride-st / pad-0 conv reads,
+// made contiguous so that conv runs as a plain stride-1 1x1 conv (A-stationary / ping-pong engines) and its weight
+// gradient as a plain GEMM (the ResNet shortcut convs; fused_resnet.py).  One thread per 16-byte chunk, a run of
+// C/8 consecutive threads per pixel: each pixel's channels are one contiguous 2*C-byte read.
+__global__ void __launch_bounds__(NT) subsample_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int H,
+                                                       int W, int C, int Ho, int Wo, int st, long total) {
+    const int C8 = C >> 3;
+    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+        const long pix = i / C8;
+        const int c = (int)(i - pix * C8) * 8;
+        const long nh = pix / Wo;
+        const int j = (int)(pix - nh * Wo);
+        const long n = nh / Ho;
+        const int h = (int)(nh - n * Ho);
+        const long src = ((n * H + (long)st * h) * W + (long)st * j) * C + c;
+        *reinterpret_cast<u16x8_t*>(y + pix * C + c) = *reinterpret_cast<const u16x8_t*>(x + src);
+    }
+}
+
 }  // namespace
 
 PDNN_API int pdnn_colsum_splits(long rows) {
@@ -315,4 +334,15 @@ PDNN_API int pdnn_transpose_bf16_multi(const bf16_t* const* srcs, bf16_t* const*
         if (e) return e;
     }
     return 0;
+}
+
+// y = x[:, ::st, ::st, :] (NHWC bf16): Ho = (H - 1) / st + 1, Wo likewise; C % 8 == 0
+PDNN_API int pdnn_subsample(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int st, hipStream_t s) {
+    if (C % 8 || st < 1 || N < 1 || H < 1 || W < 1) return (int)hipErrorInvalidValue;
+    const int Ho = (H - 1) / st + 1, Wo = (W - 1) / st + 1;
+    const long total = (long)N * Ho * Wo * (C / 8);
+    long g = (total + NT - 1) / NT;
+    if (g > 2048) g = 2048;        // a pure copy: 8 blocks per CU of grid-stride threads keep enough loads in flight
+    hipLaunchKernelGGL(subsample_kernel, dim3((unsigned)g), dim3(NT), 0, s, x, y, H, W, C, Ho, Wo, st, total);
+    PDNN_LAUNCH_RET;
 }

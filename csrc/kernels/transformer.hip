@@ -259,16 +259,17 @@ __global__ void __launch_bounds__(NT) embedding_fwd_kernel(const int64_t* __rest
     }
 }
 
-// dwte[idx[r]] += g[r] (fp32 atomics; rows hitting the same token accumulate), dwpe[r % T] += g[r]
+// dwte[idx[r]] += sc * g[r] (fp32 atomics; rows hitting the same token accumulate), dwpe[r % T] += g[r]; either
+// table may be absent (the split tied-embedding path reduces dwpe and the wte rows separately: parallel/ddp.py)
 __global__ void __launch_bounds__(NT) embedding_bwd_kernel(const int64_t* __restrict__ idx,
                                                            const bf16_t* __restrict__ g, float* __restrict__ dwte,
-                                                           float* __restrict__ dwpe, int rows, int T, int D) {
+                                                           float* __restrict__ dwpe, int rows, int T, int D, float sc) {
     const long total = (long)rows * D;
     for (long i = (long)blockIdx.x * NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
         const long r = i / D;
         const int c = (int)(i - r * D);
         const float v = bf2f(g[i]);
-        atomicAdd(dwte + idx[r] * D + c, v);
+        if (dwte) atomicAdd(dwte + idx[r] * D + c, sc * v);
         if (dwpe) atomicAdd(dwpe + (long)(r % T) * D + c, v);
     }
 }
@@ -329,6 +330,16 @@ PDNN_API int pdnn_embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf1
 PDNN_API int pdnn_embedding_bwd(const int64_t* idx, const bf16_t* g, float* dwte, float* dwpe, int rows, int T, int D,
                                 hipStream_t st) {
     hipLaunchKernelGGL(embedding_bwd_kernel, dim3(stream_grid((long)rows * D, NT)), dim3(NT), 0, st, idx, g, dwte,
-                       dwpe, rows, T, D);
+                       dwpe, rows, T, D, 1.f);
+    PDNN_LAUNCH_RET;
+}
+
+// the same with the wte rows scaled by sc (dwte or dwpe may be null)
+PDNN_API int pdnn_embedding_bwd_scaled(const int64_t* idx, const bf16_t* g, float* dwte, float* dwpe, int rows, int T,
+                                       int D, float sc, hipStream_t st) {
+    if (D < 1 || T < 1 || rows < 0) return (int)hipErrorInvalidValue;
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(embedding_bwd_kernel, dim3(stream_grid((long)rows * D, NT)), dim3(NT), 0, st, idx, g, dwte,
+                       dwpe, rows, T, D, sc);
     PDNN_LAUNCH_RET;
 }

@@ -6,7 +6,7 @@ S4 tf flags).  All reference flag names and defaults are accept
 
 New:  --mode ddp|ps|single (default: ps when --comm-type is Bcast/Async and world > 1, i.e. the
 reference's behaviour; ddp when --comm-type AllReduce), --comm-type AllReduce, --bucket-cap-mb,
---dtype bf16|fp32, --synthetic, --data-dir, --max-steps, --optimizer sgd|adam|adamw, --weight-decay,
+--dtype bf16|fp32|fp8, --synthetic, --data-dir, --max-steps, --optimizer sgd|adam|adamw, --weight-decay,
 --n-to-collect (backup workers), --interval-ms, --no-shortcircuit, --evaluator,
 --inject-straggler RANK:MS[,RANK:MS], --straggler-mode (k-of-n inside DDP), --checkpoint-dir, --resume,
 --trace FILE, --metrics FILE.
@@ -37,7 +37,10 @@ def add_fit_args(p: argparse.ArgumentParser):
     # --- new
     p.add_argument("--mode", type=str, default=None, choices=["ddp", "ps", "single"])
     p.add_argument("--bucket-cap-mb", type=float, default=32.0)
-    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32", "fp8"],
+                   help="compute dtype on the GPU: bf16 (default), fp8 = BASELINE config 5 (the ResNet Bottlenecks' "
+                        "3x3 convs / GPT-2's block linears on the fp8 MFMA kernels with delayed scaling, everything "
+                        "else bf16; fp32 master weights in every case), fp32 = plain torch fp32 (no fused kernels)")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--data-dir", type=str, default=None)
     p.add_argument("--max-steps", type=int, default=None)
@@ -162,7 +165,16 @@ def main(argv=None):
                                           args.network)
     nc = 1000 if args.dataset.upper() == "IMAGENET" else 10
     model = build_model(args.network, nc).to(dev)
-    xdt = torch.bfloat16 if (dev.type == "cuda" and args.dtype == "bf16") else torch.float32
+    if args.dtype == "fp8":
+        if dev.type != "cuda":
+            raise SystemExit("--dtype fp8 needs the GPU (the fp8 kernels are MFMA-only)")
+        if hasattr(model, "enable_fp8"):
+            model.enable_fp8()
+        elif hasattr(getattr(model, "config", None), "fp8"):
+            model.config.fp8 = True
+        else:
+            raise SystemExit(f"--dtype fp8: network {args.network} has no fp8 path (ResNet Bottlenecks, GPT-2)")
+    xdt = torch.bfloat16 if (dev.type == "cuda" and args.dtype in ("bf16", "fp8")) else torch.float32
 
     def to_dev(batch):
         x, y = batch

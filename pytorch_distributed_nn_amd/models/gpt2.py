@@ -133,6 +133,16 @@ class GPT2(nn.Module):
         ARRIVED before use, which only the per-op hook guarantees)."""
         return bool(getattr(idx, "is_cuda", False))
 
+    def ddp_tied_rows(self):
+        """The tied token-embedding / LM-head weight: DistributedDataParallel all-reduces its dense (LM-head) gradient
+        as soon as the head's backward has produced it and gathers the embedding's rows at the end (split_tied)."""
+        return self.transformer.wte.weight if self.lm_head.weight is self.transformer.wte.weight else None
+
+    def _row_tail(self):
+        ref = self.__dict__.get("_pdnn_row_tail")
+        ddp = ref() if ref is not None else None
+        return ddp if ddp is not None and ddp._tail is self.transformer.wte.weight else None
+
     def num_params(self, non_embedding=True):
         n = sum(p.numel() for p in self.parameters())
         return n - self.transformer.wpe.weight.numel() if non_embedding else n
@@ -169,7 +179,13 @@ class GPT2(nn.Module):
         wte_k, wpe_k = OF.weight_bf16(wte), OF.weight_bf16(wpe)
         # tied wte: with targets the fused LM head and the embedding both accumulate into its arena gradient
         hd = targets is not None and direct_grad(wte) is not None
-        x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, wte, wpe, hd)
+        ddp = self._row_tail() if hd and torch.is_grad_enabled() else None
+        if ddp is not None:
+            # split under DistributedDataParallel: the head announces wte, the embedding's rows go through
+            # ddp.reduce_sparse_rows (wte is not an autograd input of the embedding)
+            x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, None, wpe, False, (ddp, wte))
+        else:
+            x = TX.EmbeddingFn.apply(idx.reshape(-1).long().contiguous(), T, wte_k, wpe_k, wte, wpe, hd)
         for blk in tr.h:
             params, shadows = blk.fused_params()
             metas = blk.fp8_metas(x.device) if c.fp8 else None
@@ -178,19 +194,46 @@ class GPT2(nn.Module):
             xf = TX.layer_norm(x, tr.ln_f.weight, tr.ln_f.bias, c.eps)
             return OF.linear(xf, wte).view(B, T, -1)
         return TX.LMHeadLossFn.apply(x, targets.reshape(-1).long().contiguous(), c.eps, wte_k, tr.ln_f.weight,
-                                     tr.ln_f.bias, wte, hd)
+                                     tr.ln_f.bias, wte, hd, ddp is not None)
 
     def _forward_reference(self, idx, targets=None):
         B, T = idx.shape
         tr = self.transformer
         pos = torch.arange(T, device=idx.device)
-        x = tr.wte(idx) + tr.wpe(pos)
+        ddp = self._row_tail() if targets is not None and torch.is_grad_enabled() else None
+        if ddp is not None:     # split tied embedding (see forward): the rows reach wte through the DDP tail
+            x = _RowTailEmbedding.apply(idx, tr.wte.weight.detach(), tr.wpe(pos), (ddp, tr.wte.weight))
+        else:
+            x = tr.wte(idx) + tr.wpe(pos)
         for blk in tr.h:
             x = blk(x)
         logits = self.lm_head(tr.ln_f(x))
         if targets is None:
             return logits
         return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
+
+
+class _RowTailEmbedding(torch.autograd.Function):
+    """x = table[idx] + pos (reference path): the table is a detached view of the tied wte, so autograd's only edge
+    into wte is the LM head's; the embedding rows reach wte.grad through DistributedDataParallel.reduce_sparse_rows
+    in the backward.  ``pos`` [T][D] carries the autograd edge (its gradient is g summed over the batch); ``tail`` =
+    (ddp, wte) is a tuple so that autograd adds no edge into wte (which would hold wte's AccumulateGrad -- and with it
+    DDP's bucket 0 -- until this node has run)."""
+
+    @staticmethod
+    def forward(ctx, idx, table, pos, tail):
+        ctx.save_for_backward(idx)
+        ctx.ddp, ctx.wte = tail
+        return F.embedding(idx, table) + pos
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        ddp, wte = ctx.ddp, ctx.wte
+        ctx.ddp = ctx.wte = None
+        gw = wte.grad
+        ddp.reduce_sparse_rows(wte, idx, g, lambda i, r, sc: gw.index_add_(0, i, r.to(gw.dtype), alpha=sc))
+        return None, None, g.sum(0), None
 
 
 def build_gpt2(name: str = "gpt2_small", **kw) -> GPT2:

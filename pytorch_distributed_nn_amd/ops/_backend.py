@@ -41,6 +41,8 @@ _SIGS = {
     "pdnn_gemm_stats_rows": [I],
     "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
+    "pdnn_conv3x3s2": [P, P, P, I, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P, P, P],
+    "pdnn_conv3x3s2_supported": [I, I, I, I, I],
     "pdnn_conv3x3_fp8_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],
@@ -81,6 +83,7 @@ _SIGS = {
     "pdnn_pp_gemm_nt_splitk": [P, L, P, L, P, L, I, I, I, P, I, P],
     "pdnn_pp_splitk_splits": [I, I, I],
     "pdnn_transpose_bf16": [P, L, P, L, I, I, P],
+    "pdnn_subsample": [P, P, I, I, I, I, I, P],
     "pdnn_transpose_bf16_multi": [P, P, P, P, I, P],
     "pdnn_set_staged_store": [I],
     "pdnn_bn_reduce_rows": [L, I],
@@ -126,6 +129,7 @@ _SIGS = {
     "pdnn_flash_attn_bwd": [P, P, P, P, P, P, I, I, I, F, I, P],
     "pdnn_embedding_fwd": [P, P, P, P, I, I, I, P],
     "pdnn_embedding_bwd": [P, P, P, P, I, I, I, P],
+    "pdnn_embedding_bwd_scaled": [P, P, P, P, I, I, I, F, P],
     "pdnn_gemm_fp8": [P, L, P, L, P, L, I, I, I, P, P, I, P, P, P, I, P],
     "pdnn_fp8_probe": [P, P, P, I, P],
     "pdnn_amax_bf16": [P, L, P, P],

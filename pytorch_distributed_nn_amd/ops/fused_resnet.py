@@ -216,6 +216,17 @@ class Fp8Conv2:
         self.bwd = Fp8Act(device, e5m2=True)
 
 
+def _shortcut_fwd(x, kd, stride, training, bn_params, bufs, mom, eps):
+    """The projection shortcut conv + BN statistics -> ((td, mean, invstd, scale, shift), its input).  Stride 2
+    (tuning ds_sub): the conv reads a contiguous copy of x's even pixels, so it runs as a stride-1 1x1 conv and its
+    weight gradient as a plain GEMM (the implicit-GEMM engine's strided gathers ran the ResNet-50 shortcut forwards at
+    7-10% and their weight gradients at 5-13% of the bf16 peak: 0.86 + 1.04 ms per step, r5_52 trace)."""
+    if stride > 1 and tuning.get("ds_sub") and x.shape[-1] % 8 == 0:
+        xs = K.subsample(x, stride)
+        return _conv_bn(xs, kd, 1, 0, None, training, bn_params, bufs, mom, eps), xs
+    return _conv_bn(x, kd, stride, 0, None, training, bn_params, bufs, mom, eps), x
+
+
 def _bn_back(g2d, t2d, mean, inv, gamma, mode, msrc=None, msc=None, msh=None, sink=None, bn_params=None):
     slab, _, rows = K.bn_bwd_reduce(g2d, t2d, mean, inv, mode=mode, msrc=msrc, mscale=msc, mshift=msh)
     if sink is not None:
@@ -332,16 +343,17 @@ class BottleneckFn(torch.autograd.Function):
         w1, g1, b1, w2, g2, b2, w3, g3, b3 = params[:9]
         k1, k2, k3 = shadows[:3]
         side_down = None
+        xd = x                           # the shortcut conv's input (x, or its stride-2 subsample)
         side = _side_stream(x.device) if down else None
         if side is not None:
             # the shortcut conv only depends on x: run it (and its BN statistics) beside conv1 -> conv2 -> conv3
             main = torch.cuda.current_stream(x.device)
             K.stream_wait(side, main)
             with torch.cuda.stream(side):
-                side_down = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]), bufs[6:8],
-                                     mom, eps)
+                side_down, xd = _shortcut_fwd(x, shadows[3], stride, training, (params[10], params[11]), bufs[6:8],
+                                              mom, eps)
             x.record_stream(side)
-            for t in side_down:
+            for t in side_down + (xd,):
                 t.record_stream(main)
         t1, m1, i1, s1, h1 = _conv_bn(x, k1, 1, 0, None, training, (g1, b1), bufs[0:2], mom, eps)
         C1 = t1.shape[-1]
@@ -349,6 +361,10 @@ class BottleneckFn(torch.autograd.Function):
             # a1 = relu(bn1(t1)) is never materialised: the halo conv and the direct weight gradient apply BN1 + ReLU
             # while staging t1 (each element staged ~1.2x: one read of t1 instead of a bn_apply pass writing a1;
             # +0.2% ResNet-50 / +0.3% ResNet-152 same box, gpurun_out/r4_52)
+            a1, pro1, src1 = None, (s1, h1), t1
+        elif stride == 2 and K.conv3x3s2_fold_ok(tuple(t1.shape), w2.shape[0]):
+            # stride 2 (tuning s2_halo bit 4): the half-resolution halo conv applies BN1 + ReLU while staging each
+            # parity plane of t1, the weight gradient through its operand prologue
             a1, pro1, src1 = None, (s1, h1), t1
         else:
             # the implicit-GEMM engine gathers every element 9 times: materialise a1 once instead
@@ -380,8 +396,8 @@ class BottleneckFn(torch.autograd.Function):
                 K.stream_wait(main, side)
                 td, md, idd, sd, hd = side_down
             else:
-                td, md, idd, sd, hd = _conv_bn(x, shadows[3], stride, 0, None, training, (params[10], params[11]),
-                                               bufs[6:8], mom, eps)
+                (td, md, idd, sd, hd), xd = _shortcut_fwd(x, shadows[3], stride, training, (params[10], params[11]),
+                                                          bufs[6:8], mom, eps)
             out, mb = K.bn_apply(t3.view(-1, C3), s3, h3, res=td.view(-1, C3), rscale=sd, rshift=hd, relu=True,
                                  want_mask=training)
         else:
@@ -397,7 +413,8 @@ class BottleneckFn(torch.autograd.Function):
                                                 (tuple(t1.shape), k1, tuple(x.shape), 1, 0)])
         # backward needs only the ReLU mask of `out`: 1 bit per element (mask mode 3), not the bf16 tensor
         ctx.save_for_backward(x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
-                              g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2)
+                              g1, g2, g3, params[10] if down else None, k1, k2, k3, shadows[3] if down else None, a2,
+                              xd if (down and xd is not x) else None)
         ctx.conf = (stride, training, down)
         ctx.params = params
         ctx.fp8 = fp8
@@ -406,7 +423,7 @@ class BottleneckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (x, t1, a1, t2, t3, td, mb, m1, i1, s1, h1, m2, i2, s2, h2, m3, i3, md, idd,
-         g1, g2, g3, gd, k1, k2, k3, kd, a2) = ctx.saved_tensors
+         g1, g2, g3, gd, k1, k2, k3, kd, a2, xs) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused Bottleneck backward requires training-mode BatchNorm")
@@ -476,7 +493,8 @@ class BottleneckFn(torch.autograd.Function):
             dy1 = dt1
         if down:
             dtd = dtd.view(td.shape)
-            dwd = sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
+            # (with the subsampled input the shortcut's weight gradient is a plain GEMM: dtd^T . xs)
+            dwd = sink.wgrad(P[9], xs, dtd, 1, 1, 1, 0) if xs is not None else sink.wgrad(P[9], x, dtd, 1, 1, stride, 0)
             dx = K.conv_dgrad(dy1, k1, x.shape, 1, 0, pre=pre1, wprep=w1p)
             # shortcut branch accumulated in place: a stride-2 1x1 dgrad only touches the pixels its taps
             # reach, so no zero-filled full-size buffer and no extra full read/write pass
@@ -505,9 +523,10 @@ class BasicBlockFn(torch.autograd.Function):
         a1 = K.bn_apply(t1.view(-1, C1), s1, h1, relu=True).view(t1.shape)    # 3x3 consumer: materialise
         t2, m2, i2, s2, h2 = _conv_bn(a1, k2, 1, 1, None, training, (g2, b2), bufs[2:4], mom, eps)
         C2 = t2.shape[-1]
+        xd = x
         if down:
             wd, gd, bd = params[6:]
-            td, md, idd, sd, hd = _conv_bn(x, shadows[2], stride, 0, None, training, (gd, bd), bufs[4:6], mom, eps)
+            (td, md, idd, sd, hd), xd = _shortcut_fwd(x, shadows[2], stride, training, (gd, bd), bufs[4:6], mom, eps)
             out, mb = K.bn_apply(t2.view(-1, C2), s2, h2, res=td.view(-1, C2), rscale=sd, rshift=hd, relu=True,
                                  want_mask=training)
         else:
@@ -515,14 +534,15 @@ class BasicBlockFn(torch.autograd.Function):
             out, mb = K.bn_apply(t2.view(-1, C2), s2, h2, res=x.view(-1, C2), relu=True, want_mask=training)
         out = out.view(t2.shape)
         ctx.save_for_backward(x, t1, a1, t2, td, mb, m1, i1, s1, h1, m2, i2, md, idd, g1, g2,
-                              params[7] if down else None, k1, k2, shadows[2] if down else None)
+                              params[7] if down else None, k1, k2, shadows[2] if down else None,
+                              xd if xd is not x else None)
         ctx.conf = (stride, training, down)
         ctx.params = params
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        (x, t1, a1, t2, td, mb, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd) = ctx.saved_tensors
+        (x, t1, a1, t2, td, mb, m1, i1, s1, h1, m2, i2, md, idd, g1, g2, gd, k1, k2, kd, xs) = ctx.saved_tensors
         stride, training, down = ctx.conf
         if not training:
             raise RuntimeError("fused BasicBlock backward requires training-mode BatchNorm")
@@ -556,7 +576,7 @@ class BasicBlockFn(torch.autograd.Function):
             pre1, dy1 = None, dt1
         if down:
             dtd = dtd.view(td.shape)
-            dwd = sink.wgrad(P[6], x, dtd, 1, 1, stride, 0)
+            dwd = sink.wgrad(P[6], xs, dtd, 1, 1, 1, 0) if xs is not None else sink.wgrad(P[6], x, dtd, 1, 1, stride, 0)
             dx = K.conv_dgrad(dy1, k1, x.shape, stride, 1, pre=pre1)
             dx = K.conv_dgrad(dtd, kd, x.shape, stride, 0, res=dx, out=dx)      # shortcut, in place
         else:

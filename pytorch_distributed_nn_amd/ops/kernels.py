@@ -96,6 +96,16 @@ def gemm_nt_splitk(x, w, splits=None, ws=None):
     return out
 
 
+def subsample(x, st=2):
+    """x[:, ::st, ::st, :] of an NHWC bf16 tensor, contiguous (the input a 1x1 / stride-st conv reads)."""
+    _bf16_c(x, "subsample.x")
+    N, H, W, C = x.shape
+    _chk(C % 8 == 0, "subsample: C % 8 == 0")
+    y = torch.empty(N, (H - 1) // st + 1, (W - 1) // st + 1, C, device=x.device, dtype=BF16)
+    call("pdnn_subsample", ptr(x), ptr(y), N, H, W, C, int(st), stream())
+    return y
+
+
 def transpose_bf16(x, out=None):
     """out[C][R] = x[R][C] (bf16, 2-D, unit column stride)."""
     _chk(x.dtype == BF16 and x.dim() == 2 and x.stride(1) == 1, "transpose_bf16: 2-D bf16 with unit column stride")
@@ -225,6 +235,45 @@ def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
             and lib().pdnn_conv3x3_supported(N, H, W, Cin, Cout) == 1)
 
 
+def _s2_ok(N, H, W, C, K, R, S, st, pad, bit):
+    """3x3 / stride-2 / pad-1 conv of an H x W x C input with K outputs on the half-resolution halo kernels
+    (csrc/kernels/conv_s2.hip) for this direction (tuning s2_halo bit: 1 data gradient, 2 forward)."""
+    return (R == 3 and S == 3 and st == 2 and pad == 1 and (_tuning.get("s2_halo") & bit) != 0
+            and lib().pdnn_conv3x3s2_supported(N, H, W, C, K) == 1)
+
+
+def conv3x3s2_fold_ok(x_shape, Ko):
+    """Whether a 3x3 / stride-2 conv of this input takes its input's BN + ReLU as the forward kernel's operand
+    prologue (tuning s2_halo bit 4): its activation need not be materialised."""
+    N, H, W, C = x_shape
+    return (_tuning.get("s2_halo") & 4) != 0 and _s2_ok(N, H, W, C, Ko, 3, 3, 2, 1, 2)
+
+
+def conv3x3s2(x, w, dgrad=False, want_stats=False, bn=None, pre=None, pro=None, out_hw=None):
+    """Stride-2 3x3 conv on the halo kernels.  Forward: y (N, H/2, W/2, K) = conv(x (N, H, W, C), w [K][3][3][C]),
+    BN statistics bins (want_stats) and the forward prologue pro = (scale, shift).  Data gradient (dgrad=True):
+    x = dy (N, Ho, Wo, K), w = conv3x3_flip(W) [C][3][3][K] -> dx (N, 2Ho, 2Wo, C) with the fused BN backward
+    (bn, as conv_dgrad) and the BN-backward operand prologue (pre, _pre_args)."""
+    Nimg, H, W, C = x.shape
+    N = w.shape[0]
+    if dgrad:
+        Ho, Wo = H * 2, W * 2
+    else:
+        Ho, Wo = H // 2, W // 2
+    y = torch.empty(Nimg, Ho, Wo, N, device=x.device, dtype=BF16)
+    slab = None
+    t = mean = inv = msc = msh = None
+    if want_stats or bn is not None:
+        slab = stat_bins(N, x.device)
+    if bn is not None:
+        t, mean, inv, msc, msh = bn
+        _chk(tuple(t.shape) == (Nimg, Ho, Wo, N), "conv3x3s2: bn_x shape")
+    psc, psh = pro if pro is not None else (None, None)
+    call("pdnn_conv3x3s2", ptr(x), ptr(w), ptr(y), Nimg, Ho if dgrad else H, Wo if dgrad else W, C, N, int(dgrad),
+         ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x), ptr(psc), ptr(psh), stream())
+    return y, slab
+
+
 # 1x1 / stride-1 convs with K in {64, 128, 256} run on the A-stationary kernel (csrc/kernels/conv3x3.hip), K >= 512
 # on the long-reduction one (conv1x1_wide.hip): set_panel_mode(0) sends them back to the implicit-GEMM engines
 _P1 = {"mode": 1}
@@ -327,6 +376,8 @@ def conv_fwd(x, w, st, pad, pro=None, want_stats=False):
     Ho, Wo = conv_out_hw(H, W, R, S, st, pad)
     if _conv3x3_ok(N, H, W, C, K, R, S, st, pad):
         return conv3x3(x, w, want_stats=want_stats, pro=pro)
+    if _s2_ok(N, H, W, C, K, R, S, st, pad, 2):
+        return conv3x3s2(x, w, want_stats=want_stats, pro=pro)
     if (pro is None or C <= 256) and _panel_ok(N * H * W, C, K, R, S, st, pad, fwd=True):
         y, slab = conv1x1_panel(x.view(-1, C), w.view(K, C), want_stats=want_stats, pro=pro)
         return y.view(N, H, W, K), slab
@@ -366,6 +417,7 @@ def dgrad_pre_ok(dy_shape, w_shape, st, pad):
     N, Ho, Wo, K = dy_shape
     Kw, R, S, C = w_shape
     return (_conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad)
+            or _s2_ok(N, 2 * Ho, 2 * Wo, C, K, R, S, st, pad, 1)
             or (_panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
 
 
@@ -377,7 +429,7 @@ def dgrad_weight(dy_shape, w, x_shape, st, pad):
     N, Ho, Wo, K = dy_shape
     _, H, W, C = x_shape
     Kw, R, S, C2 = w.shape
-    if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad):
+    if _conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad) or _s2_ok(N, H, W, C, K, R, S, st, pad, 1):
         return conv3x3_flip(w)
     if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad):
         return transpose_bf16(w.view(K, C))
@@ -425,6 +477,10 @@ def conv_dgrad(dy, w, x_shape, st, pad, res=None, bn=None, out=None, res_mask=No
         # dx = conv3x3(dy, W') with the tap-flipped transposed weight (stride 1: dy and dx share H x W)
         y, slab = conv3x3(dy, wprep if wprep is not None else conv3x3_flip(w), res=res, bn=bn, out=out,
                           res_mask=res_mask, pre=pre)
+        return (y, slab) if bn is not None else y
+    if _s2_ok(N, H, W, C, K, R, S, st, pad, 1) and res is None and out is None and (H, W) == (2 * Ho, 2 * Wo):
+        # stride 2: one launch, every output parity class a 1 / 2 / 2 / 4-tap unit-offset conv of dy (conv_s2.hip)
+        y, slab = conv3x3s2(dy, wprep if wprep is not None else conv3x3_flip(w), dgrad=True, bn=bn, pre=pre)
         return (y, slab) if bn is not None else y
     if _panel_dgrad_k(K) and _panel_ok(N * H * W, K, C, R, S, st, pad) and (out is None or res is not None):
         # dx[P][C] = dy[P][K] . W[K][C]: the panel kernel with the transposed weight W^T [C][K]
@@ -985,9 +1041,16 @@ def embedding_fwd(idx, wte, wpe, T):
     return out
 
 
-def embedding_bwd(idx, g, dwte, dwpe, T):
+def embedding_bwd(idx, g, dwte, dwpe, T, scale=1.0):
+    """dwte[idx[r]] += scale * g[r], dwpe[r % T] += g[r] (fp32 atomics); either table may be None."""
     R, D = g.shape
-    _chk(dwte.dtype == F32 and dwte.shape[1] == D and (dwpe is None or dwpe.shape[1] == D), "embedding_bwd")
+    _chk((dwte is None or (dwte.dtype == F32 and dwte.shape[1] == D and dwte.is_contiguous()))
+         and (dwpe is None or (dwpe.dtype == F32 and dwpe.shape[1] == D and dwpe.is_contiguous()))
+         and idx.dtype == torch.int64 and idx.numel() == R, "embedding_bwd")
+    if dwte is None or scale != 1.0:
+        call("pdnn_embedding_bwd_scaled", ptr(idx), ptr(g.contiguous()), ptr(dwte), ptr(dwpe), R, T, D, float(scale),
+             stream())
+        return
     call("pdnn_embedding_bwd", ptr(idx), ptr(g.contiguous()), ptr(dwte), ptr(dwpe), R, T, D, stream())
 
 

@@ -134,17 +134,34 @@ def layer_norm(x, weight, bias, eps=1e-5):
 # ------------------------------------------------------------------------------------------------
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe, head_direct=False):
+    def forward(ctx, idx, T, wte_k, wpe_k, wte, wpe, head_direct=False, tail=None):
         ctx.save_for_backward(idx)
-        ctx.conf = (T, wte.shape, wpe.shape)
+        ctx.conf = (T, wte_k.shape, wpe.shape)
         ctx.wpe, ctx.wte = wpe, wte
         ctx.head_direct = head_direct       # the tied LM head accumulates its wte gradient in the arena too
+        ctx.tail = tail                     # (ddp, wte): split tied embedding, wte is NOT an input (wte=None)
         return K.embedding_fwd(idx, wte_k, wpe_k, T)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         T, s_te, s_pe = ctx.conf
+        if ctx.tail is not None:
+            # split tied embedding (parallel/ddp.py reduce_sparse_rows): the LM head's dense gradient was announced
+            # (and its bucket all-reduced) at the start of the backward; these B*T rows are gathered from every rank
+            # and added on top after it
+            ddp, wte = ctx.tail
+            ctx.tail = None
+            tpe = direct_grad(ctx.wpe)
+            dwpe = tpe if tpe is not None else torch.zeros(s_pe, device=g.device, dtype=F32)
+            K.embedding_bwd(idx, g, None, dwpe, T)
+            if tpe is not None:
+                grad_ready(ctx.wpe)
+                dwpe = None
+            gw = wte.grad
+            ddp.reduce_sparse_rows(wte, idx, g, lambda i, r, sc: K.embedding_bwd(i, r, gw, None, T, scale=sc))
+            ctx.wpe = ctx.wte = None
+            return None, None, None, None, None, dwpe, None, None
         # wte is tied with the LM head, whose backward ran first and (with a flat arena) already accumulated
         # its part in place: the embedding adds its rows on top (atomics) and announces the parameter, so no
         # zero-filled temporaries and no autograd sum of the two gradients
@@ -160,7 +177,7 @@ class EmbeddingFn(torch.autograd.Function):
             grad_ready(ctx.wte)
             dwte = None
         ctx.wpe = ctx.wte = None
-        return None, None, None, None, dwte, dwpe, None
+        return None, None, None, None, dwte, dwpe, None, None
 
 
 # ------------------------------------------------------------------------------------------------
@@ -297,8 +314,9 @@ class LMHeadLossFn(torch.autograd.Function):
     """loss = mean CE(LN_f(x) . Wte^T, targets); logits bf16 [B*T][V] live only inside this op."""
 
     @staticmethod
-    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte, head_direct=False):
+    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte, head_direct=False, split=False):
         ctx.head_direct = head_direct
+        ctx.split = split                   # split tied embedding: the head announces wte itself
         xf, m, r = K.layernorm_fwd(x, lnw, lnb, eps)
         logits = BL.linear_fwd(xf, wte_k)
         _, lse, acc = K.xent_fwd(logits, targets)
@@ -320,6 +338,8 @@ class LMHeadLossFn(torch.autograd.Function):
         if tte is not None:     # tied weight: the embedding backward adds its part and announces it
             BL.wgrad_acc(dlogits, xf, tte)
             dwte = None
+            if ctx.split:       # ... unless its rows are reduced separately: the dense part is complete now
+                grad_ready(ctx.wte)
         else:
             dwte = _wgrad(dlogits, xf, wte_k.shape)     # summed with the embedding's by autograd
         sink = _Sink()
@@ -327,4 +347,4 @@ class LMHeadLossFn(torch.autograd.Function):
         ctx.params = None
         ctx.wte = None
         sink.done()
-        return dx, None, None, None, dlnw, dlnb, dwte, None
+        return dx, None, None, None, dlnw, dlnb, dwte, None, None

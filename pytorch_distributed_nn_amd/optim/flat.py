@@ -130,14 +130,23 @@ class FlatParams:
         return start, end
 
 
-def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float):
+def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float, early=()):
     """Gradient buckets over the flat arena in REVERSE parameter order (the order backward produces
-    them), a small first bucket so communication starts early.  -> ([(start, end, n_params)], {id(p): b})."""
+    them), a small first bucket so communication starts early.  -> ([(start, end, n_params)], {id(p): b}).
+
+    ``early``: parameters whose gradient is complete at the START of the backward although they come first in
+    arena order (GPT-2's tied token embedding: its LM-head part, once the embedding rows are reduced separately,
+    DistributedDataParallel.reduce_sparse_rows).  They form bucket 0, launched as soon as they are ready; they must
+    be the leading parameters of the arena (their range and the rest's stay contiguous), else they are ignored."""
     n = len(fp.params)
     ends = fp.offsets[1:] + [fp.numel]
-    groups, cur, cur_bytes = [], [], 0
+    pos = {id(q): i for i, q in enumerate(fp.params)}
+    lead = sorted(pos[id(q)] for q in early if id(q) in pos)
+    if lead != list(range(len(lead))):
+        lead = []
+    groups, cur, cur_bytes = ([lead] if lead else []), [], 0
     cap = first_mb * 2 ** 20
-    for i in reversed(range(n)):
+    for i in reversed(range(len(lead), n)):
         nb = (ends[i] - fp.offsets[i]) * 4
         if cur and cur_bytes + nb > cap:          # close the bucket before it would overflow
             groups.append(cur)

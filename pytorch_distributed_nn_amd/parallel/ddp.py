@@ -222,7 +222,8 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_cap_mb: float | None = None, broadcast_buffers: bool = True, comm_dtype=None,
                  average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
                  num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True,
-                 buffer_sync_interval: int = 1, comm_timing: bool = False, native_comm: bool | None = None):
+                 buffer_sync_interval: int = 1, comm_timing: bool = False, native_comm: bool | None = None,
+                 split_tied: bool | None = None):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -274,7 +275,26 @@ class DistributedDataParallel(nn.Module):
         if native_comm and self._comm and self.nccl and self.flat.grad.is_cuda:
             from .rccl_native import NativeComm
             self._native = NativeComm(self.pg, self.flat.grad.device)
-        self._build_buckets(bucket_cap_mb, bucket_cap_mb if first_bucket_cap_mb is None else first_bucket_cap_mb)
+        # split tied embedding (GPT-2's wte = LM head): the head's dense gradient is complete at the START of the
+        # backward, the embedding's rows only at its end.  Reduced as one parameter, its 147 MiB bucket could only
+        # launch after the embedding backward -- fully exposed at N > 1.  Split: the dense
+        # part is bucket 0, all-reduced right after the head's weight gradient; the embedding's B*T rows are
+        # gathered (ids + bf16 rows) and added after it (reduce_sparse_rows).  Not with modes that post-process
+        # whole buckets (straggler counts, k-of-n, bf16 wire).
+        self._tail = None
+        early = []
+        if split_tied is None:
+            split_tied = os.environ.get("PDNN_DDP_SPLIT_TIED", "1") == "1"
+        tied = module.ddp_tied_rows() if split_tied and hasattr(module, "ddp_tied_rows") else None
+        if (tied is not None and self._comm and not straggler_mode and num_aggregate == 0 and deadline_ms == 0
+                and comm_dtype is None):
+            early = [tied]
+        self._build_buckets(bucket_cap_mb, bucket_cap_mb if first_bucket_cap_mb is None else first_bucket_cap_mb,
+                            early)
+        if early and self._pbucket.get(id(early[0])) == 0 and self.buckets[0][2] == 1:
+            import weakref
+            self._tail = early[0]
+            module._pdnn_row_tail = weakref.ref(self)
         self._hooks = [register_grad_ready_hook(p, self._on_grad) for p in self.flat.params]
         self.step = 0
         self.last_counts = None          # per-bucket contributor counts of the last step (k-of-n)
@@ -357,8 +377,8 @@ class DistributedDataParallel(nn.Module):
                     o += n
 
     # ------------------------------------------------------------------ buckets
-    def _build_buckets(self, cap_mb, first_mb):
-        self.buckets, self._pbucket = reverse_buckets(self.flat, cap_mb, first_mb)
+    def _build_buckets(self, cap_mb, first_mb, early=()):
+        self.buckets, self._pbucket = reverse_buckets(self.flat, cap_mb, first_mb, early)
         if self.comm_dtype is not None:
             self._wire = [torch.empty(e - s, dtype=self.comm_dtype, device=self.flat.grad.device) for s, e, _ in self.buckets]
 
@@ -400,6 +420,8 @@ class DistributedDataParallel(nn.Module):
         self._ready = [0] * len(self.buckets)
         self._next = 0
         self._works = []
+        self._work_of = {}
+        self._tail_pending = None
         self._armed = False
         self._aborted = False
         self._contrib = [0.0] * len(self.buckets)
@@ -506,12 +528,14 @@ class DistributedDataParallel(nn.Module):
             t.record_stream(cs)
             self._ev_start[b], self._ev_done[b] = ev0, ev1
             self._works.append((b, work))
+            self._work_of[b] = work
             return
         if self._native is not None:
             work = self._native.all_reduce(t, avg=op == dist.ReduceOp.AVG)
         else:
             work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
         self._works.append((b, work))
+        self._work_of[b] = work
         if self._ovl_active():
             # the bucket's optimizer update on the optimizer stream, as soon as its all-reduce is done, beside
             # the backward of the earlier layers (whose weights it does not touch)
@@ -527,7 +551,14 @@ class DistributedDataParallel(nn.Module):
     def _ovl_active(self):
         return (self._ovl_opt is not None and self.comm_dtype is None and not self.straggler_mode
                 and self.kofn is None and not self.comm_timing and not self._aborted and self.flat.grad.is_cuda
-                and not self._ovl_opt._graph)
+                and not self._ovl_opt._graph and self._ovl_reduced_is_final())
+
+    def _ovl_reduced_is_final(self):
+        """Whether a bucket is final the moment its collective completes: RCCL reduces with native AVG, and a
+        SUM is final when no average is wanted or there is one rank.  Over gloo (SUM, then ``grad *= 1/world``
+        in _finish after every wait) a per-bucket update would consume world x the averaged gradient,
+        so the overlap stays off there and opt.step() runs after the backward as usual."""
+        return self.nccl or not self.average or self.world == 1
 
     def overlap_optimizer(self, opt):
         """Apply ``opt``'s update bucket by bucket during the backward: each bucket's range of the flat arena is
@@ -535,9 +566,14 @@ class DistributedDataParallel(nn.Module):
         the earlier layers; ``opt.step()`` after the backward then has nothing left to do (it still works as usual
         for a step without buckets, e.g. under ``no_sync``).  ``opt`` must be a fused flat optimizer whose single
         param group spans exactly this wrapper's buckets.  Returns ``opt``; None (no overlap) when it does not
-        qualify."""
+        qualify.
+
+        The updates run DURING the backward: the hyper-parameters (lr, momentum, weight decay) are read when the
+        step's first bucket launches, and nothing that runs between ``backward()`` and ``opt.step()`` (gradient
+        clipping, manual gradient edits, lr changes) reaches them -- Trainer refuses ``grad_clip`` with it."""
         ok = opt._overlap_ok() if hasattr(opt, "_overlap_ok") else None
-        if ok is None or ok[0] is not self.flat:
+        if ok is None or ok[0] is not self.flat or self._tail is not None:
+            # (a split tied embedding gets its sparse rows after its bucket's collective: not final there)
             return None
         s, e = ok[1]
         ranges = sorted((bs, be) for bs, be, _ in self.buckets)
@@ -601,6 +637,10 @@ class DistributedDataParallel(nn.Module):
             self.grad_scale_dev = None
             for opt in getattr(self, "_optimizers", []):
                 opt.grad_scale_dev = None
+        if self._tail_pending is not None:        # split tied embedding: its gathered rows on top of the average
+            idx, rows, apply = self._tail_pending
+            self._tail_pending = None
+            apply(idx, rows, 1.0 / self.world if self.average else 1.0)
         if self.kofn is not None:
             self.kofn.cleanup(self.step)
         self.last_contrib = list(self._contrib)
@@ -608,6 +648,31 @@ class DistributedDataParallel(nn.Module):
         self.aborted_steps += int(self._aborted)
         self.step_comm_log.append(time.perf_counter() - self._t0)
         self._reset()
+
+    # ------------------------------------------------------------------ split tied embedding
+    def reduce_sparse_rows(self, p, idx, rows, apply):
+        """The embedding part of a split tied parameter (``self._tail``, see __init__): ``rows[m]`` is this rank's
+        gradient for row ``idx[m]`` of ``p`` (every rank passes the same number of rows).  The rows and ids of every
+        rank are all-gathered (bf16 rows stay bf16 on the wire: ~12.6 MB per rank for GPT-2 at B*T = 8192) and
+        ``apply(idx_all, rows_all, scale)`` adds them into p's gradient at the end of the backward (_finish), after
+        every bucket's collective has completed and the arena holds its final average (or the bf16 wire copy):
+        scale = 1/world when averaging.  Outside a synchronised step (no_sync) the local rows are added as they
+        are, at once."""
+        idx = idx.reshape(-1).contiguous()
+        rows = rows.reshape(idx.numel(), -1).contiguous()
+        if not (self._sync and self._comm) or self._aborted or p is not self._tail:
+            apply(idx, rows, 1.0)
+            return
+        if self._work_of.get(self._pbucket[id(p)]) is None:
+            raise RuntimeError("reduce_sparse_rows: the dense part of the split tied parameter was not announced "
+                               "(its grad-ready hook must fire before the embedding backward)")
+        if self.world > 1:
+            ia = torch.empty(self.world * idx.numel(), dtype=idx.dtype, device=idx.device)
+            ra = torch.empty((self.world * rows.shape[0], rows.shape[1]), dtype=rows.dtype, device=rows.device)
+            dist.all_gather_into_tensor(ia, idx, group=self.pg)
+            dist.all_gather_into_tensor(ra, rows, group=self.pg)
+            idx, rows = ia, ra
+        self._tail_pending = (idx, rows, apply)
 
     # ------------------------------------------------------------------ public API
     def backward(self, loss):
@@ -624,6 +689,9 @@ class DistributedDataParallel(nn.Module):
     def close(self):
         if self.kofn is not None:
             self.kofn.stop()
+        if self._native is not None:
+            self._native.close()
+            self._native = None
 
     def _buffer_sync_due(self):
         return (self.broadcast_buffers and self._comm and self.module.training

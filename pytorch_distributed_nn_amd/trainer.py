@@ -122,6 +122,10 @@ class Trainer:
                 loss.backward()
         m2 = self._mark()
         if self.grad_clip:
+            if getattr(self.model, "_ovl_opt", None) is not None:
+                # the optimizer already ran per bucket inside the backward (DistributedDataParallel.
+                # overlap_optimizer): clipping now would be silently skipped
+                raise ValueError("grad_clip cannot be combined with DistributedDataParallel.overlap_optimizer")
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip)
         with self._span("optimizer"):
             self.opt.step()

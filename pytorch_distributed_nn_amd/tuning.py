@@ -24,6 +24,12 @@ colsum_atomic      1        accumulating bias-gradient column sums in one launch
                             deterministic partial rows + level-2 launch; GPT-2 542.3k vs 538.0k tok/s, r5_10)
 bias_in_wgrad      1        GPT-2 linear bias gradients as fused row sums inside the weight-gradient GEMM (0: a
                             column-sum pass over the output gradient)
+ds_sub             1        stride-2 1x1 shortcut convs read a contiguous copy of their input's even pixels (one
+                            subsample pass): the forward then runs as a stride-1 1x1 conv, the weight gradient as a
+                            plain GEMM on the ping-pong engine (0: the implicit-GEMM engine's strided gathers)
+s2_halo            3        3x3 / stride-2 convs on the half-resolution halo kernels (csrc/kernels/conv_s2.hip), a bit
+                            mask: 1 data gradient, 2 forward, 4 forward reads t1 through the BN1 + ReLU prologue (a1
+                            not materialised; the weight gradient then takes the same prologue); 0 = implicit GEMM
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there
@@ -33,7 +39,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1}
 
 _VALUES = dict(DEFAULTS)
 

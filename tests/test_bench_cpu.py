@@ -42,6 +42,22 @@ def test_bench_world2_prints_one_line_with_comm_block():
     assert abs(rec["value"] - rec["config"]["global_batch"] * 1e3 / rec["ms_per_step"]) < 0.01 * rec["value"]
     assert rec["comm"]["world"] == 2 and len(rec["comm"]["bucket_mb"]) >= 1
     assert rec["n1_point"] == "DDP path"
+    # at N > 1 the comm block carries the all-reduce bus-bandwidth probe (fp32 + bf16 wire)
+    bw = rec["comm"]["allreduce_busbw"]
+    assert {b["dtype"] for b in bw} == {"float32", "bfloat16"} and all(b["busbw_GBps"] > 0 for b in bw)
+    assert rec["extra_configs"] is None          # the config-4/5 child runs belong to the 1-GPU command only
+
+
+def test_bench_world2_gpt2_split_tied_embedding():
+    """GPT-2 at N > 1: 32 MB bucket cap (128 MB only where the all-reduce is a no-op), the tied wte's LM-head part
+    is bucket 0 and its embedding rows are gathered separately (comm.split_tied_embedding)."""
+    r = _torchrun(2, ["--model", "gpt2_tiny", "--batch", "2", "--seq-len", "32", "--steps", "2", "--warmup", "1"],
+                  {}, 300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["bucket_mb"] == 32.0
+    assert rec["comm"]["split_tied_embedding"] is True
+    assert abs(rec["comm"]["bucket_mb"][0] - 512 * 128 * 4 / 2 ** 20) < 1e-6      # bucket 0 = the tied wte alone
 
 
 def test_bench_world2_hang_prints_diagnostics_and_exits():

@@ -401,3 +401,22 @@ def test_bn_buffer_broadcast_issued_after_backward_keeps_every_forward_semantics
     for same, pre, moved in out:
         assert all(same) and moved
         assert pre == [False, True, True, True]
+
+
+def _ovl_predicate(rank, world):
+    from pytorch_distributed_nn_amd.models import build_model
+    from pytorch_distributed_nn_amd.parallel.ddp import DistributedDataParallel
+    m = build_model("mlp2", 10)
+    avg = DistributedDataParallel(m, bucket_cap_mb=0.5)
+    # gloo reduces with SUM and divides by the world size only after every wait: a bucket is not final when its
+    # collective completes, so per-bucket optimizer updates (overlap_optimizer) must stay off
+    assert not avg.nccl and avg.world == 2
+    assert not avg._ovl_reduced_is_final()
+    m2 = build_model("mlp2", 10)
+    summed = DistributedDataParallel(m2, bucket_cap_mb=0.5, average=False)
+    assert summed._ovl_reduced_is_final()
+    return True
+
+
+def test_overlap_optimizer_never_consumes_unaveraged_gloo_buckets():
+    assert all(run_world(_ovl_predicate, 2))

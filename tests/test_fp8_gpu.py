@@ -315,3 +315,19 @@ def test_conv3x3_fp8_forward_prologue(K):
     d0 = K.conv3x3_wgrad_fp8(a, dy, act0, ad)
     d1 = K.conv3x3_wgrad_fp8(t, dy, act0, ad, pro=(sc, sh))
     assert torch.equal(d0, d1)
+
+
+def test_cli_dtype_fp8_resnet152_trains(tmp_path):
+    """SURVEY §5.6 / VERDICT r5 #6: ``cli.py --dtype fp8 --network ResNet152 --synthetic`` trains on the fp8 path (the
+    Bottlenecks' 3x3 convs on the fp8 halo kernels) -- finite, decreasing loss over a few steps at a small batch."""
+    import json
+    from pytorch_distributed_nn_amd import cli
+    m = tmp_path / "metrics.jsonl"
+    hist = cli.main(["--network", "ResNet152", "--dataset", "ImageNet", "--synthetic", "--dtype", "fp8",
+                     "--batch-size", "16", "--max-steps", "6", "--log-interval", "1", "--lr", "0.05",
+                     "--momentum", "0.9", "--metrics", str(m), "--mode", "single", "--test-batch-size", "16"])
+    recs = [json.loads(ln) for ln in open(m) if ln.strip()]
+    losses = [r["loss"] for r in recs if r.get("loss") is not None]
+    assert len(losses) >= 5 and all(l == l and l < 50 for l in losses), losses
+    assert losses[-1] < 1.5 * losses[0]               # no divergence in the first steps from random init
+    assert hist is not None
