@@ -431,6 +431,183 @@ __global__ void __launch_bounds__(W3_NT, 1) conv3x3_wgrad8_kernel(W3Args a, W8Sc
             }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Stride-2 weight gradient (the 3x3 / stride-2 / pad-1 conv2 of a ResNet stage-transition Bottleneck; reference:
+// pytorch_code/model_ops/resnet.py:39-56):
+//   dW[ko][r][s][c] = sum over half-resolution pixels p = (n, i, j) of dy[p][ko] * x[n][2i + r - 1][2j + s - 1][c].
+// Tap (r, s) reads the input's parity plane (a, b) = (r != 1, s != 1) at half-resolution offset (dr, ds), dr = -1 for
+// r = 0 and 0 for r = 1, 2 (likewise ds).  Every plane is a half-resolution image, so the stride-1 kernel's padded halo
+// layout holds it unchanged and the plane's taps are immediate offsets (dr + 1, ds + 1) of one address.  A tile's dy is
+// staged once and its four plane halos follow one after the other (stage = (tile, plane), 1 / 2 / 2 / 4 taps), each
+// gathered from NHWC x with stride-2 pixel addresses into registers under the previous stage's MFMAs.  FP: the BN + ReLU
+// of the layer below applied while staging (a1 never materialised).  a.H / a.W: the half-resolution extent.
+template <int WT, bool FP>
+__global__ void __launch_bounds__(W3_NT, 1) conv3x3s2_wgrad_kernel(W3Args a) {
+    constexpr int PITCH = WT + 2;
+    constexpr int XW = 2 * WT;                // input width
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const dimg = reinterpret_cast<bf16_t*>(smem);
+    char* const halo = smem + W3_BM * 64 * 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pair = blockIdx.x / a.G, part = blockIdx.x - pair * a.G;
+    const int ko0 = (pair / a.cch) * 64, c0 = (pair % a.cch) * 64;
+    const int t0 = (int)((long)part * a.tiles / a.G), t1 = (int)((long)(part + 1) * a.tiles / a.G);
+    const int hbytes = a.hrows * PITCH * W3_PB;
+    [[maybe_unused]] W3Pro pro;
+    if constexpr (FP) w3_pro_load(a, c0 + (tid & 7) * 8, pro);
+
+    const int fn = wave & 3, fmb = (wave >> 2) * 2;
+    f32x4_t acc[2][9];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[f][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int DCH = W3_BM * 8 / W3_NT;
+    constexpr int HCH = W3_HMAX * 8 / W3_NT;
+    u16x8_t rd[DCH], rh[HCH];
+    uint32_t okm = 0;
+    int s_gstart = 0, s_istart = 0;
+
+    auto geo = [&](int t, int& p0, int& plast, int& gstart, int& istart) {
+        p0 = t * W3_BM;
+        plast = min(a.P, p0 + W3_BM) - 1;
+        gstart = (int)fdiv((uint32_t)p0, a.dW) - 1;
+        istart = gstart < 0 ? -1 : (int)fdiv((uint32_t)gstart, a.dH);
+    };
+    // registers <- (tile t's dy if with_dy) + plane (pa, pb) of its input rows gstart .. gr1 (half resolution)
+    auto load_regs = [&](int t, int pa, int pb, bool with_dy) {
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        s_gstart = gstart;
+        s_istart = istart;
+        if (with_dy) {
+#pragma unroll
+            for (int j = 0; j < DCH; ++j) {
+                const int i = tid + j * W3_NT, row = i >> 3;
+                const int p = p0 + row;
+                const bool ok = p < a.P;
+                rd[j] = *reinterpret_cast<const u16x8_t*>(a.dy + (long)(ok ? p : plast) * a.Ko + ko0 + (i & 7) * 8);
+                okm = ok ? (okm | (1u << j)) : (okm & ~(1u << j));
+            }
+        }
+        const int gr1 = (int)fdiv((uint32_t)plast, a.dW);
+        const int nch = (gr1 + 1 - gstart) * WT * 8;        // rows gstart .. gr1 (the taps reach one row up only)
+        const long gp0 = (long)gstart * WT;
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            const long gp = gp0 + (i >> 3);
+            const bool ok = i < nch && gp >= 0 && gp < a.P;
+            const int gc = (int)(gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp));
+            const int gr = (int)fdiv((uint32_t)gc, a.dW);
+            const long xp = (long)(2 * gr + pa) * XW + 2 * (gc - gr * WT) + pb;
+            rh[j] = *reinterpret_cast<const u16x8_t*>(a.x + xp * a.C + c0 + (i & 7) * 8);
+            okm = ok ? (okm | (16u << j)) : (okm & ~(16u << j));
+        }
+    };
+    auto zero_halo = [&]() {
+        for (int o = tid * 16; o < hbytes; o += W3_NT * 16) *reinterpret_cast<u16x8_t*>(halo + o) = c3_zero8();
+    };
+    auto store_lds = [&](bool with_dy) {
+        if (with_dy) {
+#pragma unroll
+            for (int j = 0; j < DCH; ++j) {
+                const int i = tid + j * W3_NT;
+                *reinterpret_cast<u16x8_t*>(dimg + mimg_off<64>(i >> 3, i & 7)) = mask16(rd[j], (okm >> j) & 1);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < HCH; ++j) {
+            const int i = tid + j * W3_NT;
+            if (((okm >> (4 + j)) & 1) != 0) {
+                const int gp = s_gstart * WT + (i >> 3);
+                const int gr = (int)fdiv((uint32_t)gp, a.dW);
+                const int xx = gp - gr * WT;
+                const int img = (int)fdiv((uint32_t)gr, a.dH);
+                const int hrow = gr - s_gstart + 2 * (img - s_istart) + 1;
+                u16x8_t hv = rh[j];
+                if constexpr (FP) hv = w3_pro(pro, hv);
+                *reinterpret_cast<u16x8_t*>(halo + (hrow * PITCH + xx + 1) * W3_PB + (i & 7) * 16) = hv;
+            }
+        }
+    };
+
+    const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+    const int cbyte = (fn * 16 + 4 * pq) * 2;
+    const int s0 = t0 * 4, s1 = t1 * 4;
+
+    if (s0 < s1) {
+        load_regs(t0, 0, 0, true);
+        zero_halo();
+    }
+    __syncthreads();
+    if (s0 < s1) store_lds(true);
+    __syncthreads();
+    for (int st = s0; st < s1; ++st) {
+        const int t = st >> 2, plane = st & 3;
+        const bool more = st + 1 < s1;
+        int p0, plast, gstart, istart;
+        geo(t, p0, plast, gstart, istart);
+        if (more) {
+            const int nx = (st + 1) & 3;
+            load_regs((st + 1) >> 2, nx >> 1, nx & 1, nx == 0);          // under this stage's MFMAs
+        }
+        // plane (pa, pb): taps r in {1} (pa = 0) or {0, 2}, s likewise; compile-time per plane (static accumulators)
+        static_for<0, 4>([&](auto PL) {
+            constexpr int PA = decltype(PL)::value >> 1, PB = decltype(PL)::value & 1;
+            if (plane != decltype(PL)::value) return;
+#pragma unroll 1
+            for (int ks = 0; ks < W3_BM / 32; ++ks) {
+                bf16x8_t af[2];
+#pragma unroll
+                for (int f = 0; f < 2; ++f) af[f] = frag_mnmajor<64>(dimg, (fmb + f) * 16, ks, lane);
+                int base[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int p = min(p0 + ks * 32 + 8 * g + q + 4 * h, plast);
+                    const int gr = (int)fdiv((uint32_t)p, a.dW);
+                    const int xx = p - gr * WT;
+                    const int img = (int)fdiv((uint32_t)gr, a.dH);
+                    const int hrow = gr - gstart + 2 * (img - istart) + 1;
+                    base[h] = ((hrow - 1) * PITCH + xx) * W3_PB + cbyte;
+                }
+                static_for<0, (1 + PA) * (1 + PB)>([&](auto K) {
+                    constexpr int k = decltype(K)::value;
+                    constexpr int kr = PB ? (k >> 1) : k, kc = PB ? (k & 1) : 0;
+                    constexpr int r = PA ? 2 * kr : 1, s = PB ? 2 * kc : 1;
+                    constexpr int off = ((r == 0 ? 0 : 1) * PITCH + (s == 0 ? 0 : 1)) * W3_PB;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[0] + off));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(halo + base[1] + off));
+                    typedef __attribute__((ext_vector_type(8))) short s16x8;
+                    const s16x8 xv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    const bf16x8_t xf = __builtin_bit_cast(bf16x8_t, xv);
+#pragma unroll
+                    for (int f = 0; f < 2; ++f)
+                        acc[f][3 * r + s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], xf, acc[f][3 * r + s], 0, 0, 0);
+                });
+            }
+        });
+        __syncthreads();                          // every wave is done reading this stage's images
+        if (more) {
+            zero_halo();
+            __syncthreads();
+            store_lds(((st + 1) & 3) == 0);
+            __syncthreads();
+        }
+    }
+    float* ws = a.ws + (long)blockIdx.x * W3_PS;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ko = (fmb + f) * 16 + 4 * g + j;
+                ws[(ko * 9 + tap) * 64 + fn * 16 + (lane & 15)] = acc[f][tap][j];
+            }
+}
+
 int w3_hrows(int H, int W);
 int w8_smem(int H, int W);
 
@@ -615,6 +792,60 @@ PDNN_API int pdnn_conv3x3_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, in
     if (W == 56) W3_W(56); else if (W == 28) W3_W(28); else if (W == 14) W3_W(14); else W3_W(7);
 #undef W3_W
 #undef W3_GO
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    const long outs = (long)Ko * 9 * (C / 4);
+#define W3_R(PG) hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel<PG>, dim3((unsigned)cdiv(outs, 256 / PG)), dim3(256), 0, st, \
+                                    (const float*)ws, dw, Ko, C, a.cch, a.G)
+    if (a.G >= 256) W3_R(32);
+    else if (a.G >= 128) W3_R(16);
+    else if (a.G >= 64) W3_R(8);
+    else if (a.G >= 32) W3_R(4);
+    else if (a.G >= 16) W3_R(2);
+    else W3_R(1);
+#undef W3_R
+    PDNN_LAUNCH_RET;
+}
+
+// Whether the stride-2 direct weight gradient takes this conv (input H x W even, half-resolution width 7 / 14 / 28,
+// channel multiples of 64, the plane halo within the stride-1 kernel's limits).
+PDNN_API int pdnn_conv3x3s2_wgrad_supported(int Nimg, int H, int W, int C, int Ko) {
+    if (H % 2 || W % 2) return 0;
+    const int Wo = W / 2;
+    if (Wo != 7 && Wo != 14 && Wo != 28) return 0;
+    return pdnn_conv3x3_wgrad_supported(Nimg, H / 2, Wo, C, Ko);
+}
+
+PDNN_API int pdnn_conv3x3s2_wgrad_ws(int Nimg, int H, int W, int C, int Ko) {
+    return pdnn_conv3x3_wgrad_ws(Nimg, H / 2, W / 2, C, Ko);
+}
+
+// dw [Ko][3][3][C] fp32 += weight gradient of y = conv3x3/s2/p1(x [Nimg][H][W][C]) given dy [Nimg][H/2][W/2][Ko];
+// pro_sc / pro_sh: x is the pre-activation of relu(x * sc + sh), applied as the planes are staged.
+PDNN_API int pdnn_conv3x3s2_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int Nimg, int H, int W, int C, int Ko,
+                                  float* ws, const float* pro_sc, const float* pro_sh, hipStream_t st) {
+    if (!pdnn_conv3x3s2_wgrad_supported(Nimg, H, W, C, Ko) || !ws || (!pro_sc != !pro_sh))
+        return (int)hipErrorInvalidValue;
+    const int Ho = H / 2, Wo = W / 2;
+    W3Args a{};
+    a.x = x; a.dy = dy; a.ws = ws;
+    a.H = Ho; a.W = Wo; a.C = C; a.Ko = Ko; a.P = Nimg * Ho * Wo;
+    a.dW = w3_fdiv(Wo); a.dH = w3_fdiv(Ho);
+    w3_plan(a.P, C, Ko, a.tiles, a.cch, a.G);
+    a.hrows = w3_hrows(Ho, Wo);
+    a.psc = pro_sc; a.psh = pro_sh;
+    const bool fp = pro_sc != nullptr;
+    const int sm = w3_smem(Ho, Wo);
+    const int grid = (Ko / 64) * a.cch * a.G;
+#define W3S_GO(WT, F)                                                                                            \
+    do {                                                                                                         \
+        w3_attr((const void*)conv3x3s2_wgrad_kernel<WT, F>);                                                     \
+        hipLaunchKernelGGL((conv3x3s2_wgrad_kernel<WT, F>), dim3(grid), dim3(W3_NT), sm, st, a);                 \
+    } while (0)
+#define W3S_W(WT) do { if (fp) W3S_GO(WT, true); else W3S_GO(WT, false); } while (0)
+    if (Wo == 28) W3S_W(28); else if (Wo == 14) W3S_W(14); else W3S_W(7);
+#undef W3S_W
+#undef W3S_GO
     const int e = (int)hipGetLastError();
     if (e) return e;
     const long outs = (long)Ko * 9 * (C / 4);

@@ -22,10 +22,12 @@ namespace pg {
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
     X(pp_dgrad_bn_k, 1024, "1x1 data gradients with the BN-backward epilogue on the ping-pong engine from this "   \
                            "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")                 \
-    X(comm_cus, 16, "CUs the persistent grids (ping-pong GEMMs, stem) leave free for RCCL's channel blocks while " \
-                    "a multi-rank process group is live (set_comm_world > 1; 0 = fill the chip). A persistent block " \
-                    "holds its CU for the whole kernel, so a bucket all-reduce issued beside it would wait for the " \
-                    "GEMM to drain; 16 = 2 per XCD (unmeasured at N > 1: no multi-GPU box this round)")
+    X(comm_cus, 0, "CUs the persistent grids (ping-pong GEMMs, stem) leave free for RCCL's channel blocks while " \
+                   "a multi-rank process group is live (set_comm_world > 1; 0 = fill the chip). A persistent block " \
+                   "holds its CU for the whole kernel, so a bucket all-reduce issued beside it waits for the GEMM to " \
+                   "drain.  Priced at a forced comm world of 8 on one GPU (gpurun_out/r6_01): 16 / 8 cost GPT-2 " \
+                   "4.9% / 4.7% (587.0k / 587.8k vs 617.0k tok/s: the ping-pong grids lose their whole-round fill), " \
+                   "ResNet-50 0.4%; the benefit is unmeasured without a multi-GPU box, so off")
 
 struct Tune {
 #define PDNN_TUNE_FIELD(n, d, doc) int n = d;

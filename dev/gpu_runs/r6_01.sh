@@ -8,10 +8,10 @@ cd $GRAFT_REPO_ROOT
 run() {
   local n=$1; shift
   local m=$1; shift
-  env "$@" timeout -k 10 300 python3 bench.py --model $m --no-plain-run --diag-steps 0 > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; return 1; }
+  env "$@" timeout -k 10 300 python3 bench.py --model $m --no-plain-run --no-extra-configs --diag-steps 0 > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; return 1; }
   python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['ms_per_step'])"
 }
-timeout -k 10 400 python3 bench.py > $O/base.json 2> $O/base.err || { tail -20 $O/base.err; exit 1; }
+timeout -k 10 400 python3 bench.py --no-extra-configs > $O/base.json 2> $O/base.err || { tail -20 $O/base.err; exit 1; }
 cat $O/base.json
 run pg_q8 resnet50 GPU_MAX_HW_QUEUES=8 &&
 run nat resnet50 PDNN_DDP_NATIVE_COMM=1 &&

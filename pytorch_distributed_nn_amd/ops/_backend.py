@@ -43,6 +43,9 @@ _SIGS = {
     "pdnn_conv3x3_supported": [I, I, I, I, I],
     "pdnn_conv3x3s2": [P, P, P, I, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P, P, P],
     "pdnn_conv3x3s2_supported": [I, I, I, I, I],
+    "pdnn_conv3x3s2_wgrad": [P, P, P, I, I, I, I, I, P, P, P, P],
+    "pdnn_conv3x3s2_wgrad_supported": [I, I, I, I, I],
+    "pdnn_conv3x3s2_wgrad_ws": [I, I, I, I, I],
     "pdnn_conv3x3_fp8_supported": [I, I, I, I, I],
     "pdnn_conv3x3_stats_rows": [I, I, I],
     "pdnn_conv3x3_flip": [P, P, I, I, P],

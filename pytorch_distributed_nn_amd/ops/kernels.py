@@ -237,16 +237,25 @@ def _conv3x3_ok(N, H, W, Cin, Cout, R, S, st, pad):
 
 def _s2_ok(N, H, W, C, K, R, S, st, pad, bit):
     """3x3 / stride-2 / pad-1 conv of an H x W x C input with K outputs on the half-resolution halo kernels
-    (csrc/kernels/conv_s2.hip) for this direction (tuning s2_halo bit: 1 data gradient, 2 forward)."""
-    return (R == 3 and S == 3 and st == 2 and pad == 1 and (_tuning.get("s2_halo") & bit) != 0
-            and lib().pdnn_conv3x3s2_supported(N, H, W, C, K) == 1)
+    (csrc/kernels/conv_s2.hip) for this direction (tuning s2_halo bit: 1 data gradient, 2 forward, 16 the data
+    gradient's BN-backward operand prologue).  The forward goes there only while its grid fills the chip at least
+    twice (>= 512 blocks of 256 pixels x 128 channels): ResNet-50 stage 2 111 vs 139 us on the implicit-GEMM engine,
+    stages 3 / 4 (392 / 196 blocks) 102 / 152 vs 91 / 101 (tools/bench_conv_s2.py, gpurun_out/r6_02); bit 32 forces
+    it (tests)."""
+    tb = _tuning.get("s2_halo")
+    if not (R == 3 and S == 3 and st == 2 and pad == 1 and (tb & bit) != 0):
+        return False
+    if bit == 2 and not (tb & 32) and -(-N * (H // 2) * (W // 2) // 256) * (K // 128) < 512:
+        return False
+    return lib().pdnn_conv3x3s2_supported(N, H, W, C, K) == 1
 
 
 def conv3x3s2_fold_ok(x_shape, Ko):
     """Whether a 3x3 / stride-2 conv of this input takes its input's BN + ReLU as the forward kernel's operand
     prologue (tuning s2_halo bit 4): its activation need not be materialised."""
     N, H, W, C = x_shape
-    return (_tuning.get("s2_halo") & 4) != 0 and _s2_ok(N, H, W, C, Ko, 3, 3, 2, 1, 2)
+    return (_tuning.get("s2_halo") & 4) != 0 and _s2_ok(N, H, W, C, Ko, 3, 3, 2, 1, 2) and (
+        (_tuning.get("s2_halo") & 8) == 0 or lib().pdnn_conv3x3s2_wgrad_supported(N, H, W, C, Ko) == 1)
 
 
 def conv3x3s2(x, w, dgrad=False, want_stats=False, bn=None, pre=None, pro=None, out_hw=None):
@@ -417,7 +426,7 @@ def dgrad_pre_ok(dy_shape, w_shape, st, pad):
     N, Ho, Wo, K = dy_shape
     Kw, R, S, C = w_shape
     return (_conv3x3_ok(N, Ho, Wo, K, C, R, S, st, pad)
-            or _s2_ok(N, 2 * Ho, 2 * Wo, C, K, R, S, st, pad, 1)
+            or (_s2_ok(N, 2 * Ho, 2 * Wo, C, K, R, S, st, pad, 1) and (_tuning.get("s2_halo") & 16) != 0)
             or (_panel_dgrad_k(K) and _panel_ok(N * Ho * Wo, K, C, R, S, st, pad)))
 
 
@@ -526,6 +535,12 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
         # prologue relu(x * sc + sh) applied as the halo is staged
         ws = torch.empty(lib().pdnn_conv3x3_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
         call("pdnn_conv3x3_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(sc), ptr(sh), stream())
+        return out
+    if (R == 3 and S == 3 and st == 2 and pad == 1 and (_tuning.get("s2_halo") & 8) != 0
+            and lib().pdnn_conv3x3s2_wgrad_supported(N, H, W, C, K) == 1):
+        # stride 2: the direct kernel over the input's four parity planes (conv3x3_wgrad.hip conv3x3s2_wgrad_kernel)
+        ws = torch.empty(lib().pdnn_conv3x3s2_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
+        call("pdnn_conv3x3s2_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(sc), ptr(sh), stream())
         return out
     if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _WGRAD1X1_PP_PIX
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):

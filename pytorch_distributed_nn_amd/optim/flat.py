@@ -130,14 +130,17 @@ class FlatParams:
         return start, end
 
 
-def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float, early=()):
+def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float, early=(), last_mb: float | None = None):
     """Gradient buckets over the flat arena in REVERSE parameter order (the order backward produces
     them), a small first bucket so communication starts early.  -> ([(start, end, n_params)], {id(p): b}).
 
     ``early``: parameters whose gradient is complete at the START of the backward although they come first in
     arena order (GPT-2's tied token embedding: its LM-head part, once the embedding rows are reduced separately,
     DistributedDataParallel.reduce_sparse_rows).  They form bucket 0, launched as soon as they are ready; they must
-    be the leading parameters of the arena (their range and the rest's stay contiguous), else they are ignored."""
+    be the leading parameters of the arena (their range and the rest's stay contiguous), else they are ignored.
+
+    ``last_mb``: cap of the LAST bucket (the first layers' gradients, ready only when the backward ends, so its
+    collective is the one nothing hides): a larger final group is split so its tail holds at most this much."""
     n = len(fp.params)
     ends = fp.offsets[1:] + [fp.numel]
     pos = {id(q): i for i, q in enumerate(fp.params)}
@@ -156,6 +159,18 @@ def reverse_buckets(fp: FlatParams, cap_mb: float, first_mb: float, early=()):
         cur_bytes += nb
     if cur:
         groups.append(cur)
+    if last_mb is not None and len(groups) > (1 if lead else 0):
+        last = groups[-1]                     # indices in descending order: the final ones are ready last
+        tail, tb = [], 0
+        for i in reversed(last):
+            nb = (ends[i] - fp.offsets[i]) * 4
+            if tail and tb + nb > last_mb * 2 ** 20:
+                break
+            tail.append(i)
+            tb += nb
+        if len(tail) < len(last):
+            groups[-1] = [i for i in last if i not in set(tail)]
+            groups.append(sorted(tail, reverse=True))
     buckets, pbucket = [], {}
     for bi, idxs in enumerate(groups):
         lo, hi = min(idxs), max(idxs)

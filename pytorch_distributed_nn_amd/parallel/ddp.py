@@ -222,8 +222,7 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_cap_mb: float | None = None, broadcast_buffers: bool = True, comm_dtype=None,
                  average: bool = True, straggler_mode: bool = False, device_ids=None, tracer=None,
                  num_aggregate: int = 0, deadline_ms: float = 0.0, throttle: bool = True,
-                 buffer_sync_interval: int = 1, comm_timing: bool = False, native_comm: bool | None = None,
-                 split_tied: bool | None = None):
+                 buffer_sync_interval: int = 1, comm_timing: bool = False, split_tied: bool | None = None, last_bucket_cap_mb: float | None = 32.0):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -267,14 +266,6 @@ class DistributedDataParallel(nn.Module):
             if _backend.available():
                 K.set_comm_world(self.world)
         self._broadcast_init()
-        # native_comm (opt-in, PDNN_DDP_NATIVE_COMM=1): bucket all-reduces issued through RCCL directly, ordered by
-        # fence-free events instead of ProcessGroupNCCL's per-collective stream-sync event (parallel/rccl_native.py)
-        if native_comm is None:
-            native_comm = os.environ.get("PDNN_DDP_NATIVE_COMM") == "1"
-        self._native = None
-        if native_comm and self._comm and self.nccl and self.flat.grad.is_cuda:
-            from .rccl_native import NativeComm
-            self._native = NativeComm(self.pg, self.flat.grad.device)
         # split tied embedding (GPT-2's wte = LM head): the head's dense gradient is complete at the START of the
         # backward, the embedding's rows only at its end.  Reduced as one parameter, its 147 MiB bucket could only
         # launch after the embedding backward -- fully exposed at N > 1.  Split: the dense
@@ -289,6 +280,7 @@ class DistributedDataParallel(nn.Module):
         if (tied is not None and self._comm and not straggler_mode and num_aggregate == 0 and deadline_ms == 0
                 and comm_dtype is None):
             early = [tied]
+        self._last_cap = last_bucket_cap_mb      # the final bucket's collective is the exposed one (reverse_buckets)
         self._build_buckets(bucket_cap_mb, bucket_cap_mb if first_bucket_cap_mb is None else first_bucket_cap_mb,
                             early)
         if early and self._pbucket.get(id(early[0])) == 0 and self.buckets[0][2] == 1:
@@ -378,7 +370,8 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self, cap_mb, first_mb, early=()):
-        self.buckets, self._pbucket = reverse_buckets(self.flat, cap_mb, first_mb, early)
+        self.buckets, self._pbucket = reverse_buckets(self.flat, cap_mb, first_mb, early,
+                                                      getattr(self, "_last_cap", None))
         if self.comm_dtype is not None:
             self._wire = [torch.empty(e - s, dtype=self.comm_dtype, device=self.flat.grad.device) for s, e, _ in self.buckets]
 
@@ -530,10 +523,7 @@ class DistributedDataParallel(nn.Module):
             self._works.append((b, work))
             self._work_of[b] = work
             return
-        if self._native is not None:
-            work = self._native.all_reduce(t, avg=op == dist.ReduceOp.AVG)
-        else:
-            work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
+        work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
         self._works.append((b, work))
         self._work_of[b] = work
         if self._ovl_active():
@@ -689,9 +679,6 @@ class DistributedDataParallel(nn.Module):
     def close(self):
         if self.kofn is not None:
             self.kofn.stop()
-        if self._native is not None:
-            self._native.close()
-            self._native = None
 
     def _buffer_sync_due(self):
         return (self.broadcast_buffers and self._comm and self.module.training

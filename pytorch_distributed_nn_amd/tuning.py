@@ -28,8 +28,15 @@ ds_sub             1        stride-2 1x1 shortcut convs read a contiguous copy o
                             subsample pass): the forward then runs as a stride-1 1x1 conv, the weight gradient as a
                             plain GEMM on the ping-pong engine (0: the implicit-GEMM engine's strided gathers)
 s2_halo            3        3x3 / stride-2 convs on the half-resolution halo kernels (csrc/kernels/conv_s2.hip), a bit
-                            mask: 1 data gradient, 2 forward, 4 forward reads t1 through the BN1 + ReLU prologue (a1
-                            not materialised; the weight gradient then takes the same prologue); 0 = implicit GEMM
+                            mask: 1 data gradient (ResNet-50 bs 256: 210 / 135 / 126 vs 320 / 228 / 205 us per stage on
+                            the implicit-GEMM engine), 2 forward where its grid fills the chip (stage 2: 111 vs 139 us;
+                            32 forces it everywhere), 16 the data gradient's BN2-backward operand prologue (+45-55 us
+                            per call: slower than the separate apply pass), 8 weight gradient on the direct kernel over
+                            the input's parity planes (conv3x3_wgrad.hip: 372-389 vs 158-159 us -- four halo stagings
+                            per tile for 1-4 taps each), 4 forward reads t1 through the BN1 + ReLU prologue (a1 not
+                            materialised; the weight gradient then takes the prologue: 292-296 vs 158-159 us on the
+                            implicit-GEMM engine).  Step A/B (gpurun_out/r6_02): 3 -> 11,650 img/s, 0 11,602, 11 11,452,
+                            15 11,416.  0 = implicit GEMM everywhere
 =================  =======  ===========================================================================
 
 Every other former switch is fixed at its measured optimum where it is used, with the measurement cited there

@@ -32,6 +32,16 @@ def K():
     return kernels
 
 
+@pytest.fixture(autouse=True)
+def every_s2_route():
+    """Route every direction through the stride-2 kernels (tuning s2_halo: 1 dgrad, 2 + 32 forward at any grid size,
+    8 direct weight gradient, 16 dgrad operand prologue), whatever the measured defaults send where."""
+    from pytorch_distributed_nn_amd import tuning
+    old = tuning.set("s2_halo", 1 | 2 | 8 | 16 | 32)
+    yield
+    tuning.set("s2_halo", old)
+
+
 def ref_fwd(x, w):
     return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 2, 1).permute(0, 2, 3, 1)
 
@@ -163,3 +173,25 @@ def test_shortcut_on_subsample_matches_strided_conv(K):
     d1 = K.conv_wgrad(xs, dy, 1, 1, 1, 0)
     d0 = K.conv_wgrad(x, dy, 1, 1, 2, 0)
     assert rel(d1, d0) < 5e-3
+
+
+@pytest.mark.parametrize("shape", [(4, 56, 56, 128, 128), (3, 28, 28, 256, 256), (5, 14, 14, 512, 512),
+                                   (3, 28, 56, 64, 192), (7, 6, 14, 128, 64)])
+def test_s2_wgrad_direct(K, shape):
+    """dW of a 3x3 / stride-2 / pad-1 conv on the parity-plane direct kernel against fp32 torch, accumulated (+=),
+    with tiles straddling images and partial last tiles; and with the BN + ReLU prologue bitwise equal to the kernel on
+    the materialised activation."""
+    N, H, W, C, Ko = shape
+    assert K.lib().pdnn_conv3x3s2_wgrad_supported(N, H, W, C, Ko) == 1
+    x = torch.randn(N, H, W, C, device="cuda").to(BF)
+    dy = torch.randn(N, H // 2, W // 2, Ko, device="cuda").to(BF)
+    wr = torch.zeros(Ko, C, 3, 3, device="cuda", requires_grad=True)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, None, 2, 1)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    ref = wr.grad.permute(0, 2, 3, 1)
+    base = torch.randn(Ko, 3, 3, C, device="cuda")
+    out = K.conv_wgrad(x, dy, 3, 3, 2, 1, out=base.clone())
+    assert rel(out - base, ref) < 5e-3
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    a = K.bn_apply(x.view(-1, C), sc, sh, relu=True).view_as(x)
+    assert torch.equal(K.conv_wgrad(x, dy, 3, 3, 2, 1, pro=(sc, sh)), K.conv_wgrad(a, dy, 3, 3, 2, 1))

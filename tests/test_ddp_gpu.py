@@ -75,7 +75,6 @@ def _rccl_job(rank, world):
     fref = flatten_module(ref)
     net = DistributedDataParallel(m, bucket_cap_mb=4.0, first_bucket_cap_mb=0.5)
     assert net._comm and net.nccl
-    assert (net._native is not None) == (os.environ.get("PDNN_DDP_NATIVE_COMM") == "1")
     opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
     g = torch.Generator().manual_seed(1)
     rels, moved = [], []
@@ -97,11 +96,9 @@ def _rccl_job(rank, world):
     return rels, moved, len(net.step_comm_log), len(net.buckets)
 
 
-@pytest.mark.parametrize("native", ["0", "1"])
-def test_ddp_rccl_single_rank_rehearsal(native):
-    """native "1": the bucket all-reduces go through the framework's own RCCL communicator (rccl_native.py)."""
+def test_ddp_rccl_single_rank_rehearsal():
     res = run_world(_rccl_job, 1, (), timeout=600, device=None, backend="nccl",
-                    env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1", "PDNN_DDP_NATIVE_COMM": native})
+                    env={"PDNN_FORCE_PG": "1", "PDNN_DDP_FORCE_COMM": "1"})
     rels, moved, ncomm, nb = res[0]
     assert ncomm == 3 and nb >= 2
     assert max(rels) < 1e-5, rels           # AVG over one rank passes gradients through
@@ -307,30 +304,3 @@ def test_ddp_comm_timing_records():
             assert all(d >= s for s, d in zip(r["bucket_ready_ms"], r["bucket_done_ms"])), r
             assert r["bwd_end_ms"] > 0 and r["tail_ms"] >= 0 and r["bn_bcast_ms"] is not None, r
         assert rel < (1e-2 if name == "bf16" else 1e-5), (name, rel)
-
-
-def _native_comm_job(rank, world):
-    import torch.distributed as dist
-    from pytorch_distributed_nn_amd.parallel.rccl_native import NativeComm
-    c = NativeComm(None, torch.device("cuda"))
-    out = []
-    for dt in (torch.float32, torch.bfloat16):
-        x = torch.randn(1 << 20, device="cuda").to(dt)
-        ref = x.clone()
-        w = c.all_reduce(x, avg=False)
-        w.wait()
-        w = c.all_reduce(x, avg=True)
-        w.wait()
-        torch.cuda.synchronize()
-        out.append(((x.float() - ref.float()).abs().max().item(), w.is_completed()))
-    c.close()
-    assert dist.get_world_size() == 1
-    return out
-
-
-def test_native_rccl_allreduce_single_rank():
-    """SUM / AVG over one rank leave the tensor unchanged; wait() orders the current stream after RCCL's."""
-    res = run_world(_native_comm_job, 1, (), timeout=150, device=None, backend="nccl",
-                    env={"PDNN_FORCE_PG": "1"})[0]
-    for err, done in res:
-        assert err == 0.0 and done

@@ -51,21 +51,24 @@ def main():
         pre = (t2, zero, one, g, zero, zero, torch.empty_like(dy))
         flops = 2.0 * N * Ho * Wo * C * C * 9
         row = {"shape": [H, W, C]}
-        for name, mode in (("gemm", 0), ("halo", 3)):
+        for name, mode in (("gemm", 0), ("halo", 11)):
             old = tuning.set("s2_halo", mode)
             r = {"fwd_us": timeit(lambda: K.conv_fwd(x, w, 2, 1, want_stats=True), a.iters)}
             if mode:
                 r["fwd_pro_us"] = timeit(lambda: K.conv_fwd(x, w, 2, 1, want_stats=True, pro=(one, zero)), a.iters)
                 r["dgrad_pre_us"] = timeit(lambda: K.conv_dgrad(dy, w, x.shape, 2, 1, bn=bn, pre=pre), a.iters)
             r["dgrad_us"] = timeit(lambda: K.conv_dgrad(dy, w, x.shape, 2, 1, bn=bn), a.iters)
+            dw = torch.zeros(C, 3, 3, C, device="cuda")
+            r["wgrad_us"] = timeit(lambda: K.conv_wgrad(x, dy, 3, 3, 2, 1, out=dw), a.iters)
+            r["wgrad_pro_us"] = timeit(lambda: K.conv_wgrad(x, dy, 3, 3, 2, 1, pro=(one, zero), out=dw), a.iters)
             tuning.set("s2_halo", old)
             for k in list(r):
                 r[k] = round(r[k], 1)
                 r[k.replace("_us", "_tflops")] = round(flops / r[k] / 1e6, 1)
             row[name] = r
-            tot[name] = tot.get(name, 0.0) + r["fwd_us"] + r["dgrad_us"]
+            tot[name] = tot.get(name, 0.0) + r["fwd_us"] + r["dgrad_us"] + r["wgrad_us"]
         print(json.dumps(row), flush=True)
-    print(json.dumps({"total_fwd_plus_dgrad_us": {k: round(v, 1) for k, v in tot.items()}}), flush=True)
+    print(json.dumps({"total_fwd_dgrad_wgrad_us": {k: round(v, 1) for k, v in tot.items()}}), flush=True)
 
 
 if __name__ == "__main__":
