@@ -143,6 +143,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3s2_kernel(C3Args a) {
             u16x8_t v[J], tv[PRE ? J : 1];
             bool okj[J];
             int gpj[J];
+            [[maybe_unused]] long srcj[FP ? J : 1];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
                 const int i = i0 + j * 256 + tid;
@@ -155,6 +156,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3s2_kernel(C3Args a) {
                     const int gr = (int)fdiv((uint32_t)gc, a.dW);
                     src = (long)(2 * gr + pa) * (2 * Wo) + 2 * (gc - gr * Wo) + pb;
                 }
+                if constexpr (FP) srcj[j] = src;
                 v[j] = *reinterpret_cast<const u16x8_t*>(a.x + src * a.C + c0 + (i & 7) * 8);
                 if constexpr (PRE) tv[j] = *reinterpret_cast<const u16x8_t*>(a.pre_t + src * a.C + c0 + (i & 7) * 8);
             }
@@ -166,7 +168,14 @@ __global__ void __launch_bounds__(256, 2) conv3x3s2_kernel(C3Args a) {
                     if (a.pre_out && cls == 0 && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
                         *reinterpret_cast<u16x8_t*>(a.pre_out + (long)gpj[j] * a.C + c0 + (tid & 7) * 8) = v[j];
                 }
-                if constexpr (FP) v[j] = fpro_apply_lds<64>(coef, (tid & 7) * 8, v[j]);
+                if constexpr (FP) {
+                    v[j] = fpro_apply_lds<64>(coef, (tid & 7) * 8, v[j]);
+                    // a1 as a by-product (pre_out): the own plane pixels' BN + ReLU values -- every input pixel is one
+                    // plane pixel of exactly one tile -- so the weight gradient reads a materialised a1 and no
+                    // bn_apply pass runs
+                    if (a.pre_out && nt == 0 && okj[j] && gpj[j] >= p0 && gpj[j] <= plast)
+                        *reinterpret_cast<u16x8_t*>(a.pre_out + srcj[j] * a.C + c0 + (tid & 7) * 8) = v[j];
+                }
                 v[j] = mask16(v[j], okj[j]);
             }
 #pragma unroll
@@ -233,11 +242,196 @@ __global__ void __launch_bounds__(256, 2) conv3x3s2_kernel(C3Args a) {
             orow[fm] = (long)p * a.N;
         }
     }
-    c3_epilogue_rows<NB, EPI>(a, acc, tile, orow, n0, wave, lane, pv);
+    // statistics rows: the 4 class blocks of a pixel tile add into different bins (tile-major stats index 4 tile + cls)
+    c3_epilogue_rows<NB, EPI>(a, acc, DG ? tile * 4 + cls : tile, orow, n0, wave, lane, pv);
 }
+
+// Data gradient, class pairs: a block owns 64 output channels of TWO parity classes -- pair 0 = (0,0) + (1,1)
+// (1 + 4 taps), pair 1 = (0,1) + (1,0) (2 + 2) -- so each staged dy halo feeds 4-5 taps instead of 1-4 and the two
+// kinds of blocks carry nearly equal work; the accumulators (2 classes x 64 pixels x 64 channels per wave) take the
+// registers of the single-class 128-wide tile.  Plain / fused-BN-backward epilogues (no operand prologue).
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) conv3x3s2_dgrad_pair_kernel(C3Args a) {
+    constexpr int NB = 64, FN = NB / 16;
+    constexpr int BCH = NB * 8 / 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* const halo = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* const bbuf = halo + (a.halo_max + 1) * 64;          // [2][NB][64] K-major, kimg_off swizzle
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int T = a.tiles * a.ntiles;
+    const int pair = blockIdx.x < T ? 0 : 1;                    // the 5-tap pair first
+    const int t = xcd_remap(blockIdx.x - pair * T, T);
+    const int tile = t / a.ntiles, nt = t - tile * a.ntiles;
+    const int p0 = tile * C3_BM, n0 = nt * NB;
+    const int plast = min(a.P, p0 + C3_BM) - 1;
+    const int Wo = a.W;
+    const int gr0 = (int)fdiv((uint32_t)p0, a.dW), gr1 = (int)fdiv((uint32_t)plast, a.dW);
+    const int hpx = (gr1 - gr0 + 2) * Wo;                      // dy rows gr0 .. gr1 + 1
+    const long gp0 = (long)gr0 * Wo;
+    // the pair's classes (slot 0, slot 1) and their tap counts
+    const int cl0 = pair ? 1 : 0, cl1 = pair ? 2 : 3;
+    const int nt0 = pair ? 2 : 1, ntot = pair ? 4 : 5;
+
+    int hb[4], py[4], px[4];
+    bool pv[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int p = p0 + wave * 64 + f * 16 + (lane & 15);
+        pv[f] = p < a.P;
+        const int pp = pv[f] ? p : plast;
+        const int gr = (int)fdiv((uint32_t)pp, a.dW);
+        px[f] = pp - gr * Wo;
+        py[f] = gr - (int)fdiv((uint32_t)gr, a.dH) * a.H;
+        hb[f] = (gr - gr0) * Wo + px[f];
+    }
+    const int zpx = a.halo_max;
+    if (tid < 8) *reinterpret_cast<u16x8_t*>(halo + zpx * 64 + tid * 8) = c3_zero8();
+
+    f32x4_t acc[2][4][FN];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[c][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int cch = a.C >> 6;
+    const long wrow = 9L * a.C;
+    u16x8_t rb[BCH];
+    auto load_b = [&](int c0, int tw) {
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            rb[i] = *reinterpret_cast<const u16x8_t*>(a.w + (long)(n0 + row) * wrow + (long)tw * a.C + c0 + q * 8);
+        }
+    };
+    auto store_b = [&](int buf) {
+        bf16_t* B = bbuf + buf * NB * 64;
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int li = tid + 256 * i, row = li >> 3, q = li & 7;
+            *reinterpret_cast<u16x8_t*>(B + kimg_off(row, q)) = rb[i];
+        }
+    };
+    // global tap g of the pair (0 .. ntot-1) -> class slot, (di, dj) offsets, W' tap index
+    auto tap_of = [&](int g, int& slot, int& dr, int& ds, int& tw) {
+        slot = g >= nt0 ? 1 : 0;
+        const int k = g - (slot ? nt0 : 0);
+        const int cls = slot ? cl1 : cl0, pa = cls >> 1, pb = cls & 1;
+        const int kr = pb ? (k >> 1) : k, kc = pb ? (k & 1) : 0;
+        dr = kr;
+        ds = kc;
+        tw = 8 - (3 * (pa + 1 - 2 * kr) + (pb + 1 - 2 * kc));
+    };
+
+    for (int ck = 0; ck < cch; ++ck) {
+        const int c0 = ck << 6;
+        if (ck) __syncthreads();
+        const int nch = hpx * 8;
+        constexpr int J = S2_J;
+        for (int i0 = 0; i0 < nch; i0 += 256 * J) {
+            u16x8_t v[J];
+            bool okj[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int i = i0 + j * 256 + tid;
+                const long gp = gp0 + (i >> 3);
+                okj[j] = i < nch && gp >= 0 && gp < a.P;
+                const long gc = gp < 0 ? 0 : (gp >= a.P ? a.P - 1 : gp);
+                v[j] = *reinterpret_cast<const u16x8_t*>(a.x + gc * a.C + c0 + (i & 7) * 8);
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int i = i0 + j * 256 + tid;
+                const int off = i < nch ? halo_off(i >> 3, i & 7) : zpx * 64 + (i & 7) * 8;
+                *reinterpret_cast<u16x8_t*>(halo + off) = mask16(v[j], okj[j]);
+            }
+        }
+        {
+            int sl, dr, ds, tw;
+            tap_of(0, sl, dr, ds, tw);
+            load_b(c0, tw);
+        }
+        store_b(0);
+        __syncthreads();
+        // the class slots one after the other (compile-time accumulator index), the global tap counter g running on
+        // through both (weight double buffer parity, next-tap prefetch across the slot boundary)
+        static_for<0, 2>([&](auto SL) {
+            const int gend = SL ? ntot : nt0;
+#pragma unroll 1
+            for (int g = SL ? nt0 : 0; g < gend; ++g) {
+                int sl, dr, ds, tw;
+                tap_of(g, sl, dr, ds, tw);
+                if (g + 1 < ntot) {
+                    int sl1, dr1, ds1, tw1;
+                    tap_of(g + 1, sl1, dr1, ds1, tw1);
+                    load_b(c0, tw1);
+                }
+                int hp[4];
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    const bool ok = pv[f] && py[f] + dr < a.H && px[f] + ds < Wo;
+                    hp[f] = ok ? hb[f] + dr * Wo + ds : zpx;
+                }
+                const bf16_t* B = bbuf + (g & 1) * NB * 64;
+#pragma unroll 1
+                for (int ks = 0; ks < 2; ++ks) {
+                    bf16x8_t af[4], bfr[FN];
+                    const int q = ks * 4 + (lane >> 4);
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                        af[f] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(halo + halo_off(hp[f], q)));
+#pragma unroll
+                    for (int f = 0; f < FN; ++f) bfr[f] = frag_kmajor(B, f * 16 + (lane & 15), ks, lane);
+#pragma unroll
+                    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                        for (int fn = 0; fn < FN; ++fn)
+                            acc[SL][fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[SL][fm][fn], 0, 0, 0);
+                }
+                if (g + 1 < ntot) {
+                    store_b((g + 1) & 1);
+                    __syncthreads();
+                }
+            }
+        });
+    }
+
+    static_for<0, 2>([&](auto SL) {
+        const int cls = SL ? cl1 : cl0, ca = cls >> 1, cb = cls & 1;
+        long orow[4];
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+            const int p = p0 + wave * 64 + fm * 16 + (lane & 15);
+            const int pp = pv[fm] ? p : plast;
+            const int gr = (int)fdiv((uint32_t)pp, a.dW);
+            orow[fm] = ((long)(2 * gr + ca) * (2 * Wo) + 2 * (pp - gr * Wo) + cb) * a.N;
+        }
+        c3_epilogue_rows<NB, EPI>(a, acc[SL], tile * 4 + cls, orow, n0, wave, lane, pv);
+    });
+}
+
+int s2p_smem(int Wo);
 
 int s2_halo_max(int Wo) { return ((C3_BM - 1 + Wo - 1) / Wo + 2) * Wo; }
 int s2_smem(int Wo) { return (s2_halo_max(Wo) + 1) * 128 + 2 * S2_NB * 128; }
+
+int s2p_smem(int Wo) { return (s2_halo_max(Wo) + 1) * 128 + 2 * 64 * 128; }
+
+template <int EPI>
+int s2p_launch(C3Args a, hipStream_t st) {
+    static int attr_done = 0;
+    const int sm = s2p_smem(a.W);
+    if (sm > attr_done) {
+        (void)hipFuncSetAttribute((const void*)conv3x3s2_dgrad_pair_kernel<EPI>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        attr_done = sm;
+    }
+    a.ntiles = a.N / 64;
+    hipLaunchKernelGGL((conv3x3s2_dgrad_pair_kernel<EPI>), dim3(a.tiles * a.ntiles * 2), dim3(256), sm, st, a);
+    PDNN_LAUNCH_RET;
+}
 
 template <bool DG, int EPI, bool PRE, bool FP>
 int s2_launch(const C3Args& a, hipStream_t st) {
@@ -276,17 +470,18 @@ PDNN_API int pdnn_conv3x3s2_supported(int Nimg, int H, int W, int C, int N) {
 
 // Forward (dgrad = 0): y [Nimg][H/2][W/2][N] = conv3x3/s2/p1(x [Nimg][H][W][C], w [N][3][3][C]); stats: the output's
 // BN statistics bins (else plain); pro_sc / pro_sh: x is the pre-activation t of relu(t * sc + sh), applied while
-// staging.
+// staging, and written to pre_out [Nimg][H][W][C] when given (the activation the weight gradient reads).
 // Data gradient (dgrad = 1): x = dy [Nimg][H/2][W/2][C] (C = the conv's output channels K), w = conv3x3_flip's
 // W' [N][3][3][C] (N = the conv's input channels), y = dx [Nimg][H][W][N]; bn_x (with stats): the fused BN backward
 // of the layer that produced the conv's input (gm = dx * mask, sums into stats); pre_*: the BN-backward apply of dy's
-// own BatchNorm in the operand staging (dt written to pre_out).
+// own BatchNorm in the operand staging (dt written to pre_out).  pair: the data gradient without the prologue on the
+// class-pair kernel (two parity classes per block).
 PDNN_API int pdnn_conv3x3s2(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg, int H, int W, int C, int N,
                             int dgrad, float* stats, const bf16_t* bn_x, const float* bn_mean, const float* bn_invstd,
                             const float* bn_mscale, const float* bn_mshift, const bf16_t* pre_t,
                             const float* pre_mean, const float* pre_invstd, const float* pre_gamma,
                             const float* pre_dgamma, const float* pre_dbeta, bf16_t* pre_out, const float* pro_sc,
-                            const float* pro_sh, hipStream_t st) {
+                            const float* pro_sh, int pair, hipStream_t st) {
     if (!pdnn_conv3x3s2_supported(Nimg, H, W, dgrad ? N : C, dgrad ? C : N)) return (int)hipErrorInvalidValue;
     C3Args a{};
     a.x = x; a.w = w; a.y = y;
@@ -302,9 +497,11 @@ PDNN_API int pdnn_conv3x3s2(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nim
     a.pro_sc = pro_sc; a.pro_sh = pro_sh;
     if (!pro_sc != !pro_sh || (bn_x && !stats)) return (int)hipErrorInvalidValue;
     if (pre_t && !(pre_mean && pre_invstd && pre_dgamma && pre_dbeta)) return (int)hipErrorInvalidValue;
-    if (!pre_t && pre_out) return (int)hipErrorInvalidValue;
+    // pre_out: dt of the data gradient's BN-backward prologue, or (forward with pro_sc) the prologue's output a1
+    if (pre_out && !pre_t && !(pro_sc && !dgrad)) return (int)hipErrorInvalidValue;
     if (dgrad) {
         if (pro_sc) return (int)hipErrorInvalidValue;
+        if (pair && !pre_t) return bn_x ? s2p_launch<C3_BNB>(a, st) : (stats ? (int)hipErrorInvalidValue : s2p_launch<C3_PLAIN>(a, st));
         if (bn_x) return pre_t ? s2_launch<true, C3_BNB, true, false>(a, st) : s2_launch<true, C3_BNB, false, false>(a, st);
         if (stats) return (int)hipErrorInvalidValue;
         return pre_t ? s2_launch<true, C3_PLAIN, true, false>(a, st) : s2_launch<true, C3_PLAIN, false, false>(a, st);

@@ -13,7 +13,7 @@ run() {
   env "$@" timeout -k 10 300 python3 bench.py --model $m --no-plain-run --no-extra-configs --diag-steps 3 > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; return 1; }
   python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['ms_per_step'])"
 }
-run r_def resnet50 PDNN_TUNE=s2_halo=3 && run r_ds0 resnet50 PDNN_TUNE=ds_sub=0 && run r_s0 resnet50 PDNN_TUNE=s2_halo=0,ds_sub=0 && run r_def2 resnet50 PDNN_TUNE=s2_halo=3 && run r_ds0b resnet50 PDNN_TUNE=ds_sub=0 && run r_s1 resnet50 PDNN_TUNE=s2_halo=1 || exit 1
+run r_def resnet50 PDNN_TUNE=ds_sub=1 && run r_ds0 resnet50 PDNN_TUNE=ds_sub=0 && run r_def2 resnet50 PDNN_TUNE=ds_sub=1 && run r_ds0b resnet50 PDNN_TUNE=ds_sub=0 || exit 1
 run g_split gpt2_small PDNN_DDP_SPLIT_TIED=1 && run g_nosplit gpt2_small PDNN_DDP_SPLIT_TIED=0 && run g_split2 gpt2_small PDNN_DDP_SPLIT_TIED=1 || exit 1
 python3 -c "import json;d=json.load(open('$O/g_split.json'));c=d['comm'];print('split bucket_mb',c['bucket_mb'],'ready',c['fp32']['bucket_ready_ms'],'bwd_end',c['fp32']['backward_end_ms'])"
 export TMPDIR=/tmp

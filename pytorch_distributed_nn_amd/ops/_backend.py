@@ -41,7 +41,7 @@ _SIGS = {
     "pdnn_gemm_stats_rows": [I],
     "pdnn_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, P],
     "pdnn_conv3x3_supported": [I, I, I, I, I],
-    "pdnn_conv3x3s2": [P, P, P, I, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P, P, P],
+    "pdnn_conv3x3s2": [P, P, P, I, I, I, I, I, I, P] + [P] * 5 + [P] * 7 + [P, P, I, P],
     "pdnn_conv3x3s2_supported": [I, I, I, I, I],
     "pdnn_conv3x3s2_wgrad": [P, P, P, I, I, I, I, I, P, P, P, P],
     "pdnn_conv3x3s2_wgrad_supported": [I, I, I, I, I],

@@ -362,6 +362,11 @@ class BottleneckFn(torch.autograd.Function):
             # while staging t1 (each element staged ~1.2x: one read of t1 instead of a bn_apply pass writing a1;
             # +0.2% ResNet-50 / +0.3% ResNet-152 same box, gpurun_out/r4_52)
             a1, pro1, src1 = None, (s1, h1), t1
+        elif stride == 2 and K.conv3x3s2_a1_ok(tuple(t1.shape), w2.shape[0]) and not (
+                fp8_meta is not None and K.conv3x3_fp8_ok(*t1.shape, w2.shape[0])):
+            # stride 2 (tuning s2_halo bit 64): the half-resolution halo conv applies BN1 + ReLU while staging t1's
+            # parity planes and writes the result as a1 for the weight gradient -- no separate bn_apply pass
+            a1, pro1, src1 = torch.empty_like(t1), (s1, h1), t1
         elif stride == 2 and K.conv3x3s2_fold_ok(tuple(t1.shape), w2.shape[0]):
             # stride 2 (tuning s2_halo bit 4): the half-resolution halo conv applies BN1 + ReLU while staging each
             # parity plane of t1, the weight gradient through its operand prologue
@@ -374,6 +379,12 @@ class BottleneckFn(torch.autograd.Function):
                            and K.conv3x3_fp8_ok(*t1.shape, w2.shape[0])) else None
         if fp8 is not None:
             t2, m2, i2, s2, h2 = _conv3x3_bn_fp8(src1, w2, fp8.fwd, training, (g2, b2), bufs[2:4], mom, eps, pro=pro1)
+        elif a1 is not None and pro1 is not None:      # a1 written by the stride-2 forward (bit 64 above)
+            t2, slab2 = K.conv3x3s2(t1, k2, want_stats=training, pro=pro1, pro_out=a1)
+            if training:
+                m2, i2, s2, h2 = _bn_train(slab2, t2.numel() // t2.shape[-1], (g2, b2), bufs[2:4], mom, eps)
+            else:
+                m2, i2, s2, h2 = _bn_eval((g2, b2), bufs[2:4], eps)
         else:
             t2, m2, i2, s2, h2 = _conv_bn(src1, k2, stride, 1, pro1, training, (g2, b2), bufs[2:4], mom, eps)
         # a2 = relu(bn2(t2)): on the A-stationary 1x1 kernel conv3 applies BN2 + ReLU to its activation fragments

@@ -258,7 +258,15 @@ def conv3x3s2_fold_ok(x_shape, Ko):
         (_tuning.get("s2_halo") & 8) == 0 or lib().pdnn_conv3x3s2_wgrad_supported(N, H, W, C, Ko) == 1)
 
 
-def conv3x3s2(x, w, dgrad=False, want_stats=False, bn=None, pre=None, pro=None, out_hw=None):
+def conv3x3s2_a1_ok(x_shape, Ko):
+    """Whether the stride-2 forward runs on the halo kernel here with its input's BN + ReLU applied while staging AND
+    written out as a by-product (tuning s2_halo bit 64): the activation a1 is materialised for the weight gradient
+    without a bn_apply pass."""
+    N, H, W, C = x_shape
+    return (_tuning.get("s2_halo") & 64) != 0 and _s2_ok(N, H, W, C, Ko, 3, 3, 2, 1, 2)
+
+
+def conv3x3s2(x, w, dgrad=False, want_stats=False, bn=None, pre=None, pro=None, pro_out=None):
     """Stride-2 3x3 conv on the halo kernels.  Forward: y (N, H/2, W/2, K) = conv(x (N, H, W, C), w [K][3][3][C]),
     BN statistics bins (want_stats) and the forward prologue pro = (scale, shift).  Data gradient (dgrad=True):
     x = dy (N, Ho, Wo, K), w = conv3x3_flip(W) [C][3][3][K] -> dx (N, 2Ho, 2Wo, C) with the fused BN backward
@@ -278,8 +286,14 @@ def conv3x3s2(x, w, dgrad=False, want_stats=False, bn=None, pre=None, pro=None, 
         t, mean, inv, msc, msh = bn
         _chk(tuple(t.shape) == (Nimg, Ho, Wo, N), "conv3x3s2: bn_x shape")
     psc, psh = pro if pro is not None else (None, None)
+    pargs = _pre_args(pre, x)
+    if pro_out is not None:         # forward: the prologue's output (a1) written as a by-product
+        _chk(not dgrad and pro is not None and pre is None and pro_out.shape == x.shape and pro_out.dtype == BF16
+             and pro_out.is_contiguous(), "conv3x3s2: pro_out needs the forward prologue and x's shape")
+        pargs = (None,) * 6 + (ptr(pro_out),)
+    pair = int(dgrad and pre is None and (_tuning.get("s2_halo") & 128) != 0)
     call("pdnn_conv3x3s2", ptr(x), ptr(w), ptr(y), Nimg, Ho if dgrad else H, Wo if dgrad else W, C, N, int(dgrad),
-         ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), *_pre_args(pre, x), ptr(psc), ptr(psh), stream())
+         ptr(slab), ptr(t), ptr(mean), ptr(inv), ptr(msc), ptr(msh), *pargs, ptr(psc), ptr(psh), pair, stream())
     return y, slab
 
 

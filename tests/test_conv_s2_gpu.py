@@ -75,6 +75,10 @@ def test_s2_forward_prologue_matches_materialised(K, shape):
     y1, s1 = K.conv3x3s2(t, w, want_stats=True, pro=(sc, sh))
     assert torch.equal(y0, y1)
     slab_close(s0, s1)
+    # the prologue's output written as a by-product (s2_halo bit 64): bitwise bn_apply's a1
+    a_out = torch.full_like(t, float("nan"))
+    y2, _ = K.conv3x3s2(t, w, want_stats=True, pro=(sc, sh), pro_out=a_out)
+    assert torch.equal(y2, y0) and torch.equal(a_out, a)
 
 
 def _dgrad_ref(w, dy, x_shape):
@@ -195,3 +199,26 @@ def test_s2_wgrad_direct(K, shape):
     sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
     a = K.bn_apply(x.view(-1, C), sc, sh, relu=True).view_as(x)
     assert torch.equal(K.conv_wgrad(x, dy, 3, 3, 2, 1, pro=(sc, sh)), K.conv_wgrad(a, dy, 3, 3, 2, 1))
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_s2_dgrad_class_pairs_match_single_class(K, shape):
+    """The class-pair data-gradient kernel (s2_halo bit 128: two parity classes per block) gives the single-class
+    kernel's gm bitwise (same MFMA order per output) and its BN-backward sums up to atomic order."""
+    from pytorch_distributed_nn_amd import tuning
+    N, H, W, C, Ko = shape
+    w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.05).to(BF)
+    dy = torch.randn(N, H // 2, W // 2, Ko, device="cuda").to(BF)
+    t = torch.randn(N, H, W, C, device="cuda").to(BF)
+    mean, inv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    msc, msh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.3
+    g0, s0 = K.conv_dgrad(dy, w, (N, H, W, C), 2, 1, bn=(t, mean, inv, msc, msh))
+    d0 = K.conv_dgrad(dy, w, (N, H, W, C), 2, 1)
+    old = tuning.set("s2_halo", tuning.get("s2_halo") | 128)
+    try:
+        g1, s1 = K.conv_dgrad(dy, w, (N, H, W, C), 2, 1, bn=(t, mean, inv, msc, msh))
+        d1 = K.conv_dgrad(dy, w, (N, H, W, C), 2, 1)
+    finally:
+        tuning.set("s2_halo", old)
+    assert torch.equal(g1, g0) and torch.equal(d1, d0)
+    slab_close(s1, s0)

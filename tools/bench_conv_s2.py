@@ -51,13 +51,20 @@ def main():
         pre = (t2, zero, one, g, zero, zero, torch.empty_like(dy))
         flops = 2.0 * N * Ho * Wo * C * C * 9
         row = {"shape": [H, W, C]}
-        for name, mode in (("gemm", 0), ("halo", 11)):
+        for name, mode in (("gemm", 0), ("halo", 1 | 2 | 8 | 16 | 32)):
             old = tuning.set("s2_halo", mode)
             r = {"fwd_us": timeit(lambda: K.conv_fwd(x, w, 2, 1, want_stats=True), a.iters)}
             if mode:
                 r["fwd_pro_us"] = timeit(lambda: K.conv_fwd(x, w, 2, 1, want_stats=True, pro=(one, zero)), a.iters)
                 r["dgrad_pre_us"] = timeit(lambda: K.conv_dgrad(dy, w, x.shape, 2, 1, bn=bn, pre=pre), a.iters)
             r["dgrad_us"] = timeit(lambda: K.conv_dgrad(dy, w, x.shape, 2, 1, bn=bn), a.iters)
+            if mode:
+                tuning.set("s2_halo", mode | 128)
+                r["dgrad_pair_us"] = timeit(lambda: K.conv_dgrad(dy, w, x.shape, 2, 1, bn=bn), a.iters)
+                tuning.set("s2_halo", mode)
+                a1 = torch.empty_like(x)
+                r["fwd_pro_a1_us"] = timeit(lambda: K.conv3x3s2(x, w, want_stats=True, pro=(one, zero), pro_out=a1),
+                                            a.iters)
             dw = torch.zeros(C, 3, 3, C, device="cuda")
             r["wgrad_us"] = timeit(lambda: K.conv_wgrad(x, dy, 3, 3, 2, 1, out=dw), a.iters)
             r["wgrad_pro_us"] = timeit(lambda: K.conv_wgrad(x, dy, 3, 3, 2, 1, pro=(one, zero), out=dw), a.iters)
