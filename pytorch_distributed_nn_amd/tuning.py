@@ -27,7 +27,7 @@ bias_in_wgrad      1        GPT-2 linear bias gradients as fused row sums inside
 ds_sub             1        stride-2 1x1 shortcut convs read a contiguous copy of their input's even pixels (one
                             subsample pass): the forward then runs as a stride-1 1x1 conv, the weight gradient as a
                             plain GEMM on the ping-pong engine (0: the implicit-GEMM engine's strided gathers)
-s2_halo            67       3x3 / stride-2 convs on the half-resolution halo kernels (csrc/kernels/conv_s2.hip), a bit
+s2_halo            3        3x3 / stride-2 convs on the half-resolution halo kernels (csrc/kernels/conv_s2.hip), a bit
                             mask: 1 data gradient (ResNet-50 bs 256: 210 / 135 / 126 vs 320 / 228 / 205 us per stage on
                             the implicit-GEMM engine), 2 forward where its grid fills the chip (stage 2: 111 vs 139 us;
                             32 forces it everywhere), 16 the data gradient's BN2-backward operand prologue (+45-55 us
@@ -36,7 +36,9 @@ s2_halo            67       3x3 / stride-2 convs on the half-resolution halo ker
                             per tile for 1-4 taps each), 4 forward reads t1 through the BN1 + ReLU prologue (a1 not
                             materialised; the weight gradient then takes the prologue: 292-296 vs 158-159 us on the
                             implicit-GEMM engine), 64 that prologue writes a1 as a by-product where the forward runs
-                            on the halo kernel (no bn_apply pass; the weight gradient reads a1 as before).  Step A/B (gpurun_out/r6_02): 3 -> 11,650 img/s, 0 11,602, 11 11,452,
+                            on the halo kernel (no bn_apply pass; measured neutral: 11,822 / 11,826 vs 11,810 / 11,842
+                            img/s, r6_06), 128 the data gradient on two parity classes per block (neutral to worse:
+                            223 / 161 / 143 vs 225 / 141 / 125 us per stage).  Step A/B (gpurun_out/r6_02): 3 -> 11,650 img/s, 0 11,602, 11 11,452,
                             15 11,416.  0 = implicit GEMM everywhere
 =================  =======  ===========================================================================
 
@@ -47,7 +49,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 67, "ds_sub": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1}
 
 _VALUES = dict(DEFAULTS)
 
