@@ -800,7 +800,10 @@ PDNN_API int pdnn_conv3x3_stats_rows(int Nimg, int H, int W) {
     return (int)cdiv((long)Nimg * H * W, C3_BM) * 4;
 }
 
+PDNN_API int pdnn_conv3x3_flip_tiled(const bf16_t* w, bf16_t* wt, int K, int C, hipStream_t st);
+
 PDNN_API int pdnn_conv3x3_flip(const bf16_t* w, bf16_t* wt, int K, int C, hipStream_t st) {
+    if (K % 8 == 0 && C % 8 == 0) return pdnn_conv3x3_flip_tiled(w, wt, K, C, st);     // elementwise.hip
     hipLaunchKernelGGL(conv3x3_flip_kernel, dim3(stream_grid(9L * K * C, 256)), dim3(256), 0, st, w, wt, K, C);
     PDNN_LAUNCH_RET;
 }

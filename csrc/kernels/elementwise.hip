@@ -285,6 +285,16 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __res
     transpose_tile(src, lds, dst, ldd, R, C, blockIdx.y * 64, blockIdx.x * 64, t);
 }
 
+// W'[c][8 - tap][k] = W[k][tap][c]: the tap-flipped transposed 3x3 weight of the data gradients (conv3x3.hip, conv_s2.hip)
+// as nine 64 x 64-tiled transposes in one launch (blockIdx.z = tap).  The element-wise flip took 25 us a call at
+// ResNet-50 stage 4 on the forward's side stream (r6_03 trace: 11 calls, 0.27 ms per step).
+__global__ void __launch_bounds__(256) conv3x3_flip_tiled_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                                                 int K, int C) {
+    __shared__ bf16_t t[64][66];
+    const int tap = blockIdx.z;
+    transpose_tile(w + (long)tap * C, 9L * C, wt + (long)(8 - tap) * K, 9L * K, K, C, blockIdx.y * 64, blockIdx.x * 64, t);
+}
+
 // Many contiguous matrices in one launch (the transposed weight copies of a whole transformer, refreshed
 // once per optimizer step instead of one ~5 us launch per weight inside the backward).  The table rides in
 // the kernel arguments; block b belongs to the last entry with tile0 <= b (binary search, scalar loads).
@@ -344,5 +354,11 @@ PDNN_API int pdnn_subsample(const bf16_t* x, bf16_t* y, int N, int H, int W, int
     long g = (total + NT - 1) / NT;
     if (g > 2048) g = 2048;        // a pure copy: 8 blocks per CU of grid-stride threads keep enough loads in flight
     hipLaunchKernelGGL(subsample_kernel, dim3((unsigned)g), dim3(NT), 0, s, x, y, H, W, C, Ho, Wo, st, total);
+    PDNN_LAUNCH_RET;
+}
+
+PDNN_API int pdnn_conv3x3_flip_tiled(const bf16_t* w, bf16_t* wt, int K, int C, hipStream_t st) {
+    if (K < 1 || C < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv3x3_flip_tiled_kernel, dim3((C + 63) / 64, (K + 63) / 64, 9), dim3(256), 0, st, w, wt, K, C);
     PDNN_LAUNCH_RET;
 }
