@@ -45,6 +45,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
     __bf16 b = (__bf16)f;
     return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> packed bf16 pair (lo = a) in ONE v_cvt_pk_bf16_f32 (the scalar form above takes two conversions, a
+// shift and an or per pair)
+typedef float f32x2_cv_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_cv_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk2bf(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_cv_t{a, b}, bf16x2_cv_t));
+}
 
 template <typename T> struct Ld;
 template <> struct Ld<float> {

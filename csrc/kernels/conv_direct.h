@@ -243,8 +243,8 @@ __device__ __forceinline__ void c3_epilogue_rows(const C3Args& a, f32x4_t (&acc)
                         }
                     }
                 }
-                pk[fm][h][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                pk[fm][h][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                pk[fm][h][0] = pk2bf(v[0], v[1]);
+                pk[fm][h][1] = pk2bf(v[2], v[3]);
             }
             if constexpr (EPI == C3_STATS || EPI == C3_BNB) {
 #pragma unroll

@@ -68,6 +68,9 @@ struct GemmArgs {
     const bf16_t* ep_dgelu;   // multiply the result by gelu'(u), u read from here (GELU backward)
     int acc_c;                // E_F32 (pp engine): C += result instead of C = result
     long long* dbg;           // pp engine: per-block phase timestamps (tools/pp_one.py --trace), or null
+    int epi_slack;            // pp engine, plain bf16 epilogues: byte size of C (buffer-store range) with the
+                              // store drain deferred under the next item's slices (tuning pp_epi_slack); 0 = off
+    int epi_pair;             // pp engine: both wave groups' epilogues in one barrier interval (tuning pp_epi_pair)
 };
 
 // GELU (tanh form) through the hardware transcendentals: 0.5 (1 + tanh u) = 1 / (1 + exp(-2u)) = s, one v_exp_f32

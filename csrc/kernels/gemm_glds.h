@@ -483,8 +483,8 @@ gemm_glds_kernel(GemmArgs a) {
                             q_[fn][j] += rr * rr;
                         }
                     }
-                    pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                    pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                    pk[fn][0] = pk2bf(v[0], v[1]);
+                    pk[fn][1] = pk2bf(v[2], v[3]);
                 } else {
                     if (!mv || n >= a.N) continue;
                     float* C = reinterpret_cast<float*>(a.C) + off;

@@ -604,8 +604,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                             q[j] += r * r;
                         }
                     }
-                    pk[fm][fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                    pk[fm][fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                    pk[fm][fn][0] = pk2bf(v[0], v[1]);
+                    pk[fm][fn][1] = pk2bf(v[2], v[3]);
                 } else {
                     if (!ok) continue;
                     float* C = reinterpret_cast<float*>(a.C) + orow[fm] * a.ldc + n;

@@ -72,6 +72,8 @@ __device__ __forceinline__ int pp_koff(int row, int chunk) { return row * PP_SK 
 
 typedef __attribute__((ext_vector_type(8))) int v8i_t;
 typedef __attribute__((ext_vector_type(4))) int v4i_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 // fp8 fragment of the 16x16x128 MFMA from a 128-byte-row image: lane l holds k-bytes [32 (l >> 4), +32)
 // of its row = 16-byte chunks 2g, 2g + 1 (g = l >> 4)
 __device__ __forceinline__ v8i_t frag8(const bf16_t* img, int row, int lane) {
@@ -287,6 +289,20 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
         return a.rowsum != nullptr && n0_ == 0 && wc == 0;
     };
     bool cur_rs = rs_on(0);
+    // Deferred store drain (tuning pp_epi_slack, plain bf16 epilogues): vmcnt counts stores too on gfx9 and
+    // retires in issue order, so the first load wait after an epilogue -- vmcnt((D-2) NIT) for the next slice --
+    // also waited for every store of the tile just written.  Here the epilogue stores are buffer stores (lanes
+    // past the edges get an offset beyond the range, which the hardware drops), so every wave issues exactly
+    // SE0 (SE1 with the GELU pre-activation) of them per item, and the next D-1 load segments, whose awaited
+    // slices were issued before those stores, wait for vmcnt((D-2) NIT + SE) instead: the stores drain under
+    // the next item's MFMAs.
+    constexpr bool SLK = EM == E_BF16 && FX == 0;
+    constexpr int SE0 = C::FM * (C::FN / 2 + C::FN % 2), SE1 = SE0 + C::FM * C::FN;
+    static_assert(!SLK || (D - 2) * NIT + SE1 <= 63, "vmcnt immediate");
+    const bool slk_on = SLK && a.epi_slack > 0;
+    const bool slk_aux = slk_on && a.relu == 2 && a.ep_aux != nullptr;
+    int slk = 0;                                         // load segments left that may wait with the stores in flight
+    constexpr uint32_t OOB = 0x80000000u;                // > any range (epi_slack < 2^31)
     auto epilogue = [&]() {
             // ---------------- epilogue of item `cur`: lane holds C[m0 + arow + 16 fm + lm][n0 + bcol + 16 fn + 4 lg + j]
             if (dbg && cur < 31) dbg[2 + 2 * cur] = wall_clock64();
@@ -377,7 +393,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                             u16x4_t pre;
 #pragma unroll
                             for (int j = 0; j < 4; ++j) pre[j] = f2bf(v[j]);
-                            if (a.ep_aux && ok) *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
+                            if (slk_aux) {
+                                const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+                                    a.ep_aux, 0, a.epi_slack, 0x00020000);
+                                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, pre), xr,
+                                                                      ok ? (uint32_t)(off * 2) : OOB, 0, 0);
+                            } else if (a.ep_aux && ok) {
+                                *reinterpret_cast<u16x4_t*>(a.ep_aux + off) = pre;
+                            }
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(bf2f(pre[j]));
                         }
@@ -425,16 +448,21 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                                 }
                             }
                         }
-                        pk[fn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                        pk[fn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                        pk[fn][0] = pk2bf(v[0], v[1]);
+                        pk[fn][1] = pk2bf(v[2], v[3]);
                     }
                     bf16_t* const Crow = reinterpret_cast<bf16_t*>(a.C) + orow * a.ldc;
+                    [[maybe_unused]] __amdgpu_buffer_rsrc_t cr;
+                    if constexpr (SLK) cr = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.epi_slack, 0x00020000);
 #pragma unroll
                     for (int fp = 0; fp < C::FN / 2; ++fp) {   // 16-byte stores: permlane16 swap pairs fragments
                         const auto s0_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][0], pk[2 * fp + 1][0], false, false);
                         const auto s1_ = __builtin_amdgcn_permlane16_swap(pk[2 * fp][1], pk[2 * fp + 1][1], false, false);
                         const int n = n0 + bcol + (2 * fp + (lg & 1)) * 16 + 8 * (lg >> 1);
-                        if (mv && n + 8 <= a.N) {
+                        if (slk_on) {                          // (N % 8 == 0: whole 16-byte groups)
+                            const uint32_t bo = mv && n + 8 <= a.N ? (uint32_t)((orow * a.ldc + n) * 2) : OOB;
+                            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{s0_[0], s1_[0], s0_[1], s1_[1]}, cr, bo, 0, 0);
+                        } else if (mv && n + 8 <= a.N) {
                             *reinterpret_cast<uint4*>(Crow + n) = make_uint4(s0_[0], s1_[0], s0_[1], s1_[1]);
                         } else if (mv && n < a.N) {
                             const uint32_t w4[4] = {s0_[0], s1_[0], s0_[1], s1_[1]};
@@ -443,8 +471,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     }
                     if constexpr (C::FN % 2) {                 // odd fragment count: 8-byte stores for the last one
                         const int n = n0 + bcol + (C::FN - 1) * 16 + 4 * lg;
-                        if (mv && n + 4 <= a.N)
+                        if (slk_on) {
+                            const uint32_t bo = mv && n + 4 <= a.N ? (uint32_t)((orow * a.ldc + n) * 2) : OOB;
+                            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk[C::FN - 1][0], pk[C::FN - 1][1]}, cr, bo, 0, 0);
+                        } else if (mv && n + 4 <= a.N) {
                             *reinterpret_cast<uint2*>(Crow + n) = make_uint2(pk[C::FN - 1][0], pk[C::FN - 1][1]);
+                        }
                     }
                     if constexpr (SUMS) {
                         // flush one slab row pair per 64 rows (4 fragments) of the wave; the slab has one row pair
@@ -534,14 +566,27 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             for (int i = 0; i < C::FM; ++i)
 #pragma unroll
                 for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
+            if (slk_on) slk = D - 1;
     };
     {
         for (int q = 0; q < Q; ++q) {
             // ---------------- load segment ----------------
             const bool more = q + D < Q;
-            if (more) pp_vmwait<(D - 2) * NIT>();       // stream slice q+1 landed (this wave's copies)
-            else pp_retire<NIT, D>(Q - q - 2);
+            if (more) {                                  // stream slice q+1 landed (this wave's copies)
+                if constexpr (SLK) {
+                    if (slk > 0) {                       // ... issued before the last epilogue's stores
+                        --slk;
+                        if (slk_aux) pp_vmwait<(D - 2) * NIT + SE1>();
+                        else pp_vmwait<(D - 2) * NIT + SE0>();
+                    } else {
+                        pp_vmwait<(D - 2) * NIT>();
+                    }
+                } else {
+                    pp_vmwait<(D - 2) * NIT>();
+                }
+            } else {
+                pp_retire<NIT, D>(Q - q - 2);
+            }
             const bf16_t* A_ = sb + rd_off;
             const bf16_t* B_ = A_ + C::IMA;
             rd_off = rd_off + C::SLOT == NB * C::SLOT ? 0 : rd_off + C::SLOT;
@@ -650,7 +695,15 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
             if (++s < cur_n) continue;
+            // epilogue pairing (tuning pp_epi_pair): the staggered groups would write their halves of the tile in
+            // consecutive barrier intervals, each one's epilogue beside the other's last / first compute segment,
+            // i.e. two epilogue-long intervals per item with one wave per SIMD working.  Group 0 waits out group
+            // 1's last compute segment at one extra barrier and group 1 takes one extra barrier after its
+            // epilogue: both epilogues share one interval and the stagger resumes (RAW / WAR of the ring unchanged:
+            // every read and refill keeps its order against the barriers it depended on)
+            if (a.epi_pair && grp == 0) __builtin_amdgcn_s_barrier();
             epilogue();
+            if (a.epi_pair && grp == 1) __builtin_amdgcn_s_barrier();
         }
         if (grp == 0) __builtin_amdgcn_s_barrier();      // balance the stagger
     }
@@ -812,6 +865,12 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     GemmArgs b = a;
     b.nb2 = splits;
     b.dbg = g_pp_trace;
+    b.epi_slack = 0;
+    b.epi_pair = tune().pp_epi_pair;
+    if constexpr (EM == E_BF16 && FX == 0) {
+        const long bytes = (long)a.M * a.ldc * 2;
+        if (tune().pp_epi_slack && !a.scatter && a.N % 8 == 0 && bytes < (1L << 31)) b.epi_slack = (int)bytes;
+    }
     if constexpr (C::DT == 2) {            // 64-deep slices (callers: K % 64 == 0, no split-K)
         b.ktiles_per_split = a.K / 64;
         b.ksl_rem = 0;

@@ -17,6 +17,15 @@ namespace pg {
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
     X(pp_sk64, 1, "96 / 128-wide ping-pong tiles with K-major operands and K % 64 == 0 (no split-K) stream 64-deep "  \
                   "slices (128-byte rows) instead of 32-deep; 0 = 32-deep")                                    \
+    X(pp_epi_slack, 1, "ping-pong plain bf16 epilogues store through buffer stores (every wave issues the same " \
+                       "count) and the next item's first load waits leave them in flight, so a tile's store drain " \
+                       "overlaps the next item's MFMAs instead of stalling its first slice; 0 = drain at once. "  \
+                       "LM-head forward 888 -> 873 us alone, bit-identical (gpurun_out/r6_09, r6_12)")            \
+    X(pp_epi_pair, 1, "ping-pong engine: the two staggered wave groups write their tile halves in the same barrier " \
+                      "interval (one extra barrier each per item) instead of one after the other beside the other " \
+                      "group's compute (two epilogue-long intervals per item at one wave per SIMD).  With "         \
+                      "pp_epi_slack: LM-head forward 888 -> 759 us, GPT-2 N = 768 GEMMs -10..16%, GPT-2 step "      \
+                      "591k -> 622k tok/s, ResNet-50 11,835 -> 11,899 img/s same box, bit-identical (r6_12)")       \
     X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
                            "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \

@@ -480,6 +480,38 @@ def test_pp_narrow_tile_forms_with_epilogues(K, bn, form, M, N, Kd):
         K.tune_set("pp", old_pp)
 
 
+@pytest.mark.parametrize("bn", [96, 128, 192, 256, 288])
+@pytest.mark.parametrize("M,N,Kd", [(8192, 3072, 768), (4000, 1000, 320), (2048, 8192, 64)])
+def test_pp_epilogue_store_slack_and_pairing(K, bn, M, N, Kd):
+    """Deferred store drain (tuning pp_epi_slack: buffer-store epilogue, the next items' load waits relaxed) and
+    epilogue pairing (pp_epi_pair: both wave groups' epilogues in one barrier interval) give the bits of the
+    plain schedule -- several items per block, ragged edges (dropped out-of-range stores), GELU's second output
+    -- and match the fp32 reference."""
+    old_bn, old_pp = K.tune_set("pp_bn", bn), K.tune_set("pp", 2)
+    old_sl, old_pr = K.tune_get("pp_epi_slack"), K.tune_get("pp_epi_pair")
+    try:
+        x, w = rnd(M, Kd), rnd(N, Kd, scale=0.05)
+        bias = torch.randn(N, device="cuda")
+        outs = {}
+        for sl, pr in ((0, 0), (1, 0), (0, 1), (1, 1)):
+            K.tune_set("pp_epi_slack", sl)
+            K.tune_set("pp_epi_pair", pr)
+            aux = torch.full((M, N), 7.0, device="cuda", dtype=torch.bfloat16)
+            y = K.gemm_nt_ex(x, w, bias=bias, act=2, aux=aux)
+            outs[sl, pr] = (y, aux, K.gemm_nt_ex(x, w))
+        for key in ((1, 0), (0, 1), (1, 1)):
+            for a, b in zip(outs[0, 0], outs[key]):
+                assert torch.equal(a, b), key
+        ref = x.float() @ w.float().t()
+        assert rel(outs[1, 1][2], ref) < 1e-2
+        assert rel(outs[1, 1][1], ref + bias) < 1e-2
+    finally:
+        K.tune_set("pp_bn", old_bn)
+        K.tune_set("pp", old_pp)
+        K.tune_set("pp_epi_slack", old_sl)
+        K.tune_set("pp_epi_pair", old_pr)
+
+
 def test_transpose_bf16_multi(K):
     """One launch over many matrices (ragged edges, > 64 entries so the host splits the table)."""
     shapes = [(768, 2304), (3072, 768), (100, 37), (8, 8), (50257, 768)] + [(64 + i, 72 + 3 * i) for i in range(70)]
