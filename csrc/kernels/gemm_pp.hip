@@ -296,8 +296,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
     // SE0 (SE1 with the GELU pre-activation) of them per item, and the next D-1 load segments, whose awaited
     // slices were issued before those stores, wait for vmcnt((D-2) NIT + SE) instead: the stores drain under
     // the next item's MFMAs.
-    constexpr bool SLK = EM == E_BF16 && FX == 0;
-    constexpr int SE0 = C::FM * (C::FN / 2 + C::FN % 2), SE1 = SE0 + C::FM * C::FN;
+    // (fp32 epilogues -- weight gradients, split-K slabs -- likewise: one 16-byte store per fragment)
+    constexpr bool SLK = (EM == E_BF16 || EM == E_F32) && FX == 0;
+    constexpr int SE0 = EM == E_F32 ? C::FM * C::FN : C::FM * (C::FN / 2 + C::FN % 2);
+    constexpr int SE1 = EM == E_F32 ? SE0 : SE0 + C::FM * C::FN;
     static_assert(!SLK || (D - 2) * NIT + SE1 <= 63, "vmcnt immediate");
     const bool slk_on = SLK && a.epi_slack > 0;
     const bool slk_aux = slk_on && a.relu == 2 && a.ep_aux != nullptr;
@@ -528,9 +530,25 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                     // otherwise store / accumulate (acc_c) into C
                     const bool slab = splits > 1;
                     float* const Cb = reinterpret_cast<float*>(a.C) + (slab ? z * a.sC1 : 0);
+                    [[maybe_unused]] __amdgpu_buffer_rsrc_t cr;
+                    if constexpr (SLK) cr = __builtin_amdgcn_make_buffer_rsrc(Cb, 0, a.epi_slack, 0x00020000);
 #pragma unroll
                     for (int fn = 0; fn < C::FN; ++fn) {
                         const int n = n0 + bcol + fn * 16 + 4 * lg;
+                        if (slk_on) {              // (N, ldc % 4 == 0: whole float4 groups; no bias / activation)
+                            const bool ok = mv && n < a.N;
+                            float v[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = acc[fm][fn][j] * alpha;
+                            if (a.acc_c && !slab && ok) {
+                                const float4 o = *reinterpret_cast<const float4*>(Cb + (long)m * a.ldc + n);
+                                v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+                            }
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                __builtin_bit_cast(u32x4_t, f32x4_t{v[0], v[1], v[2], v[3]}), cr,
+                                ok ? (uint32_t)(((long)m * a.ldc + n) * 4) : OOB, 0, 0);
+                            continue;
+                        }
                         if (!mv || n >= a.N) continue;
                         float v[4];
 #pragma unroll
@@ -870,6 +888,11 @@ int launch_cfg(const GemmArgs& a, int splits, hipStream_t st) {
     if constexpr (EM == E_BF16 && FX == 0) {
         const long bytes = (long)a.M * a.ldc * 2;
         if (tune().pp_epi_slack && !a.scatter && a.N % 8 == 0 && bytes < (1L << 31)) b.epi_slack = (int)bytes;
+    }
+    if constexpr (EM == E_F32 && FX == 0) {          // range of one output (or one split-K slab)
+        const long bytes = (long)a.M * a.ldc * 4;
+        if (tune().pp_epi_slack >= 2 && a.N % 4 == 0 && a.ldc % 4 == 0 && !a.bias && a.relu == 0 && bytes < (1L << 31))
+            b.epi_slack = (int)bytes;
     }
     if constexpr (C::DT == 2) {            // 64-deep slices (callers: K % 64 == 0, no split-K)
         b.ktiles_per_split = a.K / 64;

@@ -17,10 +17,12 @@ namespace pg {
     X(pp_bn, 0, "force the ping-pong tile width (96/128/192/256/288; 0 automatic; tests)")                \
     X(pp_sk64, 1, "96 / 128-wide ping-pong tiles with K-major operands and K % 64 == 0 (no split-K) stream 64-deep "  \
                   "slices (128-byte rows) instead of 32-deep; 0 = 32-deep")                                    \
-    X(pp_epi_slack, 1, "ping-pong plain bf16 epilogues store through buffer stores (every wave issues the same " \
-                       "count) and the next item's first load waits leave them in flight, so a tile's store drain " \
-                       "overlaps the next item's MFMAs instead of stalling its first slice; 0 = drain at once. "  \
-                       "LM-head forward 888 -> 873 us alone, bit-identical (gpurun_out/r6_09, r6_12)")            \
+    X(pp_epi_slack, 2, "ping-pong plain epilogues store through buffer stores (every wave issues the same count) " \
+                       "and the next item's first load waits leave them in flight, so a tile's store drain overlaps " \
+                       "the next item's MFMAs instead of stalling its first slice: 1 = bf16 outputs, 2 = also the "  \
+                       "fp32 ones (weight gradients, split-K slabs), 0 = drain at once.  Bit-identical; LM-head "    \
+                       "forward 888 -> 873 us (r6_09, r6_12); 2 vs 1: GPT-2 624.2k / 625.5k -> 632.0k / 630.9k "    \
+                       "tok/s, ResNet-50 11,911 -> 11,929 img/s same box (r6_13)")                                   \
     X(pp_epi_pair, 1, "ping-pong engine: the two staggered wave groups write their tile halves in the same barrier " \
                       "interval (one extra barrier each per item) instead of one after the other beside the other " \
                       "group's compute (two epilogue-long intervals per item at one wave per SIMD).  With "         \

@@ -448,6 +448,17 @@ def test_pp_wgrad_uneven_splits(K, Kd, M, N, splits):
     K.pp_wgrad(x, y, out2, splits=splits, rowsum=rs)
     assert rel(out2, x.float().t() @ y.float()) < 2e-5
     assert rel(rs, rs_ref) < 2e-5
+    # fp32 epilogues through buffer stores with the drain deferred (pp_epi_slack 2): the same bits
+    outs = []
+    for sl in (1, 2):
+        old = K.tune_set("pp_epi_slack", sl)
+        try:
+            o = out.clone()
+            K.pp_wgrad(x, y, o, splits=splits)
+            outs.append(o)
+        finally:
+            K.tune_set("pp_epi_slack", old)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("bn,form", [(96, "sk64"), (96, "sk32"), (128, "sk64"), (128, "sk32")])
