@@ -1124,8 +1124,9 @@ PDNN_API int pdnn_pp_gemm_nt_splitk(const bf16_t* X, long ldx, const bf16_t* W, 
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = W; a.ldb = ldw; a.alpha = 1.f;
     const int nsl = K / PP_SK;
-    while (nsl % splits) --splits;
-    a.ktiles_per_split = nsl / splits;
+    if (splits > nsl) splits = nsl;
+    a.ktiles_per_split = nsl / splits;             // the first nsl % splits splits take one slice more
+    a.ksl_rem = nsl % splits;
     const long sz = (long)M * N + 64;             // padded slab stride (see pdnn_pp_wgrad)
     a.C = ws; a.ldc = N; a.sC1 = sz;
     int e = launch_bn<A_KMAJOR, B_KMAJOR, E_F32>(a, 256, splits, st);
@@ -1135,7 +1136,11 @@ PDNN_API int pdnn_pp_gemm_nt_splitk(const bf16_t* X, long ldx, const bf16_t* W, 
     PDNN_LAUNCH_RET;
 }
 
-// split count for pdnn_pp_gemm_nt_splitk: whole rounds of 256 x 256 tiles over the CUs, each item >= 64 slices
+// split count for pdnn_pp_gemm_nt_splitk (uneven splits: the first nsl % s take one slice more), minimising
+//   rounds x (slices of the longest item + 10) x 0.8 us  +  2 x slab bytes / 5 TB/s
+// (256 x 256 tiles, ~0.8 us per 32-deep slice and item round, ~10 slices' worth of per-item prologue / epilogue;
+// the slabs are written and read back by the reduction).  The tied LM head's data gradient (8192 x 768 x 50304)
+// went from 2 splits (192 of 256 CUs) to 8 (three whole rounds).
 PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
     using namespace pg;
     const long tiles = cdiv(M, PP_BM) * cdiv(N, 256);
@@ -1143,9 +1148,10 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
     int best = 1;
     double bt = 1e300;
     for (int s = 1; s <= 16; ++s) {
-        if (nsl % s || nsl / s < 64) continue;
-        const double t = (double)cdiv(tiles * s, cus) / s + 0.02 * s;     // rounds per unit work + slab cost
-        if (t < bt) { bt = t; best = s; }
+        if (nsl / s < 32) break;
+        const double t = (double)cdiv(tiles * s, cus) * (cdiv(nsl, s) + 10) * 0.8
+                       + (s > 1 ? 2.0 * s * M * N * 4 / 5e6 : 0.0);
+        if (t < bt * 0.999) { bt = t; best = s; }
     }
     return best;
 }
