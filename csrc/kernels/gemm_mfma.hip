@@ -999,6 +999,14 @@ PDNN_API int pdnn_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nimg
     a.g.dHW = make_fdiv(Ho * Wo); a.g.dW = make_fdiv(Wo);
     a.pro_scale = pro_scale; a.pro_shift = pro_shift; a.stats = stats;
     a.ktiles_per_split = (int)cdiv(a.K, BK);
+    if (R == 1 && S == 1 && st == 1 && pad == 0 && !pro_scale && C >= tune().pp_conv_fwd_c) {
+        // 1x1 stride-1 without a prologue is the plain GEMM y[P][Ko] = x[P][C] . w[Ko][C]^T: the ping-pong engine
+        // with its statistics epilogue (ResNet-50's conv1 / shortcut forwards with C >= 512)
+        GemmArgs p{};
+        p.M = a.M; p.N = Ko; p.K = C;
+        p.A = x; p.lda = C; p.B = w; p.ldb = C; p.C = y; p.ldc = Ko; p.alpha = 1.f; p.stats = stats;
+        if (pp_supported(p, A_KMAJOR, B_KMAJOR, E_BF16, 1, 1)) return pp_launch(p, A_KMAJOR, B_KMAJOR, E_BF16, stream);
+    }
     if (pro_scale) return launch<A_CONV, B_KMAJOR, E_BF16, true, false>(a, 1, stream);
     return launch<A_CONV, B_KMAJOR, E_BF16, false, false>(a, 1, stream);
 }

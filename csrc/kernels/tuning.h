@@ -31,6 +31,10 @@ namespace pg {
     X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
                            "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
+    X(pp_conv_fwd_c, 512, "1x1 / stride-1 conv forwards without an operand prologue on the ping-pong engine " \
+                          "(statistics epilogue) from this many input channels (1 << 20 = never: the implicit-GEMM " \
+                          "engines).  ResNet-50's conv1 / shortcut forwards with C >= 512: 11,907 / 11,956 -> "     \
+                          "12,015 / 12,007 img/s same box (gpurun_out/r6_16)")                                      \
     X(pp_dgrad_bn_k, 1024, "1x1 data gradients with the BN-backward epilogue on the ping-pong engine from this "   \
                            "reduction length (ResNet-50 conv3 stages 3-4; gpurun_out/r4_15-17)")                 \
     X(comm_cus, 0, "CUs the persistent grids (ping-pong GEMMs, stem) leave free for RCCL's channel blocks while " \
