@@ -70,7 +70,10 @@ def test_graph_step_matches_eager(name, opt_name, shape, lr, tol):
         assert abs(a - b) < tol * max(1.0, abs(a)), (losses_e, losses_g)
     d = _delta_rel(mg._pdnn_flat.data, me._pdnn_flat.data, p0)
     d_eager = _delta_rel(mt._pdnn_flat.data, me._pdnn_flat.data, p0)      # run-to-run drift of the eager path
-    assert d < max(2.5 * tol, 3.0 * d_eager), (d, d_eager)
+    # the eager drift (fp32-atomic BN statistic bins) may widen the bound, but only up to a fixed multiple of tol:
+    # a real graph / eager divergence cannot hide behind a noisy eager pair
+    assert d_eager < 4.0 * tol, (d, d_eager)
+    assert d < max(2.5 * tol, 3.0 * min(d_eager, 4.0 * tol)), (d, d_eager)
     # bf16 shadow refreshed by the replayed optimizer kernel
     fp = mg._pdnn_flat
     assert ((fp.shadow.float() - fp.data).norm() / fp.data.norm()).item() < 5e-3

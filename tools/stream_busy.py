@@ -12,6 +12,7 @@ def main():
     ap.add_argument("--last", type=int, default=3)
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--step-kernel", default="(sgd|adam)_kernel")
+    ap.add_argument("--full", action="store_true", help="keep template arguments and the grid size in the names")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
@@ -29,7 +30,7 @@ def main():
             busy[q] += d
             n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("pg::", "").replace("void ", "")
             n = re.sub(r"\((?!anon).*", "", n)
-            kern[q][re.sub(r"<.*", "", n)] += d
+            kern[q][f"{n} grid={r.get('Grid_Size', r.get('Grid_Size_X', ''))}" if a.full else re.sub(r"<.*", "", n)] += d
     n = len(steps)
     print(f"steps={n} span ms/step={sum(spans) / n:.3f} " + " ".join(f"queue{q}={v / n / 1e3:.3f}ms" for q, v in sorted(busy.items())))
     for q in sorted(kern):
