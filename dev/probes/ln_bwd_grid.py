@@ -1,5 +1,7 @@
 """LayerNorm backward grid sweep on GPT-2's shape (8192 x 768, with the residual-gradient add): rows per block x
-block cap (tuning ln_bwd_rows / ln_bwd_blocks), us per call including its bins finalize."""
+block cap, us per call including its bins finalize.  The two tuning entries it sets (ln_bwd_rows / ln_bwd_blocks)
+existed only for this sweep (gpurun_out/r6_19, profiles/layernorm_bwd_grid_r6.txt) and were removed with the
+defaults kept; re-add them to csrc/kernels/tuning.h (pdnn_layernorm_bwd_blocks) to rerun it."""
 import json
 import os
 import sys
