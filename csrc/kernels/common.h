@@ -37,6 +37,20 @@ __device__ __forceinline__ float* stat_row(float* slab, long row, int C) {
     return slab + (long)(2 * (row & (STAT_BINS - 1))) * C;
 }
 __device__ __forceinline__ void stat_add(float* p, float v) { atomicAdd(p, v); }
+// The statistics of one 16-column MFMA fragment in ONE atomic instruction: after row16_sum every lane of a 16-lane
+// row holds the 4 columns' sums (s) and second sums (q) of its column group lg = lane >> 4; lane lm = lane & 15 < 4
+// adds s[lm] to column 4 lg + lm of the s row, lane 4 <= lm < 8 adds q[lm - 4] to the q row (ps / pq: this lane's
+// column group, column 4 lg), 32 lanes on two 64-byte lines.  It replaces eight 4-lane atomics (one per (j, s|q)):
+// ResNet-50's A-stationary 1x1 forwards spent 23-57 us per call on them (gpurun_out/r6_21).  `ok` (per lane):
+// this lane's column exists; qx (optional) transforms the q value of column j before the add.
+__device__ __forceinline__ float sel4(const float (&v)[4], int j) {
+    return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
+}
+__device__ __forceinline__ void stat_add_frag(float* ps, float* pq, int lane, const float (&s)[4], const float (&q)[4],
+                                              bool ok) {
+    const int lm = lane & 15, j = lm & 3;
+    if (lm < 8 && ok) stat_add(lm < 4 ? ps + j : pq + j, lm < 4 ? sel4(s, j) : sel4(q, j));
+}
 
 __device__ __forceinline__ float bf2f(bf16_t v) {
     return __uint_as_float(((uint32_t)v) << 16);

@@ -252,15 +252,17 @@ __device__ __forceinline__ void c3_epilogue_rows(const C3Args& a, f32x4_t (&acc)
                     s[j] = row16_sum(s[j]);
                     q[j] = row16_sum(q[j]);
                 }
-                if ((lane & 15) == 0) {
+                {
                     float* ps = stat_row(a.stats, (long)tile * 4 + wave, a.N) + n;
-                    float* pq = ps + a.N;
                     if constexpr (EPI == C3_BNB) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) q[j] = (q[j] - a.ep_mean[n + j] * s[j]) * a.ep_invstd[n + j];
+                        // lane lm in 4..7 adds column j = lm - 4's sum gm * xhat: only its own mean / invstd
+                        const int j = lane & 3;
+                        if ((lane & 12) == 4) {
+                            const float qj = (sel4(q, j) - a.ep_mean[n + j] * sel4(s, j)) * a.ep_invstd[n + j];
+                            q[0] = q[1] = q[2] = q[3] = qj;
+                        }
                     }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) { stat_add(ps + j, s[j]); stat_add(pq + j, q[j]); }
+                    stat_add_frag(ps, ps + a.N, lane, s, q, true);
                 }
             }
         }

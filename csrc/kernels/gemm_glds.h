@@ -525,15 +525,12 @@ gemm_glds_kernel(GemmArgs a) {
                     const int grp = m0 + wm * WTM + (fm / 4) * 64;           // first row of these 64
                     const int slab_row = a.stats_row0 + grp / 64;
                     // the slab has one row pair per 64 rows of M rounded up to 128 (the 128-tile layout)
-                    if (lm == 0 && grp < ((a.M + 127) / 128) * 128) {
+                    if (grp < ((a.M + 127) / 128) * 128) {
 #pragma unroll
                         for (int fn = 0; fn < FN; ++fn) {
                             const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
                             float* ps = stat_row(a.stats, slab_row, a.N) + n;
-                            float* pq = ps + a.N;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (n + j < a.N) { stat_add(ps + j, s_[fn][j]); stat_add(pq + j, q_[fn][j]); }
+                            stat_add_frag(ps, ps + a.N, lane, s_[fn], q_[fn], n + (lm & 3) < a.N);
                         }
                     }
 #pragma unroll

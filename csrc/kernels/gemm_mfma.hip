@@ -624,18 +624,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
                 }
             }
         }
-        if (want_stats && lm == 0) {
+        if (want_stats) {
             const long row = (long)(a.stats_row0 + tm * 2 + wm) * 2;
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) {
                 const int n = n0 + wn * WTN + fn * 16 + 4 * lg;
-                if (n >= a.N) continue;
                 float* ps = stat_row(a.stats, row / 2, a.N) + n;
-                float* pq = ps + a.N;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (n + j < a.N) { stat_add(ps + j, ss[fn][j]); stat_add(pq + j, qs[fn][j]); }
-                }
+                stat_add_frag(ps, ps + a.N, lane, ss[fn], qs[fn], n + (lm & 3) < a.N);
             }
         }
         if constexpr (EM == E_BF16) {

@@ -492,26 +492,22 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmArgs a) {
                                     q_[fn][j] = row16_sum(q_[fn][j]);
                                 }
                             const int g64 = m0 + arow + (fm / 4) * 64;
-                            if (lm == 0 && g64 < ((a.M + 127) / 128) * 128) {
+                            if (g64 < ((a.M + 127) / 128) * 128) {
 #pragma unroll
                                 for (int fn = 0; fn < C::FN; ++fn) {
                                     const int n = n0 + bcol + fn * 16 + 4 * lg;
-                                    if (n < a.N) {
-                                        if constexpr ((FX & FX_BNB) != 0) {
-                                            const float4 mu = *reinterpret_cast<const float4*>(a.ep_mean + n);
-                                            const float4 is = *reinterpret_cast<const float4*>(a.ep_invstd + n);
-                                            q_[fn][0] = is.x * (q_[fn][0] - mu.x * s_[fn][0]);
-                                            q_[fn][1] = is.y * (q_[fn][1] - mu.y * s_[fn][1]);
-                                            q_[fn][2] = is.z * (q_[fn][2] - mu.z * s_[fn][2]);
-                                            q_[fn][3] = is.w * (q_[fn][3] - mu.w * s_[fn][3]);
-                                        }
-                                        float* ps = stat_row(a.stats, g64 / 64, a.N) + n;
-#pragma unroll
-                                        for (int j = 0; j < 4; ++j) {
-                                            stat_add(ps + j, s_[fn][j]);
-                                            stat_add(ps + a.N + j, q_[fn][j]);
+                                    const int jj = lm & 3;
+                                    const bool okn = n + jj < a.N;
+                                    if constexpr ((FX & FX_BNB) != 0) {
+                                        // lanes lm 4..7 add column jj's sum gm * xhat (their own mean / invstd)
+                                        if ((lm & 12) == 4 && okn) {
+                                            const float qj = a.ep_invstd[n + jj] *
+                                                             (sel4(q_[fn], jj) - a.ep_mean[n + jj] * sel4(s_[fn], jj));
+                                            q_[fn][0] = q_[fn][1] = q_[fn][2] = q_[fn][3] = qj;
                                         }
                                     }
+                                    float* ps = stat_row(a.stats, g64 / 64, a.N) + n;
+                                    stat_add_frag(ps, ps + a.N, lane, s_[fn], q_[fn], okn);
                                 }
                             }
 #pragma unroll
