@@ -225,9 +225,13 @@ FastDiv sw_fdiv(uint32_t d) {
     return f;
 }
 
+// blocks (each a fixed run of tiles; two fit a CU): tuning stem_wgrad_blocks.  At the end of the ResNet backward this
+// kernel can start while the side stream still holds CUs; a grid of exactly two blocks per CU then leaves a late
+// CU with two runs in sequence
 int sw_blocks(long P) {
     const long tiles = (P + SW_BM - 1) / SW_BM;
-    return (int)(tiles < 512 ? tiles : 512);     // two per CU
+    const long cap = pg::tune().stem_wgrad_blocks;
+    return (int)(tiles < cap ? tiles : cap);
 }
 }  // namespace
 

@@ -28,6 +28,10 @@ namespace pg {
                       "group's compute (two epilogue-long intervals per item at one wave per SIMD).  With "         \
                       "pp_epi_slack: LM-head forward 888 -> 759 us, GPT-2 N = 768 GEMMs -10..16%, GPT-2 step "      \
                       "591k -> 622k tok/s, ResNet-50 11,835 -> 11,899 img/s same box, bit-identical (r6_12)")       \
+    X(stem_wgrad_blocks, 2048, "ImageNet stem weight gradient: grid cap (fixed runs of 96-pixel tiles per block; two " \
+                               "blocks fit a CU).  At 512 the kernel took 325-330 or 498-501 us inside the ResNet-50 "  \
+                               "step (a launch overlapping the side stream's last kernel leaves a CU with two runs in " \
+                               "sequence), 2048: 330-360 (gpurun_out/r6_26); alone 370 vs 390 us (r6_25)")              \
     X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
                            "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
