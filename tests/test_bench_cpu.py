@@ -49,7 +49,7 @@ def test_bench_world2_prints_one_line_with_comm_block():
 
 
 def test_bench_world2_gpt2_split_tied_embedding():
-    """GPT-2 at N > 1: 32 MB bucket cap (128 MB only where the all-reduce is a no-op), the tied wte's LM-head part
+    """GPT-2 at N > 1: 32 MB bucket cap (256 MB only where the all-reduce is a no-op), the tied wte's LM-head part
     is bucket 0 and its embedding rows are gathered separately (comm.split_tied_embedding)."""
     r = _torchrun(2, ["--model", "gpt2_tiny", "--batch", "2", "--seq-len", "32", "--steps", "2", "--warmup", "1"],
                   {}, 300)
