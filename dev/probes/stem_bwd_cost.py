@@ -44,6 +44,12 @@ def main():
     out = {"stem_wgrad_warm_us": [round(w, 1) for w in warm], "stem_wgrad_cold_us": sorted(round(c, 1) for c in cold)}
     fn2 = lambda: K.stem_wgrad_nchw(x, dt, acc=acc)   # noqa: E731
     out["stem_wgrad_nopre_warm_us"] = sorted(round(ev_time(fn2), 1) for _ in range(10))
+    dy = (torch.randn(N, 56, 56, 64, device="cuda") * 0.1).to(BF)
+    idx = torch.randint(0, 9, (N, 56, 56, 64), device="cuda", dtype=torch.uint8)
+    fn3 = lambda: K.maxpool_bwd_bnred(dy, idx, t, v[0], v[1], v[2], v[3])   # noqa: E731
+    fn3()
+    torch.cuda.synchronize()
+    out["maxpool_bwd_bnred_us"] = sorted(round(ev_time(fn3), 1) for _ in range(10))
     print(json.dumps(out), flush=True)
 
 
