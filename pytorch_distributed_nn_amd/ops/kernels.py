@@ -556,7 +556,7 @@ def conv_wgrad(x, dy, R, S, st, pad, pro=None, out=None):
         ws = torch.empty(lib().pdnn_conv3x3s2_wgrad_ws(N, H, W, C, K), device=x.device, dtype=F32)
         call("pdnn_conv3x3s2_wgrad", ptr(x), ptr(dy), ptr(out), N, H, W, C, K, ptr(ws), ptr(sc), ptr(sh), stream())
         return out
-    if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _WGRAD1X1_PP_PIX
+    if (pro is None and R == 1 and S == 1 and st == 1 and pad == 0 and P <= _tuning.get("wgrad1x1_pp_pix")
             and P % 32 == 0 and K % 8 == 0 and C % 8 == 0):
         # plain GEMM dW[K][C] = dy[P][K]^T . x[P][C] on the ping-pong engine (split-K slabs, split count from
         # the long-reduction model): ResNet stages 2-4 (tools/bench_wgrad1x1.py, gpurun_out/r3_33, r3_38).  The joint

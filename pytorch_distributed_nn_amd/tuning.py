@@ -24,6 +24,9 @@ colsum_atomic      1        accumulating bias-gradient column sums in one launch
                             deterministic partial rows + level-2 launch; GPT-2 542.3k vs 538.0k tok/s, r5_10)
 bias_in_wgrad      1        GPT-2 linear bias gradients as fused row sums inside the weight-gradient GEMM (0: a
                             column-sum pass over the output gradient)
+wgrad1x1_pp_pix    200704   1x1 / stride-1 weight gradients without an operand prologue on the ping-pong engine up to
+                            this many pixels (ResNet-50 stages 2-4 at bs 256; stage 1 stays on the implicit-GEMM
+                            engine's split-K atomics: tools/bench_wgrad1x1.py, gpurun_out/r3_38-40)
 ds_sub             1        stride-2 1x1 shortcut convs read a contiguous copy of their input's even pixels (one
                             subsample pass): the forward then runs as a stride-1 1x1 conv, the weight gradient as a
                             plain GEMM on the ping-pong engine (0: the implicit-GEMM engine's strided gathers)
@@ -49,7 +52,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1, "wgrad1x1_pp_pix": 200704}
 
 _VALUES = dict(DEFAULTS)
 
