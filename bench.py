@@ -260,12 +260,13 @@ def main():
     if use_ddp and on_gpu and a.opt_overlap and isinstance(net, DistributedDataParallel):
         opt_overlap = net.overlap_optimizer(opt) is not None
 
-    # auto: graphed on one GPU, except the ImageNet ResNets, whose weight gradients run on a side stream
+    # auto: graphed on one GPU, except the ImageNet ResNets and GPT-2, whose weight gradients run on a side stream
     # concurrently with the data-gradient chain (ops/fused_resnet.py): eager launches overlap the two
     # streams (ResNet-50 8,635 vs 8,013 img/s serial), a replayed hipGraph ran the branches nearly serially
     # (8,160-8,196 img/s; gpurun_out/r2_32)
     from pytorch_distributed_nn_amd import tuning
-    side_overlap = not lm and not small and tuning.get("side_wgrad") == 1
+    side_overlap = (not lm and not small and tuning.get("side_wgrad") == 1) or (
+        lm and tuning.get("gpt2_side_wgrad") >= 1 and tuning.get("side_wgrad") == 1)
     use_graph = a.graph == "on" or (a.graph == "collectives") or (a.graph == "auto" and not use_ddp
                                                                    and not side_overlap)
     if use_graph:

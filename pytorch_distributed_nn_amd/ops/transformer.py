@@ -192,10 +192,16 @@ def _wgrad(g, x, shape):
 class _Sink:
     """Routes parameter gradients straight into the flat arena when possible (optim.flat.direct_grad):
     the GEMM / column-sum / LayerNorm kernels accumulate in place, the op returns None for the parameter
-    and announces it with grad_ready.  Otherwise the gradient is returned to autograd."""
+    and announces it with grad_ready.  Otherwise the gradient is returned to autograd.
+
+    tuning gpt2_side_wgrad: arena-bound weight gradients run on the ResNets' weight-gradient side stream
+    (ops/fused_resnet.py) beside the data-gradient chain, joined like theirs (at the end of the backward when
+    every hook reading them is side-aware, i.e. DDP's bucket launches)."""
 
     def __init__(self):
         self.ready = []
+        self.side = None
+        self.forked = False
 
     def _tgt(self, p):
         t = direct_grad(p)
@@ -203,13 +209,34 @@ class _Sink:
             self.ready.append(p)
         return t
 
+    def _side(self, g):
+        if not _tuning.get("gpt2_side_wgrad") or not g.is_cuda:
+            return None
+        from .fused_resnet import _side_stream
+        return _side_stream(g.device)
+
     def linear(self, p_w, p_b, g, x):
         tw = self._tgt(p_w)
         tb = self._tgt(p_b) if p_b is not None else None
+        bias_in = tb if _tuning.get("bias_in_wgrad") else None
+        side = self._side(g) if tw is not None and (p_b is None or tb is not None) else None
+        if side is not None:
+            main = torch.cuda.current_stream(g.device)
+            K.stream_wait(side, main)
+            with torch.cuda.stream(side):
+                bias_done = BL.wgrad_acc(g, x, tw, bias=bias_in)
+                if p_b is not None and not bias_done:
+                    K.colsum(g, out=tb, accumulate=True, deterministic=not _tuning.get("colsum_atomic"))
+            for t in (g, x):
+                t.record_stream(side)
+            self.side, self.forked = side, True
+            from .fused_resnet import _FORKS
+            _FORKS[g.device.index] = _FORKS.get(g.device.index, 0) + 1
+            return None, None
         bias_done = False
         if tw is not None:
             # the bias gradient fused into the weight-gradient GEMM when both land in the arena
-            bias_done = BL.wgrad_acc(g, x, tw, bias=tb if _tuning.get("bias_in_wgrad") else None)
+            bias_done = BL.wgrad_acc(g, x, tw, bias=bias_in)
             rw = None
         else:
             rw = _wgrad(g, x, p_w.shape)
@@ -230,6 +257,13 @@ class _Sink:
         return K.layernorm_bwd(dy, x, w, m, r, dres=dres)
 
     def done(self):
+        if self.forked:
+            self.forked = False
+            from .fused_resnet import _join_at_backward_end
+            if all(getattr(fn, "_pdnn_side_aware", False) for p in self.ready for fn in getattr(p, "_pdnn_grad_hooks", ())):
+                _join_at_backward_end(self.side)
+            else:
+                K.stream_wait(torch.cuda.current_stream(self.side.device), self.side)
         for p in self.ready:
             grad_ready(p)
 

@@ -523,6 +523,18 @@ def test_pp_epilogue_store_slack_and_pairing(K, bn, M, N, Kd):
         K.tune_set("pp_epi_pair", old_pr)
 
 
+@pytest.mark.parametrize("splits", [None, 1, 2, 3, 5, 8])
+def test_gemm_nt_splitk_uneven(K, splits):
+    """The split-K GEMM of the tied LM head's data gradient (K = vocabulary): split counts that do not divide the
+    K slices give the first K % s splits one slice more; every split count (and the planned one) must give the
+    reference product."""
+    M, N, Kd = 512, 768, 50304
+    x, w = rnd(M, Kd, scale=0.1), rnd(N, Kd, scale=0.05)
+    y = K.gemm_nt_splitk(x, w, splits=splits)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert rel(y, x.float() @ w.float().t()) < 1e-2
+
+
 def test_transpose_bf16_multi(K):
     """One launch over many matrices (ragged edges, > 64 entries so the host splits the table)."""
     shapes = [(768, 2304), (3072, 768), (100, 37), (8, 8), (50257, 768)] + [(64 + i, 72 + 3 * i) for i in range(70)]

@@ -214,6 +214,37 @@ def test_gpt2_flat_arena_grads_match_autograd_path():
         assert rel2(pf.grad, p.grad) < 1e-3, n
 
 
+def test_gpt2_side_stream_weight_gradients():
+    """tuning gpt2_side_wgrad: the linear weight gradients accumulate into the arena on the side stream beside the
+    data-gradient chain (joined at the end of the backward); the gradients must equal the one-stream run's, also
+    over two steps (the next step's zero_grad and forward must wait for the side stream)."""
+    from pytorch_distributed_nn_amd import tuning
+    from pytorch_distributed_nn_amd.optim import AdamW, flatten_module
+    B, T = 4, 128
+    grads = {}
+    for v in (0, 1):
+        old = tuning.set("gpt2_side_wgrad", v)
+        try:
+            torch.manual_seed(0)
+            m = _tiny(seed=5).cuda()
+            fp = flatten_module(m)
+            opt = AdamW(m.parameters(), lr=1e-3)
+            g = torch.Generator(device="cuda").manual_seed(9)
+            out = []
+            for _ in range(2):
+                idx = torch.randint(0, m.config.vocab_size, (B, T), device="cuda", generator=g)
+                tgt = torch.randint(0, m.config.vocab_size, (B, T), device="cuda", generator=g)
+                opt.zero_grad()
+                m(idx, tgt).backward()
+                out.append(fp.grad.clone())
+                opt.step()
+            grads[v] = out
+        finally:
+            tuning.set("gpt2_side_wgrad", old)
+    for a, b in zip(grads[0], grads[1]):
+        assert rel2(b, a) < 1e-4
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 def test_gpt2_prefetched_transposes_track_optimizer_steps(mode):
     """tuning wt_prefetch 1 / 2: the forward refreshes every transposed weight copy in one launch
