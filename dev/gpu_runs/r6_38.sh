@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPT-2 LayerNorm parameter-gradient reduction on the side stream: tests + A/B
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r6_38
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_transformer_gpu.py tests/test_ddp_gpu.py tests/test_graphs_gpu.py tests/test_trajectory_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+run() {
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python3 bench.py --model gpt2_small --no-extra-configs > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; return 1; }
+  python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['ms_per_step'],'plain',d['plain_step_1gpu']['value'])"
+}
+for i in 1 2; do
+run g_$i || exit 1
+done
+echo done
