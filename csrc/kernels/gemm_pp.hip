@@ -1159,7 +1159,8 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
 // 256 wide x 6 splits 62.9 us vs 128 x 3 68.6 us).  A forced width (tuning pp_bn) is kept.
 PDNN_API int pdnn_pp_wgrad_plan(int M, int N, int K) {
     using namespace pg;
-    const int cus = device_cus();
+    const int pc = tune().wgrad_plan_cus;
+    const int cus = pc > 0 && pc < device_cus() ? pc : device_cus();
     const int nsl = K / PP_SK;
     const int force = tune().pp_bn;
     int best_bn = 128, best_s = 1;
