@@ -50,6 +50,7 @@ __device__ __forceinline__ void attn_block(int ntile, int H, bool heavy_is_last,
 #endif
 }
 constexpr int NTA = 256;
+constexpr float RESC = 8.f;     // forward lazy-rescale threshold (log2 units)
 constexpr float LOG2E = 1.4426950408889634f;
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -120,14 +121,21 @@ struct TileLd {
     }
 };
 
-__device__ __forceinline__ float xmax16(float v) {
-    v = fmaxf(v, __shfl_xor(v, 16, 64));
-    return fmaxf(v, __shfl_xor(v, 32, 64));
+// max / sum over the four 16-lane rows (lanes l, l^16, l^32, l^48) by VALU lane swaps: v_permlane16_swap /
+// v_permlane32_swap with both operands v return (v, partner) in some order per lane, so combining the pair is
+// the xor-16 / xor-32 step (no ds_bpermute round trip through the LDS pipe)
+__device__ __forceinline__ float pl16(float v, bool mx) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float a = __uint_as_float(r[0]), b = __uint_as_float(r[1]);
+    return mx ? fmaxf(a, b) : a + b;
 }
-__device__ __forceinline__ float xsum16(float v) {
-    v += __shfl_xor(v, 16, 64);
-    return v + __shfl_xor(v, 32, 64);
+__device__ __forceinline__ float pl32(float v, bool mx) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float a = __uint_as_float(r[0]), b = __uint_as_float(r[1]);
+    return mx ? fmaxf(a, b) : a + b;
 }
+__device__ __forceinline__ float rmax4(float v) { return pl32(pl16(v, true), true); }
+__device__ __forceinline__ float rsum4(float v) { return pl32(pl16(v, false), false); }
 
 // ---------------------------------------------------------------------------------------------- forward
 __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
@@ -217,8 +225,12 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
                 for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kf][f][r]);
-                const float mn = fmaxf(m[f], xmax16(mx) * c);      // scaled-score domain (c > 0)
-                const bool moved = __any(mn != m[f]);
+                // lazy rescale (cdna_hip_programming.md T13): the running maximum moves only when some query's tile
+                // maximum exceeds it by more than 2^RESC in probability terms; below that the tile's P values use
+                // the stale maximum (P <= 2^RESC, exact after the final 1 / l) and O and l keep their scale
+                const float mt = rmax4(mx) * c;                     // scaled-score domain (c > 0)
+                const bool moved = __any(mt > m[f] + RESC);
+                const float mn = moved ? fmaxf(m[f], mt) : m[f];
                 const float alpha = moved ? __builtin_amdgcn_exp2f(m[f] - mn) : 1.f;
                 float rs = 0.f;
 #pragma unroll
@@ -229,7 +241,7 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
                         s[kf][f][r] = p;
                         rs += p;
                     }
-                l[f] = l[f] * alpha + xsum16(rs);
+                l[f] = l[f] * alpha + rs;                           // this lane's partial; rows summed at the end
                 m[f] = mn;
                 if (moved) {
 #pragma unroll
@@ -263,6 +275,7 @@ __global__ void __launch_bounds__(NTA) attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
         const int qi = q0 + 16 * f + (lane & 15);
+        l[f] = rsum4(l[f]);
         const float inv = 1.f / l[f];
         bf16_t* op = out + ((long)b * T + qi) * D + h * HD;
 #pragma unroll
@@ -469,8 +482,7 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
 #pragma unroll
             for (int j = 0; j < 8; ++j) sd += x[j] * y[j];
         }
-        sd += __shfl_xor(sd, 16, 64);
-        sd += __shfl_xor(sd, 32, 64);
+        sd = rsum4(sd);
         dq_ = sd;
         if (g == 0) delta[((long)b * H + h) * T + ql] = sd;
     } else {

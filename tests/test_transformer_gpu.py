@@ -295,6 +295,30 @@ def test_gpt2_tiny_trains():
     assert math.isfinite(loss.item()) and loss.item() < 0.7 * first
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_growing_scores(K, causal):
+    """Scores whose row maximum keeps growing (and jumps) across key tiles: the forward's lazy rescale (the
+    running maximum moves only past a 2^8 margin) must give the same output and log-sum-exp."""
+    from pytorch_distributed_nn_amd.ops import transformer as TX
+    B, T, H = 1, 1024, 2
+    D = 64 * H
+    g = torch.Generator(device="cuda").manual_seed(7)
+    qkv = torch.randn(B * T, 3 * D, device="cuda", generator=g)
+    ramp = torch.linspace(0.2, 6.0, T, device="cuda").view(T, 1)
+    ramp[600:] += 4.0                                        # a jump well past the margin
+    qkv[:, D:2 * D] *= ramp                                  # later keys score higher
+    qkv[:, :D] *= 2.0
+    qkv = qkv.to(torch.bfloat16)
+    y, lse2 = K.flash_attn_fwd(qkv, B, T, H, 0.125, causal)
+    ref = TX.attention_reference(qkv.float(), B, T, H, causal)
+    assert rel2(y, ref) < 1e-2
+    q, k, _ = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if causal:
+        s = s.masked_fill(torch.ones(T, T, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
+    assert rel(lse2, torch.logsumexp(s, -1) * 1.4426950408889634) < 1e-3
+
+
 @pytest.mark.parametrize("B,T,H,causal", [(2, 256, 3, True), (1, 128, 2, False), (2, 1024, 2, True), (1, 384, 1, False)])
 def test_flash_attention(K, B, T, H, causal):
     from pytorch_distributed_nn_amd.ops import transformer as TX
