@@ -313,7 +313,9 @@ __global__ void __launch_bounds__(NTA) attn_bwd_delta_kernel(const bf16_t* __res
     delta[(bidx * H + h) * T + t] = s;
 }
 
-// dK, dV for 64 keys per block (wave w: keys k0 + 16 w .. +15); loop over 64-query tiles
+// dK, dV for 64 NF keys per block (wave w: NF 16-key fragments from k0 = 64 NF kb + 16 NF w); loop over 64-query
+// tiles.  NF = 2 reads every Q / dO fragment out of LDS once for two key fragments (see attn_bwd_dq_kernel).
+template <int NF>
 __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
                                                             const float* __restrict__ lse2, const float* __restrict__ delta,
                                                             bf16_t* __restrict__ dqkv, int T, int H, float scale,
@@ -323,7 +325,7 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
     // compute loop they were waited on behind the next tile's prefetch loads (vmcnt is in order), every tile
     __shared__ __attribute__((aligned(16))) float lsd[2][2][64];              // [buf][lse2|delta][query]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-    const int nkb = T / 64;
+    const int nkb = T / (64 * NF);
     int kb, h, b;
     attn_block(nkb, H, false, kb, h, b);             // early key tiles have the most work: launched first
     const int D = H * HD;
@@ -334,21 +336,24 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
     const bf16_t* dOp = dO + (long)b * T * D + h * HD;
     const float* L2 = lse2 + ((long)b * H + h) * T;
     const float* Dl = delta + ((long)b * H + h) * T;
-    const int k0 = kb * 64 + 16 * w;
-    const int kl = k0 + (lane & 15);                 // this lane's key
+    const int k0 = kb * 64 * NF + 16 * NF * w;
     const float c = scale * LOG2E;
 
-    bf16x8_t kf[2], vf[2];
+    bf16x8_t kf[NF][2], vf[NF][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-        kf[ks] = gfrag(Kp + (long)k0 * ld, ld, ks, lane);
-        vf[ks] = gfrag(Vp + (long)k0 * ld, ld, ks, lane);
-    }
-    f32x4_t dv[4], dk[4];
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dv[i] = dk[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < 2; ++ks) {
+            kf[f][ks] = gfrag(Kp + (long)(k0 + 16 * f) * ld, ld, ks, lane);
+            vf[f][ks] = gfrag(Vp + (long)(k0 + 16 * f) * ld, ld, ks, lane);
+        }
+    f32x4_t dv[NF][4], dk[NF][4];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dv[f][i] = dk[f][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    const int qb0 = causal ? kb : 0;
+    const int qb0 = causal ? kb * NF : 0;            // first query tile that reaches this block's first key
     const int nqb = T / 64;
     // threads 0-15 move the tile's lse2, 16-31 its delta (one float4 each)
     const float* lsrc = tid < 16 ? L2 + 4 * tid : Dl + 4 * (tid - 16);
@@ -376,18 +381,23 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
         if (!causal || qs + 63 >= k0) {
             const bf16_t* Qi = smem[cur][0];
             const bf16_t* Oi = smem[cur][1];
-            // S[q][key], dP[q][key]: lane holds rows q = qs + 16 qi + 4 g + r, column key = kl
-            f32x4_t s[4], dp[4];
+            // S[q][key], dP[q][key]: lane holds rows q = qs + 16 qi + 4 g + r, column key = k0 + 16 f + (lane & 15)
+            f32x4_t s[NF][4], dp[NF][4];
 #pragma unroll
             for (int qi = 0; qi < 4; ++qi) {
-                f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-                z = mfma(frag_rows(Qi, 16 * qi, 0, lane), kf[0], z);
-                s[qi] = mfma(frag_rows(Qi, 16 * qi, 1, lane), kf[1], z);
-                f32x4_t y = {0.f, 0.f, 0.f, 0.f};
-                y = mfma(frag_rows(Oi, 16 * qi, 0, lane), vf[0], y);
-                dp[qi] = mfma(frag_rows(Oi, 16 * qi, 1, lane), vf[1], y);
+                const bf16x8_t q0f = frag_rows(Qi, 16 * qi, 0, lane), q1f = frag_rows(Qi, 16 * qi, 1, lane);
+                const bf16x8_t o0f = frag_rows(Oi, 16 * qi, 0, lane), o1f = frag_rows(Oi, 16 * qi, 1, lane);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                    z = mfma(q0f, kf[f][0], z);
+                    s[f][qi] = mfma(q1f, kf[f][1], z);
+                    f32x4_t y = {0.f, 0.f, 0.f, 0.f};
+                    y = mfma(o0f, vf[f][0], y);
+                    dp[f][qi] = mfma(o1f, vf[f][1], y);
+                }
             }
-            const bool diag = causal && qs < k0 + 16;    // wave-uniform: only these tiles need the mask
+            const bool diag = causal && qs < k0 + 16 * NF;  // wave-uniform: only these tiles need the mask
 #pragma unroll
             for (int qi = 0; qi < 4; ++qi) {
                 const int qr = qs + 16 * qi + 4 * g;
@@ -395,19 +405,27 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
                 const float4 dl = *reinterpret_cast<const float4*>(&lsd[cur][1][16 * qi + 4 * g]);
                 const float la[4] = {lv.x, lv.y, lv.z, lv.w}, da[4] = {dl.x, dl.y, dl.z, dl.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) s[qi][r] = __builtin_amdgcn_exp2f(fmaf(s[qi][r], c, -la[r]));
-                if (diag) {
+                for (int f = 0; f < NF; ++f) {
+                    const int kl = k0 + 16 * f + (lane & 15);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (kl > qr + r) s[qi][r] = 0.f;
+                    for (int r = 0; r < 4; ++r) s[f][qi][r] = __builtin_amdgcn_exp2f(fmaf(s[f][qi][r], c, -la[r]));
+                    if (diag) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (kl > qr + r) s[f][qi][r] = 0.f;
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dp[f][qi][r] = s[f][qi][r] * (dp[f][qi][r] - da[r]);
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) dp[qi][r] = s[qi][r] * (dp[qi][r] - da[r]);
             }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                const bf16x8_t pb = pack_acc(s[2 * kk], s[2 * kk + 1]);
-                const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+                bf16x8_t pb[NF], sb[NF];
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    pb[f] = pack_acc(s[f][2 * kk], s[f][2 * kk + 1]);
+                    sb[f] = pack_acc(dp[f][2 * kk], dp[f][2 * kk + 1]);
+                }
                 // all eight transposed fragments of this k-step issued before the MFMAs that use them (one at a
                 // time, every MFMA waited out its own LDS read)
                 bf16x8_t fo[4], fq[4];
@@ -417,10 +435,12 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
                     fq[df] = frag_tr_perm(Qi, 16 * df, kk, lane);
                 }
 #pragma unroll
-                for (int df = 0; df < 4; ++df) {
-                    dv[df] = mfma(fo[df], pb, dv[df]);
-                    dk[df] = mfma(fq[df], sb, dk[df]);
-                }
+                for (int df = 0; df < 4; ++df)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) {
+                        dv[f][df] = mfma(fo[df], pb[f], dv[f][df]);
+                        dk[f][df] = mfma(fq[df], sb[f], dk[f][df]);
+                    }
             }
         }
         if (more) {
@@ -431,25 +451,31 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dkdv_kernel(const bf16_t* __rest
         __syncthreads();
     }
     // lane holds dK^T / dV^T [d = 16 df + 4 g + r][key = kl]
-    bf16_t* dkp = dqkv + ((long)b * T + kl) * ld + D + h * HD;
-    bf16_t* dvp = dkp + D;
 #pragma unroll
-    for (int df = 0; df < 4; ++df) {
-        u16x4_t a, v;
+    for (int f = 0; f < NF; ++f) {
+        const int kl = k0 + 16 * f + (lane & 15);
+        bf16_t* dkp = dqkv + ((long)b * T + kl) * ld + D + h * HD;
+        bf16_t* dvp = dkp + D;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            a[r] = f2bf(dk[df][r] * scale);
-            v[r] = f2bf(dv[df][r]);
+        for (int df = 0; df < 4; ++df) {
+            u16x4_t a, v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                a[r] = f2bf(dk[f][df][r] * scale);
+                v[r] = f2bf(dv[f][df][r]);
+            }
+            *reinterpret_cast<u16x4_t*>(dkp + 16 * df + 4 * g) = a;
+            *reinterpret_cast<u16x4_t*>(dvp + 16 * df + 4 * g) = v;
         }
-        *reinterpret_cast<u16x4_t*>(dkp + 16 * df + 4 * g) = a;
-        *reinterpret_cast<u16x4_t*>(dvp + 16 * df + 4 * g) = v;
     }
 }
 
-// dQ for 64 queries per block (wave w: queries q0 + 16 w .. +15); loop over 64-key tiles
+// dQ for 64 NF queries per block (wave w: NF 16-query fragments from q0 = 64 NF qb + 16 NF w); loop over 64-key
+// tiles.  NF = 2 reads every K / V fragment out of LDS once for two query fragments: at NF = 1 a wave's 24 MFMAs
+// per tile came with 24 KB of LDS reads, which saturated the LDS array (256 B/clk/CU) at the MFMA rate.
 // DELTA: the block also forms delta = rowsum(dO . O) of its queries (the four 16-lane groups of a query row take
 // 16 dims each) and writes it for attn_bwd_dkdv_kernel, which then runs after it: no separate delta launch
-template <bool DELTA>
+template <bool DELTA, int NF>
 __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dO,
                                                           const float* __restrict__ lse2, float* __restrict__ delta,
                                                           const bf16_t* __restrict__ o,
@@ -457,7 +483,7 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
                                                           int causal) {
     __shared__ __attribute__((aligned(16))) bf16_t smem[2][2][64 * HD];     // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-    const int nqb = T / 64;
+    const int nqb = T / (64 * NF);
     int qb, h, b;
     attn_block(nqb, H, true, qb, h, b);
     const int D = H * HD;
@@ -466,40 +492,48 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
     const bf16_t* Kp = Q + D;
     const bf16_t* Vp = Q + 2 * D;
     const bf16_t* dOp = dO + (long)b * T * D + h * HD;
-    const int q0 = qb * 64 + 16 * w;
-    const int ql = q0 + (lane & 15);
+    const int q0 = qb * 64 * NF + 16 * NF * w;
     const float c = scale * LOG2E;
-    const float lq = lse2[((long)b * H + h) * T + ql];
-    float dq_;
-    if constexpr (DELTA) {
-        const long ro = ((long)b * T + ql) * D + h * HD + 16 * g;
-        float sd = 0.f;
+    int ql[NF];
+    float lq[NF], dq_[NF];
 #pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2) {
-            float x[8], y[8];
-            unpack8(*reinterpret_cast<const u16x8_t*>(o + ro + 8 * c2), x);
-            unpack8(*reinterpret_cast<const u16x8_t*>(dO + ro + 8 * c2), y);
+    for (int f = 0; f < NF; ++f) {
+        ql[f] = q0 + 16 * f + (lane & 15);
+        lq[f] = lse2[((long)b * H + h) * T + ql[f]];
+        if constexpr (DELTA) {
+            const long ro = ((long)b * T + ql[f]) * D + h * HD + 16 * g;
+            float sd = 0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sd += x[j] * y[j];
+            for (int c2 = 0; c2 < 2; ++c2) {
+                float x[8], y[8];
+                unpack8(*reinterpret_cast<const u16x8_t*>(o + ro + 8 * c2), x);
+                unpack8(*reinterpret_cast<const u16x8_t*>(dO + ro + 8 * c2), y);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sd += x[j] * y[j];
+            }
+            sd = rsum4(sd);
+            dq_[f] = sd;
+            if (g == 0) delta[((long)b * H + h) * T + ql[f]] = sd;
+        } else {
+            dq_[f] = delta[((long)b * H + h) * T + ql[f]];
         }
-        sd = rsum4(sd);
-        dq_ = sd;
-        if (g == 0) delta[((long)b * H + h) * T + ql] = sd;
-    } else {
-        dq_ = delta[((long)b * H + h) * T + ql];
     }
 
-    bf16x8_t qf[2], of[2];
+    bf16x8_t qf[NF][2], of[NF][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-        qf[ks] = gfrag(Q + (long)q0 * ld, ld, ks, lane);
-        of[ks] = gfrag(dOp + (long)q0 * D, D, ks, lane);
-    }
-    f32x4_t dq[4];
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dq[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < 2; ++ks) {
+            qf[f][ks] = gfrag(Q + (long)(q0 + 16 * f) * ld, ld, ks, lane);
+            of[f][ks] = gfrag(dOp + (long)(q0 + 16 * f) * D, D, ks, lane);
+        }
+    f32x4_t dq[NF][4];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dq[f][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    const int nkb = causal ? qb + 1 : T / 64;
+    const int nkb = causal ? (qb + 1) * NF : T / 64;
     TileLd tk, tv;
     tk.load(Kp, ld, tid);
     tv.load(Vp, ld, tid);
@@ -514,41 +548,52 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
             tv.load(Vp + (long)(kb + 1) * 64 * ld, ld, tid);
         }
         const int k0 = kb * 64;
-        if (!causal || k0 <= q0 + 15) {
+        if (!causal || k0 <= q0 + 16 * NF - 1) {
             const bf16_t* Ki = smem[cur][0];
             const bf16_t* Vi = smem[cur][1];
-            // S^T[key][q], dP^T[key][q]: lane holds rows key = k0 + 16 ki + 4 g + r, column q = ql
-            f32x4_t s[4], dp[4];
+            // S^T[key][q], dP^T[key][q]: lane holds rows key = k0 + 16 ki + 4 g + r, column q = ql[f]
+            f32x4_t s[NF][4], dp[NF][4];
 #pragma unroll
             for (int ki = 0; ki < 4; ++ki) {
-                f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-                z = mfma(frag_rows(Ki, 16 * ki, 0, lane), qf[0], z);
-                s[ki] = mfma(frag_rows(Ki, 16 * ki, 1, lane), qf[1], z);
-                f32x4_t y = {0.f, 0.f, 0.f, 0.f};
-                y = mfma(frag_rows(Vi, 16 * ki, 0, lane), of[0], y);
-                dp[ki] = mfma(frag_rows(Vi, 16 * ki, 1, lane), of[1], y);
+                const bf16x8_t k0f = frag_rows(Ki, 16 * ki, 0, lane), k1f = frag_rows(Ki, 16 * ki, 1, lane);
+                const bf16x8_t v0f = frag_rows(Vi, 16 * ki, 0, lane), v1f = frag_rows(Vi, 16 * ki, 1, lane);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+                    z = mfma(k0f, qf[f][0], z);
+                    s[f][ki] = mfma(k1f, qf[f][1], z);
+                    f32x4_t y = {0.f, 0.f, 0.f, 0.f};
+                    y = mfma(v0f, of[f][0], y);
+                    dp[f][ki] = mfma(v1f, of[f][1], y);
+                }
             }
             const bool diag = causal && k0 + 63 > q0;     // wave-uniform: only these tiles need the mask
 #pragma unroll
-            for (int ki = 0; ki < 4; ++ki) {
+            for (int f = 0; f < NF; ++f)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(fmaf(s[ki][r], c, -lq));
-                if (diag) {
+                for (int ki = 0; ki < 4; ++ki) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (k0 + 16 * ki + 4 * g + r > ql) s[ki][r] = 0.f;
+                    for (int r = 0; r < 4; ++r) s[f][ki][r] = __builtin_amdgcn_exp2f(fmaf(s[f][ki][r], c, -lq[f]));
+                    if (diag) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (k0 + 16 * ki + 4 * g + r > ql[f]) s[f][ki][r] = 0.f;
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dp[f][ki][r] = s[f][ki][r] * (dp[f][ki][r] - dq_[f]);
                 }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) dp[ki][r] = s[ki][r] * (dp[ki][r] - dq_);
-            }
-#pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                const bf16x8_t sb = pack_acc(dp[2 * kk], dp[2 * kk + 1]);
+                bf16x8_t sb[NF];
+#pragma unroll
+                for (int f = 0; f < NF; ++f) sb[f] = pack_acc(dp[f][2 * kk], dp[f][2 * kk + 1]);
                 bf16x8_t fk[4];                  // fragments issued before the MFMAs (as in attn_bwd_dkdv)
 #pragma unroll
                 for (int df = 0; df < 4; ++df) fk[df] = frag_tr_perm(Ki, 16 * df, kk, lane);
 #pragma unroll
-                for (int df = 0; df < 4; ++df) dq[df] = mfma(fk[df], sb, dq[df]);
+                for (int df = 0; df < 4; ++df)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) dq[f][df] = mfma(fk[df], sb[f], dq[f][df]);
             }
         }
         if (more) {
@@ -557,13 +602,16 @@ __global__ void __launch_bounds__(NTA) attn_bwd_dq_kernel(const bf16_t* __restri
         }
         __syncthreads();
     }
-    bf16_t* dqp = dqkv + ((long)b * T + ql) * ld + h * HD;
 #pragma unroll
-    for (int df = 0; df < 4; ++df) {
-        u16x4_t a;
+    for (int f = 0; f < NF; ++f) {
+        bf16_t* dqp = dqkv + ((long)b * T + ql[f]) * ld + h * HD;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = f2bf(dq[df][r] * scale);
-        *reinterpret_cast<u16x4_t*>(dqp + 16 * df + 4 * g) = a;
+        for (int df = 0; df < 4; ++df) {
+            u16x4_t a;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = f2bf(dq[f][df][r] * scale);
+            *reinterpret_cast<u16x4_t*>(dqp + 16 * df + 4 * g) = a;
+        }
     }
 }
 }  // namespace
@@ -584,24 +632,41 @@ PDNN_API int pdnn_flash_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse2, in
     PDNN_LAUNCH_RET;
 }
 
+static void launch_dkdv(const bf16_t* qkv, const bf16_t* dO, const float* lse2, const float* delta, bf16_t* dqkv, int B,
+                        int T, int H, float scale, int causal, hipStream_t st) {
+    if (pg::tune().attn_bwd_wide & 2)
+        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, attn_grid(T / 128, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                           dqkv, T, H, scale, causal);
+    else
+        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                           dqkv, T, H, scale, causal);
+}
+
 // dO [B*T][H*64], out/lse2 from the forward -> dqkv [B*T][3*H*64]; delta: fp32 [B][H][T] scratch.
 PDNN_API int pdnn_flash_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dO, const float* lse2,
                                  float* delta, bf16_t* dqkv, int B, int T, int H, float scale, int causal,
                                  hipStream_t st) {
     if (T % 128) return (int)hipErrorInvalidValue;
+    const bool wq = pg::tune().attn_bwd_wide & 1;
     if (pg::tune().attn_delta_in_dq) {       // dQ first (it writes delta), then dK / dV
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
-                           out, dqkv, T, H, scale, causal);
-        hipLaunchKernelGGL(attn_bwd_dkdv_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv,
-                           T, H, scale, causal);
+        if (wq)
+            hipLaunchKernelGGL((attn_bwd_dq_kernel<true, 2>), attn_grid(T / 128, H, B), dim3(NTA), 0, st, qkv, dO, lse2,
+                               delta, out, dqkv, T, H, scale, causal);
+        else
+            hipLaunchKernelGGL((attn_bwd_dq_kernel<true, 1>), attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2,
+                               delta, out, dqkv, T, H, scale, causal);
+        launch_dkdv(qkv, dO, lse2, delta, dqkv, B, T, H, scale, causal, st);
         PDNN_LAUNCH_RET;
     }
     const long n = (long)B * T * H;
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n + NTA - 1) / NTA)), dim3(NTA), 0, st, out, dO, delta,
                        B * T, T, H);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta, dqkv, T, H,
-                       scale, causal);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
-                       out, dqkv, T, H, scale, causal);
+    launch_dkdv(qkv, dO, lse2, delta, dqkv, B, T, H, scale, causal, st);
+    if (wq)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<false, 2>), attn_grid(T / 128, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                           out, dqkv, T, H, scale, causal);
+    else
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<false, 1>), attn_grid(T / 64, H, B), dim3(NTA), 0, st, qkv, dO, lse2, delta,
+                           out, dqkv, T, H, scale, causal);
     PDNN_LAUNCH_RET;
 }

@@ -37,6 +37,11 @@ namespace pg {
                            "beside the data-gradient chain, where fewer splits mean less fp32 slab traffic (fc / fc2 " \
                            "7 -> 3 splits, qkv 8 -> 4): GPT-2 671.5k / 670.6k -> 680.9k / 679.6k tok/s same box "      \
                            "(gpurun_out/r6_40; 160: 681.1k / 679.1k, 64: 669.1k / 666.8k, r6_41)")                     \
+    X(attn_bwd_wide, 1, "flash-attention backward kernels with two 16-row fragments per wave (half the LDS "       \
+                        "fragment reads per MFMA), a bit mask: 1 dQ (32 queries per wave), 2 dK / dV (32 keys per wave). " \
+                        "Alone (B8 T1024 causal) 0: 87.4 us, 1: 90.1, 3: 90.3; B32: 330 / 315 / 302 us; in the GPT-2 " \
+                        "step beside the side-stream weight gradients 1: 688.5k / 687.4k vs 0: 680.6k / 681.8k tok/s, " \
+                        "3: 688.6k / 683.3k (gpurun_out/r6_45)")                                                    \
     X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
                            "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \
