@@ -130,6 +130,75 @@ __global__ void __launch_bounds__(NT) xent_bwd_kernel(const T* __restrict__ logi
         Ld<T>::put(d, i, sc * (p - (i == y ? 1.f : 0.f)));
     }
 }
+// Training forward that also writes the UNSCALED gradient softmax - onehot (bf16, in place over the logits allowed):
+// the row is held in registers (MAXC 16-byte chunks per lane, V <= 8 * NT * MAXC), so it is read from HBM once
+// and written once -- the separate backward pass (a second full read of the logits) disappears.  The caller
+// applies grad_out / count to the products of the gradient (the LM head's 8192 x 768 operands), not to it.
+template <int MAXC>
+__global__ void __launch_bounds__(NT) xent_fwd_grad_kernel(const bf16_t* __restrict__ logits, long ld, int V,
+                                                           const int64_t* __restrict__ labels, int ignore,
+                                                           float* __restrict__ loss, float* __restrict__ lse,
+                                                           bf16_t* dlogits, long ldd) {
+    __shared__ float red[NT / 64];
+    const long row = blockIdx.x;
+    const u16x8_t* x8 = reinterpret_cast<const u16x8_t*>(logits + row * ld);
+    u16x8_t* d8 = reinterpret_cast<u16x8_t*>(dlogits + row * ldd);
+    const int n8 = V / 8;
+    u16x8_t r[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int i = threadIdx.x + c * NT;
+        if (i < n8) r[c] = x8[i];
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int i = threadIdx.x + c * NT;
+        if (i < n8) {
+            float v[8];
+            unpack8(r[c], v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
+        }
+    }
+    mx = wave_max(mx);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = mx;
+    __syncthreads();
+    float M = red[0];
+#pragma unroll
+    for (int k = 1; k < NT / 64; ++k) M = fmaxf(M, red[k]);
+    __syncthreads();
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int i = threadIdx.x + c * NT;
+        if (i < n8) {
+            float v[8];
+            unpack8(r[c], v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sum += __expf(v[j] - M);
+        }
+    }
+    const float l = M + __logf(block_sum<NT>(sum, red));
+    const int64_t y = labels[row];
+    const bool ign = (y == ignore || y < 0 || y >= V);
+    if (threadIdx.x == 0) {
+        lse[row] = l;
+        loss[row] = ign ? 0.f : l - bf2f(logits[row * ld + y]);
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int i = threadIdx.x + c * NT;
+        if (i < n8) {
+            float v[8];
+            unpack8(r[c], v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ign ? 0.f : __expf(v[j] - l) - (8 * i + j == y ? 1.f : 0.f);
+            d8[i] = pack8(v);
+        }
+    }
+}
 }  // namespace
 
 // dtype: 0 = fp32 logits, 1 = bf16 logits
@@ -197,5 +266,22 @@ PDNN_API int pdnn_xent_bwd(const void* logits, long ld, int rows, int V, const i
     else
         hipLaunchKernelGGL((xent_bwd_kernel<float, false>), dim3(rows), dim3(NT), 0, st, (const float*)logits, ld,
                            V, labels, ignore, lse, gscale, denom, count, (float*)dlogits, ldd);
+    PDNN_LAUNCH_RET;
+}
+
+// bf16 logits [rows][ld] (V % 8 == 0, ld % 8 == 0, ldd % 8 == 0, 16-byte aligned, V <= 51200) -> per-row loss / lse,
+// loss_sum / count SET as in pdnn_xent_fwd, and dlogits = softmax - onehot UNSCALED (dlogits == logits allowed).
+PDNN_API int pdnn_xent_fwd_grad(const bf16_t* logits, long ld, int rows, int V, const int64_t* labels, int ignore,
+                                float* loss, float* lse, float* loss_sum, float* count, bf16_t* dlogits, long ldd,
+                                hipStream_t st) {
+    constexpr int MAXC = 25;
+    if (V % 8 || ld % 8 || ldd % 8 || V > 8 * NT * MAXC || !loss || !lse ||
+        ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 15))
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(xent_fwd_grad_kernel<MAXC>, dim3(rows), dim3(NT), 0, st, logits, ld, V, labels, ignore, loss, lse,
+                       dlogits, ldd);
+    if (loss_sum)
+        hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(1024), 0, st, (const float*)loss, labels, rows, V, ignore,
+                           loss_sum, count);
     PDNN_LAUNCH_RET;
 }

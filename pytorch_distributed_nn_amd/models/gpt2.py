@@ -194,7 +194,7 @@ class GPT2(nn.Module):
             xf = TX.layer_norm(x, tr.ln_f.weight, tr.ln_f.bias, c.eps)
             return OF.linear(xf, wte).view(B, T, -1)
         return TX.LMHeadLossFn.apply(x, targets.reshape(-1).long().contiguous(), c.eps, wte_k, tr.ln_f.weight,
-                                     tr.ln_f.bias, wte, hd, ddp is not None)
+                                     tr.ln_f.bias, wte, hd, ddp is not None, torch.is_grad_enabled())
 
     def _forward_reference(self, idx, targets=None):
         B, T = idx.shape

@@ -107,6 +107,7 @@ _SIGS = {
     "pdnn_avgpool_bwd": [P, P, I, I, I, P],
     "pdnn_xent_fwd": [P, L, I, I, P, I, P, P, P, P, I, P],
     "pdnn_xent_bwd": [P, L, I, I, P, I, P, P, F, P, P, L, I, P],
+    "pdnn_xent_fwd_grad": [P, L, I, I, P, I, P, P, P, P, P, L, P],
     "pdnn_sgd_step": [P, P, P, P, L, F, F, F, F, I, P, F, I, P, P],
     "pdnn_adam_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, F, P, F, P, P],
     "pdnn_cast_f32_bf16": [P, P, L, F, P],

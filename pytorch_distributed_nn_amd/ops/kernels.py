@@ -867,6 +867,31 @@ def xent_fwd(logits, labels, ignore_index=-100):
     return loss, lse, acc
 
 
+def xent_fwd_grad_ok(logits):
+    """Whether xent_fwd_grad takes these logits (bf16, row-major, 16-byte rows, V <= 51200)."""
+    R, V = logits.shape
+    return (logits.dtype == BF16 and logits.stride(1) == 1 and V % 8 == 0 and logits.stride(0) % 8 == 0
+            and V <= 51200 and logits.data_ptr() % 16 == 0)
+
+
+def xent_fwd_grad(logits, labels, ignore_index=-100, out=None):
+    """Training forward of the cross-entropy that also writes d logits = softmax - onehot, UNSCALED (the caller
+    applies grad_out / count downstream), into ``out`` (default: in place over ``logits``).  One read and one
+    write of the logits instead of the forward's read plus the backward's read and write.  Returns
+    (loss per row, lse, acc = [loss sum, valid-label count], dlogits)."""
+    _chk(xent_fwd_grad_ok(logits), "xent_fwd_grad: bf16 row-major logits, V % 8 == 0, V <= 51200")
+    R, V = logits.shape
+    d = logits if out is None else out
+    _chk(d.shape == logits.shape and d.dtype == BF16 and d.stride(1) == 1 and d.stride(0) % 8 == 0
+         and d.data_ptr() % 16 == 0, "xent_fwd_grad: bf16 row-major output")
+    loss = torch.empty(R, device=logits.device, dtype=F32)
+    lse = torch.empty(R, device=logits.device, dtype=F32)
+    acc = torch.empty(2, device=logits.device, dtype=F32)
+    call("pdnn_xent_fwd_grad", ptr(logits), logits.stride(0), R, V, ptr(labels), int(ignore_index), ptr(loss),
+         ptr(lse), ptr(acc), ptr(acc[1:]), ptr(d), d.stride(0), stream())
+    return loss, lse, acc, d
+
+
 def xent_bwd(logits, labels, lse, gscale_dev, denom, ignore_index=-100, count=None):
     """d logits = softmax - onehot, times gscale_dev[0] / denom, or gscale_dev[0] / max(count[0], 1) with
     ``count`` (fp32 device scalar: xent_fwd's count of non-ignored rows, the mean reduction)."""

@@ -348,12 +348,19 @@ class LMHeadLossFn(torch.autograd.Function):
     """loss = mean CE(LN_f(x) . Wte^T, targets); logits bf16 [B*T][V] live only inside this op."""
 
     @staticmethod
-    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte, head_direct=False, split=False):
+    def forward(ctx, x, targets, eps, wte_k, lnw, lnb, wte, head_direct=False, split=False, training=False):
         ctx.head_direct = head_direct
         ctx.split = split                   # split tied embedding: the head announces wte itself
         xf, m, r = K.layernorm_fwd(x, lnw, lnb, eps)
         logits = BL.linear_fwd(xf, wte_k)
-        _, lse, acc = K.xent_fwd(logits, targets)
+        # training (grad mode on at the call): the forward also writes the unscaled gradient softmax - onehot over
+        # the logits (one read + one write of the 8192 x 50304 logits instead of three passes); the backward then
+        # scales the head's 8192 x 768 products by grad_out / count instead of the logits gradient
+        ctx.fused = training and _tuning.get("xent_fused") and logits.is_cuda and K.xent_fwd_grad_ok(logits)
+        if ctx.fused:
+            _, lse, acc, _ = K.xent_fwd_grad(logits, targets)
+        else:
+            _, lse, acc = K.xent_fwd(logits, targets)
         ctx.save_for_backward(x, xf, m, r, logits, targets, lse, acc, lnw, wte_k)
         ctx.eps = eps
         ctx.params = (lnw, lnb)
@@ -366,8 +373,16 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1)
         if gs.dtype != torch.float32:
             gs = gs.float()
-        dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0, count=acc[1:2])
-        dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
+        if ctx.fused:           # logits hold softmax - onehot: scale the products instead (device scalar, no sync)
+            dlogits = logits
+            sc = gs / acc[1:2].clamp_min(1.0)
+            dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
+            dxf.mul_(sc)
+            xf = xf.clone()
+            xf.mul_(sc)
+        else:
+            dlogits = K.xent_bwd(logits, targets, lse, gs, 1.0, count=acc[1:2])
+            dxf = BL.linear_dgrad(dlogits, wte_k, p=ctx.wte)
         tte = direct_grad(ctx.wte) if ctx.head_direct else None
         if tte is not None:     # tied weight: the embedding backward adds its part and announces it
             BL.wgrad_acc(dlogits, xf, tte)
@@ -381,4 +396,4 @@ class LMHeadLossFn(torch.autograd.Function):
         ctx.params = None
         ctx.wte = None
         sink.done()
-        return dx, None, None, None, dlnw, dlnb, dwte, None, None
+        return dx, None, None, None, dlnw, dlnb, dwte, None, None, None

@@ -279,6 +279,14 @@ def test_xent(K, V):
     assert acc[1].item() == R - 1
     dm = K.xent_bwd(lg, y, lse, gs, 1.0, count=acc[1:2])
     assert rel(dm, lr.grad / (R - 1)) < 1e-2
+    # training forward with the unscaled gradient written in place (bf16, V % 8 == 0 only)
+    if V % 8 == 0:
+        lg2 = lg.clone()
+        loss2, lse2, acc2, d2 = K.xent_fwd_grad(lg2, y)
+        assert d2.data_ptr() == lg2.data_ptr()
+        assert rel(lse2, lse) < 1e-5 and rel(loss2, loss) < 1e-4
+        assert acc2[1].item() == acc[1].item() and rel(acc2[:1], acc[:1]) < 1e-5
+        assert rel(d2, lr.grad) < 1e-2 and d2[3].abs().max().item() == 0.0
 
 
 def test_sgd_adam(K):

@@ -245,6 +245,37 @@ def test_gpt2_side_stream_weight_gradients():
         assert rel2(b, a) < 1e-4
 
 
+def test_gpt2_fused_xent_gradients():
+    """tuning xent_fused: the training forward writes softmax - onehot over the logits and the backward scales the
+    LM head's products by grad_out / count; gradients (also for a scaled loss) and the loss must match the separate
+    passes, and an evaluation forward (no grad) the same loss."""
+    from pytorch_distributed_nn_amd import tuning
+    from pytorch_distributed_nn_amd.ops import kernels as K
+    B, T = 4, 128
+    res = {}
+    for v in (0, 1):
+        old = tuning.set("xent_fused", v)
+        try:
+            m = _tiny(seed=5).cuda()
+            assert m.config.vocab_size % 8 == 0
+            g = torch.Generator(device="cuda").manual_seed(9)
+            idx = torch.randint(0, m.config.vocab_size, (B, T), device="cuda", generator=g)
+            tgt = torch.randint(0, m.config.vocab_size, (B, T), device="cuda", generator=g)
+            tgt[0, :5] = -100
+            loss = m(idx, tgt)
+            (loss * 3.0).backward()
+            with torch.no_grad():
+                ev = m(idx, tgt)
+            res[v] = (loss.detach(), ev, {n: p.grad.clone() for n, p in m.named_parameters()})
+        finally:
+            tuning.set("xent_fused", old)
+    assert K.xent_fwd_grad_ok(torch.empty(8, m.config.vocab_size, device="cuda", dtype=torch.bfloat16))
+    assert abs(res[1][0].item() - res[0][0].item()) < 1e-4 * abs(res[0][0].item())
+    assert abs(res[1][1].item() - res[0][1].item()) < 1e-4 * abs(res[0][1].item())
+    for n, a in res[0][2].items():
+        assert rel2(res[1][2][n], a) < 1e-2, n
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 def test_gpt2_prefetched_transposes_track_optimizer_steps(mode):
     """tuning wt_prefetch 1 / 2: the forward refreshes every transposed weight copy in one launch
