@@ -1157,10 +1157,11 @@ PDNN_API int pdnn_pp_splitk_splits(int M, int N, int K) {
 // with u = 0.60 / 0.805 us per 32-deep slice per item round for the 128 / 256-wide MN-major tiles and ~5.5 TB/s for
 // the slabs, fitted to the GPT-2 shapes (dev/probes/wgrad_sweep.py, gpurun_out/r5_33: e.g. fc 3072 x 768 x 8192
 // 256 wide x 6 splits 62.9 us vs 128 x 3 68.6 us).  A forced width (tuning pp_bn) is kept.
-PDNN_API int pdnn_pp_wgrad_plan(int M, int N, int K) {
+// plan_cus > 0: plan for that many CUs (a weight gradient on the side stream beside the data-gradient chain), else
+// the device's.
+PDNN_API int pdnn_pp_wgrad_plan(int M, int N, int K, int plan_cus) {
     using namespace pg;
-    const int pc = tune().wgrad_plan_cus;
-    const int cus = pc > 0 && pc < device_cus() ? pc : device_cus();
+    const int cus = plan_cus > 0 && plan_cus < device_cus() ? plan_cus : device_cus();
     const int nsl = K / PP_SK;
     const int force = tune().pp_bn;
     int best_bn = 128, best_s = 1;

@@ -32,11 +32,6 @@ namespace pg {
                                "blocks fit a CU).  At 512 the kernel took 325-330 or 498-501 us inside the ResNet-50 "  \
                                "step (a launch overlapping the side stream's last kernel leaves a CU with two runs in " \
                                "sequence), 2048: 330-360 (gpurun_out/r6_26); alone 370 vs 390 us (r6_25)")              \
-    X(wgrad_plan_cus, 128, "CUs the linear weight-gradient plan (pdnn_pp_wgrad_plan: tile width and K-splits) "    \
-                           "assumes it may fill (0 = the device's).  GPT-2's weight gradients run on the side stream " \
-                           "beside the data-gradient chain, where fewer splits mean less fp32 slab traffic (fc / fc2 " \
-                           "7 -> 3 splits, qkv 8 -> 4): GPT-2 671.5k / 670.6k -> 680.9k / 679.6k tok/s same box "      \
-                           "(gpurun_out/r6_40; 160: 681.1k / 679.1k, 64: 669.1k / 666.8k, r6_41)")                     \
     X(attn_bwd_wide, 1, "flash-attention backward kernels with two 16-row fragments per wave (half the LDS "       \
                         "fragment reads per MFMA), a bit mask: 1 dQ (32 queries per wave), 2 dK / dV (32 keys per wave). " \
                         "Alone (B8 T1024 causal) 0: 87.4 us, 1: 90.1, 3: 90.3; B32: 330 / 315 / 302 us; in the GPT-2 " \

@@ -48,7 +48,7 @@ def main():
     for name, (Mo, No) in {"qkv": (2304, 768), "proj": (768, 768), "fc": (3072, 768), "fc2": (768, 3072)}.items():
         x, y = r(T, Mo), r(T, No)
         o = torch.zeros(Mo, No, device="cuda")
-        plan = int(lib().pdnn_pp_wgrad_plan(Mo, No, T))
+        plan = int(lib().pdnn_pp_wgrad_plan(Mo, No, T, 0))
         res = {"gemm": name + "_wgrad", "plan": plan, "auto": timeit(lambda: K.pp_wgrad(x, y, o))}
         for bn in (128, 256):
             old = K.tune_set("pp_bn", bn)

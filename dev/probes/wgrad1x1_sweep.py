@@ -33,7 +33,7 @@ for name, M, N, P in SH:
     ws = torch.empty(256 * (M * N + 64), device="cuda")
     K.set_pp_bn(0)
     sl = lib().pdnn_pp_wgrad_splits_long(M, N, P)
-    plan = lib().pdnn_pp_wgrad_plan(M, N, P)
+    plan = lib().pdnn_pp_wgrad_plan(M, N, P, 0)
     row = [f"{name} M={M} N={N} P={P}: long(s={sl})={t(lambda: K.pp_wgrad(dy, x, out, splits=sl, ws=ws)):.1f}",
            f"plan(bn{plan // 1000}s{plan % 1000})={t(lambda: K.pp_wgrad(dy, x, out, ws=ws)):.1f}"]
     nsl = P // 32

@@ -32,7 +32,7 @@ for name, M, N, sw in (("qkv", 2304, 768, SW), ("proj", 768, 768, SW), ("fc", 30
     out = torch.zeros(M, N, device="cuda")
     ws = torch.empty(max(sw) * (M * N + 64), device="cuda")
     K.set_pp_bn(0)
-    plan = lib().pdnn_pp_wgrad_plan(M, N, T)
+    plan = lib().pdnn_pp_wgrad_plan(M, N, T, 0)
     row = [f"{name} M={M} N={N}: auto(bn{plan // 1000}s{plan % 1000})={t(lambda: K.pp_wgrad(x, y, out, ws=ws)):.1f}"]
     try:
         row.append(f"torch={t(lambda: torch.mm(x.t(), y, out_dtype=torch.float32)):.1f}")

@@ -79,7 +79,7 @@ _SIGS = {
     "pdnn_set_pp_bn": [I],
     "pdnn_set_pp_trace": [P],
     "pdnn_pp_wgrad": [P, L, P, L, P, L, I, I, I, F, P, I, P, I, P],
-    "pdnn_pp_wgrad_plan": [I, I, I],
+    "pdnn_pp_wgrad_plan": [I, I, I, I],
     "pdnn_pp_wgrad_splits": [I, I, I],
     "pdnn_pp_wgrad_ws": [I, I, I],
     "pdnn_pp_wgrad_splits_long": [I, I, I],

@@ -56,18 +56,19 @@ def set_pp_bn(bn: int) -> int:
     return lib().pdnn_set_pp_bn(int(bn))
 
 
-def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None, rowsum=None, bn=0):
+def pp_wgrad(x, y, out, alpha=1.0, splits=None, ws=None, rowsum=None, bn=0, plan_cus=0):
     """out[M][N] (fp32) += alpha * x[K][M]^T @ y[K][N] on the ping-pong engine: split-K partial slabs in a
     workspace (``ws``, allocated when not given) reduced by a second kernel, or in place when one split
     covers the CUs.  ``rowsum`` (fp32 [M], optional) += alpha * x.sum(0), fused: the bias gradient of a
     linear layer beside its weight gradient.  ``splits=None``: tile width and splits from the joint plan
-    (pdnn_pp_wgrad_plan); ``bn`` (128 / 256, 0 = the engine's pick) only with explicit ``splits``."""
+    (pdnn_pp_wgrad_plan, for ``plan_cus`` CUs when > 0: a weight gradient beside other work on a side stream);
+    ``bn`` (128 / 256, 0 = the engine's pick) only with explicit ``splits``."""
     K_, M = x.shape
     K2, N = y.shape
     _chk(K_ == K2 and K_ % 32 == 0 and M % 8 == 0 and N % 8 == 0, f"pp_wgrad: bad shapes {x.shape} {y.shape}")
     _chk(out.dtype == F32 and out.shape == (M, N) and out.stride(1) == 1, "pp_wgrad: fp32 [M][N] output")
     if splits is None:
-        bn, splits = divmod(lib().pdnn_pp_wgrad_plan(M, N, K_), 1000)
+        bn, splits = divmod(lib().pdnn_pp_wgrad_plan(M, N, K_, int(plan_cus)), 1000)
     if splits > 1 and ws is None:
         ws = torch.empty(splits * (M * N + 64), device=x.device, dtype=F32)     # pdnn_pp_wgrad_ws
     _chk(splits <= 1 or ws.numel() >= splits * (M * N + 64), "pp_wgrad: workspace of splits * (M*N + 64) floats")

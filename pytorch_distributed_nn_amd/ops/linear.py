@@ -48,14 +48,14 @@ def linear_dgrad(g, wk, dgelu=None, p=None):
     return K.gemm_nt_ex(g, wt, dgelu=dgelu)
 
 
-def wgrad_acc(g, x, out, bias=None):
+def wgrad_acc(g, x, out, bias=None, plan_cus=0):
     """out[N][K] (fp32) += g[M][N]^T @ x[M][K]; with ``bias`` (fp32 [N]) also bias += column sums of g when the
     ping-pong engine runs the product (fused: one extra MFMA per g fragment).  Returns whether ``bias`` was
-    accumulated (the caller sums it otherwise)."""
+    accumulated (the caller sums it otherwise).  ``plan_cus``: see kernels.pp_wgrad."""
     M, N = g.shape
     Kd = x.shape[1]
     if M % 32 == 0 and N % 8 == 0 and Kd % 8 == 0 and out.is_contiguous() and M * N * Kd >= (1 << 24):
-        K.pp_wgrad(g, x, out, rowsum=bias)
+        K.pp_wgrad(g, x, out, rowsum=bias, plan_cus=plan_cus)
         return bias is not None
     K.gemm_tn_acc(g, x, out)
     return False

@@ -224,7 +224,7 @@ class _Sink:
             main = torch.cuda.current_stream(g.device)
             K.stream_wait(side, main)
             with torch.cuda.stream(side):
-                bias_done = BL.wgrad_acc(g, x, tw, bias=bias_in)
+                bias_done = BL.wgrad_acc(g, x, tw, bias=bias_in, plan_cus=_tuning.get("wgrad_plan_cus"))
                 if p_b is not None and not bias_done:
                     K.colsum(g, out=tb, accumulate=True, deterministic=not _tuning.get("colsum_atomic"))
             for t in (g, x):

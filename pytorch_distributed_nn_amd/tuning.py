@@ -31,6 +31,11 @@ gpt2_side_wgrad    1        GPT-2 linear weight gradients on the weight-gradient
                             chain, the compute stream at high priority (0: one stream): DDP path 636.3k / 636.9k ->
                             664.5k / 665.9k tok/s, plain eager 680k vs 646k graphed (gpurun_out/r6_35); the tied LM
                             head's weight gradient there too measured no better (r6_34) and stays on the compute stream
+wgrad_plan_cus     128      CUs the tile-width / K-split plan of a GPT-2 weight gradient on the side stream assumes
+                            (kernels.pp_wgrad plan_cus; 0: the device's): fewer splits (fc / fc2 7 -> 3, qkv 8 -> 4)
+                            mean less fp32 slab traffic beside the data-gradient chain: 671k -> 680k tok/s same box
+                            (gpurun_out/r6_40 / r6_41).  Compute-stream weight gradients (the tied LM head) plan for
+                            the whole chip
 xent_fused         1        GPT-2 training forward writes the unscaled cross-entropy gradient over the logits in the same
                             pass (ops/transformer.py LMHeadLossFn; 0: separate forward and backward passes)
 ds_sub             1        stride-2 1x1 shortcut convs read a contiguous copy of their input's even pixels (one
@@ -58,7 +63,7 @@ from __future__ import annotations
 
 import os
 
-DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1, "wgrad1x1_pp_pix": 200704, "gpt2_side_wgrad": 1, "xent_fused": 1}
+DEFAULTS = {"side_wgrad": 1, "wide1x1_dgrad": 1, "a2_fold": 1, "wt_prefetch": 0, "wt_layer_batch": 1, "colsum_atomic": 1, "bias_in_wgrad": 1, "s2_halo": 3, "ds_sub": 1, "wgrad1x1_pp_pix": 200704, "gpt2_side_wgrad": 1, "xent_fused": 1, "wgrad_plan_cus": 128}
 
 _VALUES = dict(DEFAULTS)
 
