@@ -208,31 +208,40 @@ __global__ void __launch_bounds__(NT) attn_softmax_fwd_kernel(const float* __res
     }
 }
 
-// dS[r][k] = scale * P[r][k] * (dP[r][k] - delta[r]),  delta[r] = sum_k P[r][k] dP[r][k]
+// dS[r][k] = scale * P[r][k] * (dP[r][k] - delta[r]),  delta[r] = sum_k P[r][k] dP[r][k].
+// causal: only k <= q (q = r % T) is read -- the causal dP GEMM skips the tiles above the diagonal, whose memory is
+// never written (0 * a NaN bit pattern left there would poison delta); dS is 0 above the diagonal.
 __global__ void __launch_bounds__(NT) attn_softmax_bwd_kernel(const bf16_t* __restrict__ P, long ldP,
                                                               const float* __restrict__ dP, long lddP,
                                                               bf16_t* __restrict__ dS, long lddS, int rows, int T,
-                                                              float scale) {
+                                                              float scale, int causal) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
     if (r >= rows) return;
+    const int lim = causal ? r % T + 1 : T;
     const bf16_t* p = P + (long)r * ldP;
     const float* dp = dP + (long)r * lddP;
     float d = 0.f;
     for (int k = lane * 4; k < T; k += 256) {
+        if (k >= lim) break;
         const u16x4_t pv = *reinterpret_cast<const u16x4_t*>(p + k);
         const float4 g = *reinterpret_cast<const float4*>(dp + k);
-        d += bf2f(pv[0]) * g.x + bf2f(pv[1]) * g.y + bf2f(pv[2]) * g.z + bf2f(pv[3]) * g.w;
+        const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k + j < lim) d += bf2f(pv[j]) * gg[j];
     }
     d = wave_sum(d);
     bf16_t* o = dS + (long)r * lddS;
     for (int k = lane * 4; k < T; k += 256) {
-        const u16x4_t pv = *reinterpret_cast<const u16x4_t*>(p + k);
-        const float4 g = *reinterpret_cast<const float4*>(dp + k);
-        const float gg[4] = {g.x, g.y, g.z, g.w};
-        u16x4_t out;
+        u16x4_t out = {0, 0, 0, 0};
+        if (k < lim) {
+            const u16x4_t pv = *reinterpret_cast<const u16x4_t*>(p + k);
+            const float4 g = *reinterpret_cast<const float4*>(dp + k);
+            const float gg[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) out[j] = f2bf(scale * bf2f(pv[j]) * (gg[j] - d));
+            for (int j = 0; j < 4; ++j) out[j] = k + j < lim ? f2bf(scale * bf2f(pv[j]) * (gg[j] - d)) : (bf16_t)0;
+        }
         *reinterpret_cast<u16x4_t*>(o + k) = out;
     }
 }
@@ -313,10 +322,10 @@ PDNN_API int pdnn_attn_softmax_fwd(const float* S, long ldS, bf16_t* P, long ldP
 }
 
 PDNN_API int pdnn_attn_softmax_bwd(const bf16_t* P, long ldP, const float* dP, long lddP, bf16_t* dS, long lddS,
-                                   int rows, int T, float scale, hipStream_t st) {
+                                   int rows, int T, float scale, int causal, hipStream_t st) {
     if (T % 4) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(attn_softmax_bwd_kernel, dim3((rows + 3) / 4), dim3(NT), 0, st, P, ldP, dP, lddP, dS, lddS,
-                       rows, T, scale);
+                       rows, T, scale, causal);
     PDNN_LAUNCH_RET;
 }
 

@@ -128,7 +128,7 @@ _SIGS = {
     "pdnn_layernorm_bwd_blocks": [I],
     "pdnn_layernorm_bwd": [P, P, P, P, P, P, P, P, I, I, I, P],
     "pdnn_attn_softmax_fwd": [P, L, P, L, P, I, I, F, I, P],
-    "pdnn_attn_softmax_bwd": [P, L, P, L, P, L, I, I, F, P],
+    "pdnn_attn_softmax_bwd": [P, L, P, L, P, L, I, I, F, I, P],
     "pdnn_flash_attn_fwd": [P, P, P, I, I, I, F, I, P],
     "pdnn_flash_attn_bwd": [P, P, P, P, P, P, I, I, I, F, I, P],
     "pdnn_embedding_fwd": [P, P, P, P, I, I, I, P],

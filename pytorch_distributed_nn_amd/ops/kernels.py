@@ -1061,9 +1061,11 @@ def attn_softmax_fwd(S, P, lse, rows, T, scale, causal=True):
     call("pdnn_attn_softmax_fwd", ptr(S), T, ptr(P), T, ptr(lse), rows, T, float(scale), int(causal), stream())
 
 
-def attn_softmax_bwd(P, dP, dS, rows, T, scale):
+def attn_softmax_bwd(P, dP, dS, rows, T, scale, causal=False):
+    """causal: dP above the diagonal is never read (the causal dP GEMM leaves it unwritten); dS there is 0."""
     _chk(T % 4 == 0 and dP.dtype == F32 and dS.dtype == BF16, "attn_softmax_bwd: buffers")
-    call("pdnn_attn_softmax_bwd", ptr(P), T, ptr(dP), T, ptr(dS), T, rows, T, float(scale), stream())
+    call("pdnn_attn_softmax_bwd", ptr(P), T, ptr(dP), T, ptr(dS), T, rows, T, float(scale), int(bool(causal)),
+         stream())
 
 
 def flash_attn_fwd(qkv, B, T, H, scale, causal=True):

@@ -82,7 +82,7 @@ def attention_bwd(dy, qkv, P, B, T, H, causal=True, dS_buf=None):
                    causal=1 if causal else 0)
     # dS = P * (dP - rowsum(P dP)) / sqrt(d), written over P (row-local, read-before-write per element)
     dS = P
-    K.attn_softmax_bwd(P, dP, dS, B * H * T, T, 1.0 / math.sqrt(d))
+    K.attn_softmax_bwd(P, dP, dS, B * H * T, T, 1.0 / math.sqrt(d), causal)
     # dQ = dS K : B = K stored [k][d] = [K][N]
     K.gemm_batched(dS, T, sP, 0, k, ld, (T * ld, d), 1, dq, ld, (T * ld, d), T, d, T, (B, H),
                    causal=2 if causal else 0)

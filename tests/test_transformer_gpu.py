@@ -65,6 +65,9 @@ def test_attention_fwd_bwd(K, B, T, H, causal):
     assert rel2(y, ref) < 1e-2
     dy = rnd(B * T, D)
     ref.backward(dy.float())
+    # the causal dP GEMM leaves the scratch's above-diagonal tiles unwritten: poison them (a NaN bit pattern left
+    # in reused memory reached dQ through 0 * NaN in the softmax backward's row sums)
+    S.fill_(float("nan"))
     dqkv = TX.attention_bwd(dy, qkv, P, B, T, H, causal, dS_buf=S)
     for i, n in enumerate("qkv"):
         a, b = dqkv[:, i * D:(i + 1) * D], qr.grad[:, i * D:(i + 1) * D]
