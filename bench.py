@@ -336,6 +336,29 @@ def main():
         runtime.barrier()
         sync()
     dt = time.perf_counter() - t0
+    host_probe = None
+    if os.environ.get("PDNN_BENCH_HOST_PROBE") and dev.type == "cuda":
+        # diagnostics after the timed region: host enqueue time of one step started on an idle GPU vs the step's
+        # wall time (a host time near the wall time = launch-bound); =2 also prints a cProfile of one step to stderr
+        host_probe = []
+        with ctx:
+            for k in range(3):
+                sync()
+                h0 = time.perf_counter()
+                step(a.warmup + a.steps + k)
+                h1 = time.perf_counter()
+                sync()
+                host_probe.append({"host_ms": round((h1 - h0) * 1e3, 3), "wall_ms": round((time.perf_counter() - h0) * 1e3, 3)})
+            if os.environ["PDNN_BENCH_HOST_PROBE"] == "2":
+                import cProfile
+                import pstats
+                sync()
+                pr = cProfile.Profile()
+                pr.enable()
+                step(a.warmup + a.steps + 3)
+                pr.disable()
+                sync()
+                pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(40)
     comm = None
     if use_ddp and not use_graph and isinstance(net, DistributedDataParallel) and dev.type == "cuda":
         # after the timed region (it is not perturbed): a few more steps with device-event timing of every bucket
@@ -394,6 +417,7 @@ def main():
                         ("DDP path (1-rank process group: RCCL on a GPU)" if world == 1 else "DDP path"),
             "plain_step_1gpu": plain,
             "comm": comm,
+            **({"host_probe": host_probe} if host_probe else {}),
             "model_tflops_per_gpu": round(tok / world * model.flops_per_token(S) / 1e12, 1),
             "config": {"model": f"{a.model} (12L/12H/768, vocab {V}, tied head)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": S, "parallelism": f"dp{world}",
@@ -425,6 +449,7 @@ def main():
             "plain_step_1gpu": plain,
             "extra_configs": extra,
             "comm": comm,
+            **({"host_probe": host_probe} if host_probe else {}),
             "config": {"model": (f"{a.model} (reference layout, {in_chw[1]}x{in_chw[2]}, {nc} classes)" if small else
                                  f"{a.model} (ImageNet layout, {S}x{S}, {nc} classes)"), "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
