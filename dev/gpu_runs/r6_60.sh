@@ -1,0 +1,21 @@
+#!/bin/bash
+# side-stream persistent grids capped (tuning side_grid_cus) so the compute stream keeps CUs: tests + A/B
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r6_60
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_tuning_gpu.py tests/test_fused_blocks_gpu.py tests/test_transformer_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+run() {
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python3 bench.py --no-extra-configs --no-plain-run $EXTRA > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; return 1; }
+  python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['ms_per_step'])"
+}
+for i in 1 2; do
+EXTRA="" run r0_$i PDNN_TUNE=side_grid_cus=0 || exit 1
+EXTRA="" run r224_$i PDNN_TUNE=side_grid_cus=224 || exit 1
+EXTRA="" run r192_$i PDNN_TUNE=side_grid_cus=192 || exit 1
+EXTRA="--model gpt2_small" run g0_$i PDNN_TUNE=side_grid_cus=0 || exit 1
+EXTRA="--model gpt2_small" run g192_$i PDNN_TUNE=side_grid_cus=192 || exit 1
+done
+echo done
