@@ -32,11 +32,12 @@ namespace pg {
                                "blocks fit a CU).  At 512 the kernel took 325-330 or 498-501 us inside the ResNet-50 "  \
                                "step (a launch overlapping the side stream's last kernel leaves a CU with two runs in " \
                                "sequence), 2048: 330-360 (gpurun_out/r6_26); alone 370 vs 390 us (r6_25)")              \
-    X(attn_bwd_wide, 1, "flash-attention backward kernels with two 16-row fragments per wave (half the LDS "       \
+    X(attn_bwd_wide, 3, "flash-attention backward kernels with two 16-row fragments per wave (half the LDS "       \
                         "fragment reads per MFMA), a bit mask: 1 dQ (32 queries per wave), 2 dK / dV (32 keys per wave). " \
                         "Alone (B8 T1024 causal) 0: 87.4 us, 1: 90.1, 3: 90.3; B32: 330 / 315 / 302 us; in the GPT-2 " \
                         "step beside the side-stream weight gradients 1: 688.5k / 687.4k vs 0: 680.6k / 681.8k tok/s, " \
-                        "3: 688.6k / 683.3k (gpurun_out/r6_45)")                                                    \
+                        "3: 688.6k / 683.3k (gpurun_out/r6_45); three more pairs 1 vs 3: 693.1k / 696.3k, 691.0k / "  \
+                        "693.2k, 693.8k / 694.0k (r6_62) -- level in the GPT-2 step, 4-9% faster alone at B32 / T4096")  \
     X(attn_delta_in_dq, 1, "flash-attention backward: the dQ kernel forms delta = rowsum(dO . O) itself and runs " \
                            "before dK / dV (0: a separate delta launch first)")                                  \
     X(conv3x3_force, 0, "halo 3x3 conv also for images narrower than 12 (tests)")                         \

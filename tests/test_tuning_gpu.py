@@ -11,7 +11,7 @@ BF = torch.bfloat16
 # kernel-side entries -> alternative values
 ALT = {"glds": [0, 2], "pp": [0, 2], "pp_bn": [96, 128, 192, 288], "conv3x3_force": [1], "pp_dgrad_bn_k": [512, 1 << 20],
        "comm_cus": [0, 64], "pp_sk64": [0], "pp_epi_slack": [0, 1], "pp_epi_pair": [0], "pp_conv_fwd_c": [128, 1 << 20], "stem_wgrad_blocks": [512],
-       "attn_delta_in_dq": [0], "attn_bwd_wide": [0, 3]}
+       "attn_delta_in_dq": [0], "attn_bwd_wide": [0, 1]}
 
 
 def rel(a, b):
